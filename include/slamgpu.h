@@ -1,0 +1,228 @@
+/*
+ * slamgpu.h — C-ABI of the MI355X-native local-mapping back end (libslamgpu.so).
+ *
+ * The drop-in boundary for the reference's hot path (ywrt/slam-robot):
+ *   - class Slam            (slam.h:21-65)  -> sg_slam_* (SolveFrames / SolveAllFrames / ReprojectMap,
+ *                                              iterations(), error())
+ *   - Ceres problem + solve (slam.cpp:257-521) -> sg_problem_* / sg_ba_*  (compact problem, LM solve)
+ *   - ProjectPoint          (project.h:11-54) -> device code inside the solver and sg_project_points
+ *   - HessianTracker        (hessian.h:9-270) -> sg_tracker_*           (front end, see sg_track_*)
+ *
+ * Conventions: plain pointers and sizes only, no C++/torch types.  Every entry point returns 0 (SG_OK) on
+ * success or a negative errno-style code.  The caller owns every host array it passes; the library owns
+ * its device buffers (allocated on first use, grown on demand, freed by *_destroy).  One handle per host
+ * thread; each handle owns one HIP stream on the device named in its options.
+ */
+#ifndef SLAMGPU_H_
+#define SLAMGPU_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SG_OK 0
+#define SG_EINVAL (-22)   /* bad argument / inconsistent sizes */
+#define SG_ENOMEM (-12)   /* host or device allocation failed */
+#define SG_EDEVICE (-5)   /* HIP runtime error (message via sg_last_error) */
+#define SG_ENODEV (-19)   /* no usable gfx950 device */
+#define SG_ECOMM (-71)    /* RCCL error */
+
+/* Bit positions of TrackedPoint::Flags (localmap.h:184-190). point_flags holds (1 << flag). */
+enum sg_point_flag {
+  SG_BAD_LOCATION = 0,
+  SG_NO_BASELINE = 1,
+  SG_NO_OBSERVATIONS = 2,
+  SG_MISMATCHED = 3,
+  SG_BAD_FEATURE = 4
+};
+
+/* Termination types (ceres::SolverTerminationType, Ceres 1.8 naming). */
+enum sg_termination {
+  SG_NO_CONVERGENCE = 0,
+  SG_FUNCTION_TOLERANCE = 1,
+  SG_GRADIENT_TOLERANCE = 2,
+  SG_PARAMETER_TOLERANCE = 3,
+  SG_NUMERICAL_FAILURE = 4,
+  SG_DID_NOT_RUN = 5
+};
+
+/*
+ * LocalMap (localmap.h:284-320) in structure-of-arrays form.  Frames are in LocalMap::frames order,
+ * observations grouped by frame in Frame::observations() order.  q/t/X/k are the parameter blocks the
+ * reference hands to Ceres by raw pointer (localmap.h:129-132,159-160,194-195,30); they are updated in
+ * place by a solve exactly as Ceres updates the map's own storage.
+ */
+typedef struct sg_map {
+  int32_t num_cameras;
+  double* k;                    /* [7*num_cameras]  Camera::k = k1,k2,k3,fx,fy,cx,cy */
+  int32_t num_frames;
+  double* q;                    /* [4*F] Frame::rotation().coeffs()  Eigen order [x,y,z,w] */
+  double* t;                    /* [3*F] Frame::translation() */
+  const int32_t* frame_camera;  /* [F] index into cameras */
+  const int32_t* frame_prev;    /* [F] index of Frame::previous(), -1 if none */
+  int32_t num_points;
+  double* X;                    /* [4*P] TrackedPoint::location() homogeneous [X,Y,Z,W] */
+  int32_t* point_flags;         /* [P] TrackedPoint flags bitmask */
+  double* point_uncertainty;    /* [P] TrackedPoint::uncertainty() */
+  int32_t num_obs;
+  const double* obs_pt;         /* [2*M] Observation::pt (pixels) */
+  const int32_t* obs_frame;     /* [M] */
+  const int32_t* obs_point;     /* [M] */
+  int32_t* obs_disabled;        /* [M] Observation::is_disabled */
+  double* obs_error;            /* [2*M] Observation::error, written by ReprojectMap */
+} sg_map;
+
+/*
+ * The Ceres problem that Slam::SetupProblem builds (slam.cpp:257-414), in compact form.
+ *   - one quaternion block (4, local 3 via ceres::QuaternionParameterization) + one translation block (3)
+ *     per frame; a frame's blocks are free or constant independently (the translation of a skipped
+ *     previous frame can be free through FrameDistance while its rotation is absent);
+ *   - one homogeneous point block (4, no parameterization) per point, free or constant;
+ *   - intrinsics blocks (7) per camera, constant unless cameras_free (SolveAllFrames(..., true));
+ *   - residual blocks: ReprojectionError (2) with CauchyLoss(range) per observation, FrameDistance (1)
+ *     with CauchyLoss(dist_range) per (frame, prev) pair, CameraStabilization (7) with CauchyLoss(5)
+ *     per camera when cameras_free.
+ */
+typedef struct sg_problem {
+  int32_t num_cameras;
+  double* k;                    /* [7*ncam] */
+  int32_t cameras_free;         /* 0: intrinsics constant (SolveFrames) */
+  int32_t num_frames;
+  double* q;                    /* [4*F] updated in place */
+  double* t;                    /* [3*F] updated in place */
+  int32_t* frame_camera;        /* [F] */
+  uint8_t* frame_rot_free;      /* [F] */
+  uint8_t* frame_trans_free;    /* [F] */
+  int32_t* frame_map_index;     /* [F] source frame in the sg_map, or -1 */
+  int32_t num_points;
+  double* X;                    /* [4*P] updated in place */
+  uint8_t* point_free;          /* [P] */
+  int32_t* point_map_index;     /* [P] source point in the sg_map, or -1 */
+  int32_t num_obs;
+  double* obs_pt;               /* [2*M] observed pixel */
+  int32_t* obs_frame;           /* [M] problem frame index */
+  int32_t* obs_point;           /* [M] problem point index */
+  int32_t num_dist;
+  int32_t* dist_frame;          /* [D] FrameDistance(frame.t, prev.t) */
+  int32_t* dist_prev;           /* [D] */
+  double range;                 /* CauchyLoss(range) on reprojection (slam.cpp:265) */
+  double dist_target;           /* FrameDistance(150.) (slam.cpp:403) */
+  double dist_range;            /* CauchyLoss(15) (slam.cpp:404) */
+  double stab_range;            /* CauchyLoss(5) on CameraStabilization (slam.cpp:463) */
+  void* owner_;                 /* library-owned storage (sg_problem_from_map), NULL for caller-owned */
+} sg_problem;
+
+/* ceres::Solver::Options as used by Slam::Run (slam.cpp:482-508) plus the Ceres 1.8 defaults it keeps. */
+typedef struct sg_solver_options {
+  int32_t max_num_iterations;            /* 1000 (slam.cpp:493) */
+  double function_tolerance;             /* 1e-7 (slam.cpp:494); 1e-9 when fine */
+  double gradient_tolerance;             /* 1e-10, relative to the initial gradient max-norm (Ceres 1.8) */
+  double parameter_tolerance;            /* 1e-8 */
+  double min_relative_decrease;          /* 1e-3 */
+  double initial_trust_region_radius;    /* 1e4 */
+  double max_trust_region_radius;        /* 1e16 */
+  double min_trust_region_radius;        /* 1e-32 */
+  double min_lm_diagonal;                /* 1e-6 */
+  double max_lm_diagonal;                /* 1e32 */
+  int32_t max_num_consecutive_invalid_steps; /* 5 */
+  int32_t jacobi_scaling;                /* 1 */
+  int32_t disable_termination;           /* benchmark mode: run exactly max_num_iterations LM iterations */
+} sg_solver_options;
+
+/* ceres::Solver::Summary fields the reference reads (slam.cpp:510-520). */
+typedef struct sg_solver_summary {
+  int32_t num_iterations;        /* summary.iterations.size() — includes iteration 0 (slam.cpp:517) */
+  int32_t num_successful_steps;
+  int32_t num_unsuccessful_steps;
+  int32_t num_invalid_steps;
+  int32_t termination_type;      /* enum sg_termination */
+  int32_t ok;                    /* summary.error.empty() (slam.cpp:520) */
+  double initial_cost;           /* including fixed cost */
+  double final_cost;             /* summary.final_cost (slam.cpp:518) */
+  double fixed_cost;
+  double trust_region_radius;
+  int32_t num_lm_iterations;     /* LM loop iterations executed on the device (benchmark unit) */
+  int32_t reserved;
+} sg_solver_summary;
+
+typedef struct sg_device_options {
+  int32_t device;                /* HIP device ordinal */
+  int32_t precision;             /* 0: fp64 everywhere; 1: fp32 Jacobian sweep, fp64 normal equations */
+  int32_t rank;                  /* landmark shard index (0 for single GPU) */
+  int32_t nranks;                /* 1 for single GPU */
+} sg_device_options;
+
+/* ---------------------------------------------------------------------------------------------------- */
+/* Library */
+const char* sg_version(void);
+const char* sg_last_error(void);              /* thread-local message for the last failing call */
+void sg_solver_options_default(sg_solver_options* o);
+void sg_device_options_default(sg_device_options* o);
+
+/* ---------------------------------------------------------------------------------------------------- */
+/* Problem assembly (host side of Slam::SetupProblem, slam.cpp:257-414 / SolveFrames 417-443 /
+ * SolveAllFrames 447-480).  Returns 1 in *built when the problem was built, 0 when the reference aborts
+ * ("Slam aborted due to frame set too small", slam.cpp:305-308). */
+int sg_problem_from_map_frames(const sg_map* map, int32_t num_to_solve, int32_t num_to_present,
+                               double range, sg_problem* out, int32_t* built);
+int sg_problem_from_map_all(const sg_map* map, double range, int32_t solve_cameras,
+                            sg_problem* out, int32_t* built);
+void sg_problem_free(sg_problem* p);
+/* Copy solved parameter blocks back into the map (what Ceres does through the raw pointers). */
+int sg_problem_write_back(const sg_problem* p, sg_map* map);
+/* Split a problem's landmarks into nranks shards (contiguous ranges of points sorted by first observing
+ * frame); every shard keeps all frames, cameras and FrameDistance blocks. */
+int sg_problem_shard(const sg_problem* p, int32_t rank, int32_t nranks, sg_problem* out);
+
+/* ---------------------------------------------------------------------------------------------------- */
+/* Device bundle-adjustment solver (Ceres 1.8 Levenberg-Marquardt + SPARSE_SCHUR, restated on MI355X). */
+typedef struct sg_ba sg_ba;
+int sg_ba_create(sg_ba** out, const sg_device_options* dev);
+void sg_ba_destroy(sg_ba* h);
+/* RCCL communicator for landmark sharding: id is ncclUniqueId (128 bytes), from sg_comm_unique_id. */
+int sg_comm_unique_id(void* id128);
+int sg_ba_comm_init(sg_ba* h, const void* id128, int32_t nranks, int32_t rank);
+/* Upload a problem (the problem's q/t/X are read now and written back by sg_ba_download). */
+int sg_ba_load(sg_ba* h, const sg_problem* p);
+/* Run the LM solve on the device; writes the solved blocks back into p. */
+int sg_ba_solve(sg_ba* h, const sg_solver_options* o, sg_problem* p, sg_solver_summary* s);
+/* Benchmark entry: (re)initialise from the uploaded state, then enqueue exactly n LM iterations without
+ * host synchronisation (termination disabled).  sg_ba_sync waits for completion. */
+int sg_ba_begin(sg_ba* h, const sg_solver_options* o);
+int sg_ba_iterate(sg_ba* h, int32_t n);
+int sg_ba_sync(sg_ba* h);
+int sg_ba_summary(sg_ba* h, sg_solver_summary* s);
+int sg_ba_download(sg_ba* h, sg_problem* p);
+/* Per-kernel timing over the last sg_ba_iterate calls (HIP events on the solver's stream). names is a
+ * comma-separated list; ms[i] = mean duration of kernel i per launch; counts[i] launches timed. */
+int sg_ba_set_timing(sg_ba* h, int32_t enable);
+int sg_ba_kernel_times(sg_ba* h, char* names, int32_t names_len, double* ms, int32_t* counts, int32_t max);
+/* Algorithmic byte / flop counts for the roofline (per launch of each timed kernel). */
+int sg_ba_kernel_work(sg_ba* h, double* bytes, double* flops, int32_t max);
+
+/* Residual sweep only (ReprojectionError over the uploaded observations at the current state):
+ * r[2*M] corrected residuals in problem order, returns cost (without fixed cost) and failure count. */
+int sg_ba_evaluate(sg_ba* h, double* residuals, double* cost, int32_t* num_failed);
+
+/* ---------------------------------------------------------------------------------------------------- */
+/* Slam facade (slam.h:21-65).  A handle keeps iterations()/error() like the reference's Slam object. */
+typedef struct sg_slam sg_slam;
+int sg_slam_create(sg_slam** out, const sg_device_options* dev);
+void sg_slam_destroy(sg_slam* s);
+int sg_slam_solve_frames(sg_slam* s, sg_map* map, int32_t num_to_solve, int32_t num_to_present,
+                         double range, int32_t* solved);                          /* slam.cpp:417-443 */
+int sg_slam_solve_all_frames(sg_slam* s, sg_map* map, double range, int32_t solve_cameras,
+                             int32_t* solved);                                    /* slam.cpp:447-480 */
+int sg_slam_reproject_map(sg_slam* s, sg_map* map, double* mean);               /* slam.cpp:523-548 */
+int32_t sg_slam_iterations(const sg_slam* s);                                    /* slam.h:49 */
+double sg_slam_error(const sg_slam* s);                                          /* slam.h:50 */
+int sg_slam_last_summary(const sg_slam* s, sg_solver_summary* out);
+int sg_slam_set_options(sg_slam* s, const sg_solver_options* o);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SLAMGPU_H_ */

@@ -1,0 +1,132 @@
+// ba_kernels.h — data layout shared by the bundle-adjustment kernels and their host driver.
+//
+// HBM layout (all fp64, structure-of-arrays, points in "first free block" order so that a chunk of
+// consecutive points touches a narrow window of camera blocks — the co-visibility band of a sliding
+// window BA):
+//   q[2][4F], t[2][3F], X[2][4P]   parameter state, two slots (current / candidate), switched by LmState::cur
+//   obs_pt[2M], obs_frame[M]       observations, CSR by point (poff[P+1])
+//   J[M][24]                       corrected, unscaled residual + Jacobian per observation
+//                                  (r~ 2 | Jc 2x6 [rot_local 3, t 3] | Jp 2x4 | pad 2)
+//   V[P][10], g[P][4]              point normal-equation blocks (upper 4x4) and gradient
+//   Vinv[P][10], tp[P][4]          damped, scaled inverse and V^-1 g~ (per LM iteration)
+//   cam_slab / S_slab              per-chunk partial camera blocks / Schur window (deterministic reduce)
+//   S[n][n]                        dense reduced camera system (upper blocks), n = 6 * free frames
+#ifndef SG_BA_KERNELS_H_
+#define SG_BA_KERNELS_H_
+
+#include <cstdint>
+
+namespace sg {
+
+constexpr int kChunkPts = 128;      // points per chunk (one workgroup)
+constexpr int kLanesPerPt = 4;      // lanes per point in the observation sweeps
+constexpr int kSweepThreads = kChunkPts * kLanesPerPt;  // 512
+constexpr int kSchurThreads = 256;
+constexpr int kNbwMax = 24;         // max camera blocks in a chunk window (wider points go "wide")
+constexpr int kCamV = 27;           // per camera block: upper(Jc^T Jc) 21 + Jc^T r 6
+constexpr int kJStride = 24;
+constexpr int kNScal = 16;          // per-chunk scalar slots
+constexpr int kCholThreads = 512;
+constexpr int kCholNb = 16;
+
+enum ScalSlot {
+  kCost = 0, kFail, kFixed, kFixedFail, kXnorm2, kGmax, kLinFail, kModel, kCandCost, kCandFail, kStep2,
+  kCandX2
+};
+
+// Exchange-buffer scalar slots appended after the camera blocks.
+enum CamX { kXCost = 0, kXFail, kXFixed, kXFixedFail, kXXnorm2, kXNum };
+enum UpdX { kUModel = 0, kUCandCost, kUCandFail, kUStep2, kUCandX2, kULinFail, kUNum };
+enum CholX { kCStep2 = 0, kCCandX2, kCModel, kCCandCost, kCFail, kCNum };
+
+struct Chunk {
+  int32_t p0, p1;     // point range [p0, p1) (device order)
+  int32_t b_lo, nb;   // camera-block window [b_lo, b_lo + nb)
+  int32_t cam_off;    // offset of this chunk's camera partials in cam_slab (doubles)
+  int32_t s_off;      // offset of this chunk's Schur window in S_slab (doubles)
+  int32_t wide;       // window too wide for LDS: accumulate with global atomics instead
+  int32_t pad;
+};
+
+struct LmState {
+  // options (copied from sg_solver_options)
+  int32_t max_iter, max_invalid, disable_term, jacobi;
+  double ftol, gtol, ptol, min_rel_dec, max_radius, min_radius, min_diag, max_diag;
+  // minimizer state
+  int32_t cur, need_lin, first, done;
+  int32_t termination, ok, pushed, lm_iters;
+  int32_t n_succ, n_unsucc, n_invalid, consecutive_invalid;
+  int32_t reuse_diag, pad0;
+  double radius, decrease_factor;
+  double cost, fixed_cost, initial_cost, x_norm, abs_gtol, min_pushed_cost;
+  double last_model, last_new_cost, last_rel_decrease, last_step_norm;
+};
+
+// Kernel argument bundle (passed by value through the kernarg segment).
+struct Dev {
+  LmState* st;
+  // cameras / frames
+  const double* k;
+  double* q[2];
+  double* t[2];
+  const int32_t* frame_cam;
+  const int32_t* frame_block;
+  const uint8_t* rot_free;
+  const uint8_t* trans_free;
+  int32_t F, NB, n;
+  // points / observations
+  double* X[2];
+  const uint8_t* pfree;
+  const int32_t* poff;
+  int32_t P, M;
+  const double* obs_pt;
+  const int32_t* obs_frame;
+  const uint8_t* obs_fixed;
+  double b, inv_b;               // Cauchy(range): b = range^2
+  // FrameDistance
+  int32_t D;
+  const int32_t* fd_a;           // problem frame index
+  const int32_t* fd_b;
+  const int32_t* fd_boff;        // per block CSR of incident FD residuals (entry = 2*d + side)
+  const int32_t* fd_bidx;
+  double fd_target, fd_b2, fd_inv_b2;
+  double* fd_r;                  // [D] corrected residual
+  double* fd_J;                  // [D][6] corrected, unscaled: d/dt_a, d/dt_b
+  double* fd_D;                  // [NB][9] FD diagonal (trans) block, unscaled
+  double* fd_X;                  // [D][9] FD cross block J_a J_b^T, unscaled
+  // linearization
+  double* J;
+  double* V;
+  double* g;
+  double* scale_p;
+  double* diag_p;
+  double* Vinv;
+  double* tp;
+  double* scale_c;               // [n]
+  double* diag_c;                // [n]
+  double* camdiag;               // [n] diag(J^T J) camera columns, unscaled (obs + FD)
+  double* camg;                  // [n] camera gradient, unscaled (obs + FD)
+  // chunks and partials
+  const Chunk* chunks;
+  int32_t nchunks;
+  const int32_t* blk_cbeg;       // [NB] chunk range that may cover block I
+  const int32_t* blk_cend;
+  double* cam_slab;
+  double* S_slab;
+  double* chunk_scal;            // [nchunks][kNScal]
+  double* cam_wide;              // [NB][27] (wide chunks, global atomics)
+  double* S_wide;                // [n][n]   (wide chunks, global atomics)
+  // exchange buffers (all-reduced across landmark shards)
+  double* xchg_cam;              // [NB*27 + kXNum]
+  double* xchg_max;              // [1]
+  double* S;                     // [n][n] reduced system (upper blocks), then its factor
+  double* rhs;                   // [n]
+  double* xchg_upd;              // [kUNum]
+  double* xchg_chol;             // [kCNum]
+  double* xc;                    // [n] camera solution (scaled)
+  double* work;                  // [n] solver scratch
+};
+
+}  // namespace sg
+
+#endif  // SG_BA_KERNELS_H_

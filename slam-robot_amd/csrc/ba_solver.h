@@ -1,0 +1,114 @@
+// ba_solver.h — host driver of the MI355X bundle-adjustment solver (one per sg_ba handle).
+#ifndef SG_BA_SOLVER_H_
+#define SG_BA_SOLVER_H_
+
+#include <hip/hip_runtime.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "ba_kernels.h"
+#include "common.h"
+
+namespace sg {
+
+void ValidateProblem(const sg_problem* p);
+
+// Growable device buffer.
+template <typename T>
+struct DBuf {
+  T* ptr = nullptr;
+  size_t cap = 0;
+  size_t size = 0;
+  void Resize(size_t n) {
+    size = n;
+    if (n <= cap) return;
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    cap = 0;
+    SG_HIP_CHECK(hipMalloc(&ptr, std::max<size_t>(n, 1) * sizeof(T)));
+    cap = n;
+  }
+  void Upload(const std::vector<T>& v, hipStream_t s) {
+    Resize(v.size());
+    if (!v.empty()) SG_HIP_CHECK(hipMemcpyAsync(ptr, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s));
+  }
+  void Zero(hipStream_t s) {
+    if (size) SG_HIP_CHECK(hipMemsetAsync(ptr, 0, size * sizeof(T), s));
+  }
+  ~DBuf() {
+    if (ptr) (void)hipFree(ptr);
+  }
+};
+
+class Comm;  // RCCL communicator (comm.cpp)
+
+class BaSolver {
+ public:
+  explicit BaSolver(const sg_device_options& dev);
+  ~BaSolver();
+
+  void Load(const sg_problem& p);
+  void Begin(const sg_solver_options& o);
+  void Iterate(int n);
+  void Sync();
+  void Summary(sg_solver_summary* s);
+  void Download(sg_problem* p);
+  void Solve(const sg_solver_options& o, sg_problem* p, sg_solver_summary* s);
+  void Evaluate(double* residuals, double* cost, int32_t* nfail);
+  void SetTiming(bool on);
+  int KernelTimes(char* names, int names_len, double* ms, int32_t* counts, int max);
+  int KernelWork(double* bytes, double* flops, int max);
+  void CommInit(const void* id128, int nranks, int rank);
+  static void UniqueId(void* id128);
+
+  // ReprojectMap (slam.cpp:523-548) over a whole map; used by the Slam facade.
+  double ReprojectMap(sg_map* m);
+
+  hipStream_t stream() const { return stream_; }
+
+ private:
+  sg_device_options dev_;
+  hipStream_t stream_ = nullptr;
+  std::unique_ptr<Comm> comm_;
+  bool loaded_ = false;
+  bool began_ = false;
+  // host copies of the structure
+  int F_ = 0, P_ = 0, M_ = 0, NB_ = 0, n_ = 0, D_ = 0, nchunks_ = 0, max_nb_ = 0, ncam_ = 0;
+  std::vector<int32_t> point_perm_;   // device order -> problem point
+  std::vector<int32_t> obs_perm_;     // device order -> problem observation
+  std::vector<Chunk> chunks_;
+  size_t schur_lds_ = 0;
+  // device buffers
+  DBuf<LmState> st_;
+  DBuf<double> k_, q_, t_, X_, obs_pt_, J_, V_, g_, scale_p_, diag_p_, Vinv_, tp_, scale_c_, diag_c_, camdiag_,
+      camg_, cam_slab_, S_slab_, chunk_scal_, cam_wide_, S_wide_, xchg_cam_, xchg_max_, S_, rhs_, xchg_upd_,
+      xchg_chol_, xc_, work_, fd_r_, fd_J_, fd_D_, fd_X_, red_;
+  DBuf<int32_t> frame_cam_, frame_block_, poff_, obs_frame_, fd_a_, fd_b_, fd_boff_, fd_bidx_, blk_cbeg_,
+      blk_cend_, mobs_frame_, mobs_point_, mframe_cam_;
+  DBuf<uint8_t> rot_free_, trans_free_, pfree_, obs_fixed_;
+  DBuf<Chunk> chunks_d_;
+  DBuf<int32_t> work_i_;   // Cholesky panel envelopes (panel_jmax)
+  DBuf<double> mk_, mq_, mt_, mX_, mobs_pt_, mobs_err_, mred_;
+  double range_b_ = 4.0, fd_target_ = 150.0, fd_b2_ = 225.0;
+  // timing
+  bool timing_ = false;
+  struct KTimer {
+    std::string name;
+    std::vector<hipEvent_t> ev;  // pairs
+    double total_ms = 0.0;
+    int count = 0;
+  };
+  std::vector<KTimer> timers_;
+  void TimedLaunchBegin(int id);
+  void TimedLaunchEnd(int id);
+  void CollectTimes();
+  Dev MakeDev();
+  void AllReduceSum(double* buf, size_t n);
+  void AllReduceMax(double* buf, size_t n);
+};
+
+}  // namespace sg
+
+#endif  // SG_BA_SOLVER_H_

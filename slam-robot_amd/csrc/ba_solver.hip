@@ -1,0 +1,1800 @@
+// ba_solver.hip — MI355X-native Levenberg-Marquardt bundle adjustment (the reference's Slam::Run,
+// slam.cpp:482-521, which hands the problem to Ceres 1.8 with SPARSE_SCHUR; restated here on gfx950).
+//
+// One LM iteration = the kernel chain below, enqueued without host synchronisation; the accept/reject
+// decision, trust-region update and termination tests run on the device (k_decide), so a solve is a
+// stream of identical iterations the host only polls for completion.
+//
+//   k_linearize    [chunk of 128 points, 8 lanes/point]  residuals + analytic Jacobians (HBM sweep),
+//                  point blocks V,g; camera blocks U,g_c into an LDS window (co-visibility band)
+//   k_cam_reduce   deterministic reduce of per-chunk camera partials  -> xchg_cam   (all-reduced)
+//   k_cam_finalize FrameDistance terms, cost, gradient test, Jacobi scale (iteration 0), LM diagonal
+//   k_schur        [chunk, one wave per point, lanes over observation pairs] damped V^-1 and the Schur
+//                  complement contributions -J_c^T J_p V^-1 J_p^T J_c into an LDS window
+//   k_S_reduce     deterministic reduce of per-chunk Schur windows -> dense S, rhs  (all-reduced)
+//   k_cholesky     one workgroup: add U + damping, banded Cholesky, solve, candidate camera poses
+//   k_point_update back-substitution, model cost change, candidate points, candidate cost
+//   k_upd_reduce   reduce of the per-chunk update scalars  -> xchg_upd              (all-reduced)
+//   k_decide       Ceres TrustRegionMinimizer / LevenbergMarquardtStrategy bookkeeping
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+
+#include "ba_solver.h"
+#include "comm.h"
+#include "project_math.h"
+
+namespace sg {
+
+// ------------------------------------------------------------------------------------------------
+// small device helpers
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+  return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = fmax(v, __shfl_xor(v, m));
+  return v;
+}
+// Block reduction in a fixed order (deterministic).  red: LDS scratch of >= nwaves doubles.
+template <int NT>
+__device__ __forceinline__ double block_sum(double v, double* red) {
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double s = 0.0;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) s += red[i];
+  return s;
+}
+template <int NT>
+__device__ __forceinline__ double block_max(double v, double* red) {
+  v = wave_max(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double s = 0.0;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) s = fmax(s, red[i]);
+  return s;
+}
+
+// packed upper-triangle index of a 6x6 block (a <= c)
+__device__ __forceinline__ int u6(int a, int c) { return a * (11 - a) / 2 + c; }
+// packed upper-triangle index of a 4x4 block (a <= c)
+__device__ __forceinline__ int u4(int a, int c) { return a * (7 - a) / 2 + c; }
+// packed index of a window block pair (i <= j < nb)
+__device__ __forceinline__ int wp(int i, int j, int nb) { return i * nb - i * (i - 1) / 2 + (j - i); }
+
+// Load the corrected Jacobian of observation o and apply Jacobi scaling.
+__device__ __forceinline__ void load_scaled_J(const Dev& d, int o, int b, const double* sp, double* r,
+                                              double* Jc, double* Jp) {
+  const double2* J2 = reinterpret_cast<const double2*>(d.J + (size_t)o * kJStride);
+  double buf[22];
+#pragma unroll
+  for (int i = 0; i < 11; ++i) {
+    const double2 v = J2[i];
+    buf[2 * i] = v.x;
+    buf[2 * i + 1] = v.y;
+  }
+  r[0] = buf[0];
+  r[1] = buf[1];
+  if (b >= 0) {
+    const double* sc = d.scale_c + 6 * b;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) Jc[i] = buf[2 + i] * sc[i % 6];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 12; ++i) Jc[i] = 0.0;
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) Jp[i] = buf[14 + i] * sp[i % 4];
+}
+
+// 4x4 SPD inverse via LL^T; A and Ainv packed upper (10).  Returns false on a non-positive pivot.
+__device__ __forceinline__ bool inv4_spd(const double* A, double* Ai) {
+  double L[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) L[i][j] = 0.0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    double s = A[u4(j, j)];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (k < j) s -= L[j][k] * L[j][k];
+    if (!(s > 0.0)) return false;
+    const double ljj = sqrt(s);
+    L[j][j] = ljj;
+    const double inv = 1.0 / ljj;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (i <= j) continue;
+      double t = A[u4(j, i)];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (k < j) t -= L[i][k] * L[j][k];
+      L[i][j] = t * inv;
+    }
+  }
+  // Linv (lower)
+  double Li[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) Li[i][j] = 0.0;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (i < c) continue;
+      double s = (i == c) ? 1.0 : 0.0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (k >= c && k < i) s -= L[i][k] * Li[k][c];
+      Li[i][c] = s / L[i][i];
+    }
+  }
+  // A^-1 = Linv^T Linv
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (c < a) continue;
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s += Li[k][a] * Li[k][c];
+      Ai[u4(a, c)] = s;
+    }
+  return true;
+}
+
+__device__ __forceinline__ double sym4(const double* A, int a, int c) { return a <= c ? A[u4(a, c)] : A[u4(c, a)]; }
+
+// ------------------------------------------------------------------------------------------------
+// k_linearize: the Jacobian sweep.  One chunk (<=128 points) per workgroup, 8 lanes per point; each
+// lane walks its point's observations, evaluates project.h + its analytic Jacobian, the Cauchy
+// corrector, and stores the corrected block (24 doubles, one 192-byte record per observation).
+__global__ __launch_bounds__(kSweepThreads) void k_linearize(Dev d) {
+  const LmState* st = d.st;
+  if (st->done || !st->need_lin) return;
+  const int cur = st->cur;
+  const bool first = st->first != 0;
+  const Chunk ch = d.chunks[blockIdx.x];
+  __shared__ double cam[kNbwMax * kCamV];
+  __shared__ double red[kSweepThreads / 64];
+  const int ncv = ch.wide ? 0 : ch.nb * kCamV;
+  for (int i = threadIdx.x; i < ncv; i += blockDim.x) cam[i] = 0.0;
+  __syncthreads();
+
+  const int lp = threadIdx.x / kLanesPerPt, l8 = threadIdx.x % kLanesPerPt;
+  const int p = ch.p0 + lp;
+  double cost = 0.0, fail = 0.0, fixed = 0.0, ffail = 0.0, xn2 = 0.0, gmax = 0.0;
+  double V[10], g[4];
+#pragma unroll
+  for (int i = 0; i < 10; ++i) V[i] = 0.0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) g[i] = 0.0;
+  bool pf = false;
+  if (p < ch.p1) {
+    pf = d.pfree[p] != 0;
+    const double4 Xv = reinterpret_cast<const double4*>(d.X[cur])[p];
+    const double X[4] = {Xv.x, Xv.y, Xv.z, Xv.w};
+    const int o1 = d.poff[p + 1];
+    for (int o = d.poff[p] + l8; o < o1; o += kLanesPerPt) {
+      const int f = d.obs_frame[o];
+      const double* q = d.q[cur] + 4 * f;
+      const double* t = d.t[cur] + 3 * f;
+      const double* k = d.k + 7 * d.frame_cam[f];
+      const bool fx = d.obs_fixed[o] != 0;
+      double r[2], Jc[12], Jp[8], c;
+      double2* Jo = reinterpret_cast<double2*>(d.J + (size_t)o * kJStride);
+      const bool ok = LinearizeObservation(q, t, k, X, d.obs_pt + 2 * o, d.b, d.inv_b, r, Jc, Jp, &c);
+      if (!ok || fx) {
+        if (!ok) {
+          if (fx) ffail += 1.0;
+          else fail += 1.0;
+        } else if (first) {
+          fixed += c;
+        }
+#pragma unroll
+        for (int i = 0; i < 12; ++i) Jo[i] = make_double2(0.0, 0.0);
+        continue;
+      }
+      cost += c;
+      const int b = d.frame_block[f];
+      if (b < 0) {
+#pragma unroll
+        for (int i = 0; i < 12; ++i) Jc[i] = 0.0;
+      } else {
+        if (!d.rot_free[f]) { Jc[0] = Jc[1] = Jc[2] = Jc[6] = Jc[7] = Jc[8] = 0.0; }
+        if (!d.trans_free[f]) { Jc[3] = Jc[4] = Jc[5] = Jc[9] = Jc[10] = Jc[11] = 0.0; }
+      }
+      if (!pf) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) Jp[i] = 0.0;
+      }
+      Jo[0] = make_double2(r[0], r[1]);
+#pragma unroll
+      for (int i = 0; i < 6; ++i) Jo[1 + i] = make_double2(Jc[2 * i], Jc[2 * i + 1]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) Jo[7 + i] = make_double2(Jp[2 * i], Jp[2 * i + 1]);
+      Jo[11] = make_double2(c, 0.0);
+      if (pf) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          g[a] += Jp[a] * r[0] + Jp[4 + a] * r[1];
+#pragma unroll
+          for (int cc = 0; cc < 4; ++cc)
+            if (cc >= a) V[u4(a, cc)] += Jp[a] * Jp[cc] + Jp[4 + a] * Jp[4 + cc];
+        }
+      }
+      if (b >= 0) {
+        double* dst = ch.wide ? d.cam_wide + (size_t)b * kCamV : cam + (b - ch.b_lo) * kCamV;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+#pragma unroll
+          for (int cc = 0; cc < 6; ++cc)
+            if (cc >= a) atomicAdd(dst + u6(a, cc), Jc[a] * Jc[cc] + Jc[6 + a] * Jc[6 + cc]);
+          atomicAdd(dst + 21 + a, Jc[a] * r[0] + Jc[6 + a] * r[1]);
+        }
+      }
+    }
+    // reduce the point blocks across the 8 lanes of this point
+#pragma unroll
+    for (int m = 1; m < kLanesPerPt; m <<= 1) {
+#pragma unroll
+      for (int i = 0; i < 10; ++i) V[i] += __shfl_xor(V[i], m);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) g[i] += __shfl_xor(g[i], m);
+    }
+    if (l8 == 0) {
+      double* Vd = d.V + 10 * (size_t)p;
+#pragma unroll
+      for (int i = 0; i < 10; ++i) Vd[i] = V[i];
+      reinterpret_cast<double4*>(d.g)[p] = make_double4(g[0], g[1], g[2], g[3]);
+      if (pf) {
+        gmax = fmax(fmax(fabs(g[0]), fabs(g[1])), fmax(fabs(g[2]), fabs(g[3])));
+        if (first) {
+          reinterpret_cast<double4*>(d.scale_p)[p] =
+              make_double4(1.0 / (1.0 + sqrt(V[0])), 1.0 / (1.0 + sqrt(V[4])), 1.0 / (1.0 + sqrt(V[7])),
+                           1.0 / (1.0 + sqrt(V[9])));
+          xn2 = X[0] * X[0] + X[1] * X[1] + X[2] * X[2] + X[3] * X[3];
+        }
+      } else if (first) {
+        reinterpret_cast<double4*>(d.scale_p)[p] = make_double4(1.0, 1.0, 1.0, 1.0);
+      }
+    }
+  }
+  cost = block_sum<kSweepThreads>(cost, red);
+  fail = block_sum<kSweepThreads>(fail, red);
+  fixed = block_sum<kSweepThreads>(fixed, red);
+  ffail = block_sum<kSweepThreads>(ffail, red);
+  xn2 = block_sum<kSweepThreads>(xn2, red);
+  gmax = block_max<kSweepThreads>(gmax, red);
+  double* sc = d.chunk_scal + (size_t)blockIdx.x * kNScal;
+  if (threadIdx.x == 0) {
+    sc[kCost] = cost;
+    sc[kFail] = fail;
+    sc[kFixed] = fixed;
+    sc[kFixedFail] = ffail;
+    sc[kXnorm2] = xn2;
+    sc[kGmax] = gmax;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < ncv; i += blockDim.x) d.cam_slab[ch.cam_off + i] = cam[i];
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_cam_reduce: deterministic sum of the per-chunk camera partials (+ wide-chunk atomics).
+__global__ __launch_bounds__(256) void k_cam_reduce(Dev d) {
+  const LmState* st = d.st;
+  if (st->done || !st->need_lin) return;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nv = d.NB * kCamV;
+  if (i < nv) {
+    const int b = i / kCamV, e = i % kCamV;
+    double s = d.cam_wide[i];
+    d.cam_wide[i] = 0.0;
+    for (int c = d.blk_cbeg[b]; c < d.blk_cend[b]; ++c) {
+      const Chunk ch = d.chunks[c];
+      if (ch.wide || b < ch.b_lo || b >= ch.b_lo + ch.nb) continue;
+      s += d.cam_slab[ch.cam_off + (b - ch.b_lo) * kCamV + e];
+    }
+    d.xchg_cam[i] = s;
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x < 64) {
+    // scalars: one wave, lane l sums chunks l, l+64, ... then a fixed-order tree
+    const int lane = threadIdx.x;
+    double v[kXNum] = {0, 0, 0, 0, 0};
+    double gm = 0.0;
+    for (int c = lane; c < d.nchunks; c += 64) {
+      const double* sc = d.chunk_scal + (size_t)c * kNScal;
+      v[kXCost] += sc[kCost];
+      v[kXFail] += sc[kFail];
+      v[kXFixed] += sc[kFixed];
+      v[kXFixedFail] += sc[kFixedFail];
+      v[kXXnorm2] += sc[kXnorm2];
+      gm = fmax(gm, sc[kGmax]);
+    }
+#pragma unroll
+    for (int j = 0; j < kXNum; ++j) v[j] = wave_sum(v[j]);
+    gm = wave_max(gm);
+    if (lane == 0) {
+#pragma unroll
+      for (int j = 0; j < kXNum; ++j) d.xchg_cam[nv + j] = v[j];
+      d.xchg_max[0] = gm;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_cam_finalize: one workgroup.  FrameDistance blocks (slam.cpp:86-105), total cost, gradient
+// max-norm, Jacobi scale (iteration 0), pending iteration push, max-iteration test, LM diagonal.
+__global__ __launch_bounds__(256) void k_cam_finalize(Dev d) {
+  LmState* st = d.st;
+  if (st->done) return;
+  __shared__ double red[4];
+  __shared__ double fdcost[256];
+  __shared__ int done_sh;
+  const int tid = threadIdx.x;
+  const int cur = st->cur;
+  const int nv = d.NB * kCamV;
+  if (st->need_lin) {
+    // FrameDistance residuals at x[cur]
+    double myfd = 0.0;
+    for (int dd = tid; dd < d.D; dd += blockDim.x) {
+      const int fa = d.fd_a[dd], fb = d.fd_b[dd];
+      const double* ta = d.t[cur] + 3 * fa;
+      const double* tb = d.t[cur] + 3 * fb;
+      const double e0 = ta[0] - tb[0], e1 = ta[1] - tb[1], e2 = ta[2] - tb[2];
+      const double dist = sqrt(e0 * e0 + e1 * e1 + e2 * e2);
+      const double r = 0.1 * (dist - d.fd_target);
+      double rho0, rho1;
+      Cauchy(r * r, d.fd_b2, d.fd_inv_b2, &rho0, &rho1);
+      myfd += 0.5 * rho0;
+      const double sr = sqrt(rho1);
+      d.fd_r[dd] = sr * r;
+      const double gsc = sr * 0.1 / dist;
+      const double ga[3] = {gsc * e0, gsc * e1, gsc * e2};
+      const bool af = d.trans_free[fa] && d.frame_block[fa] >= 0;
+      const bool bf = d.trans_free[fb] && d.frame_block[fb] >= 0;
+      double* Jd = d.fd_J + 6 * dd;
+      for (int j = 0; j < 3; ++j) {
+        Jd[j] = af ? ga[j] : 0.0;
+        Jd[3 + j] = bf ? -ga[j] : 0.0;
+      }
+      double* Xd = d.fd_X + 9 * dd;
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) Xd[3 * i + j] = Jd[i] * Jd[3 + j];
+    }
+    // per-thread FD cost into a fixed slot (deterministic order below)
+    fdcost[tid] = myfd;
+    __syncthreads();
+    // per camera block: gradient, diag, FD diagonal block
+    double gm = 0.0, xn2c = 0.0;
+    for (int b = tid; b < d.NB; b += blockDim.x) {
+      double fdD[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+      double gfd[3] = {0, 0, 0};
+      for (int e = d.fd_boff[b]; e < d.fd_boff[b + 1]; ++e) {
+        const int dd = d.fd_bidx[e] >> 1, side = d.fd_bidx[e] & 1;
+        const double* Jd = d.fd_J + 6 * dd + 3 * side;
+        for (int i = 0; i < 3; ++i) {
+          gfd[i] += Jd[i] * d.fd_r[dd];
+          for (int j = 0; j < 3; ++j) fdD[3 * i + j] += Jd[i] * Jd[j];
+        }
+      }
+      for (int i = 0; i < 9; ++i) d.fd_D[9 * b + i] = fdD[i];
+      const double* U = d.xchg_cam + (size_t)b * kCamV;
+      for (int a = 0; a < 6; ++a) {
+        const double gg = U[21 + a] + (a >= 3 ? gfd[a - 3] : 0.0);
+        const double dg = U[u6(a, a)] + (a >= 3 ? fdD[4 * (a - 3)] : 0.0);
+        d.camg[6 * b + a] = gg;
+        d.camdiag[6 * b + a] = dg;
+      }
+    }
+    __syncthreads();
+    // gradient max-norm over free camera columns; camera part of |x| at iteration 0
+    for (int f = tid; f < d.F; f += blockDim.x) {
+      const int b = d.frame_block[f];
+      if (b < 0) continue;
+      if (d.rot_free[f])
+        for (int a = 0; a < 3; ++a) gm = fmax(gm, fabs(d.camg[6 * b + a]));
+      if (d.trans_free[f])
+        for (int a = 3; a < 6; ++a) gm = fmax(gm, fabs(d.camg[6 * b + a]));
+      if (st->first) {
+        if (d.rot_free[f])
+          for (int a = 0; a < 4; ++a) xn2c += d.q[cur][4 * f + a] * d.q[cur][4 * f + a];
+        if (d.trans_free[f])
+          for (int a = 0; a < 3; ++a) xn2c += d.t[cur][3 * f + a] * d.t[cur][3 * f + a];
+      }
+    }
+    gm = block_max<256>(gm, red);
+    xn2c = block_sum<256>(xn2c, red);
+    if (st->first && st->jacobi)
+      for (int i = tid; i < d.n; i += blockDim.x) d.scale_c[i] = 1.0 / (1.0 + sqrt(d.camdiag[i]));
+    else if (st->first)
+      for (int i = tid; i < d.n; i += blockDim.x) d.scale_c[i] = 1.0;
+    if (tid == 0) {
+      double fd = 0.0;
+      for (int i = 0; i < (int)blockDim.x; ++i) fd += fdcost[i];
+      const double* xs = d.xchg_cam + nv;
+      const double cost = xs[kXCost] + fd;
+      const double gmax = fmax(gm, d.xchg_max[0]);
+      if (st->first) {
+        st->fixed_cost = xs[kXFixed];
+        if (xs[kXFixedFail] > 0.0) {
+          st->done = 1; st->ok = 0; st->termination = SG_DID_NOT_RUN;
+        } else if (xs[kXFail] > 0.0) {
+          st->done = 1; st->ok = 0; st->termination = SG_NUMERICAL_FAILURE;
+        } else {
+          st->cost = cost;
+          st->initial_cost = cost + st->fixed_cost;
+          st->abs_gtol = st->gtol * gmax;
+          st->pushed = 1;
+          st->min_pushed_cost = cost;
+          st->x_norm = sqrt(xs[kXXnorm2] + xn2c);
+          if (gmax <= st->abs_gtol && !st->disable_term) {
+            st->done = 1; st->ok = 1; st->termination = SG_GRADIENT_TOLERANCE;
+          }
+        }
+        st->first = 0;
+      } else {
+        if (xs[kXFail] > 0.0) {
+          st->done = 1; st->ok = 0; st->termination = SG_NUMERICAL_FAILURE;
+        } else {
+          st->cost = cost;
+          if (!st->disable_term && gmax <= st->abs_gtol) {
+            st->done = 1; st->ok = 1; st->termination = SG_GRADIENT_TOLERANCE;
+          } else if (!st->disable_term && st->radius < st->min_radius) {
+            st->done = 1; st->ok = 1; st->termination = SG_PARAMETER_TOLERANCE;
+          } else {
+            st->pushed += 1;
+            st->min_pushed_cost = fmin(st->min_pushed_cost, cost);
+          }
+        }
+      }
+      st->need_lin = 0;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    if (!st->done) {
+      if (!st->disable_term && st->pushed - 1 >= st->max_iter) {
+        st->done = 1; st->ok = 1; st->termination = SG_NO_CONVERGENCE;
+      } else if (st->disable_term && st->lm_iters >= st->max_iter) {
+        st->done = 1; st->ok = 1; st->termination = SG_NO_CONVERGENCE;
+      }
+    }
+    if (!st->done) st->lm_iters += 1;
+    done_sh = st->done;
+  }
+  __syncthreads();
+  if (done_sh) return;
+  if (!st->reuse_diag)
+    for (int i = tid; i < d.n; i += blockDim.x) {
+      const double s = d.scale_c[i];
+      d.diag_c[i] = fmin(fmax(s * s * d.camdiag[i], st->min_diag), st->max_diag);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_schur: one chunk per workgroup, one wave per point.  Damped, scaled point block V~ = S V S + D^2
+// (LL^T inverse), then every pair (s, t) of the point's observations on free frames contributes
+// -A_c,s^T (A_p,s V~^-1 A_p,t^T) A_c,t to the window block (b_s, b_t) in LDS, and the right-hand side
+// gets -A_c,s^T A_p,s V~^-1 g~_p.  Lanes of a wave hold distinct pairs -> distinct LDS addresses.
+__global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d) {
+  const LmState* st = d.st;
+  if (st->done) return;
+  extern __shared__ double win[];
+  __shared__ double red[kSchurThreads / 64];
+  const Chunk ch = d.chunks[blockIdx.x];
+  const int npair = ch.nb * (ch.nb + 1) / 2;
+  const int nwin = ch.wide ? 0 : npair * 36 + ch.nb * 6;
+  double* rhsw = win + npair * 36;
+  for (int i = threadIdx.x; i < nwin; i += blockDim.x) win[i] = 0.0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const double radius = st->radius;
+  const bool reuse = st->reuse_diag != 0;
+  double linfail = 0.0;
+  for (int p = ch.p0 + wave; p < ch.p1; p += kSchurThreads / 64) {
+    if (!d.pfree[p]) continue;
+    const double* Vp = d.V + 10 * (size_t)p;
+    double V[10];
+#pragma unroll
+    for (int i = 0; i < 10; ++i) V[i] = Vp[i];
+    const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
+    const double sp[4] = {s4.x, s4.y, s4.z, s4.w};
+    const double4 g4 = reinterpret_cast<const double4*>(d.g)[p];
+    const double gs[4] = {g4.x * sp[0], g4.y * sp[1], g4.z * sp[2], g4.w * sp[3]};
+    double dp[4];
+    if (!reuse) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+        dp[a] = fmin(fmax(sp[a] * sp[a] * V[u4(a, a)], st->min_diag), st->max_diag);
+      if (lane == 0) reinterpret_cast<double4*>(d.diag_p)[p] = make_double4(dp[0], dp[1], dp[2], dp[3]);
+    } else {
+      const double4 d4 = reinterpret_cast<const double4*>(d.diag_p)[p];
+      dp[0] = d4.x; dp[1] = d4.y; dp[2] = d4.z; dp[3] = d4.w;
+    }
+    double Vt[10];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (c >= a) Vt[u4(a, c)] = sp[a] * V[u4(a, c)] * sp[c] + (a == c ? dp[a] / radius : 0.0);
+    double Vi[10];
+    if (!inv4_spd(Vt, Vi)) {
+      linfail += (lane == 0) ? 1.0 : 0.0;
+#pragma unroll
+      for (int i = 0; i < 10; ++i) Vi[i] = NAN;
+    }
+    double tp[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      double s = 0.0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) s += sym4(Vi, a, c) * gs[c];
+      tp[a] = s;
+    }
+    if (lane == 0) {
+      double* Vo = d.Vinv + 10 * (size_t)p;
+#pragma unroll
+      for (int i = 0; i < 10; ++i) Vo[i] = Vi[i];
+      reinterpret_cast<double4*>(d.tp)[p] = make_double4(tp[0], tp[1], tp[2], tp[3]);
+    }
+    const int o0 = d.poff[p], k = d.poff[p + 1] - o0;
+    // right-hand side: -A_c,s^T (A_p,s t_p)
+    for (int s = lane; s < k; s += 64) {
+      const int o = o0 + s;
+      const int b = d.frame_block[d.obs_frame[o]];
+      if (b < 0 || d.obs_fixed[o]) continue;
+      double r[2], Jc[12], Jp[8];
+      load_scaled_J(d, o, b, sp, r, Jc, Jp);
+      const double e0 = Jp[0] * tp[0] + Jp[1] * tp[1] + Jp[2] * tp[2] + Jp[3] * tp[3];
+      const double e1 = Jp[4] * tp[0] + Jp[5] * tp[1] + Jp[6] * tp[2] + Jp[7] * tp[3];
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+        const double v = -(Jc[a] * e0 + Jc[6 + a] * e1);
+        if (ch.wide) atomicAdd(d.rhs + 6 * b + a, v);   // wide chunks go straight to the global rhs partial
+        else atomicAdd(rhsw + (b - ch.b_lo) * 6 + a, v);
+      }
+    }
+    // pairs (s <= t)
+    const int np = k * (k + 1) / 2;
+    for (int pi = lane; pi < np; pi += 64) {
+      int s = 0, rem = pi;
+      while (rem >= k - s) { rem -= k - s; ++s; }
+      const int t = s + rem;
+      const int os = o0 + s, ot = o0 + t;
+      const int bs = d.frame_block[d.obs_frame[os]], bt = d.frame_block[d.obs_frame[ot]];
+      if (bs < 0 || bt < 0 || d.obs_fixed[os] || d.obs_fixed[ot]) continue;
+      double r[2], Jcs[12], Jps[8], Jct[12], Jpt[8];
+      load_scaled_J(d, os, bs, sp, r, Jcs, Jps);
+      load_scaled_J(d, ot, bt, sp, r, Jct, Jpt);
+      // P = Jp_s Vi (2x4); M = P Jp_t^T (2x2)
+      double M[2][2];
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr) {
+        double P[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          double acc = 0.0;
+#pragma unroll
+          for (int m = 0; m < 4; ++m) acc += Jps[4 * rr + m] * sym4(Vi, m, c);
+          P[c] = acc;
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+          M[rr][u] = P[0] * Jpt[4 * u] + P[1] * Jpt[4 * u + 1] + P[2] * Jpt[4 * u + 2] + P[3] * Jpt[4 * u + 3];
+      }
+      // N = Jc_s^T M (6x2); T = N Jc_t (6x6)
+      double N[6][2];
+#pragma unroll
+      for (int a = 0; a < 6; ++a)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) N[a][u] = Jcs[a] * M[0][u] + Jcs[6 + a] * M[1][u];
+      const int I = bs < bt ? bs : bt, Jb = bs < bt ? bt : bs;
+      double* dst;
+      int ld;
+      if (ch.wide) {
+        dst = d.S_wide + (size_t)(6 * I) * d.n + 6 * Jb;
+        ld = d.n;
+      } else {
+        dst = win + wp(I - ch.b_lo, Jb - ch.b_lo, ch.nb) * 36;
+        ld = 6;
+      }
+#pragma unroll
+      for (int a = 0; a < 6; ++a)
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+          const double Tac = N[a][0] * Jct[c] + N[a][1] * Jct[6 + c];
+          const double Tca = N[c][0] * Jct[a] + N[c][1] * Jct[6 + a];
+          double v;
+          if (s == t) v = Tac;
+          else if (bs == bt) v = Tac + Tca;
+          else if (bs < bt) v = Tac;
+          else v = Tca;
+          atomicAdd(dst + a * ld + c, -v);
+        }
+    }
+  }
+  linfail = block_sum<kSchurThreads>(linfail, red);
+  if (threadIdx.x == 0) d.chunk_scal[(size_t)blockIdx.x * kNScal + kLinFail] = linfail;
+  __syncthreads();
+  for (int i = threadIdx.x; i < nwin; i += blockDim.x) d.S_slab[ch.s_off + i] = win[i];
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_S_reduce: grid (x: elements of block row I with J >= I, y: I; y == NB is the rhs row).
+__global__ __launch_bounds__(256) void k_S_reduce(Dev d) {
+  const LmState* st = d.st;
+  if (st->done) return;
+  const int I = blockIdx.y;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (I < d.NB) {
+    const int nJ = d.NB - I;
+    if (e >= nJ * 36) return;
+    const int Jb = I + e / 36, a = (e % 36) / 6, c = e % 6;
+    const size_t gi = (size_t)(6 * I + a) * d.n + 6 * Jb + c;
+    double s = d.S_wide[gi];
+    d.S_wide[gi] = 0.0;
+    for (int ci = d.blk_cbeg[I]; ci < d.blk_cend[I]; ++ci) {
+      const Chunk ch = d.chunks[ci];
+      if (ch.wide || I < ch.b_lo || Jb >= ch.b_lo + ch.nb) continue;
+      s += d.S_slab[ch.s_off + wp(I - ch.b_lo, Jb - ch.b_lo, ch.nb) * 36 + a * 6 + c];
+    }
+    d.S[gi] = s;
+  } else {
+    if (e >= d.n) return;
+    const int b = e / 6, a = e % 6;
+    double s = d.rhs[e];   // wide-chunk atomics
+    for (int ci = d.blk_cbeg[b]; ci < d.blk_cend[b]; ++ci) {
+      const Chunk ch = d.chunks[ci];
+      if (ch.wide || b < ch.b_lo || b >= ch.b_lo + ch.nb) continue;
+      s += d.S_slab[ch.s_off + ch.nb * (ch.nb + 1) / 2 * 36 + (b - ch.b_lo) * 6 + a];
+    }
+    d.xc[e] = s;       // local rhs partial (all-reduced with S); the wide-chunk accumulator is reset
+    d.rhs[e] = 0.0;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_cholesky: one workgroup.  A = S_sub + blockdiag(U) + FrameDistance + D^2 (scaled), banded
+// right-looking Cholesky A = U^T U with the rhs as an augmented column, back substitution, then the
+// candidate camera poses x+ = Plus(x, -S x_c) and the FrameDistance model/candidate terms.
+__global__ __launch_bounds__(kCholThreads) void k_cholesky(Dev d, const int32_t* panel_jmax) {
+  LmState* st = d.st;
+  if (st->done) return;
+  const int n = d.n, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nwaves = kCholThreads / 64;
+  double* A = d.S;
+  double* y = d.work;
+  const double radius = st->radius;
+  __shared__ double U11[kCholNb][kCholNb + 1];
+  __shared__ int fail_sh;
+  __shared__ double red[kCholThreads / 64];
+  if (tid == 0) fail_sh = 0;
+  // ---- assemble
+  for (int i = tid; i < d.NB * 21; i += kCholThreads) {
+    const int b = i / 21, e = i % 21;
+    int a = 0, rem = e;
+    while (rem >= 6 - a) { rem -= 6 - a; ++a; }
+    const int c = a + rem;
+    double v = d.xchg_cam[(size_t)b * kCamV + e];
+    if (a >= 3) v += d.fd_D[9 * b + 3 * (a - 3) + (c - 3)];
+    const int ra = 6 * b + a, rc = 6 * b + c;
+    v *= d.scale_c[ra] * d.scale_c[rc];
+    if (a == c) v += d.diag_c[ra] / radius;
+    A[(size_t)ra * n + rc] += v;
+  }
+  for (int dd = tid; dd < d.D; dd += kCholThreads) {
+    const int ba = d.frame_block[d.fd_a[dd]], bb = d.frame_block[d.fd_b[dd]];
+    if (ba < 0 || bb < 0 || ba == bb) continue;
+    const double* Xd = d.fd_X + 9 * dd;   // J_a J_b^T (rows: a's translation, cols: b's)
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) {
+        const int ri = 6 * ba + 3 + i, cj = 6 * bb + 3 + j;
+        const double v = Xd[3 * i + j] * d.scale_c[ri] * d.scale_c[cj];
+        if (ba < bb) A[(size_t)ri * n + cj] += v;
+        else A[(size_t)cj * n + ri] += v;
+      }
+  }
+  for (int i = tid; i < n; i += kCholThreads) y[i] = d.xc[i] + d.scale_c[i] * d.camg[i];
+  __syncthreads();
+  // ---- factor (upper), panels of kCholNb
+  const int npanel = (n + kCholNb - 1) / kCholNb;
+  for (int pk = 0; pk < npanel; ++pk) {
+    const int kb = pk * kCholNb;
+    const int w = min(kCholNb, n - kb);
+    const int jmax = min(n, panel_jmax[pk]);
+    if (wave == 0) {
+      // column-per-lane register factorisation of the diagonal block
+      double col[kCholNb];
+#pragma unroll
+      for (int r = 0; r < kCholNb; ++r) col[r] = (lane < w && r <= lane) ? A[(size_t)(kb + r) * n + kb + lane] : 0.0;
+      bool bad = false;
+#pragma unroll
+      for (int j = 0; j < kCholNb; ++j) {
+        if (j < w) {
+          const double piv = __shfl(col[j], j);
+          if (!(piv > 0.0)) bad = true;
+          const double ujj = sqrt(piv);
+          const double inv = 1.0 / ujj;
+          if (lane == j) col[j] = ujj;
+          else if (lane > j) col[j] *= inv;
+#pragma unroll
+          for (int r = j + 1; r < kCholNb; ++r) {
+            const double ujr = __shfl(col[j], r);
+            if (r < w && lane >= r) col[r] -= ujr * col[j];
+          }
+        }
+      }
+      if (lane < w) {
+#pragma unroll
+        for (int r = 0; r < kCholNb; ++r)
+          if (r <= lane) {
+            A[(size_t)(kb + r) * n + kb + lane] = col[r];
+            U11[r][lane] = col[r];
+          }
+      }
+      if (lane == 0 && bad) fail_sh = 1;
+    }
+    __syncthreads();
+    // TRSM: rows kb..kb+w of columns [kb+w, jmax) and of the rhs column
+    const int ncol = jmax - (kb + w);
+    for (int ci = tid; ci < ncol + 1; ci += kCholThreads) {
+      const bool isy = ci == ncol;
+      const int c = kb + w + ci;
+      double a[kCholNb];
+#pragma unroll
+      for (int r = 0; r < kCholNb; ++r) a[r] = (r < w) ? (isy ? y[kb + r] : A[(size_t)(kb + r) * n + c]) : 0.0;
+#pragma unroll
+      for (int j = 0; j < kCholNb; ++j) {
+        if (j < w) {
+          double s = a[j];
+#pragma unroll
+          for (int m = 0; m < kCholNb; ++m)
+            if (m < j) s -= U11[m][j] * a[m];
+          a[j] = s / U11[j][j];
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < kCholNb; ++r)
+        if (r < w) {
+          if (isy) y[kb + r] = a[r];
+          else A[(size_t)(kb + r) * n + c] = a[r];
+        }
+    }
+    __syncthreads();
+    // trailing update of rows/cols [kb+w, jmax): A[i][j] -= sum_r U[r][i] U[r][j];  y[i] -= sum_r U[r][i] y[r]
+    for (int i = kb + w + wave; i < jmax; i += nwaves) {
+      double ui[kCholNb];
+#pragma unroll
+      for (int r = 0; r < kCholNb; ++r) ui[r] = (r < w) ? A[(size_t)(kb + r) * n + i] : 0.0;
+      for (int j = i + lane; j < jmax; j += 64) {
+        double s = 0.0;
+#pragma unroll
+        for (int r = 0; r < kCholNb; ++r)
+          if (r < w) s += ui[r] * A[(size_t)(kb + r) * n + j];
+        A[(size_t)i * n + j] -= s;
+      }
+      if (lane == 0) {
+        double s = 0.0;
+#pragma unroll
+        for (int r = 0; r < kCholNb; ++r)
+          if (r < w) s += ui[r] * y[kb + r];
+        y[i] -= s;
+      }
+    }
+    __syncthreads();
+  }
+  // ---- back substitution U x = y, blocked from the bottom
+  for (int pk = npanel - 1; pk >= 0; --pk) {
+    const int kb = pk * kCholNb;
+    const int w = min(kCholNb, n - kb);
+    if (wave == 0) {
+      double yv = (lane < w) ? y[kb + lane] : 0.0;
+      for (int j = w - 1; j >= 0; --j) {
+        const double ujj = A[(size_t)(kb + j) * n + kb + j];
+        const double xj = __shfl(yv, j) / ujj;
+        if (lane == j) yv = xj;
+        else if (lane < j) yv -= A[(size_t)(kb + lane) * n + kb + j] * xj;
+      }
+      if (lane < w) y[kb + lane] = yv;
+    }
+    __syncthreads();
+    // rows i < kb with a nonzero coupling to this panel: y[i] -= sum_r U[i][kb+r] x[kb+r]
+    for (int i = tid; i < kb; i += kCholThreads) {
+      double s = 0.0;
+      for (int r = 0; r < w; ++r) s += A[(size_t)i * n + kb + r] * y[kb + r];
+      y[i] -= s;
+    }
+    __syncthreads();
+  }
+  for (int i = tid; i < n; i += kCholThreads) d.xc[i] = y[i];
+  __syncthreads();
+  // ---- candidate camera poses and FrameDistance terms
+  const int cur = st->cur, nxt = cur ^ 1;
+  double step2 = 0.0, candx2 = 0.0, model = 0.0, candcost = 0.0;
+  for (int f = tid; f < d.F; f += kCholThreads) {
+    const double* q = d.q[cur] + 4 * f;
+    const double* t = d.t[cur] + 3 * f;
+    double* qn = d.q[nxt] + 4 * f;
+    double* tn = d.t[nxt] + 3 * f;
+    const int b = d.frame_block[f];
+    double qq[4] = {q[0], q[1], q[2], q[3]}, tt[3] = {t[0], t[1], t[2]};
+    if (b >= 0) {
+      if (d.rot_free[f]) {
+        double dl[3];
+        for (int a = 0; a < 3; ++a) dl[a] = -y[6 * b + a] * d.scale_c[6 * b + a];
+        QuatPlus(q, dl, qq);
+        for (int a = 0; a < 4; ++a) {
+          step2 += (qq[a] - q[a]) * (qq[a] - q[a]);
+          candx2 += qq[a] * qq[a];
+        }
+      }
+      if (d.trans_free[f]) {
+        for (int a = 0; a < 3; ++a) {
+          tt[a] = t[a] - y[6 * b + 3 + a] * d.scale_c[6 * b + 3 + a];
+          step2 += (tt[a] - t[a]) * (tt[a] - t[a]);
+          candx2 += tt[a] * tt[a];
+        }
+      }
+    }
+    for (int a = 0; a < 4; ++a) qn[a] = qq[a];
+    for (int a = 0; a < 3; ++a) tn[a] = tt[a];
+  }
+  __syncthreads();
+  for (int dd = tid; dd < d.D; dd += kCholThreads) {
+    const int fa = d.fd_a[dd], fb = d.fd_b[dd];
+    const int ba = d.frame_block[fa], bb = d.frame_block[fb];
+    const double* Jd = d.fd_J + 6 * dd;
+    double m = 0.0;
+    for (int j = 0; j < 3; ++j) {
+      if (ba >= 0) m += Jd[j] * d.scale_c[6 * ba + 3 + j] * (-y[6 * ba + 3 + j]);
+      if (bb >= 0) m += Jd[3 + j] * d.scale_c[6 * bb + 3 + j] * (-y[6 * bb + 3 + j]);
+    }
+    model -= m * (d.fd_r[dd] + 0.5 * m);
+    const double* ta = d.t[nxt] + 3 * fa;
+    const double* tb = d.t[nxt] + 3 * fb;
+    const double e0 = ta[0] - tb[0], e1 = ta[1] - tb[1], e2 = ta[2] - tb[2];
+    const double r = 0.1 * (sqrt(e0 * e0 + e1 * e1 + e2 * e2) - d.fd_target);
+    double rho0, rho1;
+    Cauchy(r * r, d.fd_b2, d.fd_inv_b2, &rho0, &rho1);
+    candcost += 0.5 * rho0;
+  }
+  step2 = block_sum<kCholThreads>(step2, red);
+  candx2 = block_sum<kCholThreads>(candx2, red);
+  model = block_sum<kCholThreads>(model, red);
+  candcost = block_sum<kCholThreads>(candcost, red);
+  if (tid == 0) {
+    d.xchg_chol[kCStep2] = step2;
+    d.xchg_chol[kCCandX2] = candx2;
+    d.xchg_chol[kCModel] = model;
+    d.xchg_chol[kCCandCost] = candcost;
+    d.xchg_chol[kCFail] = fail_sh ? 1.0 : 0.0;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_point_update: back-substitution x_p = V~^-1 (g~_p - A_p^T A_c x_c), model cost change
+// -(A s).(r + A s / 2), candidate point X+ = X - S_p x_p and the candidate reprojection cost.
+__global__ __launch_bounds__(kSweepThreads) void k_point_update(Dev d) {
+  const LmState* st = d.st;
+  if (st->done) return;
+  const int cur = st->cur, nxt = cur ^ 1;
+  const Chunk ch = d.chunks[blockIdx.x];
+  __shared__ double red[kSweepThreads / 64];
+  const int lp = threadIdx.x / kLanesPerPt, l8 = threadIdx.x % kLanesPerPt;
+  const int p = ch.p0 + lp;
+  double model = 0.0, candcost = 0.0, candfail = 0.0, step2 = 0.0, candx2 = 0.0;
+  if (p < ch.p1) {
+    const bool pf = d.pfree[p] != 0;
+    const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
+    const double sp[4] = {s4.x, s4.y, s4.z, s4.w};
+    const double4 Xv = reinterpret_cast<const double4*>(d.X[cur])[p];
+    const double X[4] = {Xv.x, Xv.y, Xv.z, Xv.w};
+    const int o0 = d.poff[p], o1 = d.poff[p + 1];
+    double xp[4] = {0.0, 0.0, 0.0, 0.0};
+    if (pf) {
+      double acc[4] = {0.0, 0.0, 0.0, 0.0};
+      for (int o = o0 + l8; o < o1; o += kLanesPerPt) {
+        if (d.obs_fixed[o]) continue;
+        const int b = d.frame_block[d.obs_frame[o]];
+        if (b < 0) continue;
+        double r[2], Jc[12], Jp[8];
+        load_scaled_J(d, o, b, sp, r, Jc, Jp);
+        const double* xc = d.xc + 6 * b;
+        double u0 = 0.0, u1 = 0.0;
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+          u0 += Jc[c] * xc[c];
+          u1 += Jc[6 + c] * xc[c];
+        }
+#pragma unroll
+        for (int a = 0; a < 4; ++a) acc[a] += Jp[a] * u0 + Jp[4 + a] * u1;
+      }
+#pragma unroll
+      for (int m = 1; m < kLanesPerPt; m <<= 1)
+#pragma unroll
+        for (int a = 0; a < 4; ++a) acc[a] += __shfl_xor(acc[a], m);
+      const double4 g4 = reinterpret_cast<const double4*>(d.g)[p];
+      const double rhs[4] = {g4.x * sp[0] - acc[0], g4.y * sp[1] - acc[1], g4.z * sp[2] - acc[2],
+                             g4.w * sp[3] - acc[3]};
+      const double* Vi = d.Vinv + 10 * (size_t)p;
+      double Vl[10];
+#pragma unroll
+      for (int i = 0; i < 10; ++i) Vl[i] = Vi[i];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        double s = 0.0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) s += sym4(Vl, a, c) * rhs[c];
+        xp[a] = s;
+      }
+    }
+    // step s_p = -x_p (scaled); candidate X+ = X + S_p s_p
+    double Xn[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const double dl = -xp[a] * sp[a];
+      Xn[a] = pf ? X[a] + dl : X[a];
+    }
+    if (l8 == 0) {
+      reinterpret_cast<double4*>(d.X[nxt])[p] = make_double4(Xn[0], Xn[1], Xn[2], Xn[3]);
+      if (pf) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          step2 += (Xn[a] - X[a]) * (Xn[a] - X[a]);
+          candx2 += Xn[a] * Xn[a];
+        }
+      }
+    }
+    for (int o = o0 + l8; o < o1; o += kLanesPerPt) {
+      if (d.obs_fixed[o]) continue;
+      const int f = d.obs_frame[o];
+      const int b = d.frame_block[f];
+      double r[2], Jc[12], Jp[8];
+      load_scaled_J(d, o, b, sp, r, Jc, Jp);
+      double m0 = 0.0, m1 = 0.0;
+      if (b >= 0) {
+        const double* xc = d.xc + 6 * b;
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+          m0 -= Jc[c] * xc[c];
+          m1 -= Jc[6 + c] * xc[c];
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        m0 -= Jp[c] * xp[c];
+        m1 -= Jp[4 + c] * xp[c];
+      }
+      model -= m0 * (r[0] + 0.5 * m0) + m1 * (r[1] + 0.5 * m1);
+      double uv[2];
+      if (!Project(d.q[nxt] + 4 * f, d.t[nxt] + 3 * f, d.k + 7 * d.frame_cam[f], Xn, uv)) {
+        candfail += 1.0;
+        continue;
+      }
+      const double e0 = uv[0] - d.obs_pt[2 * o], e1 = uv[1] - d.obs_pt[2 * o + 1];
+      double rho0, rho1;
+      Cauchy(e0 * e0 + e1 * e1, d.b, d.inv_b, &rho0, &rho1);
+      candcost += 0.5 * rho0;
+    }
+  }
+  model = block_sum<kSweepThreads>(model, red);
+  candcost = block_sum<kSweepThreads>(candcost, red);
+  candfail = block_sum<kSweepThreads>(candfail, red);
+  step2 = block_sum<kSweepThreads>(step2, red);
+  candx2 = block_sum<kSweepThreads>(candx2, red);
+  if (threadIdx.x == 0) {
+    double* sc = d.chunk_scal + (size_t)blockIdx.x * kNScal;
+    sc[kModel] = model;
+    sc[kCandCost] = candcost;
+    sc[kCandFail] = candfail;
+    sc[kStep2] = step2;
+    sc[kCandX2] = candx2;
+  }
+}
+
+__global__ __launch_bounds__(64) void k_upd_reduce(Dev d) {
+  const LmState* st = d.st;
+  if (st->done) return;
+  const int lane = threadIdx.x;
+  double v[kUNum] = {0, 0, 0, 0, 0, 0};
+  for (int c = lane; c < d.nchunks; c += 64) {
+    const double* sc = d.chunk_scal + (size_t)c * kNScal;
+    v[kUModel] += sc[kModel];
+    v[kUCandCost] += sc[kCandCost];
+    v[kUCandFail] += sc[kCandFail];
+    v[kUStep2] += sc[kStep2];
+    v[kUCandX2] += sc[kCandX2];
+    v[kULinFail] += sc[kLinFail];
+  }
+#pragma unroll
+  for (int j = 0; j < kUNum; ++j) v[j] = wave_sum(v[j]);
+  if (lane == 0)
+#pragma unroll
+    for (int j = 0; j < kUNum; ++j) d.xchg_upd[j] = v[j];
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_decide: TrustRegionMinimizer + LevenbergMarquardtStrategy step bookkeeping (Ceres 1.8 semantics).
+__global__ void k_decide(Dev d) {
+  LmState* st = d.st;
+  if (threadIdx.x != 0 || st->done) return;
+  const double* u = d.xchg_upd;
+  const double* c = d.xchg_chol;
+  const double model = u[kUModel] + c[kCModel];
+  const double step2 = u[kUStep2] + c[kCStep2];
+  const bool solved = u[kULinFail] == 0.0 && c[kCFail] == 0.0 && isfinite(step2) && isfinite(model);
+  const bool valid = solved && !(model < 0.0);
+  bool success = false;
+  st->last_model = model;
+  if (!valid) {
+    st->n_invalid += 1;
+    st->consecutive_invalid += 1;
+    if (!st->disable_term && st->consecutive_invalid >= st->max_invalid) {
+      st->done = 1; st->ok = 0; st->termination = SG_NUMERICAL_FAILURE;
+      return;
+    }
+  } else {
+    st->consecutive_invalid = 0;
+    const double new_cost = u[kUCandFail] > 0.0 ? DBL_MAX : u[kUCandCost] + c[kCCandCost];
+    const double step_norm = sqrt(step2);
+    st->last_new_cost = new_cost;
+    st->last_step_norm = step_norm;
+    if (!st->disable_term && step_norm <= st->ptol * (st->x_norm + st->ptol)) {
+      st->done = 1; st->ok = 1; st->termination = SG_PARAMETER_TOLERANCE;
+      return;
+    }
+    const double cost_change = st->cost - new_cost;
+    if (!st->disable_term && fabs(cost_change) < st->ftol * st->cost) {
+      st->done = 1; st->ok = 1; st->termination = SG_FUNCTION_TOLERANCE;
+      return;
+    }
+    const double rel = cost_change / model;
+    st->last_rel_decrease = rel;
+    success = rel > st->min_rel_dec;
+    if (success) {
+      st->n_succ += 1;
+      const double t = 2.0 * rel - 1.0;
+      st->radius = st->radius / fmax(1.0 / 3.0, 1.0 - t * t * t);
+      st->radius = fmin(st->max_radius, st->radius);
+      st->decrease_factor = 2.0;
+      st->reuse_diag = 0;
+      st->cur ^= 1;
+      st->x_norm = sqrt(u[kUCandX2] + c[kCCandX2]);
+      st->cost = new_cost;
+      st->need_lin = 1;   // the iteration is pushed after the gradient test in k_cam_finalize
+      return;
+    }
+  }
+  // rejected (StepRejected) or invalid (StepIsInvalid == StepRejected(0))
+  if (valid) st->n_unsucc += 1;
+  else st->n_unsucc += 1;
+  st->radius = st->radius / st->decrease_factor;
+  st->decrease_factor *= 2.0;
+  st->reuse_diag = 1;
+  if (!st->disable_term && st->radius < st->min_radius) {
+    st->done = 1; st->ok = 1; st->termination = SG_PARAMETER_TOLERANCE;
+    return;
+  }
+  st->pushed += 1;
+  st->min_pushed_cost = fmin(st->min_pushed_cost, st->cost);
+}
+
+// Zero the S accumulation target before k_S_reduce writes the new system (upper blocks only are
+// rewritten; the lower part is never read).
+__global__ void k_evaluate(Dev d, double* resid, double* cost_out, int32_t* nfail) {
+  // residual sweep at x[cur] (parity / ReprojectionError check), observation order = device order
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= d.M) return;
+  const int cur = d.st->cur;
+  // find the point of o: binary search in poff
+  int lo = 0, hi = d.P;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (d.poff[mid] <= o) lo = mid;
+    else hi = mid;
+  }
+  const int p = lo, f = d.obs_frame[o];
+  double uv[2];
+  if (!Project(d.q[cur] + 4 * f, d.t[cur] + 3 * f, d.k + 7 * d.frame_cam[f], d.X[cur] + 4 * p, uv)) {
+    resid[2 * o] = 0.0;
+    resid[2 * o + 1] = 0.0;
+    atomicAdd(nfail, 1);
+    return;
+  }
+  const double e0 = uv[0] - d.obs_pt[2 * o], e1 = uv[1] - d.obs_pt[2 * o + 1];
+  resid[2 * o] = e0;
+  resid[2 * o + 1] = e1;
+  if (!d.obs_fixed[o]) {
+    double rho0, rho1;
+    Cauchy(e0 * e0 + e1 * e1, d.b, d.inv_b, &rho0, &rho1);
+    atomicAdd(cost_out, 0.5 * rho0);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// ReprojectMap (slam.cpp:523-548): every observation of the map, disabled ones included.
+__global__ __launch_bounds__(256) void k_reproject_map(const double* k, const double* q, const double* t,
+                                                        const int32_t* frame_cam, const double* X,
+                                                        const double* pt, const int32_t* of,
+                                                        const int32_t* op, int M, double* err,
+                                                        double* partial) {
+  __shared__ double red[4];
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  double nrm = 0.0, cnt = 0.0;
+  if (o < M) {
+    const int f = of[o], p = op[o];
+    double uv[2];
+    const double px = pt[2 * o], py = pt[2 * o + 1];
+    if (Project(q + 4 * f, t + 3 * f, k + 7 * frame_cam[f], X + 4 * p, uv)) {
+      const double e0 = uv[0] - px, e1 = uv[1] - py;
+      err[2 * o] = e0;
+      err[2 * o + 1] = e1;
+      nrm = sqrt(e0 * e0 + e1 * e1);
+      cnt = 1.0;
+    } else {
+      err[2 * o] = px;   // o->error = o->pt, left as is when the projection fails (slam.cpp:529,539-541)
+      err[2 * o + 1] = py;
+    }
+  }
+  nrm = block_sum<256>(nrm, red);
+  cnt = block_sum<256>(cnt, red);
+  if (threadIdx.x == 0) {
+    partial[2 * blockIdx.x] = nrm;
+    partial[2 * blockIdx.x + 1] = cnt;
+  }
+}
+__global__ __launch_bounds__(64) void k_reproject_reduce(const double* partial, int nb, double* out) {
+  double s = 0.0, c = 0.0;
+  for (int i = threadIdx.x; i < nb; i += 64) {
+    s += partial[2 * i];
+    c += partial[2 * i + 1];
+  }
+  s = wave_sum(s);
+  c = wave_sum(c);
+  if (threadIdx.x == 0) {
+    out[0] = c > 0.0 ? s / c : 0.0;
+    out[1] = c;
+  }
+}
+
+// ================================================================================================
+// Host driver
+
+enum KernelId { kKLin = 0, kKCamReduce, kKCamFinal, kKSchur, kKSReduce, kKChol, kKPointUpd, kKUpdRed, kKDecide,
+                kKNum };
+static const char* kKernelNames[kKNum] = {"linearize", "cam_reduce", "cam_finalize", "schur", "S_reduce",
+                                          "cholesky", "point_update", "upd_reduce", "decide"};
+
+BaSolver::BaSolver(const sg_device_options& dev) : dev_(dev) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) throw Error(SG_ENODEV, "no HIP device available");
+  SG_REQUIRE(dev.device >= 0 && dev.device < ndev, SG_ENODEV, "device ordinal out of range");
+  SG_HIP_CHECK(hipSetDevice(dev.device));
+  SG_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  st_.Resize(1);
+  timers_.resize(kKNum);
+  for (int i = 0; i < kKNum; ++i) timers_[i].name = kKernelNames[i];
+}
+
+BaSolver::~BaSolver() {
+  for (auto& t : timers_)
+    for (auto e : t.ev) (void)hipEventDestroy(e);
+  if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+void BaSolver::UniqueId(void* id128) { Comm::UniqueId(id128); }
+
+void BaSolver::CommInit(const void* id128, int nranks, int rank) {
+  SG_HIP_CHECK(hipSetDevice(dev_.device));
+  comm_.reset(new Comm(id128, nranks, rank));
+  dev_.nranks = nranks;
+  dev_.rank = rank;
+}
+
+void BaSolver::AllReduceSum(double* buf, size_t n) {
+  if (comm_ && comm_->nranks() > 1) comm_->AllReduceSum(buf, n, stream_);
+}
+void BaSolver::AllReduceMax(double* buf, size_t n) {
+  if (comm_ && comm_->nranks() > 1) comm_->AllReduceMax(buf, n, stream_);
+}
+
+void BaSolver::Load(const sg_problem& p) {
+  ValidateProblem(&p);
+  SG_REQUIRE(!p.cameras_free, SG_EINVAL,
+             "free intrinsics (SolveAllFrames(..., solve_cameras=true)) are not supported by the device solver yet");
+  SG_HIP_CHECK(hipSetDevice(dev_.device));
+  F_ = p.num_frames;
+  P_ = p.num_points;
+  M_ = p.num_obs;
+  D_ = p.num_dist;
+  ncam_ = p.num_cameras;
+  range_b_ = p.range * p.range;
+  fd_target_ = p.dist_target;
+  fd_b2_ = p.dist_range * p.dist_range;
+  // camera blocks: every frame with a free rotation or translation
+  std::vector<int32_t> frame_block(F_, -1);
+  NB_ = 0;
+  for (int f = 0; f < F_; ++f)
+    if (p.frame_rot_free[f] || p.frame_trans_free[f]) frame_block[f] = NB_++;
+  n_ = 6 * NB_;
+  // point order: by first free block (points without free-frame observations last)
+  std::vector<int32_t> pfirst(P_, NB_), plast(P_, -1), pcount(P_, 0);
+  for (int o = 0; o < M_; ++o) {
+    const int pt = p.obs_point[o], b = frame_block[p.obs_frame[o]];
+    pcount[pt]++;
+    if (b >= 0) {
+      pfirst[pt] = std::min(pfirst[pt], b);
+      plast[pt] = std::max(plast[pt], b);
+    }
+  }
+  point_perm_.resize(P_);
+  std::iota(point_perm_.begin(), point_perm_.end(), 0);
+  std::stable_sort(point_perm_.begin(), point_perm_.end(),
+                   [&](int a, int b) { return pfirst[a] < pfirst[b]; });
+  std::vector<int32_t> inv_perm(P_);
+  for (int i = 0; i < P_; ++i) inv_perm[point_perm_[i]] = i;
+  // observations: CSR by device point order (stable in problem order)
+  std::vector<int32_t> poff(P_ + 1, 0);
+  for (int o = 0; o < M_; ++o) poff[inv_perm[p.obs_point[o]] + 1]++;
+  for (int i = 0; i < P_; ++i) poff[i + 1] += poff[i];
+  obs_perm_.assign(M_, 0);
+  {
+    std::vector<int32_t> fill(poff.begin(), poff.end() - 1);
+    for (int o = 0; o < M_; ++o) obs_perm_[fill[inv_perm[p.obs_point[o]]]++] = o;
+  }
+  std::vector<double> obs_pt(2 * (size_t)M_);
+  std::vector<int32_t> obs_frame(M_);
+  std::vector<uint8_t> obs_fixed(M_), pfree(P_);
+  std::vector<double> X(4 * (size_t)P_);
+  for (int i = 0; i < P_; ++i) {
+    const int pt = point_perm_[i];
+    pfree[i] = p.point_free[pt];
+    for (int a = 0; a < 4; ++a) X[4 * i + a] = p.X[4 * pt + a];
+  }
+  for (int o = 0; o < M_; ++o) {
+    const int src = obs_perm_[o];
+    obs_pt[2 * o] = p.obs_pt[2 * src];
+    obs_pt[2 * o + 1] = p.obs_pt[2 * src + 1];
+    obs_frame[o] = p.obs_frame[src];
+    obs_fixed[o] = frame_block[p.obs_frame[src]] < 0 && !p.point_free[p.obs_point[src]];
+  }
+  // chunks: up to kChunkPts consecutive points whose camera blocks fit a window of kNbwMax blocks
+  chunks_.clear();
+  max_nb_ = 0;
+  int cam_off = 0, s_off = 0;
+  for (int i = 0; i < P_;) {
+    const int pt0 = point_perm_[i];
+    const int lo = pfirst[pt0];
+    Chunk c{};
+    c.p0 = i;
+    int j = i + 1;
+    if (lo >= NB_) {              // points observed only by constant frames
+      while (j < P_ && j - i < kChunkPts) ++j;
+      c.b_lo = 0;
+      c.nb = 0;
+    } else if (plast[pt0] - lo + 1 > kNbwMax) {
+      c.wide = 1;                 // one point spanning more blocks than the LDS window: global atomics
+      c.b_lo = lo;
+      c.nb = 0;
+    } else {
+      int hi = plast[pt0];
+      while (j < P_ && j - i < kChunkPts) {
+        const int ptj = point_perm_[j];
+        if (pfirst[ptj] >= NB_) break;
+        const int h = std::max(hi, plast[ptj]);
+        if (h - lo + 1 > kNbwMax) break;
+        hi = h;
+        ++j;
+      }
+      c.b_lo = lo;
+      c.nb = hi - lo + 1;
+    }
+    c.p1 = j;
+    c.cam_off = cam_off;
+    c.s_off = s_off;
+    cam_off += c.nb * kCamV;
+    s_off += c.nb * (c.nb + 1) / 2 * 36 + c.nb * 6;
+    max_nb_ = std::max(max_nb_, c.nb);
+    chunks_.push_back(c);
+    i = j;
+  }
+  nchunks_ = (int)chunks_.size();
+  // per block: chunk range that may cover it (chunks are sorted by b_lo)
+  std::vector<int32_t> cbeg(NB_, 0), cend(NB_, 0);
+  for (int b = 0; b < NB_; ++b) {
+    int lo = nchunks_, hi2 = 0;
+    for (int c = 0; c < nchunks_; ++c) {
+      const Chunk& ch = chunks_[c];
+      if (ch.nb == 0 || ch.wide) continue;
+      if (b >= ch.b_lo && b < ch.b_lo + ch.nb) {
+        lo = std::min(lo, c);
+        hi2 = std::max(hi2, c + 1);
+      }
+    }
+    cbeg[b] = lo < nchunks_ ? lo : 0;
+    cend[b] = lo < nchunks_ ? hi2 : 0;
+  }
+  // FrameDistance
+  std::vector<int32_t> fd_a(p.dist_frame, p.dist_frame + D_), fd_b(p.dist_prev, p.dist_prev + D_);
+  std::vector<int32_t> fd_boff(NB_ + 1, 0), fd_bidx;
+  {
+    std::vector<std::vector<int32_t>> lists(NB_);
+    for (int dd = 0; dd < D_; ++dd) {
+      const int ba = frame_block[fd_a[dd]], bb = frame_block[fd_b[dd]];
+      if (ba >= 0) lists[ba].push_back(2 * dd);
+      if (bb >= 0) lists[bb].push_back(2 * dd + 1);
+    }
+    for (int b = 0; b < NB_; ++b) {
+      fd_boff[b + 1] = fd_boff[b] + (int)lists[b].size();
+      fd_bidx.insert(fd_bidx.end(), lists[b].begin(), lists[b].end());
+    }
+  }
+  // Cholesky panel envelopes: block column J's first nonzero block row lo(J)
+  std::vector<int32_t> lo_blk(NB_);
+  for (int b = 0; b < NB_; ++b) lo_blk[b] = b;
+  {
+    // exact envelope from the observations of each free point (pairs of blocks it couples)
+    for (int i = 0; i < P_; ++i) {
+      const int pt = point_perm_[i];
+      if (pfirst[pt] >= NB_) continue;
+      if (!p.point_free[pt]) continue;
+      const int lo = pfirst[pt];
+      for (int o = poff[i]; o < poff[i + 1]; ++o) {
+        const int b = frame_block[obs_frame[o]];
+        if (b >= 0) lo_blk[b] = std::min(lo_blk[b], lo);
+      }
+    }
+    for (int dd = 0; dd < D_; ++dd) {
+      const int ba = frame_block[fd_a[dd]], bb = frame_block[fd_b[dd]];
+      if (ba >= 0 && bb >= 0) {
+        const int hi3 = std::max(ba, bb), lo3 = std::min(ba, bb);
+        lo_blk[hi3] = std::min(lo_blk[hi3], lo3);
+      }
+    }
+  }
+  const int npanel = (n_ + kCholNb - 1) / kCholNb;
+  std::vector<int32_t> panel_jmax(std::max(npanel, 1), 0);
+  for (int pk = 0; pk < npanel; ++pk) {
+    const int row_hi = std::min(n_, (pk + 1) * kCholNb) - 1;   // last row of the panel
+    const int blk_hi = row_hi / 6;
+    int jmax = (pk + 1) * kCholNb;
+    // columns j whose envelope starts at or before the panel's last row block
+    for (int b = 0; b < NB_; ++b)
+      if (lo_blk[b] <= blk_hi) jmax = std::max(jmax, 6 * b + 6);
+    panel_jmax[pk] = std::min(jmax, n_);
+  }
+  // device uploads
+  hipStream_t s = stream_;
+  k_.Upload(std::vector<double>(p.k, p.k + 7 * ncam_), s);
+  std::vector<double> q2(8 * (size_t)F_), t2(6 * (size_t)F_), X2(8 * (size_t)P_);
+  std::copy(p.q, p.q + 4 * F_, q2.begin());
+  std::copy(p.q, p.q + 4 * F_, q2.begin() + 4 * F_);
+  std::copy(p.t, p.t + 3 * F_, t2.begin());
+  std::copy(p.t, p.t + 3 * F_, t2.begin() + 3 * F_);
+  std::copy(X.begin(), X.end(), X2.begin());
+  std::copy(X.begin(), X.end(), X2.begin() + 4 * P_);
+  q_.Upload(q2, s);
+  t_.Upload(t2, s);
+  X_.Upload(X2, s);
+  frame_cam_.Upload(std::vector<int32_t>(p.frame_camera, p.frame_camera + F_), s);
+  frame_block_.Upload(frame_block, s);
+  rot_free_.Upload(std::vector<uint8_t>(p.frame_rot_free, p.frame_rot_free + F_), s);
+  trans_free_.Upload(std::vector<uint8_t>(p.frame_trans_free, p.frame_trans_free + F_), s);
+  pfree_.Upload(pfree, s);
+  poff_.Upload(poff, s);
+  obs_pt_.Upload(obs_pt, s);
+  obs_frame_.Upload(obs_frame, s);
+  obs_fixed_.Upload(obs_fixed, s);
+  chunks_d_.Upload(chunks_, s);
+  blk_cbeg_.Upload(cbeg, s);
+  blk_cend_.Upload(cend, s);
+  fd_a_.Upload(fd_a, s);
+  fd_b_.Upload(fd_b, s);
+  fd_boff_.Upload(fd_boff, s);
+  fd_bidx_.Upload(fd_bidx.empty() ? std::vector<int32_t>{0} : fd_bidx, s);
+  work_i_.Upload(panel_jmax, s);
+  J_.Resize((size_t)std::max(M_, 1) * kJStride);
+  V_.Resize(10 * (size_t)std::max(P_, 1));
+  g_.Resize(4 * (size_t)std::max(P_, 1));
+  scale_p_.Resize(4 * (size_t)std::max(P_, 1));
+  diag_p_.Resize(4 * (size_t)std::max(P_, 1));
+  Vinv_.Resize(10 * (size_t)std::max(P_, 1));
+  tp_.Resize(4 * (size_t)std::max(P_, 1));
+  const size_t nn = std::max(n_, 1);
+  scale_c_.Resize(nn);
+  diag_c_.Resize(nn);
+  camdiag_.Resize(nn);
+  camg_.Resize(nn);
+  cam_slab_.Resize(std::max(cam_off, 1));
+  S_slab_.Resize(std::max(s_off, 1));
+  chunk_scal_.Resize((size_t)std::max(nchunks_, 1) * kNScal);
+  cam_wide_.Resize((size_t)std::max(NB_, 1) * kCamV);
+  S_wide_.Resize(nn * nn);
+  xchg_cam_.Resize((size_t)NB_ * kCamV + kXNum);
+  xchg_max_.Resize(1);
+  S_.Resize(nn * nn);
+  rhs_.Resize(nn);
+  xchg_upd_.Resize(kUNum);
+  xchg_chol_.Resize(kCNum);
+  xc_.Resize(nn);
+  work_.Resize(nn);
+  fd_r_.Resize(std::max(D_, 1));
+  fd_J_.Resize(6 * (size_t)std::max(D_, 1));
+  fd_D_.Resize(9 * (size_t)std::max(NB_, 1));
+  fd_X_.Resize(9 * (size_t)std::max(D_, 1));
+  cam_wide_.Zero(s);
+  S_wide_.Zero(s);
+  rhs_.Zero(s);
+  chunk_scal_.Zero(s);
+  S_.Zero(s);
+  schur_lds_ = (size_t)(max_nb_ * (max_nb_ + 1) / 2 * 36 + max_nb_ * 6) * sizeof(double);
+  if (schur_lds_ > 0)
+    SG_HIP_CHECK(hipFuncSetAttribute((const void*)k_schur, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)std::max<size_t>(schur_lds_, 1)));
+  SG_HIP_CHECK(hipStreamSynchronize(s));
+  loaded_ = true;
+  began_ = false;
+}
+
+Dev BaSolver::MakeDev() {
+  Dev d{};
+  d.st = st_.ptr;
+  d.k = k_.ptr;
+  d.q[0] = q_.ptr;
+  d.q[1] = q_.ptr + 4 * (size_t)F_;
+  d.t[0] = t_.ptr;
+  d.t[1] = t_.ptr + 3 * (size_t)F_;
+  d.frame_cam = frame_cam_.ptr;
+  d.frame_block = frame_block_.ptr;
+  d.rot_free = rot_free_.ptr;
+  d.trans_free = trans_free_.ptr;
+  d.F = F_;
+  d.NB = NB_;
+  d.n = n_;
+  d.X[0] = X_.ptr;
+  d.X[1] = X_.ptr + 4 * (size_t)P_;
+  d.pfree = pfree_.ptr;
+  d.poff = poff_.ptr;
+  d.P = P_;
+  d.M = M_;
+  d.obs_pt = obs_pt_.ptr;
+  d.obs_frame = obs_frame_.ptr;
+  d.obs_fixed = obs_fixed_.ptr;
+  d.b = range_b_;
+  d.inv_b = 1.0 / range_b_;
+  d.D = D_;
+  d.fd_a = fd_a_.ptr;
+  d.fd_b = fd_b_.ptr;
+  d.fd_boff = fd_boff_.ptr;
+  d.fd_bidx = fd_bidx_.ptr;
+  d.fd_target = fd_target_;
+  d.fd_b2 = fd_b2_;
+  d.fd_inv_b2 = 1.0 / fd_b2_;
+  d.fd_r = fd_r_.ptr;
+  d.fd_J = fd_J_.ptr;
+  d.fd_D = fd_D_.ptr;
+  d.fd_X = fd_X_.ptr;
+  d.J = J_.ptr;
+  d.V = V_.ptr;
+  d.g = g_.ptr;
+  d.scale_p = scale_p_.ptr;
+  d.diag_p = diag_p_.ptr;
+  d.Vinv = Vinv_.ptr;
+  d.tp = tp_.ptr;
+  d.scale_c = scale_c_.ptr;
+  d.diag_c = diag_c_.ptr;
+  d.camdiag = camdiag_.ptr;
+  d.camg = camg_.ptr;
+  d.chunks = chunks_d_.ptr;
+  d.nchunks = nchunks_;
+  d.blk_cbeg = blk_cbeg_.ptr;
+  d.blk_cend = blk_cend_.ptr;
+  d.cam_slab = cam_slab_.ptr;
+  d.S_slab = S_slab_.ptr;
+  d.chunk_scal = chunk_scal_.ptr;
+  d.cam_wide = cam_wide_.ptr;
+  d.S_wide = S_wide_.ptr;
+  d.xchg_cam = xchg_cam_.ptr;
+  d.xchg_max = xchg_max_.ptr;
+  d.S = S_.ptr;
+  d.rhs = rhs_.ptr;
+  d.xchg_upd = xchg_upd_.ptr;
+  d.xchg_chol = xchg_chol_.ptr;
+  d.xc = xc_.ptr;
+  d.work = work_.ptr;
+  return d;
+}
+
+void BaSolver::Begin(const sg_solver_options& o) {
+  SG_REQUIRE(loaded_, SG_EINVAL, "no problem loaded");
+  SG_HIP_CHECK(hipSetDevice(dev_.device));
+  {
+    // restart from the current parameter slot: move it to slot 0
+    LmState h{};
+    SG_HIP_CHECK(hipMemcpyAsync(&h, st_.ptr, sizeof(h), hipMemcpyDeviceToHost, stream_));
+    SG_HIP_CHECK(hipStreamSynchronize(stream_));
+    if (began_ && h.cur == 1) {
+      SG_HIP_CHECK(hipMemcpyAsync(q_.ptr, q_.ptr + 4 * (size_t)F_, 4 * (size_t)F_ * 8, hipMemcpyDeviceToDevice, stream_));
+      SG_HIP_CHECK(hipMemcpyAsync(t_.ptr, t_.ptr + 3 * (size_t)F_, 3 * (size_t)F_ * 8, hipMemcpyDeviceToDevice, stream_));
+      SG_HIP_CHECK(hipMemcpyAsync(X_.ptr, X_.ptr + 4 * (size_t)P_, 4 * (size_t)P_ * 8, hipMemcpyDeviceToDevice, stream_));
+    }
+    began_ = true;
+  }
+  LmState s{};
+  s.max_iter = o.max_num_iterations;
+  s.max_invalid = o.max_num_consecutive_invalid_steps;
+  s.disable_term = o.disable_termination;
+  s.jacobi = o.jacobi_scaling;
+  s.ftol = o.function_tolerance;
+  s.gtol = o.gradient_tolerance;
+  s.ptol = o.parameter_tolerance;
+  s.min_rel_dec = o.min_relative_decrease;
+  s.max_radius = o.max_trust_region_radius;
+  s.min_radius = o.min_trust_region_radius;
+  s.min_diag = o.min_lm_diagonal;
+  s.max_diag = o.max_lm_diagonal;
+  s.cur = 0;
+  s.need_lin = 1;
+  s.first = 1;
+  s.done = (NB_ == 0 && P_ == 0) ? 1 : 0;
+  s.ok = 1;
+  s.termination = s.done ? SG_FUNCTION_TOLERANCE : SG_NO_CONVERGENCE;
+  s.radius = o.initial_trust_region_radius;
+  s.decrease_factor = 2.0;
+  SG_HIP_CHECK(hipMemcpyAsync(st_.ptr, &s, sizeof(s), hipMemcpyHostToDevice, stream_));
+  for (auto& t : timers_) {
+    t.total_ms = 0.0;
+    t.count = 0;
+  }
+}
+
+void BaSolver::TimedLaunchBegin(int id) {
+  if (!timing_) return;
+  hipEvent_t a, b;
+  SG_HIP_CHECK(hipEventCreate(&a));
+  SG_HIP_CHECK(hipEventCreate(&b));
+  timers_[id].ev.push_back(a);
+  timers_[id].ev.push_back(b);
+  SG_HIP_CHECK(hipEventRecord(a, stream_));
+}
+void BaSolver::TimedLaunchEnd(int id) {
+  if (!timing_) return;
+  SG_HIP_CHECK(hipEventRecord(timers_[id].ev.back(), stream_));
+}
+
+void BaSolver::Iterate(int n) {
+  SG_REQUIRE(loaded_, SG_EINVAL, "no problem loaded");
+  SG_HIP_CHECK(hipSetDevice(dev_.device));
+  Dev d = MakeDev();
+  const int nc = std::max(nchunks_, 1);
+  for (int it = 0; it < n; ++it) {
+    TimedLaunchBegin(kKLin);
+    hipLaunchKernelGGL(k_linearize, dim3(nc), dim3(kSweepThreads), 0, stream_, d);
+    TimedLaunchEnd(kKLin);
+    TimedLaunchBegin(kKCamReduce);
+    const int nv = NB_ * kCamV;
+    hipLaunchKernelGGL(k_cam_reduce, dim3((nv + 255) / 256 + 1), dim3(256), 0, stream_, d);
+    TimedLaunchEnd(kKCamReduce);
+    AllReduceSum(xchg_cam_.ptr, (size_t)nv + kXNum);
+    AllReduceMax(xchg_max_.ptr, 1);
+    TimedLaunchBegin(kKCamFinal);
+    hipLaunchKernelGGL(k_cam_finalize, dim3(1), dim3(256), 0, stream_, d);
+    TimedLaunchEnd(kKCamFinal);
+    TimedLaunchBegin(kKSchur);
+    hipLaunchKernelGGL(k_schur, dim3(nc), dim3(kSchurThreads), schur_lds_, stream_, d);
+    TimedLaunchEnd(kKSchur);
+    TimedLaunchBegin(kKSReduce);
+    const int maxrow = std::max(NB_ * 36, n_);
+    hipLaunchKernelGGL(k_S_reduce, dim3((maxrow + 255) / 256, NB_ + 1), dim3(256), 0, stream_, d);
+    TimedLaunchEnd(kKSReduce);
+    if (comm_ && comm_->nranks() > 1) {
+      // the upper blocks of S and the rhs partial are summed over landmark shards
+      AllReduceSum(S_.ptr, (size_t)n_ * n_);
+      AllReduceSum(xc_.ptr, (size_t)n_);
+    }
+    TimedLaunchBegin(kKChol);
+    hipLaunchKernelGGL(k_cholesky, dim3(1), dim3(kCholThreads), 0, stream_, d, (const int32_t*)work_i_.ptr);
+    TimedLaunchEnd(kKChol);
+    TimedLaunchBegin(kKPointUpd);
+    hipLaunchKernelGGL(k_point_update, dim3(nc), dim3(kSweepThreads), 0, stream_, d);
+    TimedLaunchEnd(kKPointUpd);
+    TimedLaunchBegin(kKUpdRed);
+    hipLaunchKernelGGL(k_upd_reduce, dim3(1), dim3(64), 0, stream_, d);
+    TimedLaunchEnd(kKUpdRed);
+    AllReduceSum(xchg_upd_.ptr, kUNum);
+    TimedLaunchBegin(kKDecide);
+    hipLaunchKernelGGL(k_decide, dim3(1), dim3(64), 0, stream_, d);
+    TimedLaunchEnd(kKDecide);
+  }
+  SG_HIP_CHECK(hipGetLastError());
+}
+
+void BaSolver::Sync() { SG_HIP_CHECK(hipStreamSynchronize(stream_)); }
+
+void BaSolver::Summary(sg_solver_summary* s) {
+  LmState h{};
+  SG_HIP_CHECK(hipMemcpyAsync(&h, st_.ptr, sizeof(h), hipMemcpyDeviceToHost, stream_));
+  SG_HIP_CHECK(hipStreamSynchronize(stream_));
+  std::memset(s, 0, sizeof(*s));
+  s->num_iterations = h.pushed;
+  s->num_successful_steps = h.n_succ;
+  s->num_unsuccessful_steps = h.n_unsucc;
+  s->num_invalid_steps = h.n_invalid;
+  s->termination_type = h.termination;
+  s->ok = h.ok;
+  s->initial_cost = h.initial_cost;
+  s->final_cost = h.min_pushed_cost + h.fixed_cost;
+  s->fixed_cost = h.fixed_cost;
+  s->trust_region_radius = h.radius;
+  s->num_lm_iterations = h.lm_iters;
+}
+
+void BaSolver::Download(sg_problem* p) {
+  LmState h{};
+  SG_HIP_CHECK(hipMemcpyAsync(&h, st_.ptr, sizeof(h), hipMemcpyDeviceToHost, stream_));
+  SG_HIP_CHECK(hipStreamSynchronize(stream_));
+  std::vector<double> q(4 * (size_t)F_), t(3 * (size_t)F_), X(4 * (size_t)P_);
+  SG_HIP_CHECK(hipMemcpyAsync(q.data(), q_.ptr + 4 * (size_t)F_ * h.cur, q.size() * 8, hipMemcpyDeviceToHost, stream_));
+  SG_HIP_CHECK(hipMemcpyAsync(t.data(), t_.ptr + 3 * (size_t)F_ * h.cur, t.size() * 8, hipMemcpyDeviceToHost, stream_));
+  SG_HIP_CHECK(hipMemcpyAsync(X.data(), X_.ptr + 4 * (size_t)P_ * h.cur, X.size() * 8, hipMemcpyDeviceToHost, stream_));
+  SG_HIP_CHECK(hipStreamSynchronize(stream_));
+  std::copy(q.begin(), q.end(), p->q);
+  std::copy(t.begin(), t.end(), p->t);
+  for (int i = 0; i < P_; ++i) {
+    const int pt = point_perm_[i];
+    for (int a = 0; a < 4; ++a) p->X[4 * pt + a] = X[4 * i + a];
+  }
+}
+
+void BaSolver::Solve(const sg_solver_options& o, sg_problem* p, sg_solver_summary* s) {
+  Begin(o);
+  const int batch = 8;
+  LmState h{};
+  const long long cap = (long long)o.max_num_iterations * (o.max_num_consecutive_invalid_steps + 2) + 16;
+  long long launched = 0;
+  while (true) {
+    Iterate(batch);
+    launched += batch;
+    SG_HIP_CHECK(hipMemcpyAsync(&h, st_.ptr, sizeof(h), hipMemcpyDeviceToHost, stream_));
+    SG_HIP_CHECK(hipStreamSynchronize(stream_));
+    if (h.done) break;
+    SG_REQUIRE(launched < cap, SG_EDEVICE, "LM loop did not terminate on the device");
+  }
+  Summary(s);
+  Download(p);
+}
+
+void BaSolver::Evaluate(double* residuals, double* cost, int32_t* nfail) {
+  SG_REQUIRE(loaded_, SG_EINVAL, "no problem loaded");
+  DBuf<double> r, c;
+  DBuf<int32_t> nf;
+  r.Resize(2 * (size_t)std::max(M_, 1));
+  c.Resize(1);
+  nf.Resize(1);
+  c.Zero(stream_);
+  nf.Zero(stream_);
+  Dev d = MakeDev();
+  if (M_ > 0)
+    hipLaunchKernelGGL(k_evaluate, dim3((M_ + 255) / 256), dim3(256), 0, stream_, d, r.ptr, c.ptr, nf.ptr);
+  std::vector<double> rh(2 * (size_t)M_);
+  if (M_ > 0) SG_HIP_CHECK(hipMemcpyAsync(rh.data(), r.ptr, rh.size() * 8, hipMemcpyDeviceToHost, stream_));
+  SG_HIP_CHECK(hipMemcpyAsync(cost, c.ptr, 8, hipMemcpyDeviceToHost, stream_));
+  SG_HIP_CHECK(hipMemcpyAsync(nfail, nf.ptr, 4, hipMemcpyDeviceToHost, stream_));
+  SG_HIP_CHECK(hipStreamSynchronize(stream_));
+  for (int o = 0; o < M_; ++o) {
+    residuals[2 * obs_perm_[o]] = rh[2 * o];
+    residuals[2 * obs_perm_[o] + 1] = rh[2 * o + 1];
+  }
+}
+
+void BaSolver::SetTiming(bool on) {
+  timing_ = on;
+  for (auto& t : timers_) {
+    for (auto e : t.ev) (void)hipEventDestroy(e);
+    t.ev.clear();
+    t.total_ms = 0.0;
+    t.count = 0;
+  }
+}
+
+void BaSolver::CollectTimes() {
+  SG_HIP_CHECK(hipStreamSynchronize(stream_));
+  for (auto& t : timers_) {
+    for (size_t i = 0; i + 1 < t.ev.size(); i += 2) {
+      float ms = 0.f;
+      SG_HIP_CHECK(hipEventElapsedTime(&ms, t.ev[i], t.ev[i + 1]));
+      t.total_ms += ms;
+      t.count += 1;
+    }
+    for (auto e : t.ev) (void)hipEventDestroy(e);
+    t.ev.clear();
+  }
+}
+
+int BaSolver::KernelTimes(char* names, int names_len, double* ms, int32_t* counts, int max) {
+  CollectTimes();
+  std::string all;
+  int k = 0;
+  for (auto& t : timers_) {
+    if (k < max) {
+      ms[k] = t.count ? t.total_ms / t.count : 0.0;
+      counts[k] = t.count;
+    }
+    if (!all.empty()) all += ",";
+    all += t.name;
+    ++k;
+  }
+  if (names && names_len > 0) {
+    std::strncpy(names, all.c_str(), names_len - 1);
+    names[names_len - 1] = 0;
+  }
+  return std::min(k, max);
+}
+
+// Algorithmic bytes / flops per launch (for the roofline line in bench.py).
+int BaSolver::KernelWork(double* bytes, double* flops, int max) {
+  const double M = M_, P = P_, n = n_, NB = NB_;
+  double npairs = 0.0;  // observation pairs of free points on free frames are not tracked here: use M*k/2
+  (void)npairs;
+  std::vector<double> by(kKNum, 0.0), fl(kKNum, 0.0);
+  // linearize: read obs (16 B pt + 4 B frame + 1 B fixed) + point X 32 B + offsets 4 B; write J 192 B,
+  // V 80 B, g 32 B per point; camera partials
+  by[kKLin] = M * (16 + 4 + 1 + 192) + P * (32 + 4 + 80 + 32 + 1) + NB * kCamV * 8;
+  fl[kKLin] = M * 420.0;
+  by[kKSchur] = M * 192 + P * (80 + 32 + 32 + 32 + 80 + 32);
+  by[kKPointUpd] = M * (192 + 16 + 4) + P * (32 + 32 + 80 + 32 + 32);
+  by[kKChol] = n * n * 8 * 2;
+  fl[kKChol] = n * n * n / 3.0;
+  int k = 0;
+  for (; k < std::min(max, (int)kKNum); ++k) {
+    bytes[k] = by[k];
+    flops[k] = fl[k];
+  }
+  return k;
+}
+
+double BaSolver::ReprojectMap(sg_map* m) {
+  SG_HIP_CHECK(hipSetDevice(dev_.device));
+  const int M = m->num_obs;
+  hipStream_t s = stream_;
+  mk_.Upload(std::vector<double>(m->k, m->k + 7 * m->num_cameras), s);
+  mq_.Upload(std::vector<double>(m->q, m->q + 4 * m->num_frames), s);
+  mt_.Upload(std::vector<double>(m->t, m->t + 3 * m->num_frames), s);
+  mX_.Upload(std::vector<double>(m->X, m->X + 4 * m->num_points), s);
+  mobs_pt_.Upload(std::vector<double>(m->obs_pt, m->obs_pt + 2 * M), s);
+  mobs_frame_.Upload(std::vector<int32_t>(m->obs_frame, m->obs_frame + M), s);
+  mobs_point_.Upload(std::vector<int32_t>(m->obs_point, m->obs_point + M), s);
+  mframe_cam_.Upload(std::vector<int32_t>(m->frame_camera, m->frame_camera + m->num_frames), s);
+  mobs_err_.Resize(2 * (size_t)std::max(M, 1));
+  const int nb = std::max((M + 255) / 256, 1);
+  mred_.Resize(2 * (size_t)nb + 2);
+  mred_.Zero(s);
+  if (M > 0)
+    hipLaunchKernelGGL(k_reproject_map, dim3(nb), dim3(256), 0, s, mk_.ptr, mq_.ptr, mt_.ptr, mframe_cam_.ptr,
+                       mX_.ptr, mobs_pt_.ptr, mobs_frame_.ptr, mobs_point_.ptr, M, mobs_err_.ptr, mred_.ptr);
+  hipLaunchKernelGGL(k_reproject_reduce, dim3(1), dim3(64), 0, s, mred_.ptr, nb, mred_.ptr + 2 * nb);
+  SG_HIP_CHECK(hipGetLastError());
+  double out[2] = {0, 0};
+  if (M > 0) SG_HIP_CHECK(hipMemcpyAsync(m->obs_error, mobs_err_.ptr, 2 * (size_t)M * 8, hipMemcpyDeviceToHost, s));
+  SG_HIP_CHECK(hipMemcpyAsync(out, mred_.ptr + 2 * nb, 16, hipMemcpyDeviceToHost, s));
+  SG_HIP_CHECK(hipStreamSynchronize(s));
+  return out[0];
+}
+
+}  // namespace sg

@@ -1,0 +1,231 @@
+// capi.cpp — extern "C" entry points of libslamgpu.so (include/slamgpu.h).
+//
+// sg_ba_*   : the device solver (Ceres 1.8 LM + SPARSE_SCHUR restated on MI355X, slam.cpp:482-521)
+// sg_slam_* : the Slam object of slam.h:21-65 — SolveFrames / SolveAllFrames / ReprojectMap with
+//             iterations() and error() bookkeeping — on top of sg_problem_* and sg_ba_*.
+#include <cstring>
+#include <memory>
+
+#include "ba_solver.h"
+#include "common.h"
+
+struct sg_ba {
+  std::unique_ptr<sg::BaSolver> solver;
+};
+
+struct sg_slam {
+  std::unique_ptr<sg::BaSolver> solver;
+  sg_solver_options options;
+  int32_t iterations = 0;    // Slam::iterations_ (slam.cpp:517)
+  double error = 0.0;        // Slam::error_ (slam.cpp:518)
+  sg_solver_summary last{};
+};
+
+extern "C" {
+
+int sg_ba_create(sg_ba** out, const sg_device_options* dev) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(out, SG_EINVAL, "null output handle");
+  sg_device_options d;
+  sg_device_options_default(&d);
+  if (dev) d = *dev;
+  auto h = std::make_unique<sg_ba>();
+  h->solver.reset(new sg::BaSolver(d));
+  *out = h.release();
+  SG_CAPI_END
+}
+
+void sg_ba_destroy(sg_ba* h) { delete h; }
+
+int sg_comm_unique_id(void* id128) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(id128, SG_EINVAL, "null id buffer");
+  sg::BaSolver::UniqueId(id128);
+  SG_CAPI_END
+}
+
+int sg_ba_comm_init(sg_ba* h, const void* id128, int32_t nranks, int32_t rank) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(h && id128, SG_EINVAL, "null argument");
+  h->solver->CommInit(id128, nranks, rank);
+  SG_CAPI_END
+}
+
+int sg_ba_load(sg_ba* h, const sg_problem* p) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(h && p, SG_EINVAL, "null argument");
+  h->solver->Load(*p);
+  SG_CAPI_END
+}
+
+int sg_ba_solve(sg_ba* h, const sg_solver_options* o, sg_problem* p, sg_solver_summary* s) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(h && p && s, SG_EINVAL, "null argument");
+  sg_solver_options opt;
+  sg_solver_options_default(&opt);
+  if (o) opt = *o;
+  h->solver->Solve(opt, p, s);
+  SG_CAPI_END
+}
+
+int sg_ba_begin(sg_ba* h, const sg_solver_options* o) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(h, SG_EINVAL, "null handle");
+  sg_solver_options opt;
+  sg_solver_options_default(&opt);
+  if (o) opt = *o;
+  h->solver->Begin(opt);
+  SG_CAPI_END
+}
+
+int sg_ba_iterate(sg_ba* h, int32_t n) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(h && n >= 0, SG_EINVAL, "bad argument");
+  h->solver->Iterate(n);
+  SG_CAPI_END
+}
+
+int sg_ba_sync(sg_ba* h) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(h, SG_EINVAL, "null handle");
+  h->solver->Sync();
+  SG_CAPI_END
+}
+
+int sg_ba_summary(sg_ba* h, sg_solver_summary* s) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(h && s, SG_EINVAL, "null argument");
+  h->solver->Summary(s);
+  SG_CAPI_END
+}
+
+int sg_ba_download(sg_ba* h, sg_problem* p) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(h && p, SG_EINVAL, "null argument");
+  h->solver->Download(p);
+  SG_CAPI_END
+}
+
+int sg_ba_set_timing(sg_ba* h, int32_t enable) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(h, SG_EINVAL, "null handle");
+  h->solver->SetTiming(enable != 0);
+  SG_CAPI_END
+}
+
+int sg_ba_kernel_times(sg_ba* h, char* names, int32_t names_len, double* ms, int32_t* counts, int32_t max) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(h && ms && counts, SG_EINVAL, "null argument");
+  h->solver->KernelTimes(names, names_len, ms, counts, max);
+  SG_CAPI_END
+}
+
+int sg_ba_kernel_work(sg_ba* h, double* bytes, double* flops, int32_t max) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(h && bytes && flops, SG_EINVAL, "null argument");
+  h->solver->KernelWork(bytes, flops, max);
+  SG_CAPI_END
+}
+
+int sg_ba_evaluate(sg_ba* h, double* residuals, double* cost, int32_t* num_failed) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(h && residuals && cost && num_failed, SG_EINVAL, "null argument");
+  h->solver->Evaluate(residuals, cost, num_failed);
+  SG_CAPI_END
+}
+
+// ------------------------------------------------------------------------------------------------
+// Slam facade
+
+int sg_slam_create(sg_slam** out, const sg_device_options* dev) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(out, SG_EINVAL, "null output handle");
+  sg_device_options d;
+  sg_device_options_default(&d);
+  if (dev) d = *dev;
+  auto s = std::make_unique<sg_slam>();
+  s->solver.reset(new sg::BaSolver(d));
+  sg_solver_options_default(&s->options);
+  *out = s.release();
+  SG_CAPI_END
+}
+
+void sg_slam_destroy(sg_slam* s) { delete s; }
+
+int sg_slam_set_options(sg_slam* s, const sg_solver_options* o) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(s && o, SG_EINVAL, "null argument");
+  s->options = *o;
+  SG_CAPI_END
+}
+
+static void RunProblem(sg_slam* s, sg_problem* p, sg_map* map, const sg_solver_options& o, int32_t* solved) {
+  s->solver->Load(*p);
+  sg_solver_summary sum{};
+  s->solver->Solve(o, p, &sum);
+  if (sg_problem_write_back(p, map) != SG_OK) throw sg::Error(SG_EINVAL, sg_last_error());
+  s->iterations += sum.num_iterations;   // iterations_ += summary.iterations.size()
+  s->error = sum.final_cost;             // error_ = summary.final_cost
+  s->last = sum;
+  *solved = sum.ok;                      // summary.error.size() == 0
+}
+
+int sg_slam_solve_frames(sg_slam* s, sg_map* map, int32_t num_to_solve, int32_t num_to_present, double range,
+                         int32_t* solved) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(s && map && solved, SG_EINVAL, "null argument");
+  *solved = 0;
+  sg_problem p{};
+  int32_t built = 0;
+  int rc = sg_problem_from_map_frames(map, num_to_solve, num_to_present, range, &p, &built);
+  if (rc != SG_OK) return rc;
+  if (!built) return SG_OK;   // "Slam aborted due to frame set too small": SolveFrames returns false
+  try {
+    RunProblem(s, &p, map, s->options, solved);   // Run(false)
+  } catch (...) {
+    sg_problem_free(&p);
+    throw;
+  }
+  sg_problem_free(&p);
+  SG_CAPI_END
+}
+
+int sg_slam_solve_all_frames(sg_slam* s, sg_map* map, double range, int32_t solve_cameras, int32_t* solved) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(s && map && solved, SG_EINVAL, "null argument");
+  *solved = 0;
+  sg_problem p{};
+  int32_t built = 0;
+  int rc = sg_problem_from_map_all(map, range, solve_cameras, &p, &built);
+  if (rc != SG_OK) return rc;
+  if (!built) return SG_OK;
+  sg_solver_options o = s->options;
+  if (solve_cameras) o.function_tolerance = 1e-9;   // Run(fine = solve_cameras), slam.cpp:496-499
+  try {
+    RunProblem(s, &p, map, o, solved);
+  } catch (...) {
+    sg_problem_free(&p);
+    throw;
+  }
+  sg_problem_free(&p);
+  SG_CAPI_END
+}
+
+int sg_slam_reproject_map(sg_slam* s, sg_map* map, double* mean) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(s && map && mean, SG_EINVAL, "null argument");
+  *mean = s->solver->ReprojectMap(map);
+  SG_CAPI_END
+}
+
+int32_t sg_slam_iterations(const sg_slam* s) { return s ? s->iterations : 0; }
+double sg_slam_error(const sg_slam* s) { return s ? s->error : 0.0; }
+
+int sg_slam_last_summary(const sg_slam* s, sg_solver_summary* out) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(s && out, SG_EINVAL, "null argument");
+  *out = s->last;
+  SG_CAPI_END
+}
+
+}  // extern "C"
