@@ -203,6 +203,10 @@ int sg_ba_kernel_times(sg_ba* h, char* names, int32_t names_len, double* ms, int
 /* Algorithmic byte / flop counts for the roofline (per launch of each timed kernel). */
 int sg_ba_kernel_work(sg_ba* h, double* bytes, double* flops, int32_t max);
 
+/* Jacobian/Hessian sweep only (benchmark of the HBM-bound kernel): n linearizations at the current
+ * state (k_linearize + camera-block reduce), timed when sg_ba_set_timing is on. */
+int sg_ba_sweep(sg_ba* h, int32_t n);
+
 /* Residual sweep only (ReprojectionError over the uploaded observations at the current state):
  * r[2*M] corrected residuals in problem order, returns cost (without fixed cost) and failure count. */
 int sg_ba_evaluate(sg_ba* h, double* residuals, double* cost, int32_t* num_failed);

@@ -109,8 +109,12 @@ struct Dev {
   // chunks and partials
   const Chunk* chunks;
   int32_t nchunks;
-  const int32_t* blk_cbeg;       // [NB] chunk range that may cover block I
-  const int32_t* blk_cend;
+  const int32_t* cam_loff;       // [NB+1] CSR: per camera block, offsets of its partials in cam_slab
+  const int32_t* cam_lidx;
+  const int32_t* s_loff;         // [NB*NB+1] CSR: per block pair (I<=J), offsets of its partials in S_slab
+  const int32_t* s_lidx;
+  const int32_t* r_loff;         // [NB+1] CSR: per block, offsets of its rhs partials in S_slab
+  const int32_t* r_lidx;
   double* cam_slab;
   double* S_slab;
   double* chunk_scal;            // [nchunks][kNScal]

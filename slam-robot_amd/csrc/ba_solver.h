@@ -52,6 +52,7 @@ class BaSolver {
   void Load(const sg_problem& p);
   void Begin(const sg_solver_options& o);
   void Iterate(int n);
+  void Sweep(int n);
   void Sync();
   void Summary(sg_solver_summary* s);
   void Download(sg_problem* p);
@@ -74,6 +75,7 @@ class BaSolver {
   std::unique_ptr<Comm> comm_;
   bool loaded_ = false;
   bool began_ = false;
+  bool chol_window_ = true;
   // host copies of the structure
   int F_ = 0, P_ = 0, M_ = 0, NB_ = 0, n_ = 0, D_ = 0, nchunks_ = 0, max_nb_ = 0, ncam_ = 0;
   std::vector<int32_t> point_perm_;   // device order -> problem point
@@ -85,8 +87,8 @@ class BaSolver {
   DBuf<double> k_, q_, t_, X_, obs_pt_, J_, V_, g_, scale_p_, diag_p_, Vinv_, tp_, scale_c_, diag_c_, camdiag_,
       camg_, cam_slab_, S_slab_, chunk_scal_, cam_wide_, S_wide_, xchg_cam_, xchg_max_, S_, rhs_, xchg_upd_,
       xchg_chol_, xc_, work_, fd_r_, fd_J_, fd_D_, fd_X_, red_;
-  DBuf<int32_t> frame_cam_, frame_block_, poff_, obs_frame_, fd_a_, fd_b_, fd_boff_, fd_bidx_, blk_cbeg_,
-      blk_cend_, mobs_frame_, mobs_point_, mframe_cam_;
+  DBuf<int32_t> frame_cam_, frame_block_, poff_, obs_frame_, fd_a_, fd_b_, fd_boff_, fd_bidx_, cam_loff_,
+      cam_lidx_, s_loff_, s_lidx_, r_loff_, r_lidx_, mobs_frame_, mobs_point_, mframe_cam_;
   DBuf<uint8_t> rot_free_, trans_free_, pfree_, obs_fixed_;
   DBuf<Chunk> chunks_d_;
   DBuf<int32_t> work_i_;   // Cholesky panel envelopes (panel_jmax)

@@ -305,11 +305,9 @@ __global__ __launch_bounds__(256) void k_cam_reduce(Dev d) {
     const int b = i / kCamV, e = i % kCamV;
     double s = d.cam_wide[i];
     d.cam_wide[i] = 0.0;
-    for (int c = d.blk_cbeg[b]; c < d.blk_cend[b]; ++c) {
-      const Chunk ch = d.chunks[c];
-      if (ch.wide || b < ch.b_lo || b >= ch.b_lo + ch.nb) continue;
-      s += d.cam_slab[ch.cam_off + (b - ch.b_lo) * kCamV + e];
-    }
+    const int j0 = d.cam_loff[b], j1 = d.cam_loff[b + 1];
+#pragma unroll 4
+    for (int j = j0; j < j1; ++j) s += d.cam_slab[d.cam_lidx[j] + e];
     d.xchg_cam[i] = s;
   }
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x < 64) {
@@ -491,11 +489,54 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d) {
 // k_schur: one chunk per workgroup, one wave per point.  Damped, scaled point block V~ = S V S + D^2
 // (LL^T inverse), then every pair (s, t) of the point's observations on free frames contributes
 // -A_c,s^T (A_p,s V~^-1 A_p,t^T) A_c,t to the window block (b_s, b_t) in LDS, and the right-hand side
-// gets -A_c,s^T A_p,s V~^-1 g~_p.  Lanes of a wave hold distinct pairs -> distinct LDS addresses.
+// gets -A_c,s^T A_p,s V~^-1 g~_p.  The point's scaled observation Jacobians are staged once in a per-wave
+// LDS slab (each observation read from HBM once); lanes of a wave then hold distinct pairs -> distinct
+// LDS accumulator addresses.
+constexpr int kStageK = 32;      // observations per point staged in LDS (longer tracks read from L2)
+constexpr int kStageW = 28;      // Jc 12 | P = Jp V^-1 8 | Jp 8
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes have landed
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ void schur_pair_add(double* dst, int ld, const double* Jcs, const double* Ps,
+                                               const double* Jpt, const double* Jct, bool same_obs,
+                                               bool same_blk, bool s_first) {
+  double M[2][2];
+#pragma unroll
+  for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      M[rr][u] = Ps[4 * rr] * Jpt[4 * u] + Ps[4 * rr + 1] * Jpt[4 * u + 1] + Ps[4 * rr + 2] * Jpt[4 * u + 2] +
+                 Ps[4 * rr + 3] * Jpt[4 * u + 3];
+  double N[6][2];
+#pragma unroll
+  for (int a = 0; a < 6; ++a)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) N[a][u] = Jcs[a] * M[0][u] + Jcs[6 + a] * M[1][u];
+#pragma unroll
+  for (int a = 0; a < 6; ++a)
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+      const double Tac = N[a][0] * Jct[c] + N[a][1] * Jct[6 + c];
+      const double Tca = N[c][0] * Jct[a] + N[c][1] * Jct[6 + a];
+      double v;
+      if (same_obs) v = Tac;
+      else if (same_blk) v = Tac + Tca;
+      else if (s_first) v = Tac;
+      else v = Tca;
+      atomicAdd(dst + a * ld + c, -v);
+    }
+}
+
 __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d) {
   const LmState* st = d.st;
   if (st->done) return;
   extern __shared__ double win[];
+  __shared__ double stage[kSchurThreads / 64][kStageK][kStageW];
+  __shared__ int sblk[kSchurThreads / 64][kStageK];
   __shared__ double red[kSchurThreads / 64];
   const Chunk ch = d.chunks[blockIdx.x];
   const int npair = ch.nb * (ch.nb + 1) / 2;
@@ -504,6 +545,8 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d) {
   for (int i = threadIdx.x; i < nwin; i += blockDim.x) win[i] = 0.0;
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double (*stg)[kStageW] = stage[wave];
+  int* sb = sblk[wave];
   const double radius = st->radius;
   const bool reuse = st->reuse_diag != 0;
   double linfail = 0.0;
@@ -554,13 +597,31 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d) {
       reinterpret_cast<double4*>(d.tp)[p] = make_double4(tp[0], tp[1], tp[2], tp[3]);
     }
     const int o0 = d.poff[p], k = d.poff[p + 1] - o0;
-    // right-hand side: -A_c,s^T (A_p,s t_p)
+    const bool staged = k <= kStageK;
+    // stage: scaled Jc, P = Jp V~^-1, Jp of every observation; right-hand side -A_c,s^T (A_p,s t_p)
     for (int s = lane; s < k; s += 64) {
       const int o = o0 + s;
-      const int b = d.frame_block[d.obs_frame[o]];
-      if (b < 0 || d.obs_fixed[o]) continue;
+      const int b = d.obs_fixed[o] ? -1 : d.frame_block[d.obs_frame[o]];
       double r[2], Jc[12], Jp[8];
-      load_scaled_J(d, o, b, sp, r, Jc, Jp);
+      load_scaled_J(d, o, b < 0 ? 0 : b, sp, r, Jc, Jp);
+      if (staged) {
+        sb[s] = b;
+        double* row = stg[s];
+#pragma unroll
+        for (int i = 0; i < 12; ++i) row[i] = Jc[i];
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            double acc = 0.0;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) acc += Jp[4 * rr + m] * sym4(Vi, m, c);
+            row[12 + 4 * rr + c] = acc;
+          }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) row[20 + i] = Jp[i];
+      }
+      if (b < 0) continue;
       const double e0 = Jp[0] * tp[0] + Jp[1] * tp[1] + Jp[2] * tp[2] + Jp[3] * tp[3];
       const double e1 = Jp[4] * tp[0] + Jp[5] * tp[1] + Jp[6] * tp[2] + Jp[7] * tp[3];
 #pragma unroll
@@ -570,64 +631,53 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d) {
         else atomicAdd(rhsw + (b - ch.b_lo) * 6 + a, v);
       }
     }
+    wave_lds_sync();
     // pairs (s <= t)
     const int np = k * (k + 1) / 2;
     for (int pi = lane; pi < np; pi += 64) {
       int s = 0, rem = pi;
       while (rem >= k - s) { rem -= k - s; ++s; }
       const int t = s + rem;
-      const int os = o0 + s, ot = o0 + t;
-      const int bs = d.frame_block[d.obs_frame[os]], bt = d.frame_block[d.obs_frame[ot]];
-      if (bs < 0 || bt < 0 || d.obs_fixed[os] || d.obs_fixed[ot]) continue;
-      double r[2], Jcs[12], Jps[8], Jct[12], Jpt[8];
-      load_scaled_J(d, os, bs, sp, r, Jcs, Jps);
-      load_scaled_J(d, ot, bt, sp, r, Jct, Jpt);
-      // P = Jp_s Vi (2x4); M = P Jp_t^T (2x2)
-      double M[2][2];
+      double Jcs[12], Ps[8], Jpt[8], Jct[12];
+      int bs, bt;
+      if (staged) {
+        bs = sb[s];
+        bt = sb[t];
+        if (bs < 0 || bt < 0) continue;
 #pragma unroll
-      for (int rr = 0; rr < 2; ++rr) {
-        double P[4];
+        for (int i = 0; i < 12; ++i) Jcs[i] = stg[s][i];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          double acc = 0.0;
+        for (int i = 0; i < 8; ++i) Ps[i] = stg[s][12 + i];
 #pragma unroll
-          for (int m = 0; m < 4; ++m) acc += Jps[4 * rr + m] * sym4(Vi, m, c);
-          P[c] = acc;
-        }
+        for (int i = 0; i < 8; ++i) Jpt[i] = stg[t][20 + i];
 #pragma unroll
-        for (int u = 0; u < 2; ++u)
-          M[rr][u] = P[0] * Jpt[4 * u] + P[1] * Jpt[4 * u + 1] + P[2] * Jpt[4 * u + 2] + P[3] * Jpt[4 * u + 3];
-      }
-      // N = Jc_s^T M (6x2); T = N Jc_t (6x6)
-      double N[6][2];
-#pragma unroll
-      for (int a = 0; a < 6; ++a)
-#pragma unroll
-        for (int u = 0; u < 2; ++u) N[a][u] = Jcs[a] * M[0][u] + Jcs[6 + a] * M[1][u];
-      const int I = bs < bt ? bs : bt, Jb = bs < bt ? bt : bs;
-      double* dst;
-      int ld;
-      if (ch.wide) {
-        dst = d.S_wide + (size_t)(6 * I) * d.n + 6 * Jb;
-        ld = d.n;
+        for (int i = 0; i < 12; ++i) Jct[i] = stg[t][i];
       } else {
-        dst = win + wp(I - ch.b_lo, Jb - ch.b_lo, ch.nb) * 36;
-        ld = 6;
+        const int os = o0 + s, ot = o0 + t;
+        bs = d.obs_fixed[os] ? -1 : d.frame_block[d.obs_frame[os]];
+        bt = d.obs_fixed[ot] ? -1 : d.frame_block[d.obs_frame[ot]];
+        if (bs < 0 || bt < 0) continue;
+        double r[2], Jps[8];
+        load_scaled_J(d, os, bs, sp, r, Jcs, Jps);
+        load_scaled_J(d, ot, bt, sp, r, Jct, Jpt);
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            double acc = 0.0;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) acc += Jps[4 * rr + m] * sym4(Vi, m, c);
+            Ps[4 * rr + c] = acc;
+          }
       }
-#pragma unroll
-      for (int a = 0; a < 6; ++a)
-#pragma unroll
-        for (int c = 0; c < 6; ++c) {
-          const double Tac = N[a][0] * Jct[c] + N[a][1] * Jct[6 + c];
-          const double Tca = N[c][0] * Jct[a] + N[c][1] * Jct[6 + a];
-          double v;
-          if (s == t) v = Tac;
-          else if (bs == bt) v = Tac + Tca;
-          else if (bs < bt) v = Tac;
-          else v = Tca;
-          atomicAdd(dst + a * ld + c, -v);
-        }
+      const int I = bs < bt ? bs : bt, Jb = bs < bt ? bt : bs;
+      if (ch.wide)
+        schur_pair_add(d.S_wide + (size_t)(6 * I) * d.n + 6 * Jb, d.n, Jcs, Ps, Jpt, Jct, s == t, bs == bt, bs < bt);
+      else
+        schur_pair_add(win + wp(I - ch.b_lo, Jb - ch.b_lo, ch.nb) * 36, 6, Jcs, Ps, Jpt, Jct, s == t, bs == bt,
+                       bs < bt);
     }
+    wave_lds_sync();   // the next point reuses this wave's stage
   }
   linfail = block_sum<kSchurThreads>(linfail, red);
   if (threadIdx.x == 0) d.chunk_scal[(size_t)blockIdx.x * kNScal + kLinFail] = linfail;
@@ -649,44 +699,43 @@ __global__ __launch_bounds__(256) void k_S_reduce(Dev d) {
     const size_t gi = (size_t)(6 * I + a) * d.n + 6 * Jb + c;
     double s = d.S_wide[gi];
     d.S_wide[gi] = 0.0;
-    for (int ci = d.blk_cbeg[I]; ci < d.blk_cend[I]; ++ci) {
-      const Chunk ch = d.chunks[ci];
-      if (ch.wide || I < ch.b_lo || Jb >= ch.b_lo + ch.nb) continue;
-      s += d.S_slab[ch.s_off + wp(I - ch.b_lo, Jb - ch.b_lo, ch.nb) * 36 + a * 6 + c];
-    }
+    const int pr = I * d.NB + Jb;
+    const int j0 = d.s_loff[pr], j1 = d.s_loff[pr + 1];
+    const int ac = a * 6 + c;
+#pragma unroll 4
+    for (int j = j0; j < j1; ++j) s += d.S_slab[d.s_lidx[j] + ac];
     d.S[gi] = s;
   } else {
     if (e >= d.n) return;
     const int b = e / 6, a = e % 6;
     double s = d.rhs[e];   // wide-chunk atomics
-    for (int ci = d.blk_cbeg[b]; ci < d.blk_cend[b]; ++ci) {
-      const Chunk ch = d.chunks[ci];
-      if (ch.wide || b < ch.b_lo || b >= ch.b_lo + ch.nb) continue;
-      s += d.S_slab[ch.s_off + ch.nb * (ch.nb + 1) / 2 * 36 + (b - ch.b_lo) * 6 + a];
-    }
+    const int j0 = d.r_loff[b], j1 = d.r_loff[b + 1];
+#pragma unroll 4
+    for (int j = j0; j < j1; ++j) s += d.S_slab[d.r_lidx[j] + a];
     d.xc[e] = s;       // local rhs partial (all-reduced with S); the wide-chunk accumulator is reset
     d.rhs[e] = 0.0;
   }
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_cholesky: one workgroup.  A = S_sub + blockdiag(U) + FrameDistance + D^2 (scaled), banded
-// right-looking Cholesky A = U^T U with the rhs as an augmented column, back substitution, then the
-// candidate camera poses x+ = Plus(x, -S x_c) and the FrameDistance model/candidate terms.
-__global__ __launch_bounds__(kCholThreads) void k_cholesky(Dev d, const int32_t* panel_jmax) {
-  LmState* st = d.st;
-  if (st->done) return;
-  const int n = d.n, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int nwaves = kCholThreads / 64;
-  double* A = d.S;
-  double* y = d.work;
-  const double radius = st->radius;
-  __shared__ double U11[kCholNb][kCholNb + 1];
-  __shared__ int fail_sh;
-  __shared__ double red[kCholThreads / 64];
-  if (tid == 0) fail_sh = 0;
-  // ---- assemble
-  for (int i = tid; i < d.NB * 21; i += kCholThreads) {
+// Reduced camera system solve (the SPARSE_SCHUR + CHOLMOD step behind slam.cpp:489, restated): one
+// workgroup factors the damped, banded Schur complement A = U^T U (right-looking, 16-wide panels, the
+// rhs carried as an augmented column), then back-substitutes.  The band (co-visibility of the sliding
+// window) fits a 128x128 fp64 LDS window that slides down the diagonal; trailing updates run as
+// v_mfma_f64_16x16x4 tiles.  Bands wider than the window take the global-memory path.
+constexpr int kCholWS = 128;
+constexpr int kCholLd = kCholWS + 1;
+constexpr size_t kCholLds = (size_t)kCholWS * kCholLd * sizeof(double);
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ double& Wn(double* win, int i, int j) {
+  return win[(i & (kCholWS - 1)) * kCholLd + (j & (kCholWS - 1))];
+}
+
+// A += blockdiag(U) + FrameDistance blocks + D^2 (all Jacobi-scaled); y = rhs_sub + S g_c.
+__device__ __noinline__ void chol_assemble(const Dev& d, double* A, double* y, double radius) {
+  const int n = d.n, tid = threadIdx.x;
+  for (int i = tid; i < d.NB * 21; i += blockDim.x) {
     const int b = i / 21, e = i % 21;
     int a = 0, rem = e;
     while (rem >= 6 - a) { rem -= 6 - a; ++a; }
@@ -698,7 +747,7 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky(Dev d, const int32_t*
     if (a == c) v += d.diag_c[ra] / radius;
     A[(size_t)ra * n + rc] += v;
   }
-  for (int dd = tid; dd < d.D; dd += kCholThreads) {
+  for (int dd = tid; dd < d.D; dd += blockDim.x) {
     const int ba = d.frame_block[d.fd_a[dd]], bb = d.frame_block[d.fd_b[dd]];
     if (ba < 0 || bb < 0 || ba == bb) continue;
     const double* Xd = d.fd_X + 9 * dd;   // J_a J_b^T (rows: a's translation, cols: b's)
@@ -710,124 +759,88 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky(Dev d, const int32_t*
         else A[(size_t)cj * n + ri] += v;
       }
   }
-  for (int i = tid; i < n; i += kCholThreads) y[i] = d.xc[i] + d.scale_c[i] * d.camg[i];
-  __syncthreads();
-  // ---- factor (upper), panels of kCholNb
-  const int npanel = (n + kCholNb - 1) / kCholNb;
-  for (int pk = 0; pk < npanel; ++pk) {
-    const int kb = pk * kCholNb;
-    const int w = min(kCholNb, n - kb);
-    const int jmax = min(n, panel_jmax[pk]);
-    if (wave == 0) {
-      // column-per-lane register factorisation of the diagonal block
-      double col[kCholNb];
+  for (int i = tid; i < n; i += blockDim.x) y[i] = d.xc[i] + d.scale_c[i] * d.camg[i];
+}
+
+// Unblocked factorisation of the w x w diagonal block held column-per-lane (lanes 0..w-1, col[r] =
+// A[r][lane] for r <= lane).  Returns false on a non-positive pivot.
+__device__ __forceinline__ bool chol_diag16(double (&col)[kCholNb], int w, int lane) {
+  bool bad = false;
 #pragma unroll
-      for (int r = 0; r < kCholNb; ++r) col[r] = (lane < w && r <= lane) ? A[(size_t)(kb + r) * n + kb + lane] : 0.0;
-      bool bad = false;
+  for (int j = 0; j < kCholNb; ++j) {
+    if (j < w) {
+      const double piv = __shfl(col[j], j);
+      if (!(piv > 0.0)) bad = true;
+      const double ujj = sqrt(piv);
+      const double inv = 1.0 / ujj;
+      if (lane == j) col[j] = ujj;
+      else if (lane > j) col[j] *= inv;
 #pragma unroll
-      for (int j = 0; j < kCholNb; ++j) {
-        if (j < w) {
-          const double piv = __shfl(col[j], j);
-          if (!(piv > 0.0)) bad = true;
-          const double ujj = sqrt(piv);
-          const double inv = 1.0 / ujj;
-          if (lane == j) col[j] = ujj;
-          else if (lane > j) col[j] *= inv;
-#pragma unroll
-          for (int r = j + 1; r < kCholNb; ++r) {
-            const double ujr = __shfl(col[j], r);
-            if (r < w && lane >= r) col[r] -= ujr * col[j];
-          }
-        }
-      }
-      if (lane < w) {
-#pragma unroll
-        for (int r = 0; r < kCholNb; ++r)
-          if (r <= lane) {
-            A[(size_t)(kb + r) * n + kb + lane] = col[r];
-            U11[r][lane] = col[r];
-          }
-      }
-      if (lane == 0 && bad) fail_sh = 1;
-    }
-    __syncthreads();
-    // TRSM: rows kb..kb+w of columns [kb+w, jmax) and of the rhs column
-    const int ncol = jmax - (kb + w);
-    for (int ci = tid; ci < ncol + 1; ci += kCholThreads) {
-      const bool isy = ci == ncol;
-      const int c = kb + w + ci;
-      double a[kCholNb];
-#pragma unroll
-      for (int r = 0; r < kCholNb; ++r) a[r] = (r < w) ? (isy ? y[kb + r] : A[(size_t)(kb + r) * n + c]) : 0.0;
-#pragma unroll
-      for (int j = 0; j < kCholNb; ++j) {
-        if (j < w) {
-          double s = a[j];
-#pragma unroll
-          for (int m = 0; m < kCholNb; ++m)
-            if (m < j) s -= U11[m][j] * a[m];
-          a[j] = s / U11[j][j];
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < kCholNb; ++r)
-        if (r < w) {
-          if (isy) y[kb + r] = a[r];
-          else A[(size_t)(kb + r) * n + c] = a[r];
-        }
-    }
-    __syncthreads();
-    // trailing update of rows/cols [kb+w, jmax): A[i][j] -= sum_r U[r][i] U[r][j];  y[i] -= sum_r U[r][i] y[r]
-    for (int i = kb + w + wave; i < jmax; i += nwaves) {
-      double ui[kCholNb];
-#pragma unroll
-      for (int r = 0; r < kCholNb; ++r) ui[r] = (r < w) ? A[(size_t)(kb + r) * n + i] : 0.0;
-      for (int j = i + lane; j < jmax; j += 64) {
-        double s = 0.0;
-#pragma unroll
-        for (int r = 0; r < kCholNb; ++r)
-          if (r < w) s += ui[r] * A[(size_t)(kb + r) * n + j];
-        A[(size_t)i * n + j] -= s;
-      }
-      if (lane == 0) {
-        double s = 0.0;
-#pragma unroll
-        for (int r = 0; r < kCholNb; ++r)
-          if (r < w) s += ui[r] * y[kb + r];
-        y[i] -= s;
+      for (int r = j + 1; r < kCholNb; ++r) {
+        const double ujr = __shfl(col[j], r);
+        if (r < w && lane >= r) col[r] -= ujr * col[j];
       }
     }
-    __syncthreads();
   }
-  // ---- back substitution U x = y, blocked from the bottom
+  return !bad;
+}
+
+// Forward substitution of one column (16 rows) with U11^T.
+__device__ __forceinline__ void chol_trsm16(double (&a)[kCholNb], const double (*U11)[kCholNb + 1], int w) {
+#pragma unroll
+  for (int j = 0; j < kCholNb; ++j) {
+    if (j < w) {
+      double s = a[j];
+#pragma unroll
+      for (int m = 0; m < kCholNb; ++m)
+        if (m < j) s -= U11[m][j] * a[m];
+      a[j] = s / U11[j][j];
+    }
+  }
+}
+
+// Back substitution U x = y (U upper, rows in global A, band end per panel), blocked by 16 from the end.
+__device__ __noinline__ void chol_backsub(const double* A, double* y, int n, const int32_t* panel_jend) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
+  const int npanel = (n + kCholNb - 1) / kCholNb;
   for (int pk = npanel - 1; pk >= 0; --pk) {
     const int kb = pk * kCholNb;
     const int w = min(kCholNb, n - kb);
+    const int jend = panel_jend[pk];
+    for (int r = wave; r < w; r += nwaves) {
+      double s = 0.0;
+      for (int j = kb + w + lane; j < jend; j += 64) s += A[(size_t)(kb + r) * n + j] * y[j];
+      s = wave_sum(s);
+      if (lane == 0) y[kb + r] -= s;
+    }
+    __syncthreads();
     if (wave == 0) {
-      double yv = (lane < w) ? y[kb + lane] : 0.0;
-      for (int j = w - 1; j >= 0; --j) {
-        const double ujj = A[(size_t)(kb + j) * n + kb + j];
-        const double xj = __shfl(yv, j) / ujj;
-        if (lane == j) yv = xj;
-        else if (lane < j) yv -= A[(size_t)(kb + lane) * n + kb + j] * xj;
+      double row[kCholNb];
+#pragma unroll
+      for (int c = 0; c < kCholNb; ++c) row[c] = (lane < w && c < w && c >= lane) ? A[(size_t)(kb + lane) * n + kb + c] : 1.0;
+      double yv = lane < w ? y[kb + lane] : 0.0;
+#pragma unroll
+      for (int j = kCholNb - 1; j >= 0; --j) {
+        if (j < w) {
+          const double xj = __shfl(yv / row[j], j);
+          if (lane == j) yv = xj;
+          else if (lane < j) yv -= row[j] * xj;
+        }
       }
       if (lane < w) y[kb + lane] = yv;
     }
     __syncthreads();
-    // rows i < kb with a nonzero coupling to this panel: y[i] -= sum_r U[i][kb+r] x[kb+r]
-    for (int i = tid; i < kb; i += kCholThreads) {
-      double s = 0.0;
-      for (int r = 0; r < w; ++r) s += A[(size_t)i * n + kb + r] * y[kb + r];
-      y[i] -= s;
-    }
-    __syncthreads();
   }
-  for (int i = tid; i < n; i += kCholThreads) d.xc[i] = y[i];
-  __syncthreads();
-  // ---- candidate camera poses and FrameDistance terms
+}
+
+// Candidate camera poses x+ = Plus(x, -S x_c) for every frame, FrameDistance model / candidate terms.
+__device__ __noinline__ void chol_candidates(const Dev& d, const double* y, int fail) {
+  const LmState* st = d.st;
+  __shared__ double red[kCholThreads / 64];
+  const int tid = threadIdx.x;
   const int cur = st->cur, nxt = cur ^ 1;
   double step2 = 0.0, candx2 = 0.0, model = 0.0, candcost = 0.0;
-  for (int f = tid; f < d.F; f += kCholThreads) {
+  for (int f = tid; f < d.F; f += blockDim.x) {
     const double* q = d.q[cur] + 4 * f;
     const double* t = d.t[cur] + 3 * f;
     double* qn = d.q[nxt] + 4 * f;
@@ -856,7 +869,7 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky(Dev d, const int32_t*
     for (int a = 0; a < 3; ++a) tn[a] = tt[a];
   }
   __syncthreads();
-  for (int dd = tid; dd < d.D; dd += kCholThreads) {
+  for (int dd = tid; dd < d.D; dd += blockDim.x) {
     const int fa = d.fd_a[dd], fb = d.fd_b[dd];
     const int ba = d.frame_block[fa], bb = d.frame_block[fb];
     const double* Jd = d.fd_J + 6 * dd;
@@ -883,8 +896,203 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky(Dev d, const int32_t*
     d.xchg_chol[kCCandX2] = candx2;
     d.xchg_chol[kCModel] = model;
     d.xchg_chol[kCCandCost] = candcost;
-    d.xchg_chol[kCFail] = fail_sh ? 1.0 : 0.0;
+    d.xchg_chol[kCFail] = fail ? 1.0 : 0.0;
   }
+}
+
+// Window path: the active band lives in LDS (132 KiB); panel rows are written back for the
+// back substitution.
+__global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const int32_t* panel_jend) {
+  LmState* st = d.st;
+  if (st->done) return;
+  extern __shared__ double win[];
+  __shared__ double U11[kCholNb][kCholNb + 1];
+  __shared__ int fail_sh;
+  const int n = d.n, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nwaves = kCholThreads / 64;
+  double* A = d.S;
+  double* y = d.work;
+  if (tid == 0) fail_sh = 0;
+  chol_assemble(d, A, y, st->radius);
+  __syncthreads();
+  const int n0 = min(n, kCholWS);
+  for (int e = tid; e < n0 * n0; e += kCholThreads) {
+    const int i = e / n0, j = e % n0;
+    if (i <= j) Wn(win, i, j) = A[(size_t)i * n + j];
+  }
+  __syncthreads();
+  const int npanel = (n + kCholNb - 1) / kCholNb;
+  const int li = lane & 15, lk = lane >> 4;
+  for (int pk = 0; pk < npanel; ++pk) {
+    const int kb = pk * kCholNb;
+    const int w = min(kCholNb, n - kb);
+    const int jend = panel_jend[pk];
+    // (a) diagonal block
+    if (wave == 0) {
+      double col[kCholNb];
+#pragma unroll
+      for (int r = 0; r < kCholNb; ++r) col[r] = (lane < w && r <= lane) ? Wn(win, kb + r, kb + lane) : 0.0;
+      const bool ok = chol_diag16(col, w, lane);
+      if (lane < w) {
+#pragma unroll
+        for (int r = 0; r < kCholNb; ++r)
+          if (r <= lane) {
+            Wn(win, kb + r, kb + lane) = col[r];
+            U11[r][lane] = col[r];
+          }
+      }
+      if (lane == 0 && !ok) fail_sh = 1;
+    }
+    __syncthreads();
+    // (b) panel TRSM on columns [kb+w, jend) and the rhs column
+    const int ncol = jend - (kb + w);
+    for (int ci = tid; ci < ncol + 1; ci += kCholThreads) {
+      const bool isy = ci == ncol;
+      const int c = kb + w + ci;
+      double a[kCholNb];
+#pragma unroll
+      for (int r = 0; r < kCholNb; ++r) a[r] = (r < w) ? (isy ? y[kb + r] : Wn(win, kb + r, c)) : 0.0;
+      chol_trsm16(a, U11, w);
+#pragma unroll
+      for (int r = 0; r < kCholNb; ++r)
+        if (r < w) {
+          if (isy) y[kb + r] = a[r];
+          else Wn(win, kb + r, c) = a[r];
+        }
+    }
+    __syncthreads();
+    // (c) trailing update A22 -= U12^T U12 on the band, 16x16 MFMA tiles (upper tiles only)
+    const int m = jend - (kb + w);
+    const int T = (m + 15) >> 4;
+    const int ntiles = T * (T + 1) / 2;
+    for (int tile = wave; tile < ntiles; tile += nwaves) {
+      int ti = 0, rem = tile;
+      while (rem >= T - ti) { rem -= T - ti; ++ti; }
+      const int tj = ti + rem;
+      const int i0 = kb + w + 16 * ti, j0 = kb + w + 16 * tj;
+      f64x4 acc;
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const int row = i0 + lk + 4 * qq, col = j0 + li;
+        acc[qq] = (row < jend && col < jend && row <= col) ? Wn(win, row, col) : 0.0;
+      }
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const int k = kb + 4 * s4 + lk;
+        const bool kin = (4 * s4 + lk) < w;
+        const double av = (kin && i0 + li < jend) ? -Wn(win, k, i0 + li) : 0.0;
+        const double bv = (kin && j0 + li < jend) ? Wn(win, k, j0 + li) : 0.0;
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const int row = i0 + lk + 4 * qq, col = j0 + li;
+        if (row < jend && col < jend && row <= col) Wn(win, row, col) = acc[qq];
+      }
+    }
+    for (int i = kb + w + tid; i < jend; i += kCholThreads) {
+      double s = 0.0;
+#pragma unroll
+      for (int r = 0; r < kCholNb; ++r)
+        if (r < w) s += Wn(win, kb + r, i) * y[kb + r];
+      y[i] -= s;
+    }
+    // (d) finished panel rows -> global (for the back substitution)
+    const int wc = jend - kb;
+    for (int e = tid; e < w * wc; e += kCholThreads) {
+      const int r = e / wc, c = kb + e % wc;
+      if (c >= kb + r) A[(size_t)(kb + r) * n + c] = Wn(win, kb + r, c);
+    }
+    __syncthreads();
+    // (e) slide the window: bring in columns [kb + WS, kb + WS + w) (rows kb+w .. j)
+    const int jn0 = kb + kCholWS, jn1 = min(n, jn0 + w);
+    for (int e = tid; e < (jn1 - jn0) * kCholWS; e += kCholThreads) {
+      const int j = jn0 + e / kCholWS, i = kb + w + e % kCholWS;
+      if (i <= j) Wn(win, i, j) = A[(size_t)i * n + j];
+    }
+    __syncthreads();
+  }
+  chol_backsub(A, y, n, panel_jend);
+  for (int i = tid; i < n; i += kCholThreads) d.xc[i] = y[i];
+  __syncthreads();
+  chol_candidates(d, y, fail_sh);
+}
+
+// Global-memory path for bands wider than the LDS window.
+__global__ __launch_bounds__(kCholThreads) void k_cholesky_global(Dev d, const int32_t* panel_jend) {
+  LmState* st = d.st;
+  if (st->done) return;
+  const int n = d.n, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nwaves = kCholThreads / 64;
+  double* A = d.S;
+  double* y = d.work;
+  __shared__ double U11[kCholNb][kCholNb + 1];
+  __shared__ int fail_sh;
+  if (tid == 0) fail_sh = 0;
+  chol_assemble(d, A, y, st->radius);
+  __syncthreads();
+  const int npanel = (n + kCholNb - 1) / kCholNb;
+  for (int pk = 0; pk < npanel; ++pk) {
+    const int kb = pk * kCholNb;
+    const int w = min(kCholNb, n - kb);
+    const int jmax = panel_jend[pk];
+    if (wave == 0) {
+      double col[kCholNb];
+#pragma unroll
+      for (int r = 0; r < kCholNb; ++r) col[r] = (lane < w && r <= lane) ? A[(size_t)(kb + r) * n + kb + lane] : 0.0;
+      const bool ok = chol_diag16(col, w, lane);
+      if (lane < w) {
+#pragma unroll
+        for (int r = 0; r < kCholNb; ++r)
+          if (r <= lane) {
+            A[(size_t)(kb + r) * n + kb + lane] = col[r];
+            U11[r][lane] = col[r];
+          }
+      }
+      if (lane == 0 && !ok) fail_sh = 1;
+    }
+    __syncthreads();
+    const int ncol = jmax - (kb + w);
+    for (int ci = tid; ci < ncol + 1; ci += kCholThreads) {
+      const bool isy = ci == ncol;
+      const int c = kb + w + ci;
+      double a[kCholNb];
+#pragma unroll
+      for (int r = 0; r < kCholNb; ++r) a[r] = (r < w) ? (isy ? y[kb + r] : A[(size_t)(kb + r) * n + c]) : 0.0;
+      chol_trsm16(a, U11, w);
+#pragma unroll
+      for (int r = 0; r < kCholNb; ++r)
+        if (r < w) {
+          if (isy) y[kb + r] = a[r];
+          else A[(size_t)(kb + r) * n + c] = a[r];
+        }
+    }
+    __syncthreads();
+    for (int i = kb + w + wave; i < jmax; i += nwaves) {
+      double ui[kCholNb];
+#pragma unroll
+      for (int r = 0; r < kCholNb; ++r) ui[r] = (r < w) ? A[(size_t)(kb + r) * n + i] : 0.0;
+      for (int j = i + lane; j < jmax; j += 64) {
+        double s = 0.0;
+#pragma unroll
+        for (int r = 0; r < kCholNb; ++r)
+          if (r < w) s += ui[r] * A[(size_t)(kb + r) * n + j];
+        A[(size_t)i * n + j] -= s;
+      }
+      if (lane == 0) {
+        double s = 0.0;
+#pragma unroll
+        for (int r = 0; r < kCholNb; ++r)
+          if (r < w) s += ui[r] * y[kb + r];
+        y[i] -= s;
+      }
+    }
+    __syncthreads();
+  }
+  chol_backsub(A, y, n, panel_jend);
+  for (int i = tid; i < n; i += kCholThreads) d.xc[i] = y[i];
+  __syncthreads();
+  chol_candidates(d, y, fail_sh);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1101,7 +1309,7 @@ __global__ void k_evaluate(Dev d, double* resid, double* cost_out, int32_t* nfai
   // residual sweep at x[cur] (parity / ReprojectionError check), observation order = device order
   const int o = blockIdx.x * blockDim.x + threadIdx.x;
   if (o >= d.M) return;
-  const int cur = d.st->cur;
+  const int cur = d.st->cur & 1;
   // find the point of o: binary search in poff
   int lo = 0, hi = d.P;
   while (hi - lo > 1) {
@@ -1315,20 +1523,40 @@ void BaSolver::Load(const sg_problem& p) {
     i = j;
   }
   nchunks_ = (int)chunks_.size();
-  // per block: chunk range that may cover it (chunks are sorted by b_lo)
-  std::vector<int32_t> cbeg(NB_, 0), cend(NB_, 0);
-  for (int b = 0; b < NB_; ++b) {
-    int lo = nchunks_, hi2 = 0;
+  // deterministic reduction lists: for every camera block / block pair, the slab offsets of the chunk
+  // partials that cover it (fixed chunk order)
+  std::vector<int32_t> cam_loff(NB_ + 1, 0), cam_lidx, r_loff(NB_ + 1, 0), r_lidx;
+  std::vector<int32_t> s_loff((size_t)NB_ * NB_ + 1, 0), s_lidx;
+  {
+    std::vector<std::vector<int32_t>> cl(NB_), rl(NB_);
+    std::vector<std::vector<int32_t>> sl((size_t)NB_ * NB_);
     for (int c = 0; c < nchunks_; ++c) {
       const Chunk& ch = chunks_[c];
-      if (ch.nb == 0 || ch.wide) continue;
-      if (b >= ch.b_lo && b < ch.b_lo + ch.nb) {
-        lo = std::min(lo, c);
-        hi2 = std::max(hi2, c + 1);
+      if (ch.wide || ch.nb == 0) continue;
+      const int npair = ch.nb * (ch.nb + 1) / 2;
+      for (int i = 0; i < ch.nb; ++i) {
+        const int b = ch.b_lo + i;
+        cl[b].push_back(ch.cam_off + i * kCamV);
+        rl[b].push_back(ch.s_off + npair * 36 + i * 6);
+        for (int j = i; j < ch.nb; ++j) {
+          const int wpij = i * ch.nb - i * (i - 1) / 2 + (j - i);
+          sl[(size_t)b * NB_ + ch.b_lo + j].push_back(ch.s_off + wpij * 36);
+        }
       }
     }
-    cbeg[b] = lo < nchunks_ ? lo : 0;
-    cend[b] = lo < nchunks_ ? hi2 : 0;
+    for (int b = 0; b < NB_; ++b) {
+      cam_loff[b + 1] = cam_loff[b] + (int)cl[b].size();
+      cam_lidx.insert(cam_lidx.end(), cl[b].begin(), cl[b].end());
+      r_loff[b + 1] = r_loff[b] + (int)rl[b].size();
+      r_lidx.insert(r_lidx.end(), rl[b].begin(), rl[b].end());
+    }
+    for (size_t pr = 0; pr < sl.size(); ++pr) {
+      s_loff[pr + 1] = s_loff[pr] + (int)sl[pr].size();
+      s_lidx.insert(s_lidx.end(), sl[pr].begin(), sl[pr].end());
+    }
+    if (cam_lidx.empty()) cam_lidx.push_back(0);
+    if (r_lidx.empty()) r_lidx.push_back(0);
+    if (s_lidx.empty()) s_lidx.push_back(0);
   }
   // FrameDistance
   std::vector<int32_t> fd_a(p.dist_frame, p.dist_frame + D_), fd_b(p.dist_prev, p.dist_prev + D_);
@@ -1377,8 +1605,12 @@ void BaSolver::Load(const sg_problem& p) {
     // columns j whose envelope starts at or before the panel's last row block
     for (int b = 0; b < NB_; ++b)
       if (lo_blk[b] <= blk_hi) jmax = std::max(jmax, 6 * b + 6);
-    panel_jmax[pk] = std::min(jmax, n_);
+    jmax = std::min(jmax, n_);
+    panel_jmax[pk] = std::min(n_, (jmax + kCholNb - 1) / kCholNb * kCholNb);   // band end, 16-aligned
   }
+  chol_window_ = true;
+  for (int pk = 0; pk < npanel; ++pk)
+    if (panel_jmax[pk] - pk * kCholNb > kCholWS) chol_window_ = false;
   // device uploads
   hipStream_t s = stream_;
   k_.Upload(std::vector<double>(p.k, p.k + 7 * ncam_), s);
@@ -1402,8 +1634,12 @@ void BaSolver::Load(const sg_problem& p) {
   obs_frame_.Upload(obs_frame, s);
   obs_fixed_.Upload(obs_fixed, s);
   chunks_d_.Upload(chunks_, s);
-  blk_cbeg_.Upload(cbeg, s);
-  blk_cend_.Upload(cend, s);
+  cam_loff_.Upload(cam_loff, s);
+  cam_lidx_.Upload(cam_lidx, s);
+  s_loff_.Upload(s_loff, s);
+  s_lidx_.Upload(s_lidx, s);
+  r_loff_.Upload(r_loff, s);
+  r_lidx_.Upload(r_lidx, s);
   fd_a_.Upload(fd_a, s);
   fd_b_.Upload(fd_b, s);
   fd_boff_.Upload(fd_boff, s);
@@ -1438,6 +1674,7 @@ void BaSolver::Load(const sg_problem& p) {
   fd_J_.Resize(6 * (size_t)std::max(D_, 1));
   fd_D_.Resize(9 * (size_t)std::max(NB_, 1));
   fd_X_.Resize(9 * (size_t)std::max(D_, 1));
+  st_.Zero(s);          // LmState: slot 0 current, nothing pending (evaluate() may run before begin())
   cam_wide_.Zero(s);
   S_wide_.Zero(s);
   rhs_.Zero(s);
@@ -1447,6 +1684,8 @@ void BaSolver::Load(const sg_problem& p) {
   if (schur_lds_ > 0)
     SG_HIP_CHECK(hipFuncSetAttribute((const void*)k_schur, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)std::max<size_t>(schur_lds_, 1)));
+  SG_HIP_CHECK(hipFuncSetAttribute((const void*)k_cholesky_window, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)kCholLds));
   SG_HIP_CHECK(hipStreamSynchronize(s));
   loaded_ = true;
   began_ = false;
@@ -1503,8 +1742,12 @@ Dev BaSolver::MakeDev() {
   d.camg = camg_.ptr;
   d.chunks = chunks_d_.ptr;
   d.nchunks = nchunks_;
-  d.blk_cbeg = blk_cbeg_.ptr;
-  d.blk_cend = blk_cend_.ptr;
+  d.cam_loff = cam_loff_.ptr;
+  d.cam_lidx = cam_lidx_.ptr;
+  d.s_loff = s_loff_.ptr;
+  d.s_lidx = s_lidx_.ptr;
+  d.r_loff = r_loff_.ptr;
+  d.r_lidx = r_lidx_.ptr;
   d.cam_slab = cam_slab_.ptr;
   d.S_slab = S_slab_.ptr;
   d.chunk_scal = chunk_scal_.ptr;
@@ -1609,7 +1852,12 @@ void BaSolver::Iterate(int n) {
       AllReduceSum(xc_.ptr, (size_t)n_);
     }
     TimedLaunchBegin(kKChol);
-    hipLaunchKernelGGL(k_cholesky, dim3(1), dim3(kCholThreads), 0, stream_, d, (const int32_t*)work_i_.ptr);
+    if (chol_window_)
+      hipLaunchKernelGGL(k_cholesky_window, dim3(1), dim3(kCholThreads), kCholLds, stream_, d,
+                         (const int32_t*)work_i_.ptr);
+    else
+      hipLaunchKernelGGL(k_cholesky_global, dim3(1), dim3(kCholThreads), 0, stream_, d,
+                         (const int32_t*)work_i_.ptr);
     TimedLaunchEnd(kKChol);
     TimedLaunchBegin(kKPointUpd);
     hipLaunchKernelGGL(k_point_update, dim3(nc), dim3(kSweepThreads), 0, stream_, d);
@@ -1621,6 +1869,27 @@ void BaSolver::Iterate(int n) {
     TimedLaunchBegin(kKDecide);
     hipLaunchKernelGGL(k_decide, dim3(1), dim3(64), 0, stream_, d);
     TimedLaunchEnd(kKDecide);
+  }
+  SG_HIP_CHECK(hipGetLastError());
+}
+
+__global__ void k_force_linearize(LmState* st) {
+  if (threadIdx.x == 0) {
+    st->need_lin = 1;
+    st->done = 0;
+  }
+}
+
+void BaSolver::Sweep(int n) {
+  SG_REQUIRE(loaded_, SG_EINVAL, "no problem loaded");
+  SG_HIP_CHECK(hipSetDevice(dev_.device));
+  Dev d = MakeDev();
+  const int nc = std::max(nchunks_, 1);
+  for (int it = 0; it < n; ++it) {
+    hipLaunchKernelGGL(k_force_linearize, dim3(1), dim3(64), 0, stream_, st_.ptr);
+    TimedLaunchBegin(kKLin);
+    hipLaunchKernelGGL(k_linearize, dim3(nc), dim3(kSweepThreads), 0, stream_, d);
+    TimedLaunchEnd(kKLin);
   }
   SG_HIP_CHECK(hipGetLastError());
 }

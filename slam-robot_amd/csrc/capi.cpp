@@ -127,6 +127,13 @@ int sg_ba_kernel_work(sg_ba* h, double* bytes, double* flops, int32_t max) {
   SG_CAPI_END
 }
 
+int sg_ba_sweep(sg_ba* h, int32_t n) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(h && n >= 0, SG_EINVAL, "bad argument");
+  h->solver->Sweep(n);
+  SG_CAPI_END
+}
+
 int sg_ba_evaluate(sg_ba* h, double* residuals, double* cost, int32_t* num_failed) {
   SG_CAPI_BEGIN
   SG_REQUIRE(h && residuals && cost && num_failed, SG_EINVAL, "null argument");

@@ -109,6 +109,10 @@ class BundleAdjuster:
     def iterate(self, n: int):
         check(self.lib.sg_ba_iterate(self.h, n), "sg_ba_iterate")
 
+    def sweep(self, n: int):
+        """n Jacobian/Hessian sweeps (k_linearize) at the current state — benchmark of the HBM kernel."""
+        check(self.lib.sg_ba_sweep(self.h, n), "sg_ba_sweep")
+
     def sync(self):
         check(self.lib.sg_ba_sync(self.h), "sg_ba_sync")
 

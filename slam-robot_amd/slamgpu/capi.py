@@ -218,6 +218,7 @@ SYMBOLS = {
     "sg_ba_kernel_times": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int32, _dp, _ip, C.c_int32]),
     "sg_ba_kernel_work": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int32]),
     "sg_ba_evaluate": (C.c_int, [C.c_void_p, _dp, _dp, _ip]),
+    "sg_ba_sweep": (C.c_int, [C.c_void_p, C.c_int32]),
     "sg_slam_create": (C.c_int, [C.POINTER(C.c_void_p), C.POINTER(SgDeviceOptions)]),
     "sg_slam_destroy": (None, [C.c_void_p]),
     "sg_slam_solve_frames": (C.c_int, [C.c_void_p, C.POINTER(SgMap), C.c_int32, C.c_int32, C.c_double,
