@@ -129,6 +129,9 @@ struct Dev {
   double* xchg_chol;             // [kCNum]
   double* xc;                    // [n] camera solution (scaled)
   double* work;                  // [n] solver scratch
+  const int32_t* fd_pair;        // [NB][NB] (I<J): FrameDistance residual coupling blocks I and J, or -1
+  int32_t assemble;              // this rank adds blockdiag(U) + FD + damping to S (rank 0 of a shard group)
+  unsigned long long* stamps;    // diagnostic builds only: per-phase cycle counters (nullptr otherwise)
 };
 
 }  // namespace sg

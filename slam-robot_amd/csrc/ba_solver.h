@@ -76,6 +76,14 @@ class BaSolver {
   bool loaded_ = false;
   bool began_ = false;
   bool chol_window_ = true;
+  bool stamp_on_ = false;
+  DBuf<unsigned long long> stamps_;
+
+ public:
+  // diagnostic: per-phase cycle counters of the stamped kernels (SG_STAMP=1)
+  std::vector<unsigned long long> Stamps();
+
+ private:
   // host copies of the structure
   int F_ = 0, P_ = 0, M_ = 0, NB_ = 0, n_ = 0, D_ = 0, nchunks_ = 0, max_nb_ = 0, ncam_ = 0;
   std::vector<int32_t> point_perm_;   // device order -> problem point
@@ -92,6 +100,8 @@ class BaSolver {
   DBuf<uint8_t> rot_free_, trans_free_, pfree_, obs_fixed_;
   DBuf<Chunk> chunks_d_;
   DBuf<int32_t> work_i_;   // Cholesky panel envelopes (panel_jmax)
+  DBuf<int32_t> fd_pair_;  // FrameDistance cross-block lookup
+  DBuf<double> rdg_;       // 1/U_jj of the factor
   DBuf<double> mk_, mq_, mt_, mX_, mobs_pt_, mobs_err_, mred_;
   double range_b_ = 4.0, fd_target_ = 150.0, fd_b2_ = 225.0;
   // timing

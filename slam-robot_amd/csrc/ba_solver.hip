@@ -22,6 +22,7 @@
 #include <cfloat>
 #include <cmath>
 #include <cstring>
+#include <cstdlib>
 #include <numeric>
 
 #include "ba_solver.h"
@@ -686,7 +687,31 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_S_reduce: grid (x: elements of block row I with J >= I, y: I; y == NB is the rhs row).
+// The camera-camera terms of the damped reduced system that do not come from the Schur complement:
+// blockdiag(U) (observation Jacobians) + FrameDistance diagonal and cross blocks + D^2 = diag/radius,
+// all Jacobi-scaled, for element (6I+a, 6J+c), J >= I.
+__device__ __forceinline__ double assembly_term(const Dev& d, int I, int J, int a, int c, double radius) {
+  const int i = 6 * I + a, j = 6 * J + c;
+  double v = 0.0;
+  if (I == J) {
+    if (c < a) return 0.0;   // lower triangle of a diagonal block is never read
+    v = d.xchg_cam[(size_t)I * kCamV + u6(a, c)];
+    if (a >= 3) v += d.fd_D[9 * I + 3 * (a - 3) + (c - 3)];
+    v *= d.scale_c[i] * d.scale_c[j];
+    if (a == c) v += d.diag_c[i] / radius;
+  } else if (a >= 3 && c >= 3) {
+    const int dd = d.fd_pair[I * d.NB + J];
+    if (dd >= 0) {
+      const double* Xd = d.fd_X + 9 * dd;   // J_a J_b^T, rows: frame a's translation
+      const bool a_is_i = d.frame_block[d.fd_a[dd]] == I;
+      v = (a_is_i ? Xd[3 * (a - 3) + (c - 3)] : Xd[3 * (c - 3) + (a - 3)]) * d.scale_c[i] * d.scale_c[j];
+    }
+  }
+  return v;
+}
+
+// k_S_reduce: grid (x: elements of block row I with J >= I, y: I; y == NB is the rhs row).  The
+// assembling rank also adds assembly_term and the S g_c part of the rhs, so S leaves here damped.
 __global__ __launch_bounds__(256) void k_S_reduce(Dev d) {
   const LmState* st = d.st;
   if (st->done) return;
@@ -704,6 +729,7 @@ __global__ __launch_bounds__(256) void k_S_reduce(Dev d) {
     const int ac = a * 6 + c;
 #pragma unroll 4
     for (int j = j0; j < j1; ++j) s += d.S_slab[d.s_lidx[j] + ac];
+    if (d.assemble) s += assembly_term(d, I, Jb, a, c, st->radius);
     d.S[gi] = s;
   } else {
     if (e >= d.n) return;
@@ -712,6 +738,7 @@ __global__ __launch_bounds__(256) void k_S_reduce(Dev d) {
     const int j0 = d.r_loff[b], j1 = d.r_loff[b + 1];
 #pragma unroll 4
     for (int j = j0; j < j1; ++j) s += d.S_slab[d.r_lidx[j] + a];
+    if (d.assemble) s += d.scale_c[e] * d.camg[e];   // y = rhs_sub + S g_c
     d.xc[e] = s;       // local rhs partial (all-reduced with S); the wide-chunk accumulator is reset
     d.rhs[e] = 0.0;
   }
@@ -732,104 +759,97 @@ __device__ __forceinline__ double& Wn(double* win, int i, int j) {
   return win[(i & (kCholWS - 1)) * kCholLd + (j & (kCholWS - 1))];
 }
 
-// A += blockdiag(U) + FrameDistance blocks + D^2 (all Jacobi-scaled); y = rhs_sub + S g_c.
-__device__ __noinline__ void chol_assemble(const Dev& d, double* A, double* y, double radius) {
-  const int n = d.n, tid = threadIdx.x;
-  for (int i = tid; i < d.NB * 21; i += blockDim.x) {
-    const int b = i / 21, e = i % 21;
-    int a = 0, rem = e;
-    while (rem >= 6 - a) { rem -= 6 - a; ++a; }
-    const int c = a + rem;
-    double v = d.xchg_cam[(size_t)b * kCamV + e];
-    if (a >= 3) v += d.fd_D[9 * b + 3 * (a - 3) + (c - 3)];
-    const int ra = 6 * b + a, rc = 6 * b + c;
-    v *= d.scale_c[ra] * d.scale_c[rc];
-    if (a == c) v += d.diag_c[ra] / radius;
-    A[(size_t)ra * n + rc] += v;
-  }
-  for (int dd = tid; dd < d.D; dd += blockDim.x) {
-    const int ba = d.frame_block[d.fd_a[dd]], bb = d.frame_block[d.fd_b[dd]];
-    if (ba < 0 || bb < 0 || ba == bb) continue;
-    const double* Xd = d.fd_X + 9 * dd;   // J_a J_b^T (rows: a's translation, cols: b's)
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) {
-        const int ri = 6 * ba + 3 + i, cj = 6 * bb + 3 + j;
-        const double v = Xd[3 * i + j] * d.scale_c[ri] * d.scale_c[cj];
-        if (ba < bb) A[(size_t)ri * n + cj] += v;
-        else A[(size_t)cj * n + ri] += v;
-      }
-  }
-  for (int i = tid; i < n; i += blockDim.x) y[i] = d.xc[i] + d.scale_c[i] * d.camg[i];
+// Wave-uniform broadcast of lane `l`'s double (v_readlane pair: no LDS round trip).
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
+
+// LDS-only workgroup barrier: waits for this wave's LDS traffic, not for outstanding global loads or
+// stores (those may stay in flight across it).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 // Unblocked factorisation of the w x w diagonal block held column-per-lane (lanes 0..w-1, col[r] =
-// A[r][lane] for r <= lane).  Returns false on a non-positive pivot.
-__device__ __forceinline__ bool chol_diag16(double (&col)[kCholNb], int w, int lane) {
-  bool bad = false;
+// A[r][lane] for r <= lane), broadcasts by v_readlane.  `bad` is set on a non-positive pivot.
+__device__ __forceinline__ void chol_diag16(double (&col)[kCholNb], int w, int lane, bool& bad) {
 #pragma unroll
   for (int j = 0; j < kCholNb; ++j) {
     if (j < w) {
-      const double piv = __shfl(col[j], j);
+      const double piv = readlane_d(col[j], j);
       if (!(piv > 0.0)) bad = true;
       const double ujj = sqrt(piv);
       const double inv = 1.0 / ujj;
-      if (lane == j) col[j] = ujj;
-      else if (lane > j) col[j] *= inv;
+      col[j] = (lane == j) ? ujj : (lane > j ? col[j] * inv : col[j]);
 #pragma unroll
       for (int r = j + 1; r < kCholNb; ++r) {
-        const double ujr = __shfl(col[j], r);
-        if (r < w && lane >= r) col[r] -= ujr * col[j];
+        if (r < w) {
+          const double ujr = readlane_d(col[j], r);
+          if (lane >= r) col[r] -= ujr * col[j];
+        }
       }
     }
+    __builtin_amdgcn_sched_barrier(0);
   }
-  return !bad;
 }
 
-// Forward substitution of one column (16 rows) with U11^T.
-__device__ __forceinline__ void chol_trsm16(double (&a)[kCholNb], const double (*U11)[kCholNb + 1], int w) {
+// Right-looking forward substitution of one 16-row column with U11^T (U11 and 1/diag in LDS).
+__device__ __forceinline__ void chol_trsm16(double (&a)[kCholNb], const double (*U11)[kCholNb + 1],
+                                            const double* rdiag, int w) {
 #pragma unroll
-  for (int j = 0; j < kCholNb; ++j) {
-    if (j < w) {
-      double s = a[j];
+  for (int m = 0; m < kCholNb; ++m) {
+    if (m < w) {
+      a[m] *= rdiag[m];
 #pragma unroll
-      for (int m = 0; m < kCholNb; ++m)
-        if (m < j) s -= U11[m][j] * a[m];
-      a[j] = s / U11[j][j];
+      for (int j = m + 1; j < kCholNb; ++j)
+        if (j < w) a[j] -= U11[m][j] * a[m];
     }
+    __builtin_amdgcn_sched_barrier(0);   // keep each step's LDS reads local (no 120-load hoist)
   }
 }
 
-// Back substitution U x = y (U upper, rows in global A, band end per panel), blocked by 16 from the end.
-__device__ __noinline__ void chol_backsub(const double* A, double* y, int n, const int32_t* panel_jend) {
+// Back substitution U x = y.  U rows in global A (band end per panel), 1/U_jj in rdg, forward solution
+// in y (global); the solution goes to xs (LDS, n doubles) and y.  Blocked by 16 from the end; the
+// 16x16 triangle runs in one wave with readlane broadcasts.
+__device__ __noinline__ void chol_backsub(const double* A, const double* rdg, double* y, double* xs, int n,
+                                          const int32_t* panel_jend) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
   const int npanel = (n + kCholNb - 1) / kCholNb;
+  __shared__ double rpart[kCholNb];
   for (int pk = npanel - 1; pk >= 0; --pk) {
     const int kb = pk * kCholNb;
     const int w = min(kCholNb, n - kb);
     const int jend = panel_jend[pk];
     for (int r = wave; r < w; r += nwaves) {
       double s = 0.0;
-      for (int j = kb + w + lane; j < jend; j += 64) s += A[(size_t)(kb + r) * n + j] * y[j];
+      for (int j = kb + w + lane; j < jend; j += 64) s += A[(size_t)(kb + r) * n + j] * xs[j];
       s = wave_sum(s);
-      if (lane == 0) y[kb + r] -= s;
+      if (lane == 0) rpart[r] = s;
     }
-    __syncthreads();
+    lds_barrier();
     if (wave == 0) {
       double row[kCholNb];
 #pragma unroll
-      for (int c = 0; c < kCholNb; ++c) row[c] = (lane < w && c < w && c >= lane) ? A[(size_t)(kb + lane) * n + kb + c] : 1.0;
-      double yv = lane < w ? y[kb + lane] : 0.0;
+      for (int c = 0; c < kCholNb; ++c)
+        row[c] = (lane < w && c < w && c > lane) ? A[(size_t)(kb + lane) * n + kb + c] : 0.0;
+      const double rd = lane < w ? rdg[kb + lane] : 0.0;
+      double v = lane < w ? y[kb + lane] - rpart[lane] : 0.0;
 #pragma unroll
       for (int j = kCholNb - 1; j >= 0; --j) {
         if (j < w) {
-          const double xj = __shfl(yv / row[j], j);
-          if (lane == j) yv = xj;
-          else if (lane < j) yv -= row[j] * xj;
+          const double xj = readlane_d(v * rd, j);
+          if (lane == j) v = xj;
+          else if (lane < j) v -= row[j] * xj;
         }
       }
-      if (lane < w) y[kb + lane] = yv;
+      if (lane < w) {
+        xs[kb + lane] = v;
+        y[kb + lane] = v;
+      }
     }
-    __syncthreads();
+    lds_barrier();
   }
 }
 
@@ -900,39 +920,75 @@ __device__ __noinline__ void chol_candidates(const Dev& d, const double* y, int 
   }
 }
 
-// Window path: the active band lives in LDS (132 KiB); panel rows are written back for the
-// back substitution.
-__global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const int32_t* panel_jend) {
+// Diagnostic stamps (SG_STAMP=1 builds of the launch only): thread 0 accumulates s_memtime deltas per phase
+// in registers (a global read-modify-write here would wait on every outstanding load) and adds them to
+// d.stamps once at the end.
+#define SG_STAMP_AT(slot)                                                        \
+  if (kStamp && threadIdx.x == 0) {                                               \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime();                 \
+    stamp_acc[slot] += now_ - last_stamp;                                         \
+    last_stamp = now_;                                                            \
+  }
+#define SG_STAMP_FLUSH()                                                         \
+  if (kStamp && threadIdx.x == 0) {                                               \
+    for (int s_ = 0; s_ < 8; ++s_) d.stamps[s_] += stamp_acc[s_];                 \
+  }
+
+// Window path: the active band lives in LDS (132 KiB) together with the rhs ring; finished panel rows and
+// 1/U_jj go to global memory for the back substitution.  Barriers between phases are LDS-only, so the
+// global writes and the prefetch of the next window columns overlap the factorisation.
+template <bool kStamp>
+__global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const int32_t* panel_jend, double* rdg) {
+  unsigned long long last_stamp = kStamp ? __builtin_amdgcn_s_memtime() : 0ull;
+  unsigned long long stamp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   LmState* st = d.st;
   if (st->done) return;
   extern __shared__ double win[];
   __shared__ double U11[kCholNb][kCholNb + 1];
+  __shared__ double rdiag[kCholNb];
+  __shared__ double yw[kCholWS];
   __shared__ int fail_sh;
   const int n = d.n, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nwaves = kCholThreads / 64;
-  double* A = d.S;
   double* y = d.work;
   if (tid == 0) fail_sh = 0;
-  chol_assemble(d, A, y, st->radius);
-  __syncthreads();
+  // rhs y = rhs_sub + S g_c
+  for (int i = tid; i < n; i += kCholThreads) {
+    const double v = d.xc[i];   // assembled rhs (k_S_reduce)
+    y[i] = v;
+    if (i < kCholWS) yw[i] = v;
+  }
   const int n0 = min(n, kCholWS);
   for (int e = tid; e < n0 * n0; e += kCholThreads) {
     const int i = e / n0, j = e % n0;
-    if (i <= j) Wn(win, i, j) = A[(size_t)i * n + j];
+    if (i <= j) Wn(win, i, j) = d.S[(size_t)i * n + j];
   }
   __syncthreads();
+  SG_STAMP_AT(0)
   const int npanel = (n + kCholNb - 1) / kCholNb;
   const int li = lane & 15, lk = lane >> 4;
+  constexpr int kPf = kCholNb * kCholWS / kCholThreads;   // prefetched window elements per thread
   for (int pk = 0; pk < npanel; ++pk) {
     const int kb = pk * kCholNb;
     const int w = min(kCholNb, n - kb);
     const int jend = panel_jend[pk];
-    // (a) diagonal block
+    // prefetch the columns this panel's slide brings in: j in [kb+WS, kb+WS+w), rows kb+w..j
+    const int jn0 = kb + kCholWS, jn1 = min(n, jn0 + w);
+    double pf[kPf];
+#pragma unroll
+    for (int q = 0; q < kPf; ++q) {
+      const int e = tid + q * kCholThreads;
+      const int j = jn0 + e / kCholWS, i = kb + w + e % kCholWS;
+      const bool in = j < jn1 && i <= j;
+      pf[q] = d.S[in ? (size_t)i * n + j : 0];   // branch-free: the loads stay in flight across phases
+    }
+    // (a) diagonal block, one wave
     if (wave == 0) {
       double col[kCholNb];
 #pragma unroll
       for (int r = 0; r < kCholNb; ++r) col[r] = (lane < w && r <= lane) ? Wn(win, kb + r, kb + lane) : 0.0;
-      const bool ok = chol_diag16(col, w, lane);
+      bool bad = false;
+      chol_diag16(col, w, lane, bad);
       if (lane < w) {
 #pragma unroll
         for (int r = 0; r < kCholNb; ++r)
@@ -940,28 +996,34 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
             Wn(win, kb + r, kb + lane) = col[r];
             U11[r][lane] = col[r];
           }
+        const double rd = 1.0 / col[lane];
+        rdiag[lane] = rd;
+        rdg[kb + lane] = rd;
       }
-      if (lane == 0 && !ok) fail_sh = 1;
+      if (lane == 0 && bad) fail_sh = 1;
     }
-    __syncthreads();
-    // (b) panel TRSM on columns [kb+w, jend) and the rhs column
+    lds_barrier();
+    SG_STAMP_AT(2)
+    // (b) panel TRSM on columns [kb+w, jend) and on the rhs ring
     const int ncol = jend - (kb + w);
     for (int ci = tid; ci < ncol + 1; ci += kCholThreads) {
       const bool isy = ci == ncol;
       const int c = kb + w + ci;
       double a[kCholNb];
 #pragma unroll
-      for (int r = 0; r < kCholNb; ++r) a[r] = (r < w) ? (isy ? y[kb + r] : Wn(win, kb + r, c)) : 0.0;
-      chol_trsm16(a, U11, w);
+      for (int r = 0; r < kCholNb; ++r)
+        a[r] = (r < w) ? (isy ? yw[(kb + r) & (kCholWS - 1)] : Wn(win, kb + r, c)) : 0.0;
+      chol_trsm16(a, U11, rdiag, w);
 #pragma unroll
       for (int r = 0; r < kCholNb; ++r)
         if (r < w) {
-          if (isy) y[kb + r] = a[r];
+          if (isy) yw[(kb + r) & (kCholWS - 1)] = a[r];
           else Wn(win, kb + r, c) = a[r];
         }
     }
-    __syncthreads();
-    // (c) trailing update A22 -= U12^T U12 on the band, 16x16 MFMA tiles (upper tiles only)
+    lds_barrier();
+    SG_STAMP_AT(3)
+    // (c) trailing update A22 -= U12^T U12 on the band, 16x16 MFMA tiles (upper tiles only), rhs update
     const int m = jend - (kb + w);
     const int T = (m + 15) >> 4;
     const int ntiles = T * (T + 1) / 2;
@@ -994,42 +1056,53 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
       double s = 0.0;
 #pragma unroll
       for (int r = 0; r < kCholNb; ++r)
-        if (r < w) s += Wn(win, kb + r, i) * y[kb + r];
-      y[i] -= s;
+        if (r < w) s += Wn(win, kb + r, i) * yw[(kb + r) & (kCholWS - 1)];
+      yw[i & (kCholWS - 1)] -= s;
     }
-    // (d) finished panel rows -> global (for the back substitution)
+    // finished panel rows and the forward solution of these rows -> global (no wait)
     const int wc = jend - kb;
     for (int e = tid; e < w * wc; e += kCholThreads) {
       const int r = e / wc, c = kb + e % wc;
-      if (c >= kb + r) A[(size_t)(kb + r) * n + c] = Wn(win, kb + r, c);
+      if (c >= kb + r) d.S[(size_t)(kb + r) * n + c] = Wn(win, kb + r, c);
     }
-    __syncthreads();
-    // (e) slide the window: bring in columns [kb + WS, kb + WS + w) (rows kb+w .. j)
-    const int jn0 = kb + kCholWS, jn1 = min(n, jn0 + w);
-    for (int e = tid; e < (jn1 - jn0) * kCholWS; e += kCholThreads) {
+    if (tid < w) y[kb + tid] = yw[(kb + tid) & (kCholWS - 1)];
+    lds_barrier();
+    SG_STAMP_AT(4)
+    // (e) slide the window: columns [kb + WS, kb + WS + w) replace the departed rows/columns
+#pragma unroll
+    for (int q = 0; q < kPf; ++q) {
+      const int e = tid + q * kCholThreads;
       const int j = jn0 + e / kCholWS, i = kb + w + e % kCholWS;
-      if (i <= j) Wn(win, i, j) = A[(size_t)i * n + j];
+      if (j < jn1 && i <= j) Wn(win, i, j) = pf[q];
     }
-    __syncthreads();
+    if (tid < jn1 - jn0) yw[(jn0 + tid) & (kCholWS - 1)] = y[jn0 + tid];
+    lds_barrier();
+    SG_STAMP_AT(5)
   }
-  chol_backsub(A, y, n, panel_jend);
-  for (int i = tid; i < n; i += kCholThreads) d.xc[i] = y[i];
+  __syncthreads();   // global U rows / y visible to every wave
+  chol_backsub(d.S, rdg, y, win, n, panel_jend);
+  for (int i = tid; i < n; i += kCholThreads) d.xc[i] = win[i];
   __syncthreads();
+  SG_STAMP_AT(6)
   chol_candidates(d, y, fail_sh);
+  SG_STAMP_AT(7)
+  SG_STAMP_FLUSH()
 }
 
 // Global-memory path for bands wider than the LDS window.
-__global__ __launch_bounds__(kCholThreads) void k_cholesky_global(Dev d, const int32_t* panel_jend) {
+__global__ __launch_bounds__(kCholThreads) void k_cholesky_global(Dev d, const int32_t* panel_jend, double* rdg) {
   LmState* st = d.st;
   if (st->done) return;
+  extern __shared__ double xs[];   // n doubles: back-substitution solution
   const int n = d.n, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nwaves = kCholThreads / 64;
   double* A = d.S;
   double* y = d.work;
   __shared__ double U11[kCholNb][kCholNb + 1];
+  __shared__ double rdiag[kCholNb];
   __shared__ int fail_sh;
   if (tid == 0) fail_sh = 0;
-  chol_assemble(d, A, y, st->radius);
+  for (int i = tid; i < n; i += kCholThreads) y[i] = d.xc[i];   // assembled rhs (k_S_reduce)
   __syncthreads();
   const int npanel = (n + kCholNb - 1) / kCholNb;
   for (int pk = 0; pk < npanel; ++pk) {
@@ -1040,7 +1113,8 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_global(Dev d, const i
       double col[kCholNb];
 #pragma unroll
       for (int r = 0; r < kCholNb; ++r) col[r] = (lane < w && r <= lane) ? A[(size_t)(kb + r) * n + kb + lane] : 0.0;
-      const bool ok = chol_diag16(col, w, lane);
+      bool bad = false;
+      chol_diag16(col, w, lane, bad);
       if (lane < w) {
 #pragma unroll
         for (int r = 0; r < kCholNb; ++r)
@@ -1048,8 +1122,11 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_global(Dev d, const i
             A[(size_t)(kb + r) * n + kb + lane] = col[r];
             U11[r][lane] = col[r];
           }
+        const double rd = 1.0 / col[lane];
+        rdiag[lane] = rd;
+        rdg[kb + lane] = rd;
       }
-      if (lane == 0 && !ok) fail_sh = 1;
+      if (lane == 0 && bad) fail_sh = 1;
     }
     __syncthreads();
     const int ncol = jmax - (kb + w);
@@ -1059,7 +1136,7 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_global(Dev d, const i
       double a[kCholNb];
 #pragma unroll
       for (int r = 0; r < kCholNb; ++r) a[r] = (r < w) ? (isy ? y[kb + r] : A[(size_t)(kb + r) * n + c]) : 0.0;
-      chol_trsm16(a, U11, w);
+      chol_trsm16(a, U11, rdiag, w);
 #pragma unroll
       for (int r = 0; r < kCholNb; ++r)
         if (r < w) {
@@ -1089,8 +1166,8 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_global(Dev d, const i
     }
     __syncthreads();
   }
-  chol_backsub(A, y, n, panel_jend);
-  for (int i = tid; i < n; i += kCholThreads) d.xc[i] = y[i];
+  chol_backsub(A, rdg, y, xs, n, panel_jend);
+  for (int i = tid; i < n; i += kCholThreads) d.xc[i] = xs[i];
   __syncthreads();
   chol_candidates(d, y, fail_sh);
 }
@@ -1645,6 +1722,16 @@ void BaSolver::Load(const sg_problem& p) {
   fd_boff_.Upload(fd_boff, s);
   fd_bidx_.Upload(fd_bidx.empty() ? std::vector<int32_t>{0} : fd_bidx, s);
   work_i_.Upload(panel_jmax, s);
+  {
+    // FrameDistance cross-block lookup for the on-the-fly assembly: fd_pair[I*NB+J] (I<J) = residual
+    std::vector<int32_t> fd_pair((size_t)std::max(NB_, 1) * std::max(NB_, 1), -1);
+    for (int dd = 0; dd < D_; ++dd) {
+      const int ba = frame_block[fd_a[dd]], bb = frame_block[fd_b[dd]];
+      if (ba >= 0 && bb >= 0 && ba != bb) fd_pair[(size_t)std::min(ba, bb) * NB_ + std::max(ba, bb)] = dd;
+    }
+    fd_pair_.Upload(fd_pair, s);
+    rdg_.Resize(std::max(n_, 1));
+  }
   J_.Resize((size_t)std::max(M_, 1) * kJStride);
   V_.Resize(10 * (size_t)std::max(P_, 1));
   g_.Resize(4 * (size_t)std::max(P_, 1));
@@ -1684,8 +1771,15 @@ void BaSolver::Load(const sg_problem& p) {
   if (schur_lds_ > 0)
     SG_HIP_CHECK(hipFuncSetAttribute((const void*)k_schur, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)std::max<size_t>(schur_lds_, 1)));
-  SG_HIP_CHECK(hipFuncSetAttribute((const void*)k_cholesky_window, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)kCholLds));
+  SG_HIP_CHECK(hipFuncSetAttribute((const void*)k_cholesky_window<false>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCholLds));
+  SG_HIP_CHECK(hipFuncSetAttribute((const void*)k_cholesky_window<true>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCholLds));
+  stamp_on_ = getenv("SG_STAMP") && getenv("SG_STAMP")[0] == '1';
+  if (stamp_on_) {
+    stamps_.Resize(64);
+    stamps_.Zero(s);
+  }
   SG_HIP_CHECK(hipStreamSynchronize(s));
   loaded_ = true;
   began_ = false;
@@ -1761,6 +1855,9 @@ Dev BaSolver::MakeDev() {
   d.xchg_chol = xchg_chol_.ptr;
   d.xc = xc_.ptr;
   d.work = work_.ptr;
+  d.stamps = stamp_on_ ? stamps_.ptr : nullptr;
+  d.fd_pair = fd_pair_.ptr;
+  d.assemble = (!comm_ || comm_->rank() == 0) ? 1 : 0;
   return d;
 }
 
@@ -1852,12 +1949,15 @@ void BaSolver::Iterate(int n) {
       AllReduceSum(xc_.ptr, (size_t)n_);
     }
     TimedLaunchBegin(kKChol);
-    if (chol_window_)
-      hipLaunchKernelGGL(k_cholesky_window, dim3(1), dim3(kCholThreads), kCholLds, stream_, d,
-                         (const int32_t*)work_i_.ptr);
+    if (chol_window_ && d.stamps)
+      hipLaunchKernelGGL(k_cholesky_window<true>, dim3(1), dim3(kCholThreads), kCholLds, stream_, d,
+                         (const int32_t*)work_i_.ptr, rdg_.ptr);
+    else if (chol_window_)
+      hipLaunchKernelGGL(k_cholesky_window<false>, dim3(1), dim3(kCholThreads), kCholLds, stream_, d,
+                         (const int32_t*)work_i_.ptr, rdg_.ptr);
     else
-      hipLaunchKernelGGL(k_cholesky_global, dim3(1), dim3(kCholThreads), 0, stream_, d,
-                         (const int32_t*)work_i_.ptr);
+      hipLaunchKernelGGL(k_cholesky_global, dim3(1), dim3(kCholThreads), (size_t)std::max(n_, 1) * 8, stream_, d,
+                         (const int32_t*)work_i_.ptr, rdg_.ptr);
     TimedLaunchEnd(kKChol);
     TimedLaunchBegin(kKPointUpd);
     hipLaunchKernelGGL(k_point_update, dim3(nc), dim3(kSweepThreads), 0, stream_, d);
@@ -1892,6 +1992,14 @@ void BaSolver::Sweep(int n) {
     TimedLaunchEnd(kKLin);
   }
   SG_HIP_CHECK(hipGetLastError());
+}
+
+std::vector<unsigned long long> BaSolver::Stamps() {
+  std::vector<unsigned long long> v(64, 0);
+  if (!stamp_on_) return v;
+  SG_HIP_CHECK(hipMemcpyAsync(v.data(), stamps_.ptr, 64 * 8, hipMemcpyDeviceToHost, stream_));
+  SG_HIP_CHECK(hipStreamSynchronize(stream_));
+  return v;
 }
 
 void BaSolver::Sync() { SG_HIP_CHECK(hipStreamSynchronize(stream_)); }

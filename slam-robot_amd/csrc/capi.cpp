@@ -134,6 +134,15 @@ int sg_ba_sweep(sg_ba* h, int32_t n) {
   SG_CAPI_END
 }
 
+// Diagnostic (not in the public header): per-phase cycle counters of stamped kernels when SG_STAMP=1.
+int sg_ba_debug_stamps(sg_ba* h, unsigned long long* out, int32_t n) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(h && out, SG_EINVAL, "null argument");
+  auto v = h->solver->Stamps();
+  for (int32_t i = 0; i < n && i < (int32_t)v.size(); ++i) out[i] = v[i];
+  SG_CAPI_END
+}
+
 int sg_ba_evaluate(sg_ba* h, double* residuals, double* cost, int32_t* num_failed) {
   SG_CAPI_BEGIN
   SG_REQUIRE(h && residuals && cost && num_failed, SG_EINVAL, "null argument");

@@ -40,7 +40,8 @@ def _solve_both(oracle_lib, pa, options=None, nthreads=1):
 
 def _assert_same_minimum(oracle_lib, pg, sg, po, so):
     assert sg["ok"] == so["ok"] == 1
-    assert sg["termination"] == so["termination"]
+    assert sg["termination"] == so["termination"] or {sg["termination"], so["termination"]} <= {
+        "FUNCTION_TOLERANCE", "PARAMETER_TOLERANCE", "GRADIENT_TOLERANCE"}
     assert abs(sg["initial_cost"] - so["initial_cost"]) <= 1e-10 * so["initial_cost"]
     assert abs(sg["fixed_cost"] - so["fixed_cost"]) <= 1e-10 * max(so["fixed_cost"], 1.0)
     assert abs(sg["final_cost"] - so["final_cost"]) <= 1e-6 * so["final_cost"]
@@ -110,9 +111,31 @@ def test_wide_points_and_edge_structure(gpu_lib, oracle_lib):
     m.obs_disabled[rng.random(m.num_obs) < 0.05] = 1
     m.obs_disabled[m.obs_frame == 30] = 1
     m.point_uncertainty[:] = 1.0
+    # this scene has weakly constrained directions (a skipped frame's translation on the FrameDistance
+    # sphere, thin point tracks): with the default function tolerance the LM stops at a trajectory-dependent
+    # point along them, so both solvers run to tight tolerances here and must meet at the same minimum
+    tight = default_solver_options(function_tolerance=1e-13, parameter_tolerance=1e-13, max_num_iterations=200)
     for solve, present in ((38, 40), (9, 14), (20, 40)):
         pa = ba.problem_from_map_frames(m, solve, present, 2.0)
-        _assert_same_minimum(oracle_lib, *_solve_both(oracle_lib, pa))
+        _assert_same_minimum(oracle_lib, *_solve_both(oracle_lib, pa, tight))
+
+
+@pytest.mark.parametrize("solve,present", [(38, 40), (9, 14), (20, 40)])
+def test_wide_scene_first_steps_match_oracle(gpu_lib, oracle_lib, solve, present):
+    """Two LM iterations on the edge-structure scene: the device step (assembly of blockdiag(U), FrameDistance
+    blocks and damping into S, banded Cholesky, back substitution) matches the oracle's dense solve."""
+    m = make_scene(num_frames=40, num_points=400, seed=21, run_max=40)
+    rng = np.random.default_rng(0)
+    m.obs_disabled[rng.random(m.num_obs) < 0.05] = 1
+    m.obs_disabled[m.obs_frame == 30] = 1
+    m.point_uncertainty[:] = 1.0
+    pa = ba.problem_from_map_frames(m, solve, present, 2.0)
+    o = default_solver_options(max_num_iterations=2)
+    pg, sg, po, so = _solve_both(oracle_lib, pa, o)
+    assert sg["num_successful_steps"] == so["num_successful_steps"]
+    assert abs(sg["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"]
+    np.testing.assert_allclose(pg.t, po.t, atol=1e-6)
+    np.testing.assert_allclose(pg.q, po.q, atol=1e-9)
 
 
 def test_behind_camera_at_start_is_a_numerical_failure(gpu_lib, oracle_lib):
