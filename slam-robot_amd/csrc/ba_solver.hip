@@ -751,6 +751,7 @@ __global__ __launch_bounds__(256) void k_S_reduce(Dev d) {
 // window) fits a 128x128 fp64 LDS window that slides down the diagonal; trailing updates run as
 // v_mfma_f64_16x16x4 tiles.  Bands wider than the window take the global-memory path.
 constexpr int kCholWS = 128;
+constexpr int kPanelWaves = 3;   // 16 + 3 x 48 >= kCholWS columns
 constexpr int kCholLd = kCholWS + 1;
 constexpr size_t kCholLds = (size_t)kCholWS * kCholLd * sizeof(double);
 typedef double f64x4 __attribute__((ext_vector_type(4)));
@@ -764,6 +765,14 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
   const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
   const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
   return __hiloint2double(hi, lo);
+}
+
+// The lane id through an opaque move: comparisons against it inside a loop are not hoisted out as
+// loop-invariant 64-bit lane masks (which would otherwise pile up in SGPRs and spill).
+__device__ __forceinline__ int opaque_lane() {
+  int v = __lane_id();
+  asm volatile("v_mov_b32 %0, %0" : "+v"(v));
+  return v;
 }
 
 // LDS-only workgroup barrier: waits for this wave's LDS traffic, not for outstanding global loads or
@@ -854,7 +863,7 @@ __device__ __noinline__ void chol_backsub(const double* A, const double* rdg, do
 }
 
 // Candidate camera poses x+ = Plus(x, -S x_c) for every frame, FrameDistance model / candidate terms.
-__device__ __noinline__ void chol_candidates(const Dev& d, const double* y, int fail) {
+__device__ __forceinline__ void chol_candidates(const Dev& d, const double* y, int fail) {
   const LmState* st = d.st;
   __shared__ double red[kCholThreads / 64];
   const int tid = threadIdx.x;
@@ -924,6 +933,7 @@ __device__ __noinline__ void chol_candidates(const Dev& d, const double* y, int 
 // in registers (a global read-modify-write here would wait on every outstanding load) and adds them to
 // d.stamps once at the end.
 #define SG_STAMP_AT(slot)                                                        \
+  asm volatile("" ::: "memory");  /* phase boundary: same code motion with or without stamps */ \
   if (kStamp && threadIdx.x == 0) {                                               \
     const unsigned long long now_ = __builtin_amdgcn_s_memtime();                 \
     stamp_acc[slot] += now_ - last_stamp;                                         \
@@ -944,9 +954,8 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
   LmState* st = d.st;
   if (st->done) return;
   extern __shared__ double win[];
-  __shared__ double U11[kCholNb][kCholNb + 1];
-  __shared__ double rdiag[kCholNb];
   __shared__ double yw[kCholWS];
+  __shared__ double prow[kPanelWaves][kCholNb];
   __shared__ int fail_sh;
   const int n = d.n, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nwaves = kCholThreads / 64;
@@ -982,47 +991,81 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
       const bool in = j < jn1 && i <= j;
       pf[q] = d.S[in ? (size_t)i * n + j : 0];   // branch-free: the loads stay in flight across phases
     }
-    // (a) diagonal block, one wave
-    if (wave == 0) {
-      double col[kCholNb];
+    const double pfy = d.xc[min(jn0 + tid, n - 1)];   // rhs entries of the incoming rows (unmodified yet)
+    // (a) panel factorisation by kPanelWaves waves: rows kb..kb+15 of the band.  Every panel wave holds
+    // the 16 diagonal-block columns in lanes 0..15 (factored redundantly, so no cross-wave sync) and 48
+    // off-diagonal columns in lanes 16..63; the diagonal block, the TRSM of the off-diagonal columns and
+    // the rhs forward step run as one right-looking pass.  Row j of the diagonal block is broadcast
+    // through a per-wave LDS row (one wave: the LDS queue orders write before read, no barrier).  Rows
+    // past n are padded with identity so the unrolled loop has no branches.  The finished rows go from
+    // registers to LDS (for the trailing update), to global memory (back substitution) and to the rhs.
+    if (wave < kPanelWaves) {
+      const int lane = opaque_lane();
+      const int slot = lane < kCholNb ? lane : kCholNb + (64 - kCholNb) * wave + (lane - kCholNb);
+      const int c = kb + slot;
+      const bool v = slot < kCholWS && c < jend;
+      double* prw = prow[wave];
+      double ca[kCholNb], yv[kCholNb];
 #pragma unroll
-      for (int r = 0; r < kCholNb; ++r) col[r] = (lane < w && r <= lane) ? Wn(win, kb + r, kb + lane) : 0.0;
+      for (int r = 0; r < kCholNb; ++r) {
+        const bool real = r < w;
+        ca[r] = (real && v && r <= slot) ? Wn(win, kb + r, c) : ((!real && slot == r) ? 1.0 : 0.0);
+        yv[r] = real ? yw[(kb + r) & (kCholWS - 1)] : 0.0;
+      }
       bool bad = false;
-      chol_diag16(col, w, lane, bad);
-      if (lane < w) {
+      SG_STAMP_AT(1)
+#pragma unroll
+      for (int j = 0; j < kCholNb; ++j) {
+        if (lane < kCholNb) prw[lane] = ca[j];
+        double u[kCholNb];
+#pragma unroll
+        for (int r = j; r < kCholNb; ++r) u[r] = prw[r];
+        const double piv = u[j];
+        bad |= !(piv > 0.0);
+        double inv = __builtin_amdgcn_rsq(piv);
+        inv = inv * (1.5 - 0.5 * piv * inv * inv);   // two Newton steps: full fp64 1/sqrt
+        inv = inv * (1.5 - 0.5 * piv * inv * inv);
+        ca[j] *= inv;
+        yv[j] *= inv;
+        if (wave == 0 && lane == 0) rdg[kb + j] = inv;   // padded rows (j >= w) land in rdg's padding
+#pragma unroll
+        for (int r = j + 1; r < kCholNb; ++r) {
+          const double ur = u[r] * inv;   // U[j][r], rounded exactly as lane r rounds its own ca[j]
+          ca[r] -= ur * ca[j];
+          yv[r] -= ur * yv[j];
+        }
+        // materialise this step's updates here (otherwise they are sunk into later steps and the
+        // deferred multipliers spill)
+#pragma unroll
+        for (int r = j; r < kCholNb; ++r) {
+          asm volatile("" : "+v"(ca[r]));
+          asm volatile("" : "+v"(yv[r]));
+        }
+      }
+      SG_STAMP_AT(3)
+      // rhs of the trailing rows: y_c -= sum_r U[r][c] y_r; trailing columns' panel rows -> LDS
+      const bool trail = v && lane >= kCholNb;
+      const bool own = v && (lane >= kCholNb || wave == 0);   // diagonal block written by wave 0 only
+      double s0 = 0.0;
+#pragma unroll
+      for (int r = 0; r < kCholNb; ++r) s0 += ca[r] * yv[r];
+      if (trail) yw[c & (kCholWS - 1)] -= s0;
+#pragma unroll
+      for (int r = 0; r < kCholNb; ++r) {
+        if (r < w) {
+          if (trail) Wn(win, kb + r, c) = ca[r];
+          if (own && r <= slot) d.S[(size_t)(kb + r) * n + c] = ca[r];
+        }
+      }
+      if (wave == 0 && lane == 0) {
 #pragma unroll
         for (int r = 0; r < kCholNb; ++r)
-          if (r <= lane) {
-            Wn(win, kb + r, kb + lane) = col[r];
-            U11[r][lane] = col[r];
-          }
-        const double rd = 1.0 / col[lane];
-        rdiag[lane] = rd;
-        rdg[kb + lane] = rd;
+          if (r < w) y[kb + r] = yv[r];
+        if (bad) fail_sh = 1;
       }
-      if (lane == 0 && bad) fail_sh = 1;
     }
     lds_barrier();
     SG_STAMP_AT(2)
-    // (b) panel TRSM on columns [kb+w, jend) and on the rhs ring
-    const int ncol = jend - (kb + w);
-    for (int ci = tid; ci < ncol + 1; ci += kCholThreads) {
-      const bool isy = ci == ncol;
-      const int c = kb + w + ci;
-      double a[kCholNb];
-#pragma unroll
-      for (int r = 0; r < kCholNb; ++r)
-        a[r] = (r < w) ? (isy ? yw[(kb + r) & (kCholWS - 1)] : Wn(win, kb + r, c)) : 0.0;
-      chol_trsm16(a, U11, rdiag, w);
-#pragma unroll
-      for (int r = 0; r < kCholNb; ++r)
-        if (r < w) {
-          if (isy) yw[(kb + r) & (kCholWS - 1)] = a[r];
-          else Wn(win, kb + r, c) = a[r];
-        }
-    }
-    lds_barrier();
-    SG_STAMP_AT(3)
     // (c) trailing update A22 -= U12^T U12 on the band, 16x16 MFMA tiles (upper tiles only), rhs update
     const int m = jend - (kb + w);
     const int T = (m + 15) >> 4;
@@ -1052,20 +1095,6 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
         if (row < jend && col < jend && row <= col) Wn(win, row, col) = acc[qq];
       }
     }
-    for (int i = kb + w + tid; i < jend; i += kCholThreads) {
-      double s = 0.0;
-#pragma unroll
-      for (int r = 0; r < kCholNb; ++r)
-        if (r < w) s += Wn(win, kb + r, i) * yw[(kb + r) & (kCholWS - 1)];
-      yw[i & (kCholWS - 1)] -= s;
-    }
-    // finished panel rows and the forward solution of these rows -> global (no wait)
-    const int wc = jend - kb;
-    for (int e = tid; e < w * wc; e += kCholThreads) {
-      const int r = e / wc, c = kb + e % wc;
-      if (c >= kb + r) d.S[(size_t)(kb + r) * n + c] = Wn(win, kb + r, c);
-    }
-    if (tid < w) y[kb + tid] = yw[(kb + tid) & (kCholWS - 1)];
     lds_barrier();
     SG_STAMP_AT(4)
     // (e) slide the window: columns [kb + WS, kb + WS + w) replace the departed rows/columns
@@ -1075,7 +1104,7 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
       const int j = jn0 + e / kCholWS, i = kb + w + e % kCholWS;
       if (j < jn1 && i <= j) Wn(win, i, j) = pf[q];
     }
-    if (tid < jn1 - jn0) yw[(jn0 + tid) & (kCholWS - 1)] = y[jn0 + tid];
+    if (tid < jn1 - jn0) yw[(jn0 + tid) & (kCholWS - 1)] = pfy;
     lds_barrier();
     SG_STAMP_AT(5)
   }
@@ -1730,7 +1759,7 @@ void BaSolver::Load(const sg_problem& p) {
       if (ba >= 0 && bb >= 0 && ba != bb) fd_pair[(size_t)std::min(ba, bb) * NB_ + std::max(ba, bb)] = dd;
     }
     fd_pair_.Upload(fd_pair, s);
-    rdg_.Resize(std::max(n_, 1));
+    rdg_.Resize((size_t)std::max(n_, 1) + kCholNb);   // + padding rows of the last panel
   }
   J_.Resize((size_t)std::max(M_, 1) * kJStride);
   V_.Resize(10 * (size_t)std::max(P_, 1));
