@@ -39,6 +39,27 @@ __device__ __forceinline__ double wave_sum(double v) {
   for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
   return v;
 }
+// Full-wave sum by DPP (quad perms, half-row and row mirrors) and four readlanes: ~10x faster than the
+// ds_bpermute butterfly.  All 64 lanes must be active.  Fixed order, so deterministic; the result is
+// wave-uniform.
+template <int kCtrl>
+__device__ __forceinline__ double dpp_d(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), kCtrl, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), kCtrl, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double readlane_dd(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double wave_sum_full(double v) {
+  v += dpp_d<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_d<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_d<0x141>(v);   // row_half_mirror
+  v += dpp_d<0x140>(v);   // row_mirror: every lane holds its 16-lane row sum
+  return (readlane_dd(v, 0) + readlane_dd(v, 16)) + (readlane_dd(v, 32) + readlane_dd(v, 48));
+}
 __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) v = fmax(v, __shfl_xor(v, m));
@@ -752,6 +773,7 @@ __global__ __launch_bounds__(256) void k_S_reduce(Dev d) {
 // v_mfma_f64_16x16x4 tiles.  Bands wider than the window take the global-memory path.
 constexpr int kCholWS = 128;
 constexpr int kPanelWaves = 3;   // 16 + 3 x 48 >= kCholWS columns
+constexpr int kJendSh = 512;     // panel band ends cached in LDS (n <= 8192)
 constexpr int kCholLd = kCholWS + 1;
 constexpr size_t kCholLds = (size_t)kCholWS * kCholLd * sizeof(double);
 typedef double f64x4 __attribute__((ext_vector_type(4)));
@@ -944,6 +966,64 @@ __device__ __forceinline__ void chol_candidates(const Dev& d, const double* y, i
     for (int s_ = 0; s_ < 8; ++s_) d.stamps[s_] += stamp_acc[s_];                 \
   }
 
+// Back substitution of the window path from x_p = z_p - W_p x_rest (W = U11^-1 U12 and z = U11^-1 y per
+// panel, stored over the U rows of A and over y): one mat-vec per panel, two rows per wave, the next
+// panel's W loads in flight during the current panel's reduction.
+__device__ __forceinline__ void chol_backsub_w(const double* Wm, const double* z, double* xs, int n,
+                                               const int* jend_sh, const int32_t* panel_jend) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  static_assert(kCholThreads / 64 * 2 == kCholNb, "two panel rows per wave");
+  const int npanel = (n + kCholNb - 1) / kCholNb;
+  auto load = [&](int pk, double (&wv)[2][2], double (&zv)[2], int& jend) {
+    const int kb = pk * kCholNb;
+    jend = jend_sh[pk];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int r = kb + 2 * wave + h;
+      const bool rin = r < n;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int c = kb + kCholNb + lane + 64 * q;
+        wv[h][q] = (rin && c < jend) ? Wm[(size_t)r * n + c] : 0.0;
+      }
+      zv[h] = rin ? z[r] : 0.0;
+    }
+  };
+  double wv[2][2], zv[2];
+  int jend;
+  load(npanel - 1, wv, zv, jend);
+  for (int pk = npanel - 1; pk >= 0; --pk) {
+    const int kb = pk * kCholNb;
+    double wn[2][2] = {{0.0, 0.0}, {0.0, 0.0}}, zn[2] = {0.0, 0.0};
+    int jn = 0;
+    if (pk > 0) load(pk - 1, wn, zn, jn);
+    double sv[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      double acc = 0.0;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int c = kb + kCholNb + lane + 64 * q;
+        acc += wv[h][q] * (c < jend ? xs[c] : 0.0);
+      }
+      sv[h] = wave_sum_full(acc);
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        if (kb + 2 * wave + h < n) xs[kb + 2 * wave + h] = zv[h] - sv[h];
+    }
+    lds_barrier();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      zv[h] = zn[h];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) wv[h][q] = wn[h][q];
+    }
+    jend = jn;
+  }
+}
+
 // Window path: the active band lives in LDS (132 KiB) together with the rhs ring; finished panel rows and
 // 1/U_jj go to global memory for the back substitution.  Barriers between phases are LDS-only, so the
 // global writes and the prefetch of the next window columns overlap the factorisation.
@@ -956,6 +1036,9 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
   extern __shared__ double win[];
   __shared__ double yw[kCholWS];
   __shared__ double prow[kPanelWaves][kCholNb];
+  __shared__ double pinv[kPanelWaves][kCholNb];                // 1/U_jj of the current panel
+  __shared__ double u11w[kPanelWaves][kCholNb * kCholNb];      // U11 columns of the current panel
+  __shared__ int jend_sh[kJendSh];
   __shared__ int fail_sh;
   const int n = d.n, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nwaves = kCholThreads / 64;
@@ -972,15 +1055,16 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
     const int i = e / n0, j = e % n0;
     if (i <= j) Wn(win, i, j) = d.S[(size_t)i * n + j];
   }
+  const int npanel = (n + kCholNb - 1) / kCholNb;
+  for (int p = tid; p < npanel; p += kCholThreads) jend_sh[p] = panel_jend[p];   // npanel <= kJendSh
   __syncthreads();
   SG_STAMP_AT(0)
-  const int npanel = (n + kCholNb - 1) / kCholNb;
   const int li = lane & 15, lk = lane >> 4;
   constexpr int kPf = kCholNb * kCholWS / kCholThreads;   // prefetched window elements per thread
   for (int pk = 0; pk < npanel; ++pk) {
     const int kb = pk * kCholNb;
     const int w = min(kCholNb, n - kb);
-    const int jend = panel_jend[pk];
+    const int jend = jend_sh[pk];
     // prefetch the columns this panel's slide brings in: j in [kb+WS, kb+WS+w), rows kb+w..j
     const int jn0 = kb + kCholWS, jn1 = min(n, jn0 + w);
     double pf[kPf];
@@ -1027,7 +1111,7 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
         inv = inv * (1.5 - 0.5 * piv * inv * inv);
         ca[j] *= inv;
         yv[j] *= inv;
-        if (wave == 0 && lane == 0) rdg[kb + j] = inv;   // padded rows (j >= w) land in rdg's padding
+        if (lane == 0) pinv[wave][j] = inv;
 #pragma unroll
         for (int r = j + 1; r < kCholNb; ++r) {
           const double ur = u[r] * inv;   // U[j][r], rounded exactly as lane r rounds its own ca[j]
@@ -1045,22 +1129,38 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
       SG_STAMP_AT(3)
       // rhs of the trailing rows: y_c -= sum_r U[r][c] y_r; trailing columns' panel rows -> LDS
       const bool trail = v && lane >= kCholNb;
-      const bool own = v && (lane >= kCholNb || wave == 0);   // diagonal block written by wave 0 only
       double s0 = 0.0;
 #pragma unroll
       for (int r = 0; r < kCholNb; ++r) s0 += ca[r] * yv[r];
       if (trail) yw[c & (kCholWS - 1)] -= s0;
 #pragma unroll
-      for (int r = 0; r < kCholNb; ++r) {
-        if (r < w) {
-          if (trail) Wn(win, kb + r, c) = ca[r];
-          if (own && r <= slot) d.S[(size_t)(kb + r) * n + c] = ca[r];
-        }
+      for (int r = 0; r < kCholNb; ++r)
+        if (r < w && trail) Wn(win, kb + r, c) = ca[r];
+      // back-substitution operands: W = U11^-1 U12 (trailing lanes) and z = U11^-1 y (diagonal lanes),
+      // so the back substitution is one mat-vec per panel, x_p = z_p - W_p x_rest, with no serial
+      // triangle.  U11 columns go through this wave's LDS copy (lane k writes column k).
+      double* u11 = u11w[wave];
+      if (lane < kCholNb) {
+#pragma unroll
+        for (int r = 0; r < kCholNb; ++r) u11[lane * kCholNb + r] = ca[r];
       }
+      double t[kCholNb];
+#pragma unroll
+      for (int r = 0; r < kCholNb; ++r) t[r] = lane < kCholNb ? yv[r] : ca[r];
+#pragma unroll
+      for (int k = kCholNb - 1; k >= 0; --k) {
+        t[k] *= pinv[wave][k];
+#pragma unroll
+        for (int r = 0; r < k; ++r) t[r] -= u11[k * kCholNb + r] * t[k];
+        asm volatile("" : "+v"(t[k]));
+      }
+#pragma unroll
+      for (int r = 0; r < kCholNb; ++r)
+        if (r < w && trail) d.S[(size_t)(kb + r) * n + c] = t[r];
       if (wave == 0 && lane == 0) {
 #pragma unroll
         for (int r = 0; r < kCholNb; ++r)
-          if (r < w) y[kb + r] = yv[r];
+          if (r < w) y[kb + r] = t[r];
         if (bad) fail_sh = 1;
       }
     }
@@ -1095,9 +1195,9 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
         if (row < jend && col < jend && row <= col) Wn(win, row, col) = acc[qq];
       }
     }
-    lds_barrier();
     SG_STAMP_AT(4)
-    // (e) slide the window: columns [kb + WS, kb + WS + w) replace the departed rows/columns
+    // (e) slide the window: columns [kb + WS, kb + WS + w) replace the departed rows/columns.  Disjoint
+    // from everything the trailing update touches (columns < jend <= kb + WS), so no barrier between.
 #pragma unroll
     for (int q = 0; q < kPf; ++q) {
       const int e = tid + q * kCholThreads;
@@ -1108,12 +1208,16 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
     lds_barrier();
     SG_STAMP_AT(5)
   }
-  __syncthreads();   // global U rows / y visible to every wave
-  chol_backsub(d.S, rdg, y, win, n, panel_jend);
-  for (int i = tid; i < n; i += kCholThreads) d.xc[i] = win[i];
+  __syncthreads();   // global W rows / z visible to every wave
+  double* xs = win;  // the window is free now: the solution lives in LDS
+  chol_backsub_w(d.S, y, xs, n, jend_sh, panel_jend);
+  for (int i = tid; i < n; i += kCholThreads) {
+    d.xc[i] = xs[i];
+    y[i] = xs[i];
+  }
   __syncthreads();
   SG_STAMP_AT(6)
-  chol_candidates(d, y, fail_sh);
+  chol_candidates(d, xs, fail_sh);
   SG_STAMP_AT(7)
   SG_STAMP_FLUSH()
 }
@@ -1714,7 +1818,7 @@ void BaSolver::Load(const sg_problem& p) {
     jmax = std::min(jmax, n_);
     panel_jmax[pk] = std::min(n_, (jmax + kCholNb - 1) / kCholNb * kCholNb);   // band end, 16-aligned
   }
-  chol_window_ = true;
+  chol_window_ = npanel <= kJendSh;   // band ends cached in LDS
   for (int pk = 0; pk < npanel; ++pk)
     if (panel_jmax[pk] - pk * kCholNb > kCholWS) chol_window_ = false;
   // device uploads
