@@ -49,6 +49,7 @@ def lib():
         L.or_solve.argtypes = [C.POINTER(SgProblem), C.POINTER(SgSolverOptions), C.c_int,
                                C.POINTER(SgSolverSummary)]
         L.or_evaluate.argtypes = [C.POINTER(SgProblem), _dp, _dp, _ip]
+        L.or_reduced_system.argtypes = [C.POINTER(SgProblem), C.c_double, C.c_int, C.c_int, _dp, _dp, C.c_int]
         L.or_project_jet.argtypes = [_dp, _dp, _dp, _dp, _dp, _dp]
         L.or_project.argtypes = [C.c_int, _dp, _dp, _dp, _dp, _dp, _ip]
         L.or_quat_plus.argtypes = [_dp, _dp, _dp]
@@ -107,6 +108,20 @@ def evaluate(pa: ProblemArrays):
     ps = pa.struct()
     lib().or_evaluate(C.byref(ps), r.ctypes.data_as(_dp), C.byref(cost), C.byref(nfail))
     return r.reshape(-1, 2), cost.value, nfail.value
+
+
+def reduced_system(pa: ProblemArrays, radius: float, camera_terms: bool = True, nthreads: int = 1):
+    """Unscaled reduced camera system (S, b) at the current state: points damped by diag/radius, cameras
+    undamped; camera_terms=False gives one landmark shard's share of the multi-GPU all-reduce."""
+    nmax = 6 * pa.num_frames + 7 * (len(pa.k) // 7)
+    S = np.zeros(nmax * nmax)
+    b = np.zeros(nmax)
+    ps = pa.struct()
+    n = lib().or_reduced_system(C.byref(ps), radius, int(camera_terms), nthreads, S.ctypes.data_as(_dp),
+                                b.ctypes.data_as(_dp), nmax)
+    if n < 0:
+        raise RuntimeError("reduced system: evaluation failed")
+    return S[:n * n].reshape(n, n), b[:n]
 
 
 def project_jet(q, t, k, X):

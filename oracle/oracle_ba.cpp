@@ -297,6 +297,11 @@ class Solver {
   // Evaluate reprojection residuals at the current state (for parity tests): uncorrected r, cost.
   bool EvaluateResiduals(double* r_out, double* cost_out, int* nfail);
 
+  // Unscaled reduced camera system at the current state, points damped by diag/radius, cameras
+  // undamped: S (nF x nF) and b.  camera_terms = 0 leaves out the FrameDistance / CameraStabilization
+  // rows, giving one landmark shard's contribution to the multi-GPU all-reduce.
+  bool ReducedSystem(double radius, bool camera_terms, double* S_out, double* b_out);
+
   const std::vector<double>& scale() const { return scale_; }
   int nF() const { return nF_; }
   int nE() const { return nE_; }
@@ -344,6 +349,11 @@ class Solver {
   double ModelCostChange(const std::vector<double>& step) const;
   void Plus(const State& s, const std::vector<double>& delta, State* out) const;
   void Store(const State& s);
+
+  // ReducedSystem capture: when set, SolveLinear stops after assembling S and b.
+  double* cap_S_ = nullptr;
+  double* cap_b_ = nullptr;
+  bool cap_camera_terms_ = true;
 };
 
 void Solver::Layout() {
@@ -780,7 +790,8 @@ bool Solver::SolveLinear(const std::vector<double>& D2, std::vector<double>* xou
     for (int i = 0; i < n; ++i) b[i] += bp[tid][i];
   }
   // FrameDistance / CameraStabilization rows (no point block).
-  for (int d = 0; d < p.num_dist; ++d) {
+  const bool camera_terms = cap_S_ == nullptr || cap_camera_terms_;
+  for (int d = 0; d < (camera_terms ? p.num_dist : 0); ++d) {
     int cols[6];
     for (int j = 0; j < 3; ++j) {
       cols[j] = trans_col_[p.dist_frame[d]] >= 0 ? trans_col_[p.dist_frame[d]] + j : -1;
@@ -794,7 +805,7 @@ bool Solver::SolveLinear(const std::vector<double>& D2, std::vector<double>* xou
         if (cols[c] >= 0) S[(size_t)cols[a] * n + cols[c]] += J[a] * J[c];
     }
   }
-  if (p.cameras_free)
+  if (p.cameras_free && camera_terms)
     for (int cam = 0; cam < p.num_cameras; ++cam) {
       const int c0 = k_col_[cam];
       for (int i = 0; i < 7; ++i) {
@@ -805,6 +816,11 @@ bool Solver::SolveLinear(const std::vector<double>& D2, std::vector<double>* xou
         }
       }
     }
+  if (cap_S_) {
+    std::copy(S.begin(), S.end(), cap_S_);
+    std::copy(b.begin(), b.end(), cap_b_);
+    return false;
+  }
   for (int i = 0; i < n; ++i) S[(size_t)i * n + i] += D2[i];
   if (!Cholesky(S, n)) return false;
   CholSolve(S, n, b.data());
@@ -832,6 +848,22 @@ bool Solver::SolveLinear(const std::vector<double>& D2, std::vector<double>* xou
   }
   for (double v : x)
     if (!std::isfinite(v)) return false;
+  return true;
+}
+
+bool Solver::ReducedSystem(double radius, bool camera_terms, double* S_out, double* b_out) {
+  State x = Capture();
+  double cost = 0.0;
+  if (!Evaluate(x, true, &cost)) return false;
+  std::vector<double> diag, D2(nF_ + nE_, 0.0), xs;
+  SquaredColumnNorm(&diag);
+  for (int i = nF_; i < nF_ + nE_; ++i)
+    D2[i] = std::min(std::max(diag[i], opt_.o.min_lm_diagonal), opt_.o.max_lm_diagonal) / radius;
+  cap_S_ = S_out;
+  cap_b_ = b_out;
+  cap_camera_terms_ = camera_terms;
+  SolveLinear(D2, &xs);
+  cap_S_ = cap_b_ = nullptr;
   return true;
 }
 
@@ -1107,6 +1139,19 @@ int or_solve(sg_problem* p, const sg_solver_options* o, int nthreads, sg_solver_
   oracle::Solver solver(p, opt);
   solver.Solve(s);
   return 0;
+}
+
+// One landmark shard's (camera_terms = 0) or the whole problem's reduced camera system; returns its
+// dimension n (S is n x n row-major) or -1 if the evaluation fails.  nmax bounds the output arrays.
+int or_reduced_system(sg_problem* p, double radius, int camera_terms, int nthreads, double* S, double* b,
+                      int nmax) {
+  oracle::Options opt;
+  or_default_options(&opt.o);
+  opt.nthreads = nthreads;
+  oracle::Solver solver(p, opt);
+  if (solver.nF() > nmax) return -1;
+  if (!solver.ReducedSystem(radius, camera_terms != 0, S, b)) return -1;
+  return solver.nF();
 }
 
 // Corrected-free reprojection residuals (proj - pt) for every problem observation at the current state.
