@@ -224,6 +224,52 @@ int sg_slam_reproject_map(sg_slam* s, sg_map* map, double* mean);               
 int32_t sg_slam_iterations(const sg_slam* s);                                    /* slam.h:49 */
 double sg_slam_error(const sg_slam* s);                                          /* slam.h:50 */
 int sg_slam_last_summary(const sg_slam* s, sg_solver_summary* out);
+
+/* ------------------------------------------------------------------------------------------------
+ * Front end: HessianTracker (hessian.h:9-270) and the forward/backward matching step of Matcher
+ * (matcher.cpp:173-206 TrackFeature, 247-251 the 3 -> 6 level retry).  A tracker holds `max_images`
+ * device pyramids ("views", matcher.cpp:36-40); images are 8-bit, 3 channels, cv::Mat (BGR) memory order.
+ */
+typedef struct sg_tracker sg_tracker;
+
+typedef struct sg_tracker_options {
+  int32_t window;          /* patch size W: kWindowSize = 13 (matcher.cpp:27); 1..16 */
+  int32_t depth;           /* pyramid levels per image: MakePyramid(img, 6) (matcher.cpp:221); 1..8 */
+  int32_t max_iterations;  /* Track() Newton iterations: 10 (matcher.cpp:176) */
+  float threshold;         /* Track() convergence threshold: 0.001 (matcher.cpp:176) */
+  float fb_max;            /* forward/backward disagreement limit: 0.3 px (matcher.cpp:200) */
+  int32_t retry_levels;    /* levels of the retry after a failed attempt: 6 (matcher.cpp:248); 0 = none */
+  int32_t max_images;      /* pyramid slots held on the device */
+  int32_t reserved[5];
+} sg_tracker_options;
+
+void sg_tracker_options_default(sg_tracker_options* o);
+int sg_tracker_create(sg_tracker** out, const sg_tracker_options* o, const sg_device_options* dev);
+void sg_tracker_destroy(sg_tracker* t);
+
+/* MakePyramid (hessian.h:95-126) of one image into pyramid slot `slot`. */
+int sg_tracker_set_image(sg_tracker* t, int32_t slot, const uint8_t* bgr, int32_t width, int32_t height,
+                         int32_t stride);
+/* Download pyramid level `level` of slot `slot` (width*height floats). */
+int sg_tracker_get_level(sg_tracker* t, int32_t slot, int32_t level, float* out, int32_t* width,
+                         int32_t* height);
+/* GetPatch (hessian.h:54-93) at n points of one level: out[n][W*W], mean[n], sumsq[n]. */
+int sg_tracker_get_patches(sg_tracker* t, int32_t slot, int32_t level, int32_t n, const float* xy, float* out,
+                           float* mean, float* sumsq);
+/* Forward/backward tracking of n features from slot `from` to slot `to` (synchronous).  levels[i] is 3 or 6
+ * (matcher.cpp:234-236); to_xy: in = starting guess, out = the matcher's to_pt; accepted[i] = 1 if the
+ * feature matched; iterations (may be NULL) = Newton iterations spent per feature. */
+int sg_tracker_track(sg_tracker* t, int32_t from, int32_t to, int32_t n, const float* from_xy, float* to_xy,
+                     const int32_t* levels, int32_t* accepted, int32_t* iterations);
+/* Device-resident variant for throughput runs: load features once, run `repeats` asynchronous tracking
+ * passes (each restarts from the loaded starting guesses), then fetch the last pass's results. */
+int sg_tracker_load_features(sg_tracker* t, int32_t n, const float* from_xy, const float* to_xy,
+                             const int32_t* levels);
+int sg_tracker_run(sg_tracker* t, int32_t from, int32_t to, int32_t repeats);
+int sg_tracker_results(sg_tracker* t, float* to_xy, int32_t* accepted, int32_t* iterations);
+/* Kernel timing (HIP events on the tracker's stream) of the last sg_tracker_run: total ms of the
+ * tracking kernels and of the pyramid kernels of the last sg_tracker_set_image. */
+int sg_tracker_kernel_ms(sg_tracker* t, double* track_ms, double* pyramid_ms);
 int sg_slam_set_options(sg_slam* s, const sg_solver_options* o);
 
 #ifdef __cplusplus

@@ -170,3 +170,92 @@ def slam_solve_all_frames(m, range_=2.0, solve_cameras=False, options=None, nthr
     ok = lib().or_slam_solve_all_frames(C.byref(ms), range_, int(solve_cameras), C.byref(o), nthreads,
                                         C.byref(s))
     return bool(ok), s.as_dict()
+
+
+# ---------------------------------------------------------------------------------------------------
+# Front end (oracle_track.cpp): HessianTracker + forward/backward matcher, OpenCV primitives restated.
+
+_fp = C.POINTER(C.c_float)
+_i32p = C.POINTER(C.c_int32)
+_u8p = C.POINTER(C.c_uint8)
+
+
+def _trk():
+    L = lib()
+    if not getattr(L, "_trk_ready", False):
+        L.ort_make_pyramid.argtypes = [_u8p, C.c_int, C.c_int, C.c_int, C.c_int, _fp, _i32p]
+        L.ort_get_rect_subpix.argtypes = [_fp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float, _fp]
+        L.ort_get_patch.argtypes = [_fp, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float, _fp, _fp, _fp]
+        L.ort_mask.argtypes = [C.c_int, _fp]
+        L.ort_track_fb.argtypes = [_fp, _fp, _i32p, C.c_int, C.c_int, C.c_int, _fp, _fp, _i32p, _i32p, _i32p,
+                                   C.c_int]
+        L._trk_ready = True
+    return L
+
+
+def pyramid_sizes(w, h, depth):
+    dims = []
+    for _ in range(depth):
+        dims.append((w, h))
+        w, h = (w + 1) // 2, (h + 1) // 2
+    return dims
+
+
+def make_pyramid(bgr: np.ndarray, depth: int = 6):
+    """hessian.h:95-126 MakePyramid.  bgr: (h, w, 3) uint8.  Returns (flat float32 levels, dims[depth, 2])."""
+    bgr = np.ascontiguousarray(bgr, dtype=np.uint8)
+    h, w = bgr.shape[:2]
+    total = sum(a * b for a, b in pyramid_sizes(w, h, depth))
+    out = np.zeros(total, np.float32)
+    dims = np.zeros(2 * depth, np.int32)
+    _trk().ort_make_pyramid(bgr.ctypes.data_as(_u8p), w, h, w * 3, depth, out.ctypes.data_as(_fp),
+                            dims.ctypes.data_as(_i32p))
+    return out, dims.reshape(depth, 2)
+
+
+def pyramid_levels(flat: np.ndarray, dims: np.ndarray):
+    levels, off = [], 0
+    for w, h in dims:
+        levels.append(flat[off:off + w * h].reshape(h, w))
+        off += w * h
+    return levels
+
+
+def get_rect_subpix(img: np.ndarray, pw: int, ph: int, cx: float, cy: float):
+    img = np.ascontiguousarray(img, dtype=np.float32)
+    out = np.zeros((ph, pw), np.float32)
+    _trk().ort_get_rect_subpix(img.ctypes.data_as(_fp), img.shape[1], img.shape[0], pw, ph, cx, cy,
+                               out.ctypes.data_as(_fp))
+    return out
+
+
+def get_patch(img: np.ndarray, win: int, x: float, y: float):
+    img = np.ascontiguousarray(img, dtype=np.float32)
+    out = np.zeros((win, win), np.float32)
+    mean, sumsq = C.c_float(), C.c_float()
+    _trk().ort_get_patch(img.ctypes.data_as(_fp), img.shape[1], img.shape[0], win, x, y, out.ctypes.data_as(_fp),
+                         C.byref(mean), C.byref(sumsq))
+    return out, mean.value, sumsq.value
+
+
+def patch_mask(win: int):
+    out = np.zeros(win * win, np.float32)
+    _trk().ort_mask(win, out.ctypes.data_as(_fp))
+    return out
+
+
+def track_fb(pyr_from, pyr_to, dims, win, from_xy, to_xy, levels=None, nthreads=1):
+    """matcher.cpp:173-206 + 247-251: forward/backward tracking.  Returns (to_xy, accepted, iterations)."""
+    from_xy = np.ascontiguousarray(from_xy, dtype=np.float32).reshape(-1, 2)
+    out = np.ascontiguousarray(to_xy, dtype=np.float32).reshape(-1, 2).copy()
+    n = from_xy.shape[0]
+    lv = np.full(n, 3, np.int32) if levels is None else np.ascontiguousarray(levels, dtype=np.int32)
+    acc = np.zeros(n, np.int32)
+    it = np.zeros(n, np.int32)
+    d = np.ascontiguousarray(dims, dtype=np.int32).reshape(-1)
+    pf = np.ascontiguousarray(pyr_from, dtype=np.float32)
+    pt = np.ascontiguousarray(pyr_to, dtype=np.float32)
+    _trk().ort_track_fb(pf.ctypes.data_as(_fp), pt.ctypes.data_as(_fp), d.ctypes.data_as(_i32p), len(d) // 2, win, n,
+                        from_xy.ctypes.data_as(_fp), out.ctypes.data_as(_fp), lv.ctypes.data_as(_i32p),
+                        acc.ctypes.data_as(_i32p), it.ctypes.data_as(_i32p), nthreads)
+    return out, acc, it

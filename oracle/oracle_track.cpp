@@ -1,0 +1,413 @@
+// oracle_track.cpp — TEST INFRASTRUCTURE ONLY.  CPU restatement of the reference's front end (the
+// HessianTracker of hessian.h and the forward/backward matcher of matcher.cpp), used by tests/,
+// __graft_entry__.smoke() and bench.py's cpu_baseline leg as the checker of the device tracker.
+//
+// The reference delegates image primitives to OpenCV 2.x (unpinned system library, not vendored and not
+// installed here).  Their published algorithms are restated below (OpenCV 2.4 imgproc: color.cpp
+// RGB2Gray<uchar>, convert.cpp cvtScale_, smooth.cpp getGaussianKernel + separable filter with
+// BORDER_REFLECT_101, pyramids.cpp pyrDown_, samplers.cpp getRectSubPix_Cn_ + adjustRect).  Parity is
+// unpinned by the reference (no fixtures for this path; OpenCV unavailable): see DESIGN.md.
+// Arithmetic is float in the textbook left-to-right order (compiled with -ffp-contract=off); the
+// reference's -ffast-math build may reassociate, so device/oracle tolerances are stated in the tests.
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+namespace oracle_trk {
+
+// ------------------------------------------------------------------------------------------------
+// OpenCV primitives (restated)
+
+inline int Reflect101(int p, int n) {   // borderInterpolate(p, n, BORDER_REFLECT_101)
+  if (n == 1) return 0;
+  while (p < 0 || p >= n) {
+    if (p < 0) p = -p;
+    if (p >= n) p = 2 * n - 2 - p;
+  }
+  return p;
+}
+
+// cvtColor(img, grey, CV_RGB2GRAY) on an 8UC3 image whose memory order is BGR (hessian.h:100): the
+// weights meant for R are applied to channel 0.  Fixed point, yuv_shift 14.
+void RgbToGrayU8(const uint8_t* src, int w, int h, int stride, uint8_t* dst) {
+  const int R2Y = 4899, G2Y = 9617, B2Y = 1868, shift = 14;
+  for (int y = 0; y < h; ++y)
+    for (int x = 0; x < w; ++x) {
+      const uint8_t* p = src + (size_t)y * stride + 3 * x;
+      dst[(size_t)y * w + x] = (uint8_t)((R2Y * p[0] + G2Y * p[1] + B2Y * p[2] + (1 << (shift - 1))) >> shift);
+    }
+}
+
+// getGaussianKernel(n, sigma, CV_32F) for sigma > 0.
+std::vector<float> GaussianKernel(int n, double sigma) {
+  std::vector<float> k(n);
+  const double scale2X = -0.5 / (sigma * sigma);
+  double sum = 0.0;
+  for (int i = 0; i < n; ++i) {
+    const double x = i - (n - 1) * 0.5;
+    k[i] = (float)std::exp(scale2X * x * x);
+    sum += k[i];
+  }
+  sum = 1.0 / sum;
+  for (int i = 0; i < n; ++i) k[i] = (float)(k[i] * sum);
+  return k;
+}
+
+// GaussianBlur(img, img, Size(5,5), sigma, sigma): separable symmetric 5-tap, rows then columns,
+// BORDER_REFLECT_101; s = c*k0 + (l1 + r1)*k1 + (l2 + r2)*k2.
+void GaussianBlur5(std::vector<float>& img, int w, int h, double sigma) {
+  const std::vector<float> k = GaussianKernel(5, sigma);
+  const float k0 = k[2], k1 = k[3], k2 = k[4];
+  std::vector<float> tmp((size_t)w * h);
+  for (int y = 0; y < h; ++y) {
+    const float* r = &img[(size_t)y * w];
+    for (int x = 0; x < w; ++x) {
+      const float c = r[x];
+      const float l1 = r[Reflect101(x - 1, w)], r1 = r[Reflect101(x + 1, w)];
+      const float l2 = r[Reflect101(x - 2, w)], r2 = r[Reflect101(x + 2, w)];
+      tmp[(size_t)y * w + x] = c * k0 + (l1 + r1) * k1 + (l2 + r2) * k2;
+    }
+  }
+  for (int y = 0; y < h; ++y)
+    for (int x = 0; x < w; ++x) {
+      const float c = tmp[(size_t)y * w + x];
+      const float u1 = tmp[(size_t)Reflect101(y - 1, h) * w + x], d1 = tmp[(size_t)Reflect101(y + 1, h) * w + x];
+      const float u2 = tmp[(size_t)Reflect101(y - 2, h) * w + x], d2 = tmp[(size_t)Reflect101(y + 2, h) * w + x];
+      img[(size_t)y * w + x] = c * k0 + (u1 + d1) * k1 + (u2 + d2) * k2;
+    }
+}
+
+// pyrDown(src, dst): 1-4-6-4-1 rows then columns, BORDER_REFLECT_101, scale 1/256, dst ((w+1)/2, (h+1)/2).
+void PyrDown(const std::vector<float>& src, int w, int h, std::vector<float>& dst, int* dw, int* dh) {
+  const int ow = (w + 1) / 2, oh = (h + 1) / 2;
+  std::vector<float> rows((size_t)ow * h);
+  for (int y = 0; y < h; ++y) {
+    const float* s = &src[(size_t)y * w];
+    for (int x = 0; x < ow; ++x) {
+      const int c = 2 * x;
+      rows[(size_t)y * ow + x] = s[Reflect101(c, w)] * 6 + (s[Reflect101(c - 1, w)] + s[Reflect101(c + 1, w)]) * 4 +
+                                 s[Reflect101(c - 2, w)] + s[Reflect101(c + 2, w)];
+    }
+  }
+  dst.assign((size_t)ow * oh, 0.f);
+  for (int y = 0; y < oh; ++y) {
+    const int c = 2 * y;
+    const float* r0 = &rows[(size_t)Reflect101(c - 2, h) * ow];
+    const float* r1 = &rows[(size_t)Reflect101(c - 1, h) * ow];
+    const float* r2 = &rows[(size_t)Reflect101(c, h) * ow];
+    const float* r3 = &rows[(size_t)Reflect101(c + 1, h) * ow];
+    const float* r4 = &rows[(size_t)Reflect101(c + 2, h) * ow];
+    for (int x = 0; x < ow; ++x)
+      dst[(size_t)y * ow + x] = (r2[x] * 6 + (r1[x] + r3[x]) * 4 + r0[x] + r4[x]) * (1.f / 256.f);
+  }
+  *dw = ow;
+  *dh = oh;
+}
+
+// getRectSubPix(src, Size(pw, ph), center, dst) for CV_32F -> CV_32F (getRectSubPix_Cn_ with adjustRect:
+// bilinear inside, replicated border outside).
+void GetRectSubPix(const float* img, int w, int h, int pw, int ph, float cx, float cy, float* dst, int dstride) {
+  cx -= (pw - 1) * 0.5f;
+  cy -= (ph - 1) * 0.5f;
+  const int ipx = (int)std::floor(cx), ipy = (int)std::floor(cy);
+  const float a = cx - ipx, b = cy - ipy;
+  const float a11 = (1.f - a) * (1.f - b), a12 = a * (1.f - b), a21 = (1.f - a) * b, a22 = a * b;
+  const float b1 = 1.f - b, b2 = b;
+  // adjustRect
+  int base_col, base_row, rx, rw, ry, rh;
+  if (ipx >= 0) { base_col = ipx; rx = 0; }
+  else { base_col = 0; rx = std::min(-ipx, pw); }
+  if (ipx < w - pw) rw = pw;
+  else {
+    rw = w - ipx - 1;
+    if (rw < 0) { base_col += rw; rw = 0; }
+  }
+  if (ipy >= 0) { base_row = ipy; ry = 0; }
+  else { base_row = 0; ry = -ipy; }
+  if (ipy < h - ph) rh = ph;
+  else {
+    rh = h - ipy - 1;
+    if (rh < 0) { base_row += rh; rh = 0; }
+  }
+  const int col0 = base_col - rx;   // src pointer column after "src - rect.x"
+  int row = base_row;
+  for (int i = 0; i < ph; ++i) {
+    const bool same = (i < ry || i >= rh);
+    const float* s1 = img + (size_t)row * w;
+    const float* s2 = same ? s1 : s1 + w;
+    float* d = dst + (size_t)i * dstride;
+    int j = 0;
+    for (; j < rx; ++j) d[j] = s1[col0 + rx] * b1 + s2[col0 + rx] * b2;
+    for (; j < rw; ++j) d[j] = s1[col0 + j] * a11 + s1[col0 + j + 1] * a12 + s2[col0 + j] * a21 + s2[col0 + j + 1] * a22;
+    for (; j < pw; ++j) d[j] = s1[col0 + rw] * b1 + s2[col0 + rw] * b2;
+    if (i < rh && !same) ++row;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// HessianTracker (hessian.h)
+
+struct Patch {
+  std::vector<float> data;
+  float mean = 0.f, sumsq = 0.f;
+};
+
+// Fixed summation order for the patch sums (the reference sums sequentially in a -ffast-math build, i.e.
+// in a compiler-chosen vectorised order): 64 lane partials, partial[l] = sum over i = l (mod 64) in
+// increasing i, then a pairwise tree over consecutive partials.  This is the order of the device
+// tracker (one wave per track, DPP reduction), so the two agree bit for bit.
+inline float LaneTreeSum(const float* v, int n) {
+  float part[64];
+  for (int l = 0; l < 64; ++l) part[l] = 0.f;
+  for (int i = 0; i < n; ++i) part[i & 63] += v[i];
+  for (int width = 64; width > 4; width >>= 1)
+    for (int l = 0; l < width / 2; ++l) part[l] = part[2 * l] + part[2 * l + 1];
+  return (part[0] + part[1]) + (part[2] + part[3]);
+}
+
+struct Tracker {
+  int W, len;
+  std::vector<float> mask;
+
+  explicit Tracker(int win) : W(win), len(win * win), mask(win * win) {   // hessian.h:11-30
+    for (int y = 0; y < W; ++y)
+      for (int x = 0; x < W; ++x) {
+        const double rx = 0.5 * W - x, ry = 0.5 * W - y, rr = rx * rx + ry * ry;
+        mask[y * W + x] = (float)(1. / (15. + rr));
+      }
+    double sum = 0.0;
+    for (float v : mask) sum += v;
+    const double scale = len / sum;
+    for (float& v : mask) v = (float)(v * scale);
+  }
+
+  // hessian.h:54-93: zero-filled left/top columns when the point is near the edge, then getRectSubPix.
+  Patch GetPatch(const float* img, int w, int h, float px, float py) const {
+    Patch p;
+    p.data.assign(len, 0.f);
+    int rx = 0, ry = 0, rw = W, rh = W;
+    if (px < 0.5 * W) {
+      const int d = (int)((0.5 * W - px) + 0.9999);
+      px = (float)(px + 0.5 * d);
+      rx = d;
+      rw = W - d;
+    }
+    if (py < 0.5 * W) {
+      const int d = (int)(0.5 * W - py);
+      py = (float)(py + 0.5 * d);
+      ry = d;
+      rh = W - d;
+    }
+    if (rw > 0 && rh > 0) GetRectSubPix(img, w, h, rw, rh, px, py, &p.data[rx + ry * W], W);
+    std::vector<float> sq(len);
+    for (int i = 0; i < len; ++i) sq[i] = p.data[i] * p.data[i];
+    const float sum = LaneTreeSum(p.data.data(), len), sum_sq = LaneTreeSum(sq.data(), len);
+    p.mean = sum / len;
+    p.sumsq = sum_sq / len;
+    return p;
+  }
+
+  float Score(const Patch& p1, const Patch& p2) const {   // hessian.h:129-141
+    const float alpha = std::sqrt(p1.sumsq / p2.sumsq);
+    const float beta = p1.mean - alpha * p2.mean;
+    std::vector<float> term(len, 0.f);
+    for (int i = 0; i < len; ++i) {
+      if (p1.data[i] == 0 || p2.data[i] == 0) continue;
+      float diff = p1.data[i] - p2.data[i] * alpha - beta;
+      diff = diff * diff;
+      term[i] = diff * mask[i];
+    }
+    return LaneTreeSum(term.data(), len);
+  }
+
+  // hessian.h:147-172
+  float BruteHessian(const float* img, int w, int h, const Patch& patch, float x, float y, float* dx, float* dy,
+                     float* dxx, float* dxy, float* dyx, float* dyy) const {
+    const double hh = 0.02;
+    const double sad0 = Score(patch, GetPatch(img, w, h, x, y));
+    const double sadn1x = Score(patch, GetPatch(img, w, h, (float)(x - hh), y));
+    const double sadn1y = Score(patch, GetPatch(img, w, h, x, (float)(y - hh)));
+    const double sadp1x = Score(patch, GetPatch(img, w, h, (float)(x + hh), y));
+    const double sadp1y = Score(patch, GetPatch(img, w, h, x, (float)(y + hh)));
+    const double sadxy = Score(patch, GetPatch(img, w, h, (float)(x + hh), (float)(y + hh)));
+    *dx = (float)(0.5 * (sadp1x - sadn1x) / hh);
+    *dy = (float)(0.5 * (sadp1y - sadn1y) / hh);
+    *dxx = (float)(((sadp1x - sad0) / hh - (sad0 - sadn1x) / hh) / hh);
+    *dyy = (float)(((sadp1y - sad0) / hh - (sad0 - sadn1y) / hh) / hh);
+    *dxy = (float)(((sadxy - sadp1y) / hh - (sadp1x - sad0) / hh) / hh);
+    *dyx = (float)(((sadxy - sadp1x) / hh - (sadp1y - sad0) / hh) / hh);
+    return (float)sad0;
+  }
+
+  // hessian.h:185-241.  Returns 0 OK, 2 OUT_OF_BOUNDS; *iters = Newton iterations run.
+  int Track(const float* img, int w, int h, const Patch& patch, float threshold, int max_iterations, float* px,
+            float* py, int* iters) const {
+    float x = *px, y = *py;
+    const float margin = 0.01f;
+    int it = 0;
+    for (; it < max_iterations; ++it) {
+      if (x < margin || y < margin || (x + margin) > w || (y + margin) > h) {
+        *px = x;
+        *py = y;
+        if (iters) *iters += it;
+        return 2;
+      }
+      float mdx, mdy, mdxx, mdxy, mdyx, mdyy;
+      BruteHessian(img, w, h, patch, x, y, &mdx, &mdy, &mdxx, &mdxy, &mdyx, &mdyy);
+      // Eigen Matrix2d inverse (cofactors / determinant) times g
+      const double H00 = mdxx, H01 = mdxy, H10 = mdyx, H11 = mdyy;
+      const double det = H00 * H11 - H10 * H01;
+      const double invdet = 1.0 / det;
+      const double i00 = H11 * invdet, i10 = -H10 * invdet, i01 = -H01 * invdet, i11 = H00 * invdet;
+      const double g0 = mdx, g1 = mdy;
+      const double jj0 = i00 * g0 + i01 * g1, jj1 = i10 * g0 + i11 * g1;
+      float dx = (float)-jj0, dy = (float)-jj1;
+      if ((dx * dx + dy * dy) > 1) {
+        dx /= std::sqrt(dx * dx + dy * dy);
+        dy /= std::sqrt(dx * dx + dy * dy);   // uses the updated dx (reference quirk)
+      }
+      // x += max(-1.f, min(1.f, dx)) with std::min/std::max NaN semantics
+      const float cx = (dx < 1.f) ? dx : 1.f, cy = (dy < 1.f) ? dy : 1.f;
+      x += (-1.f < cx) ? cx : -1.f;
+      y += (-1.f < cy) ? cy : -1.f;
+      if (std::fabs(dx) < threshold && std::fabs(dy) < threshold) {
+        ++it;
+        break;
+      }
+    }
+    if (iters) *iters += it;
+    *px = x;
+    *py = y;
+    return 0;
+  }
+};
+
+struct Level {
+  const float* img;
+  int w, h;
+};
+
+// hessian.h:243-264 (TrackFeature) with GetPatches (175-183) for the source templates.
+int TrackFeature(const Tracker& T, const std::vector<Level>& src, const std::vector<Level>& dst, float sx, float sy,
+                 int levels, float threshold, int max_iterations, float* px, float* py, int* iters) {
+  const int lvls = std::min((int)std::min(src.size(), dst.size()), levels);
+  std::vector<Patch> patches(lvls);
+  float tx = sx, ty = sy;
+  for (int i = 0; i < lvls; ++i) {
+    patches[i] = T.GetPatch(src[i].img, src[i].w, src[i].h, tx, ty);
+    tx = (float)(tx * 0.5);
+    ty = (float)(ty * 0.5);
+  }
+  const double s = 1. / (1 << (lvls - 1));
+  float x = (float)(*px * s), y = (float)(*py * s);
+  for (int i = lvls - 1; i > 0; --i) {
+    const int st = T.Track(dst[i].img, dst[i].w, dst[i].h, patches[i], threshold, max_iterations, &x, &y, iters);
+    if (st != 0) return st;
+    x = (float)(x * 2.);
+    y = (float)(y * 2.);
+  }
+  const int st = T.Track(dst[0].img, dst[0].w, dst[0].h, patches[0], threshold, max_iterations, &x, &y, iters);
+  if (st != 0) return st;
+  *px = x;
+  *py = y;
+  return 0;
+}
+
+// matcher.cpp:173-206 (forward/backward TrackFeature) and the 3 -> 6 level retry of matcher.cpp:247-251.
+bool TrackFB(const Tracker& T, const std::vector<Level>& from, const std::vector<Level>& to, float fx, float fy,
+             int levels, float* tx, float* ty, int* iters) {
+  auto attempt = [&](int lv) {
+    const int s1 = TrackFeature(T, from, to, fx, fy, lv, 0.001f, 10, tx, ty, iters);
+    float bx = fx, by = fy;
+    const int s2 = TrackFeature(T, to, from, *tx, *ty, lv, 0.001f, 10, &bx, &by, iters);
+    if (s1 || s2) return false;
+    const float ex = fx - bx, ey = fy - by;   // Point2f difference, then cv::norm in double
+    return !(std::sqrt((double)ex * ex + (double)ey * ey) > 0.3);
+  };
+  if (attempt(levels)) return true;
+  if (levels == 6) return false;
+  return attempt(6);
+}
+
+}  // namespace oracle_trk
+
+using namespace oracle_trk;
+
+extern "C" {
+
+// MakePyramid (hessian.h:95-126): BGR u8 -> grey -> /255 -> GaussianBlur(5, 1.1); then per level
+// pyrDown + GaussianBlur(5, 0.8).  out holds the levels back to back; dims[2l], dims[2l+1] = w, h.
+int ort_make_pyramid(const uint8_t* bgr, int w, int h, int stride, int depth, float* out, int32_t* dims) {
+  std::vector<uint8_t> grey((size_t)w * h);
+  RgbToGrayU8(bgr, w, h, stride, grey.data());
+  std::vector<float> cur((size_t)w * h);
+  const float sc = (float)(1. / 255.);
+  for (size_t i = 0; i < cur.size(); ++i) cur[i] = (float)grey[i] * sc;
+  GaussianBlur5(cur, w, h, 1.1);
+  int cw = w, ch = h;
+  size_t off = 0;
+  for (int l = 0; l < depth; ++l) {
+    if (l > 0) {
+      std::vector<float> nxt;
+      int nw, nh;
+      PyrDown(cur, cw, ch, nxt, &nw, &nh);
+      GaussianBlur5(nxt, nw, nh, 0.8);
+      cur.swap(nxt);
+      cw = nw;
+      ch = nh;
+    }
+    std::memcpy(out + off, cur.data(), cur.size() * sizeof(float));
+    dims[2 * l] = cw;
+    dims[2 * l + 1] = ch;
+    off += cur.size();
+  }
+  return 0;
+}
+
+int ort_get_rect_subpix(const float* img, int w, int h, int pw, int ph, float cx, float cy, float* out) {
+  GetRectSubPix(img, w, h, pw, ph, cx, cy, out, pw);
+  return 0;
+}
+
+int ort_get_patch(const float* img, int w, int h, int win, float x, float y, float* out, float* mean, float* sumsq) {
+  Tracker T(win);
+  Patch p = T.GetPatch(img, w, h, x, y);
+  std::memcpy(out, p.data.data(), p.data.size() * sizeof(float));
+  *mean = p.mean;
+  *sumsq = p.sumsq;
+  return 0;
+}
+
+int ort_mask(int win, float* out) {
+  Tracker T(win);
+  std::memcpy(out, T.mask.data(), T.mask.size() * sizeof(float));
+  return 0;
+}
+
+// Forward/backward tracking of n features between two pyramids (same dims).  to_xy: in = initial guess,
+// out = tracked position (as the matcher leaves it).  accepted[i] = FB check passed.  iters (optional):
+// total Newton iterations per track.
+int ort_track_fb(const float* pyr_from, const float* pyr_to, const int32_t* dims, int depth, int win, int n,
+                 const float* from_xy, float* to_xy, const int32_t* levels, int32_t* accepted, int32_t* iters,
+                 int nthreads) {
+  std::vector<Level> from(depth), to(depth);
+  size_t off = 0;
+  for (int l = 0; l < depth; ++l) {
+    from[l] = Level{pyr_from + off, dims[2 * l], dims[2 * l + 1]};
+    to[l] = Level{pyr_to + off, dims[2 * l], dims[2 * l + 1]};
+    off += (size_t)dims[2 * l] * dims[2 * l + 1];
+  }
+  Tracker T(win);
+#pragma omp parallel for schedule(dynamic, 8) num_threads(nthreads > 0 ? nthreads : 1)
+  for (int i = 0; i < n; ++i) {
+    int it = 0;
+    accepted[i] = TrackFB(T, from, to, from_xy[2 * i], from_xy[2 * i + 1], levels ? levels[i] : 3, &to_xy[2 * i],
+                          &to_xy[2 * i + 1], &it) ? 1 : 0;
+    if (iters) iters[i] = it;
+  }
+  return 0;
+}
+
+}  // extern "C"

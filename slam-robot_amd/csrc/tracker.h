@@ -1,0 +1,60 @@
+// tracker.h — host driver of the device HessianTracker (one per sg_tracker handle).
+#ifndef SG_TRACKER_H_
+#define SG_TRACKER_H_
+
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "common.h"
+#include "dbuf.h"
+
+namespace sg {
+
+constexpr int kTrkMaxDepth = 8;
+
+struct TrackParams {
+  int window, max_iterations;
+  float threshold, fb_max;
+  int retry_levels;
+  const float* mask;
+};
+
+class Tracker {
+ public:
+  Tracker(const sg_tracker_options& o, const sg_device_options& d);
+  ~Tracker();
+
+  void SetImage(int slot, const uint8_t* bgr, int w, int h, int stride);
+  void GetLevel(int slot, int level, float* out, int* w, int* h);
+  void GetPatches(int slot, int level, int n, const float* xy, float* out, float* mean, float* sumsq);
+  void LoadFeatures(int n, const float* from_xy, const float* to_xy, const int32_t* levels);
+  void Run(int from, int to, int repeats);
+  void Results(float* to_xy, int32_t* accepted, int32_t* iterations);
+  double track_ms() const { return track_ms_; }
+  double pyramid_ms() const { return pyr_ms_; }
+
+ private:
+  struct Slot {
+    DBuf<float> pyr;
+    std::vector<int> w, h;
+    std::vector<size_t> off;
+    bool valid = false;
+  };
+  sg_tracker_options opt_;
+  sg_device_options dev_;
+  hipStream_t stream_ = nullptr;
+  hipEvent_t ev_[4] = {nullptr, nullptr, nullptr, nullptr};
+  std::vector<Slot> slots_;
+  DBuf<float> mask_, tmp_, tmp2_;
+  DBuf<uint8_t> img_;
+  DBuf<float> from_, init_, out_;
+  DBuf<int32_t> levels_, acc_, its_;
+  int n_ = 0;
+  bool ran_ = false;
+  double track_ms_ = 0.0, pyr_ms_ = 0.0;
+};
+
+}  // namespace sg
+
+#endif  // SG_TRACKER_H_

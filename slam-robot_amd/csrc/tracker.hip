@@ -1,0 +1,623 @@
+// tracker.hip — MI355X-native front end: the reference's HessianTracker (hessian.h) and the
+// forward/backward matching step of Matcher (matcher.cpp:173-206, 247-251).
+//
+//   pyramid   MakePyramid (hessian.h:95-126): BGR u8 -> grey (CV_RGB2GRAY weights on channel 0) -> /255
+//             -> GaussianBlur 5x5 sigma 1.1; per level pyrDown + GaussianBlur 5x5 sigma 0.8.  Stencil
+//             kernels, one thread per output pixel, BORDER_REFLECT_101.
+//   tracking  one wavefront per feature.  Lane l owns patch pixels l, l+64, ... ; the six Newton probes of
+//             BruteHessian (hessian.h:147-172) are sampled together, their mean / sumsq / score sums are
+//             reduced by DPP wave reductions in a batch, and the 2x2 Newton step of Track (185-241) runs
+//             in fp64 as in the reference.  TrackFeature (243-264) walks the levels coarse to fine; the
+//             matcher's forward pass, backward pass, 0.3 px check and 3 -> 6 level retry all run in the
+//             same wave.
+//
+// Arithmetic follows the oracle (oracle/oracle_track.cpp) operation for operation with FMA contraction
+// off, and the patch sums use the oracle's fixed order (64 lane-strided partials + pairwise tree), so the
+// device results are bit-identical to the oracle's.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "common.h"
+#include "tracker.h"
+
+#pragma clang fp contract(off)
+
+namespace sg {
+
+namespace {
+
+constexpr int kTrackWaves = 4;   // features per workgroup (one wave each)
+constexpr int kNP = 4;           // patch pixels per lane (W <= 16)
+
+__device__ __forceinline__ int reflect101(int p, int n) {
+  if (n == 1) return 0;
+  while (p < 0 || p >= n) {
+    if (p < 0) p = -p;
+    if (p >= n) p = 2 * n - 2 - p;
+  }
+  return p;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Pyramid kernels
+
+struct Blur5 {
+  float k0, k1, k2;
+};
+
+// level 0, row pass: grey u8 (computed from BGR on the fly) -> float /255 -> 5-tap row blur
+__global__ void k_gray_blur_row(const uint8_t* bgr, int w, int h, int stride, Blur5 k, float* out) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+  if (x >= w || y >= h) return;
+  const uint8_t* row = bgr + (size_t)y * stride;
+  const float sc = (float)(1. / 255.);
+  auto g = [&](int xx) {
+    const uint8_t* p = row + 3 * reflect101(xx, w);
+    const int v = (4899 * p[0] + 9617 * p[1] + 1868 * p[2] + (1 << 13)) >> 14;
+    return (float)(uint8_t)v * sc;
+  };
+  const float c = g(x), l1 = g(x - 1), r1 = g(x + 1), l2 = g(x - 2), r2 = g(x + 2);
+  out[(size_t)y * w + x] = c * k.k0 + (l1 + r1) * k.k1 + (l2 + r2) * k.k2;
+}
+
+__global__ void k_blur_row(const float* in, int w, int h, Blur5 k, float* out) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+  if (x >= w || y >= h) return;
+  const float* r = in + (size_t)y * w;
+  const float c = r[x], l1 = r[reflect101(x - 1, w)], r1 = r[reflect101(x + 1, w)];
+  const float l2 = r[reflect101(x - 2, w)], r2 = r[reflect101(x + 2, w)];
+  out[(size_t)y * w + x] = c * k.k0 + (l1 + r1) * k.k1 + (l2 + r2) * k.k2;
+}
+
+__global__ void k_blur_col(const float* in, int w, int h, Blur5 k, float* out) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+  if (x >= w || y >= h) return;
+  const float c = in[(size_t)y * w + x];
+  const float u1 = in[(size_t)reflect101(y - 1, h) * w + x], d1 = in[(size_t)reflect101(y + 1, h) * w + x];
+  const float u2 = in[(size_t)reflect101(y - 2, h) * w + x], d2 = in[(size_t)reflect101(y + 2, h) * w + x];
+  out[(size_t)y * w + x] = c * k.k0 + (u1 + d1) * k.k1 + (u2 + d2) * k.k2;
+}
+
+// pyrDown: the row pass values of the five source rows are recomputed per output (same arithmetic as the
+// separable form), then combined 1-4-6-4-1 and scaled by 1/256.
+__global__ void k_pyrdown(const float* in, int w, int h, float* out, int ow, int oh) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+  if (x >= ow || y >= oh) return;
+  const int c = 2 * x;
+  const int cm2 = reflect101(c - 2, w), cm1 = reflect101(c - 1, w), c0 = reflect101(c, w);
+  const int cp1 = reflect101(c + 1, w), cp2 = reflect101(c + 2, w);
+  float rv[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const float* s = in + (size_t)reflect101(2 * y + k - 2, h) * w;
+    rv[k] = s[c0] * 6 + (s[cm1] + s[cp1]) * 4 + s[cm2] + s[cp2];
+  }
+  out[(size_t)y * ow + x] = (rv[2] * 6 + (rv[1] + rv[3]) * 4 + rv[0] + rv[4]) * (1.f / 256.f);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Patch sampling (GetPatch = zero-filled left/top edge + getRectSubPix) and reductions
+
+struct LevelDev {
+  const float* img;
+  int w, h;
+};
+struct PyrDev {
+  LevelDev lv[kTrkMaxDepth];
+  int depth;
+};
+
+// Per-probe geometry (wave-uniform).
+struct Geo {
+  int zx, zy;               // zero-filled columns / rows of the W x W patch (GetPatch, hessian.h:63-75)
+  int pw, ph;               // getRectSubPix window (W - zx) x (W - zy)
+  int col0, base_row;       // adjustRect: source column of window column 0 (minus rect.x), first row
+  int rx, rw, ry, rh;       // adjustRect rect
+  float a11, a12, a21, a22, b1, b2;
+};
+
+__device__ __forceinline__ void make_geo(float px, float py, int W, int w, int h, Geo& g) {
+  g.zx = 0;
+  g.zy = 0;
+  g.pw = W;
+  g.ph = W;
+  if (px < 0.5 * W) {
+    const int d = (int)((0.5 * W - px) + 0.9999);
+    px = (float)(px + 0.5 * d);
+    g.zx = d;
+    g.pw = W - d;
+  }
+  if (py < 0.5 * W) {
+    const int d = (int)(0.5 * W - py);
+    py = (float)(py + 0.5 * d);
+    g.zy = d;
+    g.ph = W - d;
+  }
+  float cx = px - (g.pw - 1) * 0.5f, cy = py - (g.ph - 1) * 0.5f;
+  const int ipx = (int)floorf(cx), ipy = (int)floorf(cy);
+  const float a = cx - ipx, b = cy - ipy;
+  g.a11 = (1.f - a) * (1.f - b);
+  g.a12 = a * (1.f - b);
+  g.a21 = (1.f - a) * b;
+  g.a22 = a * b;
+  g.b1 = 1.f - b;
+  g.b2 = b;
+  int base_col;
+  if (ipx >= 0) { base_col = ipx; g.rx = 0; }
+  else { base_col = 0; g.rx = min(-ipx, g.pw); }
+  if (ipx < w - g.pw) g.rw = g.pw;
+  else {
+    g.rw = w - ipx - 1;
+    if (g.rw < 0) { base_col += g.rw; g.rw = 0; }
+  }
+  if (ipy >= 0) { g.base_row = ipy; g.ry = 0; }
+  else { g.base_row = 0; g.ry = -ipy; }
+  if (ipy < h - g.ph) g.rh = g.ph;
+  else {
+    g.rh = h - ipy - 1;
+    if (g.rh < 0) { g.base_row += g.rh; g.rh = 0; }
+  }
+  g.col0 = base_col - g.rx;
+}
+
+// Patch pixel (i, j) of the W x W patch.
+__device__ __forceinline__ float sample(const float* img, int w, const Geo& g, int i, int j) {
+  if (g.pw <= 0 || g.ph <= 0 || j < g.zx || i < g.zy) return 0.f;
+  const int ii = i - g.zy, jj = j - g.zx;
+  const bool same = (ii < g.ry || ii >= g.rh);
+  const int row = g.base_row + max(0, min(ii, g.rh) - g.ry);
+  const float* s1 = img + (size_t)row * w;
+  const float* s2 = same ? s1 : s1 + w;
+  if (jj < g.rx) return s1[g.col0 + g.rx] * g.b1 + s2[g.col0 + g.rx] * g.b2;
+  if (jj < g.rw) {
+    const int c = g.col0 + jj;
+    return s1[c] * g.a11 + s1[c + 1] * g.a12 + s2[c] * g.a21 + s2[c + 1] * g.a22;
+  }
+  return s1[g.col0 + g.rw] * g.b1 + s2[g.col0 + g.rw] * g.b2;
+}
+
+template <int kCtrl>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), kCtrl, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float readlane_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+// Pairwise tree over the 64 lane partials (the oracle's LaneTreeSum order).  All lanes active.
+__device__ __forceinline__ float wave_tree_sum(float v) {
+  v = v + dpp_f<0xB1>(v);    // lanes (l, l^1)
+  v = v + dpp_f<0x4E>(v);    // (l, l^2)
+  v = v + dpp_f<0x141>(v);   // half-row mirror: octets
+  v = v + dpp_f<0x140>(v);   // row mirror: 16-lane rows
+  return (readlane_f(v, 0) + readlane_f(v, 16)) + (readlane_f(v, 32) + readlane_f(v, 48));
+}
+
+struct Tmpl {
+  float v[kNP];
+  float mean, sumsq;
+};
+
+__device__ __forceinline__ void get_patch(const LevelDev& L, float px, float py, int W, int lane, Tmpl& t) {
+  Geo g;
+  make_geo(px, py, W, L.w, L.h, g);
+  const int len = W * W;
+  float s = 0.f, q = 0.f;
+#pragma unroll
+  for (int k = 0; k < kNP; ++k) {
+    const int p = lane + 64 * k;
+    float v = 0.f;
+    if (p < len) v = sample(L.img, L.w, g, p / W, p % W);
+    t.v[k] = v;
+    s += v;
+    q += v * v;
+  }
+  s = wave_tree_sum(s);
+  q = wave_tree_sum(q);
+  t.mean = s / len;
+  t.sumsq = q / len;
+}
+
+struct TrackCtx {
+  int W, len, max_it;
+  float threshold;
+  const float* mask;   // [len]
+  int lane;
+  float mk[kNP];       // this lane's mask values
+};
+
+// BruteHessian (hessian.h:147-172) + the Newton step of Track.
+__device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev& L, const Tmpl& tp, float x, float y,
+                                              float* mdx, float* mdy, float* mdxx, float* mdxy, float* mdyx,
+                                              float* mdyy) {
+  const double hh = 0.02;
+  float px[6], py[6];
+  px[0] = x;              py[0] = y;                // sad0
+  px[1] = (float)(x - hh); py[1] = y;               // sadn1x
+  px[2] = x;              py[2] = (float)(y - hh);  // sadn1y
+  px[3] = (float)(x + hh); py[3] = y;               // sadp1x
+  px[4] = x;              py[4] = (float)(y + hh);  // sadp1y
+  px[5] = (float)(x + hh); py[5] = (float)(y + hh); // sadxy
+  float pv[6][kNP], ps[6], pq[6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    Geo g;
+    make_geo(px[r], py[r], c.W, L.w, L.h, g);
+    float s = 0.f, q = 0.f;
+#pragma unroll
+    for (int k = 0; k < kNP; ++k) {
+      const int p = c.lane + 64 * k;
+      float v = 0.f;
+      if (p < c.len) v = sample(L.img, L.w, g, p / c.W, p % c.W);
+      pv[r][k] = v;
+      s += v;
+      q += v * v;
+    }
+    ps[r] = s;
+    pq[r] = q;
+  }
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    ps[r] = wave_tree_sum(ps[r]);
+    pq[r] = wave_tree_sum(pq[r]);
+  }
+  float sc[6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    const float mean = ps[r] / c.len, sumsq = pq[r] / c.len;
+    const float alpha = sqrtf(tp.sumsq / sumsq);
+    const float beta = tp.mean - alpha * mean;
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < kNP; ++k) {
+      float term = 0.f;
+      const float a = tp.v[k], b = pv[r][k];
+      if (!(a == 0 || b == 0)) {
+        float diff = a - b * alpha - beta;
+        diff = diff * diff;
+        term = diff * c.mk[k];
+      }
+      acc += term;
+    }
+    sc[r] = acc;
+  }
+#pragma unroll
+  for (int r = 0; r < 6; ++r) sc[r] = wave_tree_sum(sc[r]);
+  const double sad0 = sc[0], sadn1x = sc[1], sadn1y = sc[2], sadp1x = sc[3], sadp1y = sc[4], sadxy = sc[5];
+  *mdx = (float)(0.5 * (sadp1x - sadn1x) / hh);
+  *mdy = (float)(0.5 * (sadp1y - sadn1y) / hh);
+  *mdxx = (float)(((sadp1x - sad0) / hh - (sad0 - sadn1x) / hh) / hh);
+  *mdyy = (float)(((sadp1y - sad0) / hh - (sad0 - sadn1y) / hh) / hh);
+  *mdxy = (float)(((sadxy - sadp1y) / hh - (sadp1x - sad0) / hh) / hh);
+  *mdyx = (float)(((sadxy - sadp1x) / hh - (sadp1y - sad0) / hh) / hh);
+}
+
+// Track (hessian.h:185-241): 0 OK, 2 OUT_OF_BOUNDS.
+__device__ int track_level(const TrackCtx& c, const LevelDev& L, const Tmpl& tp, float* px, float* py, int* iters) {
+  float x = *px, y = *py;
+  const float margin = 0.01f;
+  int it = 0;
+  for (; it < c.max_it; ++it) {
+    if (x < margin || y < margin || (x + margin) > L.w || (y + margin) > L.h) {
+      *px = x;
+      *py = y;
+      *iters += it;
+      return 2;
+    }
+    float mdx, mdy, mdxx, mdxy, mdyx, mdyy;
+    brute_hessian(c, L, tp, x, y, &mdx, &mdy, &mdxx, &mdxy, &mdyx, &mdyy);
+    const double H00 = mdxx, H01 = mdxy, H10 = mdyx, H11 = mdyy;
+    const double det = H00 * H11 - H10 * H01;
+    const double invdet = 1.0 / det;
+    const double i00 = H11 * invdet, i10 = -H10 * invdet, i01 = -H01 * invdet, i11 = H00 * invdet;
+    const double g0 = mdx, g1 = mdy;
+    const double jj0 = i00 * g0 + i01 * g1, jj1 = i10 * g0 + i11 * g1;
+    float dx = (float)-jj0, dy = (float)-jj1;
+    if ((dx * dx + dy * dy) > 1) {
+      dx /= sqrtf(dx * dx + dy * dy);
+      dy /= sqrtf(dx * dx + dy * dy);   // with the updated dx, as the reference
+    }
+    const float cx = (dx < 1.f) ? dx : 1.f, cy = (dy < 1.f) ? dy : 1.f;   // std::min / std::max semantics
+    x += (-1.f < cx) ? cx : -1.f;
+    y += (-1.f < cy) ? cy : -1.f;
+    if (fabsf(dx) < c.threshold && fabsf(dy) < c.threshold) {
+      ++it;
+      break;
+    }
+  }
+  *iters += it;
+  *px = x;
+  *py = y;
+  return 0;
+}
+
+// TrackFeature (hessian.h:243-264) with the source templates of GetPatches (175-183).
+__device__ int track_feature(const TrackCtx& c, const PyrDev& src, const PyrDev& dst, float sx, float sy, int levels,
+                             float* px, float* py, int* iters) {
+  const int lvls = min(min(src.depth, dst.depth), levels);
+  const double s = 1. / (1 << (lvls - 1));
+  float x = (float)(*px * s), y = (float)(*py * s);
+  for (int i = lvls - 1; i >= 0; --i) {
+    float tx = sx, ty = sy;
+    for (int k = 0; k < i; ++k) {
+      tx = (float)(tx * 0.5);
+      ty = (float)(ty * 0.5);
+    }
+    Tmpl tp;
+    get_patch(src.lv[i], tx, ty, c.W, c.lane, tp);
+    const int st = track_level(c, dst.lv[i], tp, &x, &y, iters);
+    if (st != 0) return st;
+    if (i > 0) {
+      x = (float)(x * 2.);
+      y = (float)(y * 2.);
+    }
+  }
+  *px = x;
+  *py = y;
+  return 0;
+}
+
+__global__ __launch_bounds__(64 * kTrackWaves) void k_track_fb(PyrDev from, PyrDev to, TrackParams prm, int n,
+                                                               const float* from_xy, const float* to_init,
+                                                               const int32_t* levels, float* to_xy,
+                                                               int32_t* accepted, int32_t* iterations) {
+  const int lane = threadIdx.x & 63;
+  const int f = blockIdx.x * kTrackWaves + (threadIdx.x >> 6);
+  if (f >= n) return;   // whole wave
+  TrackCtx c;
+  c.W = prm.window;
+  c.len = prm.window * prm.window;
+  c.max_it = prm.max_iterations;
+  c.threshold = prm.threshold;
+  c.mask = prm.mask;
+  c.lane = lane;
+#pragma unroll
+  for (int k = 0; k < kNP; ++k) {
+    const int p = lane + 64 * k;
+    c.mk[k] = p < c.len ? prm.mask[p] : 0.f;
+  }
+  const float fx = from_xy[2 * f], fy = from_xy[2 * f + 1];
+  float tx = to_init[2 * f], ty = to_init[2 * f + 1];
+  const int lv0 = levels ? levels[f] : 3;
+  int iters = 0;
+  auto attempt = [&](int lv) {
+    const int s1 = track_feature(c, from, to, fx, fy, lv, &tx, &ty, &iters);
+    float bx = fx, by = fy;
+    const int s2 = track_feature(c, to, from, tx, ty, lv, &bx, &by, &iters);
+    if (s1 || s2) return false;
+    const float ex = fx - bx, ey = fy - by;
+    return !(sqrt((double)ex * ex + (double)ey * ey) > (double)prm.fb_max);
+  };
+  bool ok = attempt(lv0);
+  if (!ok && prm.retry_levels > 0 && lv0 != prm.retry_levels) ok = attempt(prm.retry_levels);
+  if (lane == 0) {
+    to_xy[2 * f] = tx;
+    to_xy[2 * f + 1] = ty;
+    accepted[f] = ok ? 1 : 0;
+    if (iterations) iterations[f] = iters;
+  }
+}
+
+__global__ __launch_bounds__(64 * kTrackWaves) void k_get_patches(LevelDev L, int W, int n, const float* xy, float* out,
+                                                                  float* mean, float* sumsq) {
+  const int lane = threadIdx.x & 63;
+  const int f = blockIdx.x * kTrackWaves + (threadIdx.x >> 6);
+  if (f >= n) return;
+  Tmpl t;
+  get_patch(L, xy[2 * f], xy[2 * f + 1], W, lane, t);
+  const int len = W * W;
+#pragma unroll
+  for (int k = 0; k < kNP; ++k) {
+    const int p = lane + 64 * k;
+    if (p < len) out[(size_t)f * len + p] = t.v[k];
+  }
+  if (lane == 0) {
+    mean[f] = t.mean;
+    sumsq[f] = t.sumsq;
+  }
+}
+
+std::vector<float> GaussianKernel5(double sigma) {   // getGaussianKernel(5, sigma, CV_32F)
+  std::vector<float> k(5);
+  const double scale2X = -0.5 / (sigma * sigma);
+  double sum = 0.0;
+  for (int i = 0; i < 5; ++i) {
+    const double x = i - 2.0;
+    k[i] = (float)std::exp(scale2X * x * x);
+    sum += k[i];
+  }
+  sum = 1.0 / sum;
+  for (int i = 0; i < 5; ++i) k[i] = (float)(k[i] * sum);
+  return k;
+}
+
+Blur5 MakeBlur(double sigma) {
+  const std::vector<float> k = GaussianKernel5(sigma);
+  return Blur5{k[2], k[3], k[4]};
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// Host side
+
+Tracker::Tracker(const sg_tracker_options& o, const sg_device_options& d) : opt_(o), dev_(d) {
+  SG_REQUIRE(o.window >= 1 && o.window <= 16, SG_EINVAL, "window must be 1..16");
+  SG_REQUIRE(o.depth >= 1 && o.depth <= kTrkMaxDepth, SG_EINVAL, "depth must be 1..8");
+  SG_REQUIRE(o.max_images >= 1 && o.max_images <= 64, SG_EINVAL, "max_images must be 1..64");
+  SG_REQUIRE(o.max_iterations >= 0, SG_EINVAL, "bad max_iterations");
+  int ndev = 0;
+  SG_HIP_CHECK(hipGetDeviceCount(&ndev));
+  SG_REQUIRE(ndev > 0 && d.device >= 0 && d.device < ndev, SG_ENODEV, "no such HIP device");
+  SG_HIP_CHECK(hipSetDevice(d.device));
+  SG_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  SG_HIP_CHECK(hipEventCreate(&ev_[0]));
+  SG_HIP_CHECK(hipEventCreate(&ev_[1]));
+  SG_HIP_CHECK(hipEventCreate(&ev_[2]));
+  SG_HIP_CHECK(hipEventCreate(&ev_[3]));
+  slots_.resize(o.max_images);
+  // hessian.h:11-30 mask
+  const int W = o.window, len = W * W;
+  std::vector<float> m(len);
+  for (int y = 0; y < W; ++y)
+    for (int x = 0; x < W; ++x) {
+      const double rx = 0.5 * W - x, ry = 0.5 * W - y, rr = rx * rx + ry * ry;
+      m[y * W + x] = (float)(1. / (15. + rr));
+    }
+  double sum = 0.0;
+  for (float v : m) sum += v;
+  const double scale = len / sum;
+  for (float& v : m) v = (float)(v * scale);
+  mask_.Upload(m, stream_);
+}
+
+Tracker::~Tracker() {
+  (void)hipSetDevice(dev_.device);
+  for (auto& e : ev_)
+    if (e) (void)hipEventDestroy(e);
+  if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+void Tracker::SetImage(int slot, const uint8_t* bgr, int w, int h, int stride) {
+  SG_REQUIRE(slot >= 0 && slot < (int)slots_.size(), SG_EINVAL, "bad slot");
+  SG_REQUIRE(bgr && w > 0 && h > 0 && stride >= 3 * w, SG_EINVAL, "bad image");
+  SG_HIP_CHECK(hipSetDevice(dev_.device));
+  Slot& s = slots_[slot];
+  s.w.assign(opt_.depth, 0);
+  s.h.assign(opt_.depth, 0);
+  s.off.assign(opt_.depth, 0);
+  size_t total = 0;
+  int cw = w, ch = h;
+  for (int l = 0; l < opt_.depth; ++l) {
+    s.w[l] = cw;
+    s.h[l] = ch;
+    s.off[l] = total;
+    total += (size_t)cw * ch;
+    cw = (cw + 1) / 2;
+    ch = (ch + 1) / 2;
+  }
+  s.pyr.Resize(total);
+  tmp_.Resize((size_t)w * h);
+  tmp2_.Resize((size_t)w * h);
+  img_.Resize((size_t)stride * h);
+  SG_HIP_CHECK(hipMemcpyAsync(img_.ptr, bgr, (size_t)stride * h, hipMemcpyHostToDevice, stream_));
+  const Blur5 b0 = MakeBlur(1.1), b1 = MakeBlur(0.8);
+  SG_HIP_CHECK(hipEventRecord(ev_[2], stream_));
+  const int bx = 256;
+  hipLaunchKernelGGL(k_gray_blur_row, dim3((w + bx - 1) / bx, h), dim3(bx), 0, stream_, img_.ptr, w, h, stride, b0,
+                     tmp_.ptr);
+  hipLaunchKernelGGL(k_blur_col, dim3((w + bx - 1) / bx, h), dim3(bx), 0, stream_, tmp_.ptr, w, h, b0, s.pyr.ptr);
+  for (int l = 1; l < opt_.depth; ++l) {
+    const int pw = s.w[l - 1], ph = s.h[l - 1], ow = s.w[l], oh = s.h[l];
+    hipLaunchKernelGGL(k_pyrdown, dim3((ow + bx - 1) / bx, oh), dim3(bx), 0, stream_, s.pyr.ptr + s.off[l - 1], pw,
+                       ph, tmp_.ptr, ow, oh);
+    hipLaunchKernelGGL(k_blur_row, dim3((ow + bx - 1) / bx, oh), dim3(bx), 0, stream_, tmp_.ptr, ow, oh, b1,
+                       tmp2_.ptr);
+    hipLaunchKernelGGL(k_blur_col, dim3((ow + bx - 1) / bx, oh), dim3(bx), 0, stream_, tmp2_.ptr, ow, oh, b1,
+                       s.pyr.ptr + s.off[l]);
+  }
+  SG_HIP_CHECK(hipEventRecord(ev_[3], stream_));
+  SG_HIP_CHECK(hipGetLastError());
+  SG_HIP_CHECK(hipStreamSynchronize(stream_));   // the host image buffer may be reused by the caller
+  float ms = 0.f;
+  SG_HIP_CHECK(hipEventElapsedTime(&ms, ev_[2], ev_[3]));
+  pyr_ms_ = ms;
+  s.valid = true;
+}
+
+void Tracker::GetLevel(int slot, int level, float* out, int* w, int* h) {
+  SG_REQUIRE(slot >= 0 && slot < (int)slots_.size() && slots_[slot].valid, SG_EINVAL, "empty slot");
+  SG_REQUIRE(level >= 0 && level < opt_.depth, SG_EINVAL, "bad level");
+  SG_HIP_CHECK(hipSetDevice(dev_.device));
+  const Slot& s = slots_[slot];
+  *w = s.w[level];
+  *h = s.h[level];
+  if (out)
+    SG_HIP_CHECK(hipMemcpyAsync(out, s.pyr.ptr + s.off[level], sizeof(float) * s.w[level] * s.h[level],
+                                hipMemcpyDeviceToHost, stream_));
+  SG_HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
+void Tracker::GetPatches(int slot, int level, int n, const float* xy, float* out, float* mean, float* sumsq) {
+  SG_REQUIRE(slot >= 0 && slot < (int)slots_.size() && slots_[slot].valid, SG_EINVAL, "empty slot");
+  SG_REQUIRE(level >= 0 && level < opt_.depth && n >= 0, SG_EINVAL, "bad level / count");
+  if (n == 0) return;
+  SG_HIP_CHECK(hipSetDevice(dev_.device));
+  const Slot& s = slots_[slot];
+  const int len = opt_.window * opt_.window;
+  DBuf<float> dxy, dout, dm, dq;
+  dxy.Upload(std::vector<float>(xy, xy + 2 * n), stream_);
+  dout.Resize((size_t)n * len);
+  dm.Resize(n);
+  dq.Resize(n);
+  LevelDev L{s.pyr.ptr + s.off[level], s.w[level], s.h[level]};
+  hipLaunchKernelGGL(k_get_patches, dim3((n + kTrackWaves - 1) / kTrackWaves), dim3(64 * kTrackWaves), 0, stream_, L,
+                     opt_.window, n, dxy.ptr, dout.ptr, dm.ptr, dq.ptr);
+  SG_HIP_CHECK(hipGetLastError());
+  SG_HIP_CHECK(hipMemcpyAsync(out, dout.ptr, sizeof(float) * n * len, hipMemcpyDeviceToHost, stream_));
+  SG_HIP_CHECK(hipMemcpyAsync(mean, dm.ptr, sizeof(float) * n, hipMemcpyDeviceToHost, stream_));
+  SG_HIP_CHECK(hipMemcpyAsync(sumsq, dq.ptr, sizeof(float) * n, hipMemcpyDeviceToHost, stream_));
+  SG_HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
+void Tracker::LoadFeatures(int n, const float* from_xy, const float* to_xy, const int32_t* levels) {
+  SG_REQUIRE(n >= 0 && (n == 0 || (from_xy && to_xy)), SG_EINVAL, "bad features");
+  SG_HIP_CHECK(hipSetDevice(dev_.device));
+  n_ = n;
+  from_.Upload(std::vector<float>(from_xy, from_xy + 2 * (size_t)n), stream_);
+  init_.Upload(std::vector<float>(to_xy, to_xy + 2 * (size_t)n), stream_);
+  std::vector<int32_t> lv(n, 3);
+  if (levels)
+    for (int i = 0; i < n; ++i) lv[i] = levels[i];
+  for (int v : lv) SG_REQUIRE(v >= 1, SG_EINVAL, "levels must be >= 1");
+  levels_.Upload(lv, stream_);
+  out_.Resize(2 * (size_t)std::max(n, 1));
+  acc_.Resize(std::max(n, 1));
+  its_.Resize(std::max(n, 1));
+}
+
+void Tracker::Run(int from, int to, int repeats) {
+  SG_REQUIRE(from >= 0 && from < (int)slots_.size() && slots_[from].valid, SG_EINVAL, "empty 'from' slot");
+  SG_REQUIRE(to >= 0 && to < (int)slots_.size() && slots_[to].valid, SG_EINVAL, "empty 'to' slot");
+  SG_REQUIRE(repeats >= 1, SG_EINVAL, "repeats must be >= 1");
+  const Slot& a = slots_[from];
+  const Slot& b = slots_[to];
+  SG_REQUIRE(a.w == b.w && a.h == b.h, SG_EINVAL, "pyramids of different sizes");
+  SG_HIP_CHECK(hipSetDevice(dev_.device));
+  PyrDev pf{}, pt{};
+  pf.depth = pt.depth = opt_.depth;
+  for (int l = 0; l < opt_.depth; ++l) {
+    pf.lv[l] = LevelDev{a.pyr.ptr + a.off[l], a.w[l], a.h[l]};
+    pt.lv[l] = LevelDev{b.pyr.ptr + b.off[l], b.w[l], b.h[l]};
+  }
+  TrackParams prm{opt_.window, opt_.max_iterations, opt_.threshold, opt_.fb_max, opt_.retry_levels, mask_.ptr};
+  SG_HIP_CHECK(hipEventRecord(ev_[0], stream_));
+  if (n_ > 0)
+    for (int r = 0; r < repeats; ++r)
+      hipLaunchKernelGGL(k_track_fb, dim3((n_ + kTrackWaves - 1) / kTrackWaves), dim3(64 * kTrackWaves), 0, stream_, pf,
+                         pt, prm, n_, from_.ptr, init_.ptr, levels_.ptr, out_.ptr, acc_.ptr, its_.ptr);
+  SG_HIP_CHECK(hipEventRecord(ev_[1], stream_));
+  SG_HIP_CHECK(hipGetLastError());
+  ran_ = true;
+}
+
+void Tracker::Results(float* to_xy, int32_t* accepted, int32_t* iterations) {
+  SG_REQUIRE(ran_, SG_EINVAL, "no tracking run");
+  SG_HIP_CHECK(hipSetDevice(dev_.device));
+  if (n_ > 0) {
+    if (to_xy) SG_HIP_CHECK(hipMemcpyAsync(to_xy, out_.ptr, sizeof(float) * 2 * n_, hipMemcpyDeviceToHost, stream_));
+    if (accepted)
+      SG_HIP_CHECK(hipMemcpyAsync(accepted, acc_.ptr, sizeof(int32_t) * n_, hipMemcpyDeviceToHost, stream_));
+    if (iterations)
+      SG_HIP_CHECK(hipMemcpyAsync(iterations, its_.ptr, sizeof(int32_t) * n_, hipMemcpyDeviceToHost, stream_));
+  }
+  SG_HIP_CHECK(hipStreamSynchronize(stream_));
+  float ms = 0.f;
+  SG_HIP_CHECK(hipEventElapsedTime(&ms, ev_[0], ev_[1]));
+  track_ms_ = ms;
+}
+
+}  // namespace sg

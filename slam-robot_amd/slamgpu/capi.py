@@ -190,6 +190,15 @@ class ProblemArrays:
 
 _LIB = None
 
+class SgTrackerOptions(C.Structure):
+    _fields_ = [("window", C.c_int32), ("depth", C.c_int32), ("max_iterations", C.c_int32),
+                ("threshold", C.c_float), ("fb_max", C.c_float), ("retry_levels", C.c_int32),
+                ("max_images", C.c_int32), ("reserved", C.c_int32 * 5)]
+
+
+_fp = C.POINTER(C.c_float)
+_u8p = C.POINTER(C.c_uint8)
+
 SYMBOLS = {
     "sg_version": (C.c_char_p, []),
     "sg_last_error": (C.c_char_p, []),
@@ -219,6 +228,17 @@ SYMBOLS = {
     "sg_ba_kernel_work": (C.c_int, [C.c_void_p, _dp, _dp, C.c_int32]),
     "sg_ba_evaluate": (C.c_int, [C.c_void_p, _dp, _dp, _ip]),
     "sg_ba_sweep": (C.c_int, [C.c_void_p, C.c_int32]),
+    "sg_tracker_options_default": (None, [C.POINTER(SgTrackerOptions)]),
+    "sg_tracker_create": (C.c_int, [C.POINTER(C.c_void_p), C.POINTER(SgTrackerOptions), C.POINTER(SgDeviceOptions)]),
+    "sg_tracker_destroy": (None, [C.c_void_p]),
+    "sg_tracker_set_image": (C.c_int, [C.c_void_p, C.c_int32, _u8p, C.c_int32, C.c_int32, C.c_int32]),
+    "sg_tracker_get_level": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, _fp, _ip, _ip]),
+    "sg_tracker_get_patches": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, _fp, _fp, _fp, _fp]),
+    "sg_tracker_track": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, _fp, _fp, _ip, _ip, _ip]),
+    "sg_tracker_load_features": (C.c_int, [C.c_void_p, C.c_int32, _fp, _fp, _ip]),
+    "sg_tracker_run": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32]),
+    "sg_tracker_results": (C.c_int, [C.c_void_p, _fp, _ip, _ip]),
+    "sg_tracker_kernel_ms": (C.c_int, [C.c_void_p, _dp, _dp]),
     "sg_slam_create": (C.c_int, [C.POINTER(C.c_void_p), C.POINTER(SgDeviceOptions)]),
     "sg_slam_destroy": (None, [C.c_void_p]),
     "sg_slam_solve_frames": (C.c_int, [C.c_void_p, C.POINTER(SgMap), C.c_int32, C.c_int32, C.c_double,

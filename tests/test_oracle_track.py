@@ -1,0 +1,100 @@
+"""CPU tests of the front-end oracle (oracle/oracle_track.cpp): the restated OpenCV primitives and the
+HessianTracker / matcher logic, pinned by known answers (parity is unpinned by reference fixtures: the
+reference has none for this path and OpenCV is not available here)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "oracle"))
+import oracle  # noqa: E402
+from slamgpu.video import ground_truth, make_frames, seed_points  # noqa: E402
+
+
+def test_grey_weights_follow_the_bgr_quirk():
+    img = np.zeros((8, 8, 3), np.uint8)
+    img[..., 0] = 255   # channel 0 (blue in a cv::Mat) gets the R weight 4899 (CV_RGB2GRAY on BGR data)
+    flat, dims = oracle.make_pyramid(img, 1)
+    assert abs(flat[0] - ((4899 * 255 + 8192) >> 14) / 255.0) < 1e-6
+    img[..., 0] = 0
+    img[..., 2] = 255
+    flat, _ = oracle.make_pyramid(img, 1)
+    assert abs(flat[0] - ((1868 * 255 + 8192) >> 14) / 255.0) < 1e-6
+
+
+def test_pyramid_sizes_and_constant_image():
+    img = np.full((37, 51, 3), 90, np.uint8)
+    flat, dims = oracle.make_pyramid(img, 6)
+    assert dims.tolist() == [[51, 37], [26, 19], [13, 10], [7, 5], [4, 3], [2, 2]]
+    v = ((4899 + 9617 + 1868) * 90 + 8192 >> 14) / 255.0
+    np.testing.assert_allclose(flat, v, rtol=2e-6)   # blur and pyrDown preserve constants
+
+
+def test_get_rect_subpix_known_answers():
+    rng = np.random.default_rng(0)
+    img = rng.random((40, 50)).astype(np.float32)
+    # integer-aligned window: exact copy
+    p = oracle.get_rect_subpix(img, 7, 5, 20.0 + 3.0, 10.0 + 2.0)
+    np.testing.assert_array_equal(p, img[10:15, 20:27])
+    # interior bilinear
+    cx, cy = 21.3, 11.6
+    p = oracle.get_rect_subpix(img, 3, 3, cx, cy)
+    x0, y0 = cx - 1.0, cy - 1.0
+    ix, iy = int(np.floor(x0)), int(np.floor(y0))
+    a, b = np.float32(x0 - ix), np.float32(y0 - iy)
+    ref = ((1 - a) * (1 - b) * img[iy:iy + 3, ix:ix + 3] + a * (1 - b) * img[iy:iy + 3, ix + 1:ix + 4]
+           + (1 - a) * b * img[iy + 1:iy + 4, ix:ix + 3] + a * b * img[iy + 1:iy + 4, ix + 1:ix + 4])
+    np.testing.assert_allclose(p, ref, atol=1e-6)
+    # left of the image: replicated first column (vertical interpolation only)
+    p = oracle.get_rect_subpix(img, 3, 3, -5.0, 11.0)
+    np.testing.assert_allclose(p, np.repeat(img[10:13, :1], 3, axis=1), atol=1e-7)
+    # below the image: replicated last row
+    p = oracle.get_rect_subpix(img, 3, 3, 21.0, 60.0)
+    np.testing.assert_allclose(p, np.repeat(img[39:40, 20:23], 3, axis=0), atol=1e-7)
+
+
+def test_get_patch_zero_fills_near_left_and_top_edges():
+    img = np.ones((60, 60), np.float32)
+    W = 13
+    p, mean, sumsq = oracle.get_patch(img, W, 2.0, 30.0)
+    d = int((0.5 * W - 2.0) + 0.9999)
+    assert (p[:, :d] == 0).all() and (p[:, d:] > 0).all()
+    p, mean, sumsq = oracle.get_patch(img, W, 30.0, 2.0)
+    d = int(0.5 * W - 2.0)
+    assert (p[:d] == 0).all() and (p[d:] > 0).all()
+    assert abs(mean - (W - d) / W) < 1e-6
+
+
+def test_mask_is_normalised():
+    m = oracle.patch_mask(13)
+    assert abs(m.mean() - 1.0) < 1e-6
+    assert m.argmax() == 13 * 7 + 7 or m[7 * 13 + 7] == m.max()
+
+
+def test_fb_tracking_recovers_known_motion():
+    f = make_frames(2)
+    pf, dims = oracle.make_pyramid(f[0])
+    pt, _ = oracle.make_pyramid(f[1])
+    pts = seed_points(400)
+    gt = ground_truth(pts, 1)
+    for W, tol in ((13, 0.06), (7, 0.12)):
+        out, acc, it = oracle.track_fb(pf, pt, dims, W, pts, pts, nthreads=4)
+        err = np.linalg.norm(out - gt, axis=1)
+        assert acc.mean() > 0.98
+        assert np.median(err[acc == 1]) < tol
+        assert (it > 0).all()
+
+
+def test_fb_rejects_wrong_correspondences_and_out_of_bounds():
+    f = make_frames(2)
+    pf, dims = oracle.make_pyramid(f[0])
+    noise = np.random.default_rng(9).integers(0, 255, f[1].shape, dtype=np.uint8)
+    pn, _ = oracle.make_pyramid(noise)
+    pts = seed_points(200)
+    out, acc, _ = oracle.track_fb(pf, pn, dims, 13, pts, pts, nthreads=4)
+    assert acc.mean() < 0.5          # unrelated image: most features fail the forward/backward check
+    edge = np.array([[0.005, 100.0], [639.999, 200.0]], np.float32)
+    out, acc, _ = oracle.track_fb(pf, pf, dims, 13, edge, edge)
+    assert not acc.any()             # OUT_OF_BOUNDS at the 0.01 margin
