@@ -270,6 +270,24 @@ int sg_tracker_results(sg_tracker* t, float* to_xy, int32_t* accepted, int32_t* 
 /* Kernel timing (HIP events on the tracker's stream) of the last sg_tracker_run: total ms of the
  * tracking kernels and of the pyramid kernels of the last sg_tracker_set_image. */
 int sg_tracker_kernel_ms(sg_tracker* t, double* track_ms, double* pyramid_ms);
+
+/* ------------------------------------------------------------------------------------------------
+ * All-pairs 256-bit descriptor matching (the matcher's brute-force descriptor distance; BASELINE config 4).
+ * Descriptors are 4 x uint64 per row.  Per query row: best_idx = argmin over train rows of
+ * popcount(q XOR t) with ties to the lowest index, best_dist, and second_dist = the second-smallest
+ * distance (equal to best_dist on a tie); -1 where the train set is too small.
+ */
+typedef struct sg_matcher sg_matcher;
+int sg_matcher_create(sg_matcher** out, const sg_device_options* dev);
+void sg_matcher_destroy(sg_matcher* m);
+int sg_hamming_match(sg_matcher* m, const uint64_t* query, int32_t nq, const uint64_t* train, int32_t nt,
+                     int32_t* best_idx, int32_t* best_dist, int32_t* second_dist);
+/* Device-resident throughput path: load once, run `repeats` asynchronous passes, fetch results and the
+ * average kernel time per pass (HIP events). */
+int sg_hamming_load(sg_matcher* m, const uint64_t* query, int32_t nq, const uint64_t* train, int32_t nt);
+int sg_hamming_run(sg_matcher* m, int32_t repeats);
+int sg_hamming_results(sg_matcher* m, int32_t* best_idx, int32_t* best_dist, int32_t* second_dist,
+                       double* kernel_ms);
 int sg_slam_set_options(sg_slam* s, const sg_solver_options* o);
 
 #ifdef __cplusplus

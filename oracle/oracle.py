@@ -259,3 +259,22 @@ def track_fb(pyr_from, pyr_to, dims, win, from_xy, to_xy, levels=None, nthreads=
                         from_xy.ctypes.data_as(_fp), out.ctypes.data_as(_fp), lv.ctypes.data_as(_i32p),
                         acc.ctypes.data_as(_i32p), it.ctypes.data_as(_i32p), nthreads)
     return out, acc, it
+
+
+def hamming_match(q: np.ndarray, t: np.ndarray, nthreads: int = 1):
+    """All-pairs 256-bit Hamming: (best_idx, best_dist, second_dist) per query row."""
+    L = lib()
+    if not getattr(L, "_ham_ready", False):
+        _u64p = C.POINTER(C.c_uint64)
+        L.ort_hamming_match.argtypes = [_u64p, C.c_int, _u64p, C.c_int, _i32p, _i32p, _i32p, C.c_int]
+        L._ham_ready = True
+    q = np.ascontiguousarray(q, dtype=np.uint64).reshape(-1, 4)
+    t = np.ascontiguousarray(t, dtype=np.uint64).reshape(-1, 4)
+    nq = q.shape[0]
+    bi = np.zeros(nq, np.int32)
+    bd = np.zeros(nq, np.int32)
+    sd = np.zeros(nq, np.int32)
+    p64 = C.POINTER(C.c_uint64)
+    L.ort_hamming_match(q.ctypes.data_as(p64), nq, t.ctypes.data_as(p64), t.shape[0], bi.ctypes.data_as(_i32p),
+                        bd.ctypes.data_as(_i32p), sd.ctypes.data_as(_i32p), nthreads)
+    return bi, bd, sd

@@ -411,3 +411,32 @@ int ort_track_fb(const float* pyr_from, const float* pyr_to, const int32_t* dims
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------------------------------------
+// 256-bit descriptor all-pairs Hamming match (BASELINE config 4; SURVEY.md 8a row a19 — no reference
+// implementation exists, the specification is: distance = popcount(a XOR b) over 4 x u64, per query the
+// argmin over the train set with ties to the lowest train index, plus the second-smallest distance).
+extern "C" int ort_hamming_match(const uint64_t* q, int nq, const uint64_t* t, int nt, int32_t* best_idx,
+                                 int32_t* best_dist, int32_t* second_dist, int nthreads) {
+#pragma omp parallel for schedule(static) num_threads(nthreads > 0 ? nthreads : 1)
+  for (int i = 0; i < nq; ++i) {
+    const uint64_t* a = q + 4 * (size_t)i;
+    int bd = 1 << 30, sd = 1 << 30, bi = -1;
+    for (int j = 0; j < nt; ++j) {
+      const uint64_t* b = t + 4 * (size_t)j;
+      const int d = __builtin_popcountll(a[0] ^ b[0]) + __builtin_popcountll(a[1] ^ b[1]) +
+                    __builtin_popcountll(a[2] ^ b[2]) + __builtin_popcountll(a[3] ^ b[3]);
+      if (d < bd) {
+        sd = bd;
+        bd = d;
+        bi = j;
+      } else if (d < sd) {
+        sd = d;
+      }
+    }
+    best_idx[i] = bi;
+    best_dist[i] = nt > 0 ? bd : -1;
+    second_dist[i] = nt > 1 ? sd : -1;
+  }
+  return 0;
+}
