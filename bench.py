@@ -40,7 +40,96 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample (0: skip)")
     ap.add_argument("--sweep-obs", type=int, default=2_000_000,
                     help="observations in the scaled Jacobian-sweep measurement (0: skip)")
+    ap.add_argument("--frontend", type=int, default=1,
+                    help="also measure the front end at N=1: KLT tracks/sec (config 3) and the 256-bit "
+                         "Hamming matcher (config 4)")
     return ap.parse_args()
+
+
+FP32_PEAK_TFLOPS = 157.3     # MI355X FP32 vector peak
+INT_PEAK_TOPS = 78.6         # 32-bit integer VALU lane-ops/s: 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz
+
+
+def bench_tracker(local, cpu_seconds):
+    """BASELINE config 3: 640x480 synthetic video, 2000 tracks, 3-level pyramid, 7x7 window, forward/backward
+    TrackFeature (matcher.cpp:173-206).  Inputs resident on the device; value = tracks / kernel time."""
+    from slamgpu.tracker import HessianTracker
+    from slamgpu.video import make_frames, seed_points
+    frames = make_frames(2)
+    pts = seed_points(2000)
+    W, depth, reps = 7, 3, 50
+    t = HessianTracker(window=W, depth=depth, device=local, retry_levels=0)
+    t.MakePyramid(frames[0], 0)
+    t.MakePyramid(frames[1], 1)
+    _, pyr_ms = t.kernel_ms()
+    t.load_features(pts, pts)
+    t.run(0, 1, 3)
+    t.results()
+    t.run(0, 1, reps)
+    out, acc, its = t.results()
+    track_ms, _ = t.kernel_ms()
+    ms = track_ms / reps
+    value = len(pts) / (ms * 1e-3)
+    flops = float(its.sum()) * 108.0 * W * W        # SURVEY.md 8d: 108 W^2 flops per Newton iteration
+    ach = flops / (ms * 1e-3) / 1e12
+    res = {"metric": "KLT tracks/sec (640x480, 2000 tracks, 3 levels, 7x7, forward+backward)",
+           "value": value, "unit": "tracks/s", "ms_per_frame_tracking": ms, "ms_pyramid": pyr_ms,
+           "tracks_per_s_with_pyramid": len(pts) / ((ms + pyr_ms) * 1e-3),
+           "accepted_frac": float(acc.mean()), "newton_iterations": int(its.sum()),
+           "roofline": {"bound": "valu", "achieved": ach, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": ach / FP32_PEAK_TFLOPS, "traffic": None, "kernel": "k_track_fb",
+                        "note": "108*W^2 flops per Newton iteration (6 probes of bilinear sampling, moments, "
+                                "score); one wave per feature"}}
+    if cpu_seconds > 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        pf, dims = oracle.make_pyramid(frames[0], depth)
+        pt, _ = oracle.make_pyramid(frames[1], depth)
+        threads = min(16, os.cpu_count() or 1)
+        done, tc = 0, 0.0
+        while tc < cpu_seconds:
+            tt = time.perf_counter()
+            oracle.track_fb(pf, pt, dims, W, pts, pts, np.full(len(pts), depth, np.int32), nthreads=threads)
+            tc += time.perf_counter() - tt
+            done += len(pts)
+        res["cpu_baseline"] = {"value": done / tc, "unit": "tracks/s", "cores": threads, "kind": "port",
+                               "sample": "%d forward/backward tracks (oracle/oracle_track.cpp, OpenMP over "
+                                         "tracks) in %.1f s" % (done, tc)}
+    return res
+
+
+def bench_hamming(local, cpu_seconds):
+    """BASELINE config 4: 10k x 10k 256-bit descriptors, all pairs, best + second-best per query."""
+    from slamgpu.matcher import HammingMatcher, make_descriptor_sets
+    A, B, truth = make_descriptor_sets(10000)
+    m = HammingMatcher(device=local)
+    m.load(B, A)
+    m.run(3)
+    m.results()
+    reps = 20
+    m.run(reps)
+    bi, bd, sd, ms = m.results()
+    pairs = float(len(A)) * len(B)
+    ops = pairs * 16.0       # per pair: 8 x v_xor_b32 + 8 x v_bcnt_u32_b32 (accumulating) on 32-bit lanes
+    ach = ops / (ms * 1e-3) / 1e12
+    res = {"metric": "256-bit Hamming all-pairs query-rows/sec (10k x 10k)", "value": len(B) / (ms * 1e-3),
+           "unit": "rows/s", "pairs_per_s": pairs / (ms * 1e-3), "ms": ms,
+           "recall_of_true_matches": float((bi[truth >= 0] == truth[truth >= 0]).mean()),
+           "roofline": {"bound": "valu-int", "achieved": ach, "peak": INT_PEAK_TOPS, "unit": "Tops/s",
+                        "frac": ach / INT_PEAK_TOPS, "traffic": None, "kernel": "k_hamming_slices"}}
+    if cpu_seconds > 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        threads = min(16, os.cpu_count() or 1)
+        done, tc = 0, 0.0
+        while tc < cpu_seconds:
+            tt = time.perf_counter()
+            oracle.hamming_match(B, A, nthreads=threads)
+            tc += time.perf_counter() - tt
+            done += len(B)
+        res["cpu_baseline"] = {"value": done / tc, "unit": "rows/s", "cores": threads, "kind": "port",
+                               "sample": "%d query rows x 10k (oracle, popcnt, OpenMP) in %.1f s" % (done, tc)}
+    return res
 
 
 def dist_env():
@@ -185,9 +274,14 @@ def main():
                          "OpenMP) in %.1f s, chunks of 5 iterations each re-linearising at start"
                          % (done_iters, t_cpu)}
 
+    frontend = None
+    if args.frontend and n_gpus == 1:
+        cs = min(args.cpu_seconds, 4.0)
+        frontend = {"tracker": bench_tracker(local, cs), "hamming": bench_hamming(local, cs)}
+
     value = n_gpus * args.steps / elapsed
     line = {
-        "metric": "local-BA iters/sec (50 KF, 20k pts)",
+        "metric": "local-BA iters/sec (50 KF, 20k pts)",  # BASELINE metric; KLT tracks/sec under "frontend"
         "value": value,
         "unit": "iters/s",
         "n_gpus": n_gpus,
@@ -211,6 +305,7 @@ def main():
         "cpu_baseline": cpu,
         "speedup_vs_cpu": (value / cpu["value"]) if cpu else None,
         "lm_state": {"final_cost": summary_after["final_cost"], "radius": summary_after["trust_region_radius"]},
+        "frontend": frontend,
     }
     print(json.dumps(line), flush=True)
     if dist is not None:
