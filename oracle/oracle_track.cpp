@@ -318,11 +318,14 @@ int TrackFeature(const Tracker& T, const std::vector<Level>& src, const std::vec
 // matcher.cpp:173-206 (forward/backward TrackFeature) and the 3 -> 6 level retry of matcher.cpp:247-251.
 bool TrackFB(const Tracker& T, const std::vector<Level>& from, const std::vector<Level>& to, float fx, float fy,
              int levels, float* tx, float* ty, int* iters) {
+  // The backward pass is skipped when the forward pass failed: the reference runs it but rejects the feature
+  // either way (matcher.cpp:193), and it never modifies to_pt.  (Only the iteration count differs.)
   auto attempt = [&](int lv) {
     const int s1 = TrackFeature(T, from, to, fx, fy, lv, 0.001f, 10, tx, ty, iters);
+    if (s1) return false;
     float bx = fx, by = fy;
     const int s2 = TrackFeature(T, to, from, *tx, *ty, lv, 0.001f, 10, &bx, &by, iters);
-    if (s1 || s2) return false;
+    if (s2) return false;
     const float ex = fx - bx, ey = fy - by;   // Point2f difference, then cv::norm in double
     return !(std::sqrt((double)ex * ex + (double)ey * ey) > 0.3);
   };

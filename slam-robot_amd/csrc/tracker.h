@@ -37,6 +37,7 @@ class Tracker {
  private:
   struct Slot {
     DBuf<float> pyr;
+    DBuf<uint8_t> table;   // per-level {image, width, height} for the tracking kernel
     std::vector<int> w, h;
     std::vector<size_t> off;
     bool valid = false;

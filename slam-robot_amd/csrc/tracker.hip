@@ -224,12 +224,30 @@ __device__ __forceinline__ void get_patch(const LevelDev& L, float px, float py,
 struct TrackCtx {
   int W, len, max_it;
   float threshold;
-  const float* mask;   // [len]
   int lane;
   float mk[kNP];       // this lane's mask values
+  int pi[kNP], pj[kNP];   // this lane's patch pixels (row, column); pi = -1 past the patch
 };
 
-// BruteHessian (hessian.h:147-172) + the Newton step of Track.
+__device__ __forceinline__ void get_patch_ctx(const TrackCtx& c, const LevelDev& L, float px, float py, Tmpl& t) {
+  Geo g;
+  make_geo(px, py, c.W, L.w, L.h, g);
+  float s = 0.f, q = 0.f;
+#pragma unroll
+  for (int k = 0; k < kNP; ++k) {
+    float v = 0.f;
+    if (c.pi[k] >= 0) v = sample(L.img, L.w, g, c.pi[k], c.pj[k]);
+    t.v[k] = v;
+    s += v;
+    q += v * v;
+  }
+  s = wave_tree_sum(s);
+  q = wave_tree_sum(q);
+  t.mean = s / c.len;
+  t.sumsq = q / c.len;
+}
+
+// BruteHessian (hessian.h:147-172): the six probes sampled together, their sums reduced in batches.
 __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev& L, const Tmpl& tp, float x, float y,
                                               float* mdx, float* mdy, float* mdxx, float* mdxy, float* mdyx,
                                               float* mdyy) {
@@ -249,9 +267,8 @@ __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev&
     float s = 0.f, q = 0.f;
 #pragma unroll
     for (int k = 0; k < kNP; ++k) {
-      const int p = c.lane + 64 * k;
       float v = 0.f;
-      if (p < c.len) v = sample(L.img, L.w, g, p / c.W, p % c.W);
+      if (c.pi[k] >= 0) v = sample(L.img, L.w, g, c.pi[k], c.pj[k]);
       pv[r][k] = v;
       s += v;
       q += v * v;
@@ -295,49 +312,11 @@ __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev&
   *mdyx = (float)(((sadxy - sadp1x) / hh - (sadp1y - sad0) / hh) / hh);
 }
 
-// Track (hessian.h:185-241): 0 OK, 2 OUT_OF_BOUNDS.
-__device__ int track_level(const TrackCtx& c, const LevelDev& L, const Tmpl& tp, float* px, float* py, int* iters) {
-  float x = *px, y = *py;
-  const float margin = 0.01f;
-  int it = 0;
-  for (; it < c.max_it; ++it) {
-    if (x < margin || y < margin || (x + margin) > L.w || (y + margin) > L.h) {
-      *px = x;
-      *py = y;
-      *iters += it;
-      return 2;
-    }
-    float mdx, mdy, mdxx, mdxy, mdyx, mdyy;
-    brute_hessian(c, L, tp, x, y, &mdx, &mdy, &mdxx, &mdxy, &mdyx, &mdyy);
-    const double H00 = mdxx, H01 = mdxy, H10 = mdyx, H11 = mdyy;
-    const double det = H00 * H11 - H10 * H01;
-    const double invdet = 1.0 / det;
-    const double i00 = H11 * invdet, i10 = -H10 * invdet, i01 = -H01 * invdet, i11 = H00 * invdet;
-    const double g0 = mdx, g1 = mdy;
-    const double jj0 = i00 * g0 + i01 * g1, jj1 = i10 * g0 + i11 * g1;
-    float dx = (float)-jj0, dy = (float)-jj1;
-    if ((dx * dx + dy * dy) > 1) {
-      dx /= sqrtf(dx * dx + dy * dy);
-      dy /= sqrtf(dx * dx + dy * dy);   // with the updated dx, as the reference
-    }
-    const float cx = (dx < 1.f) ? dx : 1.f, cy = (dy < 1.f) ? dy : 1.f;   // std::min / std::max semantics
-    x += (-1.f < cx) ? cx : -1.f;
-    y += (-1.f < cy) ? cy : -1.f;
-    if (fabsf(dx) < c.threshold && fabsf(dy) < c.threshold) {
-      ++it;
-      break;
-    }
-  }
-  *iters += it;
-  *px = x;
-  *py = y;
-  return 0;
-}
-
-// TrackFeature (hessian.h:243-264) with the source templates of GetPatches (175-183).
-__device__ int track_feature(const TrackCtx& c, const PyrDev& src, const PyrDev& dst, float sx, float sy, int levels,
-                             float* px, float* py, int* iters) {
-  const int lvls = min(min(src.depth, dst.depth), levels);
+// One TrackFeature (hessian.h:243-264) pass: templates from `src` at (sx, sy) (GetPatches, 175-183), Newton
+// iterations of Track (185-241) on `dst` coarse to fine.  0 OK (*px, *py updated), 2 OUT_OF_BOUNDS.
+__device__ __forceinline__ int track_pass(const TrackCtx& c, const LevelDev* __restrict__ src,
+                                          const LevelDev* __restrict__ dst, int lvls, float sx, float sy, float* px,
+                                          float* py, int* iters) {
   const double s = 1. / (1 << (lvls - 1));
   float x = (float)(*px * s), y = (float)(*py * s);
   for (int i = lvls - 1; i >= 0; --i) {
@@ -346,10 +325,40 @@ __device__ int track_feature(const TrackCtx& c, const PyrDev& src, const PyrDev&
       tx = (float)(tx * 0.5);
       ty = (float)(ty * 0.5);
     }
+    const LevelDev Ls = src[i], Ld = dst[i];
     Tmpl tp;
-    get_patch(src.lv[i], tx, ty, c.W, c.lane, tp);
-    const int st = track_level(c, dst.lv[i], tp, &x, &y, iters);
-    if (st != 0) return st;
+    get_patch_ctx(c, Ls, tx, ty, tp);
+    const float margin = 0.01f;
+    int it = 0;
+    bool oob = false;
+    for (; it < c.max_it; ++it) {
+      if (x < margin || y < margin || (x + margin) > Ld.w || (y + margin) > Ld.h) {
+        oob = true;
+        break;
+      }
+      float mdx, mdy, mdxx, mdxy, mdyx, mdyy;
+      brute_hessian(c, Ld, tp, x, y, &mdx, &mdy, &mdxx, &mdxy, &mdyx, &mdyy);
+      const double H00 = mdxx, H01 = mdxy, H10 = mdyx, H11 = mdyy;
+      const double det = H00 * H11 - H10 * H01;
+      const double invdet = 1.0 / det;
+      const double i00 = H11 * invdet, i10 = -H10 * invdet, i01 = -H01 * invdet, i11 = H00 * invdet;
+      const double g0 = mdx, g1 = mdy;
+      const double jj0 = i00 * g0 + i01 * g1, jj1 = i10 * g0 + i11 * g1;
+      float dx = (float)-jj0, dy = (float)-jj1;
+      if ((dx * dx + dy * dy) > 1) {
+        dx /= sqrtf(dx * dx + dy * dy);
+        dy /= sqrtf(dx * dx + dy * dy);   // with the updated dx, as the reference
+      }
+      const float cx = (dx < 1.f) ? dx : 1.f, cy = (dy < 1.f) ? dy : 1.f;   // std::min / std::max semantics
+      x += (-1.f < cx) ? cx : -1.f;
+      y += (-1.f < cy) ? cy : -1.f;
+      if (fabsf(dx) < c.threshold && fabsf(dy) < c.threshold) {
+        ++it;
+        break;
+      }
+    }
+    *iters += it;
+    if (oob) return 2;
     if (i > 0) {
       x = (float)(x * 2.);
       y = (float)(y * 2.);
@@ -360,10 +369,14 @@ __device__ int track_feature(const TrackCtx& c, const PyrDev& src, const PyrDev&
   return 0;
 }
 
-__global__ __launch_bounds__(64 * kTrackWaves) void k_track_fb(PyrDev from, PyrDev to, TrackParams prm, int n,
-                                                               const float* from_xy, const float* to_init,
-                                                               const int32_t* levels, float* to_xy,
-                                                               int32_t* accepted, int32_t* iterations) {
+// matcher.cpp TrackFeature (173-206) + FindMatches' retry with more levels (247-251), one wave per feature.
+// The attempt and pass loops share one inlined body.  The backward pass is skipped when the forward pass
+// failed: the matcher rejects the feature either way and the backward pass does not touch to_pt.
+__global__ __launch_bounds__(64 * kTrackWaves) void k_track_fb(const LevelDev* __restrict__ from_lv,
+                                                               const LevelDev* __restrict__ to_lv, int depth,
+                                                               TrackParams prm, int n, const float* from_xy,
+                                                               const float* to_init, const int32_t* levels,
+                                                               float* to_xy, int32_t* accepted, int32_t* iterations) {
   const int lane = threadIdx.x & 63;
   const int f = blockIdx.x * kTrackWaves + (threadIdx.x >> 6);
   if (f >= n) return;   // whole wave
@@ -372,27 +385,49 @@ __global__ __launch_bounds__(64 * kTrackWaves) void k_track_fb(PyrDev from, PyrD
   c.len = prm.window * prm.window;
   c.max_it = prm.max_iterations;
   c.threshold = prm.threshold;
-  c.mask = prm.mask;
   c.lane = lane;
 #pragma unroll
   for (int k = 0; k < kNP; ++k) {
     const int p = lane + 64 * k;
-    c.mk[k] = p < c.len ? prm.mask[p] : 0.f;
+    const bool in = p < c.len;
+    c.mk[k] = in ? prm.mask[p] : 0.f;
+    c.pi[k] = in ? p / c.W : -1;
+    c.pj[k] = in ? p % c.W : 0;
   }
   const float fx = from_xy[2 * f], fy = from_xy[2 * f + 1];
   float tx = to_init[2 * f], ty = to_init[2 * f + 1];
   const int lv0 = levels ? levels[f] : 3;
   int iters = 0;
-  auto attempt = [&](int lv) {
-    const int s1 = track_feature(c, from, to, fx, fy, lv, &tx, &ty, &iters);
+  bool ok = false;
+  for (int attempt = 0; attempt < 2 && !ok; ++attempt) {
+    int lv = lv0;
+    if (attempt == 1) {
+      if (prm.retry_levels <= 0 || lv0 == prm.retry_levels) break;
+      lv = prm.retry_levels;
+    }
+    const int lvls = min(depth, lv);
+    int st = 0;
     float bx = fx, by = fy;
-    const int s2 = track_feature(c, to, from, tx, ty, lv, &bx, &by, &iters);
-    if (s1 || s2) return false;
-    const float ex = fx - bx, ey = fy - by;
-    return !(sqrt((double)ex * ex + (double)ey * ey) > (double)prm.fb_max);
-  };
-  bool ok = attempt(lv0);
-  if (!ok && prm.retry_levels > 0 && lv0 != prm.retry_levels) ok = attempt(prm.retry_levels);
+    for (int pass = 0; pass < 2; ++pass) {
+      const LevelDev* src = pass ? to_lv : from_lv;
+      const LevelDev* dst = pass ? from_lv : to_lv;
+      const float sx = pass ? tx : fx, sy = pass ? ty : fy;
+      float qx = pass ? bx : tx, qy = pass ? by : ty;
+      st = track_pass(c, src, dst, lvls, sx, sy, &qx, &qy, &iters);
+      if (st != 0) break;
+      if (pass == 0) {
+        tx = qx;
+        ty = qy;
+      } else {
+        bx = qx;
+        by = qy;
+      }
+    }
+    if (st == 0) {
+      const float ex = fx - bx, ey = fy - by;
+      ok = !(sqrt((double)ex * ex + (double)ey * ey) > (double)prm.fb_max);
+    }
+  }
   if (lane == 0) {
     to_xy[2 * f] = tx;
     to_xy[2 * f + 1] = ty;
@@ -521,6 +556,13 @@ void Tracker::SetImage(int slot, const uint8_t* bgr, int w, int h, int stride) {
   }
   SG_HIP_CHECK(hipEventRecord(ev_[3], stream_));
   SG_HIP_CHECK(hipGetLastError());
+  // level table for the tracking kernel: {image, width, height} per level (scalar-loaded on the device)
+  std::vector<uint8_t> tab(sizeof(LevelDev) * opt_.depth);
+  for (int l = 0; l < opt_.depth; ++l) {
+    LevelDev L{s.pyr.ptr + s.off[l], s.w[l], s.h[l]};
+    std::memcpy(tab.data() + sizeof(LevelDev) * l, &L, sizeof(L));
+  }
+  s.table.Upload(tab, stream_);
   SG_HIP_CHECK(hipStreamSynchronize(stream_));   // the host image buffer may be reused by the caller
   float ms = 0.f;
   SG_HIP_CHECK(hipEventElapsedTime(&ms, ev_[2], ev_[3]));
@@ -587,18 +629,13 @@ void Tracker::Run(int from, int to, int repeats) {
   const Slot& b = slots_[to];
   SG_REQUIRE(a.w == b.w && a.h == b.h, SG_EINVAL, "pyramids of different sizes");
   SG_HIP_CHECK(hipSetDevice(dev_.device));
-  PyrDev pf{}, pt{};
-  pf.depth = pt.depth = opt_.depth;
-  for (int l = 0; l < opt_.depth; ++l) {
-    pf.lv[l] = LevelDev{a.pyr.ptr + a.off[l], a.w[l], a.h[l]};
-    pt.lv[l] = LevelDev{b.pyr.ptr + b.off[l], b.w[l], b.h[l]};
-  }
   TrackParams prm{opt_.window, opt_.max_iterations, opt_.threshold, opt_.fb_max, opt_.retry_levels, mask_.ptr};
   SG_HIP_CHECK(hipEventRecord(ev_[0], stream_));
   if (n_ > 0)
     for (int r = 0; r < repeats; ++r)
-      hipLaunchKernelGGL(k_track_fb, dim3((n_ + kTrackWaves - 1) / kTrackWaves), dim3(64 * kTrackWaves), 0, stream_, pf,
-                         pt, prm, n_, from_.ptr, init_.ptr, levels_.ptr, out_.ptr, acc_.ptr, its_.ptr);
+      hipLaunchKernelGGL(k_track_fb, dim3((n_ + kTrackWaves - 1) / kTrackWaves), dim3(64 * kTrackWaves), 0, stream_,
+                         (const LevelDev*)a.table.ptr, (const LevelDev*)b.table.ptr, opt_.depth, prm, n_, from_.ptr,
+                         init_.ptr, levels_.ptr, out_.ptr, acc_.ptr, its_.ptr);
   SG_HIP_CHECK(hipEventRecord(ev_[1], stream_));
   SG_HIP_CHECK(hipGetLastError());
   ran_ = true;
