@@ -14,6 +14,8 @@
 #ifndef SG_BA_KERNELS_H_
 #define SG_BA_KERNELS_H_
 
+#include <hip/hip_runtime.h>
+
 #include <cstdint>
 
 namespace sg {
@@ -21,7 +23,7 @@ namespace sg {
 constexpr int kChunkPts = 128;      // points per chunk (one workgroup)
 constexpr int kLanesPerPt = 4;      // lanes per point in the observation sweeps
 constexpr int kSweepThreads = kChunkPts * kLanesPerPt;  // 512
-constexpr int kSchurThreads = 256;
+constexpr int kSchurThreads = 512;
 constexpr int kNbwMax = 24;         // max camera blocks in a chunk window (wider points go "wide")
 constexpr int kCamV = 27;           // per camera block: upper(Jc^T Jc) 21 + Jc^T r 6
 constexpr int kJStride = 24;
@@ -131,6 +133,11 @@ struct Dev {
   double* work;                  // [n] solver scratch
   const int32_t* fd_pair;        // [NB][NB] (I<J): FrameDistance residual coupling blocks I and J, or -1
   int32_t assemble;              // this rank adds blockdiag(U) + FD + damping to S (rank 0 of a shard group)
+  int32_t dbg;                   // development switches (SG_DBG), 0 in production
+  const int32_t* obs_pnt;        // [M] point (device order) of each observation
+  const int32_t* seg_off;        // [nchunks+1] Schur segments per chunk
+  const int4* segs;              // {point lo, point hi, pair lo, pair hi}
+  const int2* pairs;             // {(s << 16) | t local observation indices, (b_s << 16) | b_t}
   unsigned long long* stamps;    // diagnostic builds only: per-phase cycle counters (nullptr otherwise)
 };
 

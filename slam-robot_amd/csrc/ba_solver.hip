@@ -508,19 +508,35 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_schur: one chunk per workgroup, one wave per point.  Damped, scaled point block V~ = S V S + D^2
-// (LL^T inverse), then every pair (s, t) of the point's observations on free frames contributes
-// -A_c,s^T (A_p,s V~^-1 A_p,t^T) A_c,t to the window block (b_s, b_t) in LDS, and the right-hand side
-// gets -A_c,s^T A_p,s V~^-1 g~_p.  The point's scaled observation Jacobians are staged once in a per-wave
-// LDS slab (each observation read from HBM once); lanes of a wave then hold distinct pairs -> distinct
-// LDS accumulator addresses.
-constexpr int kStageK = 32;      // observations per point staged in LDS (longer tracks read from L2)
-constexpr int kStageW = 28;      // Jc 12 | P = Jp V^-1 8 | Jp 8
+// k_schur: one chunk per workgroup, in point segments whose observations fit the LDS stage.  Three
+// fully parallel phases per segment (no per-point serialisation):
+//   1. thread per point: damped, scaled point block V~ = S V S + D^2, its inverse (LL^T) and t = V~^-1 g~
+//      (also written to global memory for k_point_update);
+//   2. thread per observation: P_o = J~p,o V~^-1 staged in LDS, and the rhs term -A_c,o^T (A_p,o t_p);
+//   3. thread per observation pair (s <= t) of a point, from a pair list built at load time: the 6x6 block
+//      -A_c,s^T (P_s A_p,t^T) A_c,t accumulated into the chunk's window of the reduced system (LDS atomics;
+//      windows wider than kNbwMax blocks go to global atomics).
+constexpr int kSchurLdsBytes = 150 * 1024;
 
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes have landed
-  __builtin_amdgcn_wave_barrier();
-  asm volatile("" ::: "memory");
+__device__ __forceinline__ void load_Jc_scaled(const Dev& d, int o, int b, double* Jc) {
+  const double2* J2 = reinterpret_cast<const double2*>(d.J + (size_t)o * kJStride) + 1;   // skip r
+  const double* sc = d.scale_c + 6 * b;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const double2 v = J2[i];
+    Jc[2 * i] = v.x * sc[(2 * i) % 6];
+    Jc[2 * i + 1] = v.y * sc[(2 * i + 1) % 6];
+  }
+}
+__device__ __forceinline__ void load_Jp_scaled(const Dev& d, int o, const double4& s4, double* Jp) {
+  const double2* J2 = reinterpret_cast<const double2*>(d.J + (size_t)o * kJStride) + 7;   // r 2 | Jc 12
+  const double sp[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const double2 v = J2[i];
+    Jp[2 * i] = v.x * sp[(2 * i) % 4];
+    Jp[2 * i + 1] = v.y * sp[(2 * i + 1) % 4];
+  }
 }
 
 __device__ __forceinline__ void schur_pair_add(double* dst, int ld, const double* Jcs, const double* Ps,
@@ -556,94 +572,103 @@ __device__ __forceinline__ void schur_pair_add(double* dst, int ld, const double
 __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d) {
   const LmState* st = d.st;
   if (st->done) return;
-  extern __shared__ double win[];
-  __shared__ double stage[kSchurThreads / 64][kStageK][kStageW];
-  __shared__ int sblk[kSchurThreads / 64][kStageK];
+  extern __shared__ double lds[];
   __shared__ double red[kSchurThreads / 64];
   const Chunk ch = d.chunks[blockIdx.x];
   const int npair = ch.nb * (ch.nb + 1) / 2;
   const int nwin = ch.wide ? 0 : npair * 36 + ch.nb * 6;
+  double* win = lds;
   double* rhsw = win + npair * 36;
-  for (int i = threadIdx.x; i < nwin; i += blockDim.x) win[i] = 0.0;
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  double (*stg)[kStageW] = stage[wave];
-  int* sb = sblk[wave];
+  double* vinv = lds + nwin;                  // [kChunkPts][10]
+  double* tpv = vinv + kChunkPts * 10;        // [kChunkPts][4]
+  double* Psh = tpv + kChunkPts * 4;          // [capP][8]
+  const int tid = threadIdx.x;
+  for (int i = tid; i < nwin; i += kSchurThreads) win[i] = 0.0;
   const double radius = st->radius;
   const bool reuse = st->reuse_diag != 0;
   double linfail = 0.0;
-  for (int p = ch.p0 + wave; p < ch.p1; p += kSchurThreads / 64) {
-    if (!d.pfree[p]) continue;
-    const double* Vp = d.V + 10 * (size_t)p;
-    double V[10];
+  const int sg0 = d.seg_off[blockIdx.x], sg1 = d.seg_off[blockIdx.x + 1];
+  for (int sgi = sg0; sgi < sg1; ++sgi) {
+    const int4 sg = d.segs[sgi];
+    const int q0 = sg.x, q1 = sg.y;
+    const int obs_lo = d.poff[q0], obs_hi = d.poff[q1];
+    __syncthreads();   // the previous segment's phase 3 is done with the stage
+    // phase 1: one thread per point
+    for (int t = tid; t < q1 - q0; t += kSchurThreads) {
+      const int p = q0 + t;
+      if (!d.pfree[p]) continue;
+      const double* Vp = d.V + 10 * (size_t)p;
+      double V[10];
 #pragma unroll
-    for (int i = 0; i < 10; ++i) V[i] = Vp[i];
-    const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
-    const double sp[4] = {s4.x, s4.y, s4.z, s4.w};
-    const double4 g4 = reinterpret_cast<const double4*>(d.g)[p];
-    const double gs[4] = {g4.x * sp[0], g4.y * sp[1], g4.z * sp[2], g4.w * sp[3]};
-    double dp[4];
-    if (!reuse) {
+      for (int i = 0; i < 10; ++i) V[i] = Vp[i];
+      const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
+      const double sp[4] = {s4.x, s4.y, s4.z, s4.w};
+      const double4 g4 = reinterpret_cast<const double4*>(d.g)[p];
+      const double gs[4] = {g4.x * sp[0], g4.y * sp[1], g4.z * sp[2], g4.w * sp[3]};
+      double dp[4];
+      if (!reuse) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a) dp[a] = fmin(fmax(sp[a] * sp[a] * V[u4(a, a)], st->min_diag), st->max_diag);
+        reinterpret_cast<double4*>(d.diag_p)[p] = make_double4(dp[0], dp[1], dp[2], dp[3]);
+      } else {
+        const double4 d4 = reinterpret_cast<const double4*>(d.diag_p)[p];
+        dp[0] = d4.x; dp[1] = d4.y; dp[2] = d4.z; dp[3] = d4.w;
+      }
+      double Vt[10];
 #pragma unroll
       for (int a = 0; a < 4; ++a)
-        dp[a] = fmin(fmax(sp[a] * sp[a] * V[u4(a, a)], st->min_diag), st->max_diag);
-      if (lane == 0) reinterpret_cast<double4*>(d.diag_p)[p] = make_double4(dp[0], dp[1], dp[2], dp[3]);
-    } else {
-      const double4 d4 = reinterpret_cast<const double4*>(d.diag_p)[p];
-      dp[0] = d4.x; dp[1] = d4.y; dp[2] = d4.z; dp[3] = d4.w;
-    }
-    double Vt[10];
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+        for (int c = 0; c < 4; ++c)
+          if (c >= a) Vt[u4(a, c)] = sp[a] * V[u4(a, c)] * sp[c] + (a == c ? dp[a] / radius : 0.0);
+      double Vi[10];
+      if (!inv4_spd(Vt, Vi)) {
+        linfail += 1.0;
 #pragma unroll
-      for (int c = 0; c < 4; ++c)
-        if (c >= a) Vt[u4(a, c)] = sp[a] * V[u4(a, c)] * sp[c] + (a == c ? dp[a] / radius : 0.0);
-    double Vi[10];
-    if (!inv4_spd(Vt, Vi)) {
-      linfail += (lane == 0) ? 1.0 : 0.0;
+        for (int i = 0; i < 10; ++i) Vi[i] = NAN;
+      }
+      double tp[4];
 #pragma unroll
-      for (int i = 0; i < 10; ++i) Vi[i] = NAN;
-    }
-    double tp[4];
+      for (int a = 0; a < 4; ++a) {
+        double s = 0.0;
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      double s = 0.0;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) s += sym4(Vi, a, c) * gs[c];
-      tp[a] = s;
-    }
-    if (lane == 0) {
+        for (int c = 0; c < 4; ++c) s += sym4(Vi, a, c) * gs[c];
+        tp[a] = s;
+      }
       double* Vo = d.Vinv + 10 * (size_t)p;
 #pragma unroll
-      for (int i = 0; i < 10; ++i) Vo[i] = Vi[i];
-      reinterpret_cast<double4*>(d.tp)[p] = make_double4(tp[0], tp[1], tp[2], tp[3]);
-    }
-    const int o0 = d.poff[p], k = d.poff[p + 1] - o0;
-    const bool staged = k <= kStageK;
-    // stage: scaled Jc, P = Jp V~^-1, Jp of every observation; right-hand side -A_c,s^T (A_p,s t_p)
-    for (int s = lane; s < k; s += 64) {
-      const int o = o0 + s;
-      const int b = d.obs_fixed[o] ? -1 : d.frame_block[d.obs_frame[o]];
-      double r[2], Jc[12], Jp[8];
-      load_scaled_J(d, o, b < 0 ? 0 : b, sp, r, Jc, Jp);
-      if (staged) {
-        sb[s] = b;
-        double* row = stg[s];
-#pragma unroll
-        for (int i = 0; i < 12; ++i) row[i] = Jc[i];
-#pragma unroll
-        for (int rr = 0; rr < 2; ++rr)
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            double acc = 0.0;
-#pragma unroll
-            for (int m = 0; m < 4; ++m) acc += Jp[4 * rr + m] * sym4(Vi, m, c);
-            row[12 + 4 * rr + c] = acc;
-          }
-#pragma unroll
-        for (int i = 0; i < 8; ++i) row[20 + i] = Jp[i];
+      for (int i = 0; i < 10; ++i) {
+        Vo[i] = Vi[i];
+        vinv[10 * t + i] = Vi[i];
       }
+      reinterpret_cast<double4*>(d.tp)[p] = make_double4(tp[0], tp[1], tp[2], tp[3]);
+#pragma unroll
+      for (int a = 0; a < 4; ++a) tpv[4 * t + a] = tp[a];
+    }
+    __syncthreads();
+    // phase 2: one thread per observation
+    for (int o = obs_lo + tid; o < obs_hi; o += kSchurThreads) {
+      const int p = d.obs_pnt[o];
+      if (!d.pfree[p]) continue;
+      const int lp = p - q0;
+      const int b = d.frame_block[d.obs_frame[o]];
+      const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
+      double Jp[8];
+      load_Jp_scaled(d, o, s4, Jp);
+      const double* Vi = vinv + 10 * lp;
+      double* Pr = Psh + 8 * (o - obs_lo);
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          double acc = 0.0;
+#pragma unroll
+          for (int m = 0; m < 4; ++m) acc += Jp[4 * rr + m] * sym4(Vi, m, c);
+          Pr[4 * rr + c] = acc;
+        }
       if (b < 0) continue;
+      double Jc[12];
+      load_Jc_scaled(d, o, b, Jc);
+      const double* tp = tpv + 4 * lp;
       const double e0 = Jp[0] * tp[0] + Jp[1] * tp[1] + Jp[2] * tp[2] + Jp[3] * tp[3];
       const double e1 = Jp[4] * tp[0] + Jp[5] * tp[1] + Jp[6] * tp[2] + Jp[7] * tp[3];
 #pragma unroll
@@ -653,58 +678,33 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d) {
         else atomicAdd(rhsw + (b - ch.b_lo) * 6 + a, v);
       }
     }
-    wave_lds_sync();
-    // pairs (s <= t)
-    const int np = k * (k + 1) / 2;
-    for (int pi = lane; pi < np; pi += 64) {
-      int s = 0, rem = pi;
-      while (rem >= k - s) { rem -= k - s; ++s; }
-      const int t = s + rem;
-      double Jcs[12], Ps[8], Jpt[8], Jct[12];
-      int bs, bt;
-      if (staged) {
-        bs = sb[s];
-        bt = sb[t];
-        if (bs < 0 || bt < 0) continue;
+    __syncthreads();
+    // phase 3: one thread per observation pair
+    for (int k = sg.z + tid; k < sg.w; k += kSchurThreads) {
+      const int2 pr = d.pairs[k];
+      const int os = obs_lo + (pr.x >> 16), ot = obs_lo + (pr.x & 0xffff);
+      const int bs = pr.y >> 16, bt = pr.y & 0xffff;
+      const int p = d.obs_pnt[os];
+      const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
+      double Jcs[12], Jct[12], Jpt[8];
+      load_Jc_scaled(d, os, bs, Jcs);
+      load_Jc_scaled(d, ot, bt, Jct);
+      load_Jp_scaled(d, ot, s4, Jpt);
+      double Ps[8];
 #pragma unroll
-        for (int i = 0; i < 12; ++i) Jcs[i] = stg[s][i];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) Ps[i] = stg[s][12 + i];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) Jpt[i] = stg[t][20 + i];
-#pragma unroll
-        for (int i = 0; i < 12; ++i) Jct[i] = stg[t][i];
-      } else {
-        const int os = o0 + s, ot = o0 + t;
-        bs = d.obs_fixed[os] ? -1 : d.frame_block[d.obs_frame[os]];
-        bt = d.obs_fixed[ot] ? -1 : d.frame_block[d.obs_frame[ot]];
-        if (bs < 0 || bt < 0) continue;
-        double r[2], Jps[8];
-        load_scaled_J(d, os, bs, sp, r, Jcs, Jps);
-        load_scaled_J(d, ot, bt, sp, r, Jct, Jpt);
-#pragma unroll
-        for (int rr = 0; rr < 2; ++rr)
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            double acc = 0.0;
-#pragma unroll
-            for (int m = 0; m < 4; ++m) acc += Jps[4 * rr + m] * sym4(Vi, m, c);
-            Ps[4 * rr + c] = acc;
-          }
-      }
+      for (int i = 0; i < 8; ++i) Ps[i] = Psh[8 * (os - obs_lo) + i];
       const int I = bs < bt ? bs : bt, Jb = bs < bt ? bt : bs;
       if (ch.wide)
-        schur_pair_add(d.S_wide + (size_t)(6 * I) * d.n + 6 * Jb, d.n, Jcs, Ps, Jpt, Jct, s == t, bs == bt, bs < bt);
+        schur_pair_add(d.S_wide + (size_t)(6 * I) * d.n + 6 * Jb, d.n, Jcs, Ps, Jpt, Jct, os == ot, bs == bt, bs < bt);
       else
-        schur_pair_add(win + wp(I - ch.b_lo, Jb - ch.b_lo, ch.nb) * 36, 6, Jcs, Ps, Jpt, Jct, s == t, bs == bt,
+        schur_pair_add(win + wp(I - ch.b_lo, Jb - ch.b_lo, ch.nb) * 36, 6, Jcs, Ps, Jpt, Jct, os == ot, bs == bt,
                        bs < bt);
     }
-    wave_lds_sync();   // the next point reuses this wave's stage
   }
   linfail = block_sum<kSchurThreads>(linfail, red);
-  if (threadIdx.x == 0) d.chunk_scal[(size_t)blockIdx.x * kNScal + kLinFail] = linfail;
+  if (tid == 0) d.chunk_scal[(size_t)blockIdx.x * kNScal + kLinFail] = linfail;
   __syncthreads();
-  for (int i = threadIdx.x; i < nwin; i += blockDim.x) d.S_slab[ch.s_off + i] = win[i];
+  for (int i = tid; i < nwin; i += kSchurThreads) d.S_slab[ch.s_off + i] = win[i];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1733,6 +1733,48 @@ void BaSolver::Load(const sg_problem& p) {
     i = j;
   }
   nchunks_ = (int)chunks_.size();
+  // Schur work lists: per chunk, point segments whose observations fit the LDS stage, and per segment the
+  // observation pairs (s <= t, both on free frames) of its free points
+  std::vector<int32_t> obs_pnt(M_), seg_off(nchunks_ + 1, 0);
+  std::vector<int32_t> segs_flat, pairs_flat;   // int4 per segment, int2 per pair
+  for (int i = 0; i < P_; ++i)
+    for (int o = poff[i]; o < poff[i + 1]; ++o) obs_pnt[o] = i;
+  for (int c = 0; c < nchunks_; ++c) {
+    const Chunk& ch = chunks_[c];
+    const int nwin = ch.wide ? 0 : ch.nb * (ch.nb + 1) / 2 * 36 + ch.nb * 6;
+    const int capP = (int)((kSchurLdsBytes / 8 - nwin - kChunkPts * 14) / 8);
+    SG_REQUIRE(capP >= 64, SG_EINVAL, "Schur stage too small");
+    int q = ch.p0;
+    while (q < ch.p1) {
+      int q1 = q, nobs = 0;
+      while (q1 < ch.p1 && (q1 == q || nobs + (poff[q1 + 1] - poff[q1]) <= capP)) {
+        nobs += poff[q1 + 1] - poff[q1];
+        ++q1;
+      }
+      SG_REQUIRE(nobs <= capP && nobs < 65536, SG_EINVAL, "a point has more observations than the Schur stage");
+      const int obs_lo = poff[q];
+      const int pair_lo = (int)pairs_flat.size() / 2;
+      for (int pt = q; pt < q1; ++pt) {
+        if (!pfree[pt]) continue;
+        for (int os = poff[pt]; os < poff[pt + 1]; ++os) {
+          const int bs = frame_block[obs_frame[os]];
+          if (bs < 0) continue;
+          for (int ot = os; ot < poff[pt + 1]; ++ot) {
+            const int bt = frame_block[obs_frame[ot]];
+            if (bt < 0) continue;
+            pairs_flat.push_back(((os - obs_lo) << 16) | (ot - obs_lo));
+            pairs_flat.push_back((bs << 16) | bt);
+          }
+        }
+      }
+      segs_flat.insert(segs_flat.end(), {q, q1, pair_lo, (int)pairs_flat.size() / 2});
+      q = q1;
+    }
+    seg_off[c + 1] = (int)segs_flat.size() / 4;
+  }
+  SG_REQUIRE(NB_ < 65536, SG_EINVAL, "too many camera blocks");
+  if (pairs_flat.empty()) pairs_flat.assign(2, 0);
+  if (segs_flat.empty()) segs_flat.assign(4, 0);
   // deterministic reduction lists: for every camera block / block pair, the slab offsets of the chunk
   // partials that cover it (fixed chunk order)
   std::vector<int32_t> cam_loff(NB_ + 1, 0), cam_lidx, r_loff(NB_ + 1, 0), r_lidx;
@@ -1844,6 +1886,10 @@ void BaSolver::Load(const sg_problem& p) {
   obs_frame_.Upload(obs_frame, s);
   obs_fixed_.Upload(obs_fixed, s);
   chunks_d_.Upload(chunks_, s);
+  obs_pnt_.Upload(obs_pnt.empty() ? std::vector<int32_t>{0} : obs_pnt, s);
+  seg_off_.Upload(seg_off, s);
+  segs_.Upload(segs_flat, s);
+  pairs_.Upload(pairs_flat, s);
   cam_loff_.Upload(cam_loff, s);
   cam_lidx_.Upload(cam_lidx, s);
   s_loff_.Upload(s_loff, s);
@@ -1900,10 +1946,9 @@ void BaSolver::Load(const sg_problem& p) {
   rhs_.Zero(s);
   chunk_scal_.Zero(s);
   S_.Zero(s);
-  schur_lds_ = (size_t)(max_nb_ * (max_nb_ + 1) / 2 * 36 + max_nb_ * 6) * sizeof(double);
-  if (schur_lds_ > 0)
-    SG_HIP_CHECK(hipFuncSetAttribute((const void*)k_schur, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)std::max<size_t>(schur_lds_, 1)));
+  schur_lds_ = kSchurLdsBytes;
+  SG_HIP_CHECK(hipFuncSetAttribute((const void*)k_schur, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)schur_lds_));
   SG_HIP_CHECK(hipFuncSetAttribute((const void*)k_cholesky_window<false>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCholLds));
   SG_HIP_CHECK(hipFuncSetAttribute((const void*)k_cholesky_window<true>,
@@ -1990,7 +2035,12 @@ Dev BaSolver::MakeDev() {
   d.work = work_.ptr;
   d.stamps = stamp_on_ ? stamps_.ptr : nullptr;
   d.fd_pair = fd_pair_.ptr;
+  d.obs_pnt = obs_pnt_.ptr;
+  d.seg_off = seg_off_.ptr;
+  d.segs = reinterpret_cast<const int4*>(segs_.ptr);
+  d.pairs = reinterpret_cast<const int2*>(pairs_.ptr);
   d.assemble = (!comm_ || comm_->rank() == 0) ? 1 : 0;
+  d.dbg = getenv("SG_DBG") ? atoi(getenv("SG_DBG")) : 0;
   return d;
 }
 
