@@ -23,7 +23,7 @@ namespace sg {
 constexpr int kChunkPts = 128;      // points per chunk (one workgroup)
 constexpr int kLanesPerPt = 4;      // lanes per point in the observation sweeps
 constexpr int kSweepThreads = kChunkPts * kLanesPerPt;  // 512
-constexpr int kSchurThreads = 512;
+constexpr int kSchurThreads = 256;
 constexpr int kNbwMax = 24;         // max camera blocks in a chunk window (wider points go "wide")
 constexpr int kCamV = 27;           // per camera block: upper(Jc^T Jc) 21 + Jc^T r 6
 constexpr int kJStride = 24;
@@ -48,6 +48,19 @@ struct Chunk {
   int32_t s_off;      // offset of this chunk's Schur window in S_slab (doubles)
   int32_t wide;       // window too wide for LDS: accumulate with global atomics instead
   int32_t pad;
+};
+
+// Schur work unit: up to kSegPts consecutive points (device order) sharing a window of <= kSegNbMax
+// camera blocks (or one "wide" point), with its slice of the observation-pair list.
+constexpr int kSegPts = 32;
+constexpr int kSegObsCap = 256;
+constexpr int kSegNbMax = 20;
+struct SchurSeg {
+  int32_t p0, p1;       // point range
+  int32_t b_lo, nb;     // window [b_lo, b_lo + nb)
+  int32_t s_off;        // offset of the window partial in S_slab
+  int32_t wide;         // global atomics instead of an LDS window
+  int32_t pair_lo, pair_hi;
 };
 
 struct LmState {
@@ -135,8 +148,9 @@ struct Dev {
   int32_t assemble;              // this rank adds blockdiag(U) + FD + damping to S (rank 0 of a shard group)
   int32_t dbg;                   // development switches (SG_DBG), 0 in production
   const int32_t* obs_pnt;        // [M] point (device order) of each observation
-  const int32_t* seg_off;        // [nchunks+1] Schur segments per chunk
-  const int4* segs;              // {point lo, point hi, pair lo, pair hi}
+  const struct SchurSeg* segs;   // [nseg] Schur work units
+  int32_t nseg;
+  double* seg_fail;              // [nseg] point blocks whose damped inverse failed
   const int2* pairs;             // {(s << 16) | t local observation indices, (b_s << 16) | b_t}
   unsigned long long* stamps;    // diagnostic builds only: per-phase cycle counters (nullptr otherwise)
 };

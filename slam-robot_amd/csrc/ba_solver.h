@@ -75,7 +75,10 @@ class BaSolver {
   DBuf<Chunk> chunks_d_;
   DBuf<int32_t> work_i_;   // Cholesky panel envelopes (panel_jmax)
   DBuf<int32_t> fd_pair_;
-  DBuf<int32_t> obs_pnt_, seg_off_, segs_, pairs_;   // Schur work lists  // FrameDistance cross-block lookup
+  DBuf<int32_t> obs_pnt_, pairs_;   // Schur work lists
+  DBuf<SchurSeg> segs_;
+  DBuf<double> seg_fail_;
+  int nseg_ = 0, max_seg_nb_ = 0, max_seg_obs_ = 0;  // FrameDistance cross-block lookup
   DBuf<double> rdg_;       // 1/U_jj of the factor
   DBuf<double> mk_, mq_, mt_, mX_, mobs_pt_, mobs_err_, mred_;
   double range_b_ = 4.0, fd_target_ = 150.0, fd_b2_ = 225.0;

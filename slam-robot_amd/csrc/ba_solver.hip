@@ -516,7 +516,6 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d) {
 //   3. thread per observation pair (s <= t) of a point, from a pair list built at load time: the 6x6 block
 //      -A_c,s^T (P_s A_p,t^T) A_c,t accumulated into the chunk's window of the reduced system (LDS atomics;
 //      windows wider than kNbwMax blocks go to global atomics).
-constexpr int kSchurLdsBytes = 150 * 1024;
 
 __device__ __forceinline__ void load_Jc_scaled(const Dev& d, int o, int b, double* Jc) {
   const double2* J2 = reinterpret_cast<const double2*>(d.J + (size_t)o * kJStride) + 1;   // skip r
@@ -571,140 +570,135 @@ __device__ __forceinline__ void schur_pair_add(double* dst, int ld, const double
 
 __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d) {
   const LmState* st = d.st;
-  if (st->done) return;
+  if (st->done || (int)blockIdx.x >= d.nseg) return;
   extern __shared__ double lds[];
   __shared__ double red[kSchurThreads / 64];
-  const Chunk ch = d.chunks[blockIdx.x];
-  const int npair = ch.nb * (ch.nb + 1) / 2;
-  const int nwin = ch.wide ? 0 : npair * 36 + ch.nb * 6;
+  const SchurSeg sg = d.segs[blockIdx.x];
+  const int npair = sg.nb * (sg.nb + 1) / 2;
+  const int nwin = sg.wide ? 0 : npair * 36 + sg.nb * 6;
   double* win = lds;
   double* rhsw = win + npair * 36;
-  double* vinv = lds + nwin;                  // [kChunkPts][10]
-  double* tpv = vinv + kChunkPts * 10;        // [kChunkPts][4]
-  double* Psh = tpv + kChunkPts * 4;          // [capP][8]
+  double* vinv = lds + nwin;                  // [kSegPts][10]
+  double* tpv = vinv + kSegPts * 10;          // [kSegPts][4]
+  double* Psh = tpv + kSegPts * 4;            // [segment observations][8]
   const int tid = threadIdx.x;
   for (int i = tid; i < nwin; i += kSchurThreads) win[i] = 0.0;
   const double radius = st->radius;
   const bool reuse = st->reuse_diag != 0;
   double linfail = 0.0;
-  const int sg0 = d.seg_off[blockIdx.x], sg1 = d.seg_off[blockIdx.x + 1];
-  for (int sgi = sg0; sgi < sg1; ++sgi) {
-    const int4 sg = d.segs[sgi];
-    const int q0 = sg.x, q1 = sg.y;
-    const int obs_lo = d.poff[q0], obs_hi = d.poff[q1];
-    __syncthreads();   // the previous segment's phase 3 is done with the stage
-    // phase 1: one thread per point
-    for (int t = tid; t < q1 - q0; t += kSchurThreads) {
-      const int p = q0 + t;
-      if (!d.pfree[p]) continue;
-      const double* Vp = d.V + 10 * (size_t)p;
-      double V[10];
+  const int q0 = sg.p0, q1 = sg.p1;
+  const int obs_lo = d.poff[q0], obs_hi = d.poff[q1];
+  // phase 1: one thread per point
+  for (int t = tid; t < q1 - q0; t += kSchurThreads) {
+    const int p = q0 + t;
+    if (!d.pfree[p]) continue;
+    const double* Vp = d.V + 10 * (size_t)p;
+    double V[10];
 #pragma unroll
-      for (int i = 0; i < 10; ++i) V[i] = Vp[i];
-      const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
-      const double sp[4] = {s4.x, s4.y, s4.z, s4.w};
-      const double4 g4 = reinterpret_cast<const double4*>(d.g)[p];
-      const double gs[4] = {g4.x * sp[0], g4.y * sp[1], g4.z * sp[2], g4.w * sp[3]};
-      double dp[4];
-      if (!reuse) {
+    for (int i = 0; i < 10; ++i) V[i] = Vp[i];
+    const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
+    const double sp[4] = {s4.x, s4.y, s4.z, s4.w};
+    const double4 g4 = reinterpret_cast<const double4*>(d.g)[p];
+    const double gs[4] = {g4.x * sp[0], g4.y * sp[1], g4.z * sp[2], g4.w * sp[3]};
+    double dp[4];
+    if (!reuse) {
 #pragma unroll
-        for (int a = 0; a < 4; ++a) dp[a] = fmin(fmax(sp[a] * sp[a] * V[u4(a, a)], st->min_diag), st->max_diag);
-        reinterpret_cast<double4*>(d.diag_p)[p] = make_double4(dp[0], dp[1], dp[2], dp[3]);
-      } else {
-        const double4 d4 = reinterpret_cast<const double4*>(d.diag_p)[p];
-        dp[0] = d4.x; dp[1] = d4.y; dp[2] = d4.z; dp[3] = d4.w;
-      }
-      double Vt[10];
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          if (c >= a) Vt[u4(a, c)] = sp[a] * V[u4(a, c)] * sp[c] + (a == c ? dp[a] / radius : 0.0);
-      double Vi[10];
-      if (!inv4_spd(Vt, Vi)) {
-        linfail += 1.0;
-#pragma unroll
-        for (int i = 0; i < 10; ++i) Vi[i] = NAN;
-      }
-      double tp[4];
-#pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        double s = 0.0;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) s += sym4(Vi, a, c) * gs[c];
-        tp[a] = s;
-      }
-      double* Vo = d.Vinv + 10 * (size_t)p;
-#pragma unroll
-      for (int i = 0; i < 10; ++i) {
-        Vo[i] = Vi[i];
-        vinv[10 * t + i] = Vi[i];
-      }
-      reinterpret_cast<double4*>(d.tp)[p] = make_double4(tp[0], tp[1], tp[2], tp[3]);
-#pragma unroll
-      for (int a = 0; a < 4; ++a) tpv[4 * t + a] = tp[a];
+      for (int a = 0; a < 4; ++a) dp[a] = fmin(fmax(sp[a] * sp[a] * V[u4(a, a)], st->min_diag), st->max_diag);
+      reinterpret_cast<double4*>(d.diag_p)[p] = make_double4(dp[0], dp[1], dp[2], dp[3]);
+    } else {
+      const double4 d4 = reinterpret_cast<const double4*>(d.diag_p)[p];
+      dp[0] = d4.x; dp[1] = d4.y; dp[2] = d4.z; dp[3] = d4.w;
     }
-    __syncthreads();
-    // phase 2: one thread per observation
-    for (int o = obs_lo + tid; o < obs_hi; o += kSchurThreads) {
-      const int p = d.obs_pnt[o];
-      if (!d.pfree[p]) continue;
-      const int lp = p - q0;
-      const int b = d.frame_block[d.obs_frame[o]];
-      const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
-      double Jp[8];
-      load_Jp_scaled(d, o, s4, Jp);
-      const double* Vi = vinv + 10 * lp;
-      double* Pr = Psh + 8 * (o - obs_lo);
+    double Vt[10];
 #pragma unroll
-      for (int rr = 0; rr < 2; ++rr)
+    for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          double acc = 0.0;
+      for (int c = 0; c < 4; ++c)
+        if (c >= a) Vt[u4(a, c)] = sp[a] * V[u4(a, c)] * sp[c] + (a == c ? dp[a] / radius : 0.0);
+    double Vi[10];
+    if (!inv4_spd(Vt, Vi)) {
+      linfail += 1.0;
 #pragma unroll
-          for (int m = 0; m < 4; ++m) acc += Jp[4 * rr + m] * sym4(Vi, m, c);
-          Pr[4 * rr + c] = acc;
-        }
-      if (b < 0) continue;
-      double Jc[12];
-      load_Jc_scaled(d, o, b, Jc);
-      const double* tp = tpv + 4 * lp;
-      const double e0 = Jp[0] * tp[0] + Jp[1] * tp[1] + Jp[2] * tp[2] + Jp[3] * tp[3];
-      const double e1 = Jp[4] * tp[0] + Jp[5] * tp[1] + Jp[6] * tp[2] + Jp[7] * tp[3];
-#pragma unroll
-      for (int a = 0; a < 6; ++a) {
-        const double v = -(Jc[a] * e0 + Jc[6 + a] * e1);
-        if (ch.wide) atomicAdd(d.rhs + 6 * b + a, v);   // wide chunks go straight to the global rhs partial
-        else atomicAdd(rhsw + (b - ch.b_lo) * 6 + a, v);
-      }
+      for (int i = 0; i < 10; ++i) Vi[i] = NAN;
     }
-    __syncthreads();
-    // phase 3: one thread per observation pair
-    for (int k = sg.z + tid; k < sg.w; k += kSchurThreads) {
-      const int2 pr = d.pairs[k];
-      const int os = obs_lo + (pr.x >> 16), ot = obs_lo + (pr.x & 0xffff);
-      const int bs = pr.y >> 16, bt = pr.y & 0xffff;
-      const int p = d.obs_pnt[os];
-      const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
-      double Jcs[12], Jct[12], Jpt[8];
-      load_Jc_scaled(d, os, bs, Jcs);
-      load_Jc_scaled(d, ot, bt, Jct);
-      load_Jp_scaled(d, ot, s4, Jpt);
-      double Ps[8];
+    double tp[4];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) Ps[i] = Psh[8 * (os - obs_lo) + i];
-      const int I = bs < bt ? bs : bt, Jb = bs < bt ? bt : bs;
-      if (ch.wide)
-        schur_pair_add(d.S_wide + (size_t)(6 * I) * d.n + 6 * Jb, d.n, Jcs, Ps, Jpt, Jct, os == ot, bs == bt, bs < bt);
-      else
-        schur_pair_add(win + wp(I - ch.b_lo, Jb - ch.b_lo, ch.nb) * 36, 6, Jcs, Ps, Jpt, Jct, os == ot, bs == bt,
-                       bs < bt);
+    for (int a = 0; a < 4; ++a) {
+      double s = 0.0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) s += sym4(Vi, a, c) * gs[c];
+      tp[a] = s;
+    }
+    double* Vo = d.Vinv + 10 * (size_t)p;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      Vo[i] = Vi[i];
+      vinv[10 * t + i] = Vi[i];
+    }
+    reinterpret_cast<double4*>(d.tp)[p] = make_double4(tp[0], tp[1], tp[2], tp[3]);
+#pragma unroll
+    for (int a = 0; a < 4; ++a) tpv[4 * t + a] = tp[a];
+  }
+  __syncthreads();
+  // phase 2: one thread per observation
+  for (int o = obs_lo + tid; o < obs_hi; o += kSchurThreads) {
+    const int p = d.obs_pnt[o];
+    if (!d.pfree[p]) continue;
+    const int lp = p - q0;
+    const int b = d.frame_block[d.obs_frame[o]];
+    const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
+    double Jp[8];
+    load_Jp_scaled(d, o, s4, Jp);
+    const double* Vi = vinv + 10 * lp;
+    double* Pr = Psh + 8 * (o - obs_lo);
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        double acc = 0.0;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) acc += Jp[4 * rr + m] * sym4(Vi, m, c);
+        Pr[4 * rr + c] = acc;
+      }
+    if (b < 0) continue;
+    double Jc[12];
+    load_Jc_scaled(d, o, b, Jc);
+    const double* tp = tpv + 4 * lp;
+    const double e0 = Jp[0] * tp[0] + Jp[1] * tp[1] + Jp[2] * tp[2] + Jp[3] * tp[3];
+    const double e1 = Jp[4] * tp[0] + Jp[5] * tp[1] + Jp[6] * tp[2] + Jp[7] * tp[3];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      const double v = -(Jc[a] * e0 + Jc[6 + a] * e1);
+      if (sg.wide) atomicAdd(d.rhs + 6 * b + a, v);   // wide segments go straight to the global rhs partial
+      else atomicAdd(rhsw + (b - sg.b_lo) * 6 + a, v);
     }
   }
-  linfail = block_sum<kSchurThreads>(linfail, red);
-  if (tid == 0) d.chunk_scal[(size_t)blockIdx.x * kNScal + kLinFail] = linfail;
   __syncthreads();
-  for (int i = tid; i < nwin; i += kSchurThreads) d.S_slab[ch.s_off + i] = win[i];
+  // phase 3: one thread per observation pair
+  for (int k = sg.pair_lo + tid; k < sg.pair_hi; k += kSchurThreads) {
+    const int2 pr = d.pairs[k];
+    const int os = obs_lo + (pr.x >> 16), ot = obs_lo + (pr.x & 0xffff);
+    const int bs = pr.y >> 16, bt = pr.y & 0xffff;
+    const int p = d.obs_pnt[os];
+    const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
+    double Jcs[12], Jct[12], Jpt[8];
+    load_Jc_scaled(d, os, bs, Jcs);
+    load_Jc_scaled(d, ot, bt, Jct);
+    load_Jp_scaled(d, ot, s4, Jpt);
+    double Ps[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) Ps[i] = Psh[8 * (os - obs_lo) + i];
+    const int I = bs < bt ? bs : bt, Jb = bs < bt ? bt : bs;
+    if (sg.wide)
+      schur_pair_add(d.S_wide + (size_t)(6 * I) * d.n + 6 * Jb, d.n, Jcs, Ps, Jpt, Jct, os == ot, bs == bt, bs < bt);
+    else
+      schur_pair_add(win + wp(I - sg.b_lo, Jb - sg.b_lo, sg.nb) * 36, 6, Jcs, Ps, Jpt, Jct, os == ot, bs == bt,
+                     bs < bt);
+  }
+  linfail = block_sum<kSchurThreads>(linfail, red);
+  if (tid == 0) d.seg_fail[blockIdx.x] = linfail;
+  __syncthreads();
+  for (int i = tid; i < nwin; i += kSchurThreads) d.S_slab[sg.s_off + i] = win[i];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1438,8 +1432,8 @@ __global__ __launch_bounds__(64) void k_upd_reduce(Dev d) {
     v[kUCandFail] += sc[kCandFail];
     v[kUStep2] += sc[kStep2];
     v[kUCandX2] += sc[kCandX2];
-    v[kULinFail] += sc[kLinFail];
   }
+  for (int g = lane; g < d.nseg; g += 64) v[kULinFail] += d.seg_fail[g];
 #pragma unroll
   for (int j = 0; j < kUNum; ++j) v[j] = wave_sum(v[j]);
   if (lane == 0)
@@ -1695,7 +1689,7 @@ void BaSolver::Load(const sg_problem& p) {
   // chunks: up to kChunkPts consecutive points whose camera blocks fit a window of kNbwMax blocks
   chunks_.clear();
   max_nb_ = 0;
-  int cam_off = 0, s_off = 0;
+  int cam_off = 0;
   for (int i = 0; i < P_;) {
     const int pt0 = point_perm_[i];
     const int lo = pfirst[pt0];
@@ -1725,36 +1719,64 @@ void BaSolver::Load(const sg_problem& p) {
     }
     c.p1 = j;
     c.cam_off = cam_off;
-    c.s_off = s_off;
+    c.s_off = 0;
     cam_off += c.nb * kCamV;
-    s_off += c.nb * (c.nb + 1) / 2 * 36 + c.nb * 6;
     max_nb_ = std::max(max_nb_, c.nb);
     chunks_.push_back(c);
     i = j;
   }
   nchunks_ = (int)chunks_.size();
-  // Schur work lists: per chunk, point segments whose observations fit the LDS stage, and per segment the
-  // observation pairs (s <= t, both on free frames) of its free points
-  std::vector<int32_t> obs_pnt(M_), seg_off(nchunks_ + 1, 0);
-  std::vector<int32_t> segs_flat, pairs_flat;   // int4 per segment, int2 per pair
+  // Schur segments: runs of at most kSegPts consecutive points (device order) whose observations fit the
+  // LDS stage and whose camera blocks fit a window of kSegNbMax blocks; one workgroup each, with its own
+  // window partial in S_slab.  A point spanning more blocks is a "wide" segment of its own (global
+  // atomics).  Per segment, the observation pairs (s <= t, both on free frames) of its free points.
+  std::vector<int32_t> obs_pnt(M_);
   for (int i = 0; i < P_; ++i)
     for (int o = poff[i]; o < poff[i + 1]; ++o) obs_pnt[o] = i;
-  for (int c = 0; c < nchunks_; ++c) {
-    const Chunk& ch = chunks_[c];
-    const int nwin = ch.wide ? 0 : ch.nb * (ch.nb + 1) / 2 * 36 + ch.nb * 6;
-    const int capP = (int)((kSchurLdsBytes / 8 - nwin - kChunkPts * 14) / 8);
-    SG_REQUIRE(capP >= 64, SG_EINVAL, "Schur stage too small");
-    int q = ch.p0;
-    while (q < ch.p1) {
-      int q1 = q, nobs = 0;
-      while (q1 < ch.p1 && (q1 == q || nobs + (poff[q1 + 1] - poff[q1]) <= capP)) {
-        nobs += poff[q1 + 1] - poff[q1];
-        ++q1;
+  std::vector<SchurSeg> segs;
+  std::vector<int32_t> pairs_flat;   // int2 per pair
+  int s_off = 0;
+  max_seg_nb_ = 0;
+  {
+    auto span = [&](int i) { return pfirst[point_perm_[i]] >= NB_ ? 0 : plast[point_perm_[i]] - pfirst[point_perm_[i]] + 1; };
+    for (int i = 0; i < P_;) {
+      SchurSeg sg{};
+      sg.p0 = i;
+      const int pt0 = point_perm_[i];
+      int j = i + 1, nobs = poff[i + 1] - poff[i];
+      if (span(i) > kSegNbMax) {
+        sg.wide = 1;
+        sg.b_lo = pfirst[pt0];
+        sg.nb = 0;
+      } else {
+        const bool constonly = pfirst[pt0] >= NB_;
+        int lo = constonly ? 0 : pfirst[pt0], hi = constonly ? -1 : plast[pt0];
+        while (j < P_ && j - i < kSegPts) {
+          const int ptj = point_perm_[j];
+          const int kj = poff[j + 1] - poff[j];
+          if (nobs + kj > kSegObsCap) break;
+          if ((pfirst[ptj] >= NB_) != constonly) break;
+          if (!constonly) {
+            const int l2 = std::min(lo, pfirst[ptj]), h2 = std::max(hi, plast[ptj]);
+            if (h2 - l2 + 1 > kSegNbMax) break;
+            lo = l2;
+            hi = h2;
+          }
+          nobs += kj;
+          ++j;
+        }
+        sg.b_lo = lo;
+        sg.nb = hi - lo + 1;
       }
-      SG_REQUIRE(nobs <= capP && nobs < 65536, SG_EINVAL, "a point has more observations than the Schur stage");
-      const int obs_lo = poff[q];
-      const int pair_lo = (int)pairs_flat.size() / 2;
-      for (int pt = q; pt < q1; ++pt) {
+      SG_REQUIRE(nobs < 65536, SG_EINVAL, "a point has too many observations");
+      sg.p1 = j;
+      sg.s_off = s_off;
+      s_off += sg.wide ? 0 : sg.nb * (sg.nb + 1) / 2 * 36 + sg.nb * 6;
+      max_seg_nb_ = std::max(max_seg_nb_, sg.nb);
+      max_seg_obs_ = std::max(max_seg_obs_, nobs);
+      const int obs_lo = poff[i];
+      sg.pair_lo = (int)pairs_flat.size() / 2;
+      for (int pt = i; pt < j; ++pt) {
         if (!pfree[pt]) continue;
         for (int os = poff[pt]; os < poff[pt + 1]; ++os) {
           const int bs = frame_block[obs_frame[os]];
@@ -1767,14 +1789,14 @@ void BaSolver::Load(const sg_problem& p) {
           }
         }
       }
-      segs_flat.insert(segs_flat.end(), {q, q1, pair_lo, (int)pairs_flat.size() / 2});
-      q = q1;
+      sg.pair_hi = (int)pairs_flat.size() / 2;
+      segs.push_back(sg);
+      i = j;
     }
-    seg_off[c + 1] = (int)segs_flat.size() / 4;
   }
+  nseg_ = (int)segs.size();
   SG_REQUIRE(NB_ < 65536, SG_EINVAL, "too many camera blocks");
   if (pairs_flat.empty()) pairs_flat.assign(2, 0);
-  if (segs_flat.empty()) segs_flat.assign(4, 0);
   // deterministic reduction lists: for every camera block / block pair, the slab offsets of the chunk
   // partials that cover it (fixed chunk order)
   std::vector<int32_t> cam_loff(NB_ + 1, 0), cam_lidx, r_loff(NB_ + 1, 0), r_lidx;
@@ -1785,14 +1807,17 @@ void BaSolver::Load(const sg_problem& p) {
     for (int c = 0; c < nchunks_; ++c) {
       const Chunk& ch = chunks_[c];
       if (ch.wide || ch.nb == 0) continue;
-      const int npair = ch.nb * (ch.nb + 1) / 2;
-      for (int i = 0; i < ch.nb; ++i) {
-        const int b = ch.b_lo + i;
-        cl[b].push_back(ch.cam_off + i * kCamV);
-        rl[b].push_back(ch.s_off + npair * 36 + i * 6);
-        for (int j = i; j < ch.nb; ++j) {
-          const int wpij = i * ch.nb - i * (i - 1) / 2 + (j - i);
-          sl[(size_t)b * NB_ + ch.b_lo + j].push_back(ch.s_off + wpij * 36);
+      for (int i = 0; i < ch.nb; ++i) cl[ch.b_lo + i].push_back(ch.cam_off + i * kCamV);
+    }
+    for (const SchurSeg& sg : segs) {
+      if (sg.wide || sg.nb == 0) continue;
+      const int npair = sg.nb * (sg.nb + 1) / 2;
+      for (int i = 0; i < sg.nb; ++i) {
+        const int b = sg.b_lo + i;
+        rl[b].push_back(sg.s_off + npair * 36 + i * 6);
+        for (int j = i; j < sg.nb; ++j) {
+          const int wpij = i * sg.nb - i * (i - 1) / 2 + (j - i);
+          sl[(size_t)b * NB_ + sg.b_lo + j].push_back(sg.s_off + wpij * 36);
         }
       }
     }
@@ -1887,9 +1912,10 @@ void BaSolver::Load(const sg_problem& p) {
   obs_fixed_.Upload(obs_fixed, s);
   chunks_d_.Upload(chunks_, s);
   obs_pnt_.Upload(obs_pnt.empty() ? std::vector<int32_t>{0} : obs_pnt, s);
-  seg_off_.Upload(seg_off, s);
-  segs_.Upload(segs_flat, s);
+  segs_.Upload(segs.empty() ? std::vector<SchurSeg>(1) : segs, s);
   pairs_.Upload(pairs_flat, s);
+  seg_fail_.Resize(std::max(nseg_, 1));
+  seg_fail_.Zero(s);
   cam_loff_.Upload(cam_loff, s);
   cam_lidx_.Upload(cam_lidx, s);
   s_loff_.Upload(s_loff, s);
@@ -1946,7 +1972,8 @@ void BaSolver::Load(const sg_problem& p) {
   rhs_.Zero(s);
   chunk_scal_.Zero(s);
   S_.Zero(s);
-  schur_lds_ = kSchurLdsBytes;
+  schur_lds_ = sizeof(double) * ((size_t)max_seg_nb_ * (max_seg_nb_ + 1) / 2 * 36 + max_seg_nb_ * 6 +
+                                  (size_t)kSegPts * 14 + (size_t)std::max(max_seg_obs_, 1) * 8);
   SG_HIP_CHECK(hipFuncSetAttribute((const void*)k_schur, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)schur_lds_));
   SG_HIP_CHECK(hipFuncSetAttribute((const void*)k_cholesky_window<false>,
@@ -2036,8 +2063,9 @@ Dev BaSolver::MakeDev() {
   d.stamps = stamp_on_ ? stamps_.ptr : nullptr;
   d.fd_pair = fd_pair_.ptr;
   d.obs_pnt = obs_pnt_.ptr;
-  d.seg_off = seg_off_.ptr;
-  d.segs = reinterpret_cast<const int4*>(segs_.ptr);
+  d.segs = segs_.ptr;
+  d.nseg = nseg_;
+  d.seg_fail = seg_fail_.ptr;
   d.pairs = reinterpret_cast<const int2*>(pairs_.ptr);
   d.assemble = (!comm_ || comm_->rank() == 0) ? 1 : 0;
   d.dbg = getenv("SG_DBG") ? atoi(getenv("SG_DBG")) : 0;
@@ -2120,7 +2148,7 @@ void BaSolver::Iterate(int n) {
     hipLaunchKernelGGL(k_cam_finalize, dim3(1), dim3(256), 0, stream_, d);
     TimedLaunchEnd(kKCamFinal);
     TimedLaunchBegin(kKSchur);
-    hipLaunchKernelGGL(k_schur, dim3(nc), dim3(kSchurThreads), schur_lds_, stream_, d);
+    hipLaunchKernelGGL(k_schur, dim3(std::max(nseg_, 1)), dim3(kSchurThreads), schur_lds_, stream_, d);
     TimedLaunchEnd(kKSchur);
     TimedLaunchBegin(kKSReduce);
     const int maxrow = std::max(NB_ * 36, n_);
