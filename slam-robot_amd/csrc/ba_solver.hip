@@ -568,6 +568,10 @@ __device__ __forceinline__ void schur_pair_add(double* dst, int ld, const double
     }
 }
 
+// Window blocks are padded to 37 doubles in LDS: with 36 the same element of neighbouring blocks falls on
+// 8 banks (8-way conflicts for the atomics of a wave whose lanes hold different block pairs).
+constexpr int kWinLd = 37;
+
 __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d) {
   const LmState* st = d.st;
   if (st->done || (int)blockIdx.x >= d.nseg) return;
@@ -575,9 +579,9 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d) {
   __shared__ double red[kSchurThreads / 64];
   const SchurSeg sg = d.segs[blockIdx.x];
   const int npair = sg.nb * (sg.nb + 1) / 2;
-  const int nwin = sg.wide ? 0 : npair * 36 + sg.nb * 6;
+  const int nwin = sg.wide ? 0 : npair * kWinLd + sg.nb * 6;   // LDS: blocks padded to kWinLd doubles
   double* win = lds;
-  double* rhsw = win + npair * 36;
+  double* rhsw = win + npair * kWinLd;
   double* vinv = lds + nwin;                  // [kSegPts][10]
   double* tpv = vinv + kSegPts * 10;          // [kSegPts][4]
   double* Psh = tpv + kSegPts * 4;            // [segment observations][8]
@@ -692,13 +696,19 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d) {
     if (sg.wide)
       schur_pair_add(d.S_wide + (size_t)(6 * I) * d.n + 6 * Jb, d.n, Jcs, Ps, Jpt, Jct, os == ot, bs == bt, bs < bt);
     else
-      schur_pair_add(win + wp(I - sg.b_lo, Jb - sg.b_lo, sg.nb) * 36, 6, Jcs, Ps, Jpt, Jct, os == ot, bs == bt,
-                     bs < bt);
+      schur_pair_add(win + wp(I - sg.b_lo, Jb - sg.b_lo, sg.nb) * kWinLd, 6, Jcs, Ps, Jpt, Jct, os == ot,
+                     bs == bt, bs < bt);
   }
   linfail = block_sum<kSchurThreads>(linfail, red);
   if (tid == 0) d.seg_fail[blockIdx.x] = linfail;
   __syncthreads();
-  for (int i = tid; i < nwin; i += kSchurThreads) d.S_slab[sg.s_off + i] = win[i];
+  if (!sg.wide) {
+    const int nslab = npair * 36 + sg.nb * 6;   // slab: compact 36-double blocks, then the rhs
+    for (int i = tid; i < nslab; i += kSchurThreads) {
+      const int blk = i / 36;
+      d.S_slab[sg.s_off + i] = blk < npair ? win[blk * kWinLd + (i - 36 * blk)] : rhsw[i - 36 * npair];
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1972,7 +1982,7 @@ void BaSolver::Load(const sg_problem& p) {
   rhs_.Zero(s);
   chunk_scal_.Zero(s);
   S_.Zero(s);
-  schur_lds_ = sizeof(double) * ((size_t)max_seg_nb_ * (max_seg_nb_ + 1) / 2 * 36 + max_seg_nb_ * 6 +
+  schur_lds_ = sizeof(double) * ((size_t)max_seg_nb_ * (max_seg_nb_ + 1) / 2 * kWinLd + max_seg_nb_ * 6 +
                                   (size_t)kSegPts * 14 + (size_t)std::max(max_seg_obs_, 1) * 8);
   SG_HIP_CHECK(hipFuncSetAttribute((const void*)k_schur, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)schur_lds_));
