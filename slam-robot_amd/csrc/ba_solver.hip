@@ -1031,6 +1031,43 @@ __device__ __forceinline__ void chol_backsub_w(const double* Wm, const double* z
 // Window path: the active band lives in LDS (132 KiB) together with the rhs ring; finished panel rows and
 // 1/U_jj go to global memory for the back substitution.  Barriers between phases are LDS-only, so the
 // global writes and the prefetch of the next window columns overlap the factorisation.
+// W / z of one finished panel (back-substitution operands, see chol_backsub_w): lane (wave wv0.., lane)
+// solves U11 t = U12[:, c] for one column c of the panel's band, one extra lane solves U11 z = y_panel.
+// U12 is read from the LDS window (the panel's rows stay there until the next panel's slide), U11 and 1/U_jj
+// from the panel's LDS copies.
+__device__ __forceinline__ void chol_panel_w(const double* win, const double* u11, const double* pinv,
+                                             const double* ypan, int kb, int w, int jend, int n, int wi,
+                                             double* __restrict__ S, double* __restrict__ y) {
+  const int nc = jend - (kb + kCholNb);   // band columns right of the panel (<= kCholWS - kCholNb)
+  const bool isz = wi == kCholWS - kCholNb;
+  const int c = kb + kCholNb + wi;
+  if (!(wi < nc || isz)) return;
+  double t[kCholNb];
+#pragma unroll
+  for (int r = 0; r < kCholNb; ++r) t[r] = isz ? ypan[r] : (r < w ? Wn(const_cast<double*>(win), kb + r, c) : 0.0);
+#pragma unroll
+  for (int k = kCholNb - 1; k >= 0; --k) {
+    t[k] *= pinv[k];
+#pragma unroll
+    for (int r = 0; r < k; ++r) t[r] -= u11[k * kCholNb + r] * t[k];
+  }
+  if (isz) {
+#pragma unroll
+    for (int r = 0; r < kCholNb; ++r)
+      if (r < w) y[kb + r] = t[r];
+  } else {
+#pragma unroll
+    for (int r = 0; r < kCholNb; ++r)
+      if (r < w) S[(size_t)(kb + r) * n + c] = t[r];
+  }
+}
+
+// Window path: the active band lives in LDS (132 KiB) together with the rhs ring.  Per 16-row panel:
+//   phase A  waves 0-2 factor the panel (diagonal block + off-diagonal columns + rhs in one right-looking
+//            pass, see below) while waves 3-4 turn the previous panel into back-substitution operands
+//            (W = U11^-1 U12, z = U11^-1 y) and store them to global memory;
+//   phase B  all waves apply the trailing update A22 -= U12^T U12 (MFMA f64 tiles) and slide the window.
+// Barriers are LDS-only, so global stores and the prefetch of the next window columns stay in flight.
 template <bool kStamp>
 __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const int32_t* panel_jend, double* rdg) {
   unsigned long long last_stamp = kStamp ? __builtin_amdgcn_s_memtime() : 0ull;
@@ -1040,24 +1077,32 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
   extern __shared__ double win[];
   __shared__ double yw[kCholWS];
   __shared__ double prow[kPanelWaves][kCholNb];
-  __shared__ double pinv[kPanelWaves][kCholNb];                // 1/U_jj of the current panel
-  __shared__ double u11w[kPanelWaves][kCholNb * kCholNb];      // U11 columns of the current panel
+  __shared__ double pinv[2][kCholNb];                 // 1/U_jj of the current / previous panel
+  __shared__ double u11w[2][kCholNb * kCholNb];       // U11 columns of the current / previous panel
+  __shared__ double ypan[2][kCholNb];                 // forward-substituted rhs of the panel rows
   __shared__ int jend_sh[kJendSh];
   __shared__ int fail_sh;
   const int n = d.n, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nwaves = kCholThreads / 64;
   double* y = d.work;
   if (tid == 0) fail_sh = 0;
-  // rhs y = rhs_sub + S g_c
-  for (int i = tid; i < n; i += kCholThreads) {
-    const double v = d.xc[i];   // assembled rhs (k_S_reduce)
-    y[i] = v;
-    if (i < kCholWS) yw[i] = v;
-  }
+  // rhs y = rhs_sub + S g_c (assembled by k_S_reduce); initial 128 x 128 window, all loads issued first
+  for (int i = tid; i < min(n, kCholWS); i += kCholThreads) yw[i] = d.xc[i];
   const int n0 = min(n, kCholWS);
-  for (int e = tid; e < n0 * n0; e += kCholThreads) {
-    const int i = e / n0, j = e % n0;
-    if (i <= j) Wn(win, i, j) = d.S[(size_t)i * n + j];
+  constexpr int kInit = kCholWS * kCholWS / kCholThreads;
+  {
+    double v[kInit];
+#pragma unroll
+    for (int q = 0; q < kInit; ++q) {
+      const int e = tid + q * kCholThreads, i = e / kCholWS, j = e % kCholWS;
+      const bool in = i < n0 && j < n0 && i <= j;
+      v[q] = d.S[in ? (size_t)i * n + j : 0];
+    }
+#pragma unroll
+    for (int q = 0; q < kInit; ++q) {
+      const int e = tid + q * kCholThreads, i = e / kCholWS, j = e % kCholWS;
+      if (i < n0 && j < n0 && i <= j) Wn(win, i, j) = v[q];
+    }
   }
   const int npanel = (n + kCholNb - 1) / kCholNb;
   for (int p = tid; p < npanel; p += kCholThreads) jend_sh[p] = panel_jend[p];   // npanel <= kJendSh
@@ -1069,6 +1114,7 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
     const int kb = pk * kCholNb;
     const int w = min(kCholNb, n - kb);
     const int jend = jend_sh[pk];
+    const int buf = pk & 1;
     // prefetch the columns this panel's slide brings in: j in [kb+WS, kb+WS+w), rows kb+w..j
     const int jn0 = kb + kCholWS, jn1 = min(n, jn0 + w);
     double pf[kPf];
@@ -1085,8 +1131,7 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
     // off-diagonal columns in lanes 16..63; the diagonal block, the TRSM of the off-diagonal columns and
     // the rhs forward step run as one right-looking pass.  Row j of the diagonal block is broadcast
     // through a per-wave LDS row (one wave: the LDS queue orders write before read, no barrier).  Rows
-    // past n are padded with identity so the unrolled loop has no branches.  The finished rows go from
-    // registers to LDS (for the trailing update), to global memory (back substitution) and to the rhs.
+    // past n are padded with identity so the unrolled loop has no branches.
     if (wave < kPanelWaves) {
       const int lane = opaque_lane();
       const int slot = lane < kCholNb ? lane : kCholNb + (64 - kCholNb) * wave + (lane - kCholNb);
@@ -1115,7 +1160,7 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
         inv = inv * (1.5 - 0.5 * piv * inv * inv);
         ca[j] *= inv;
         yv[j] *= inv;
-        if (lane == 0) pinv[wave][j] = inv;
+        if (wave == 0 && lane == 0) pinv[buf][j] = inv;
 #pragma unroll
         for (int r = j + 1; r < kCholNb; ++r) {
           const double ur = u[r] * inv;   // U[j][r], rounded exactly as lane r rounds its own ca[j]
@@ -1131,7 +1176,8 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
         }
       }
       SG_STAMP_AT(3)
-      // rhs of the trailing rows: y_c -= sum_r U[r][c] y_r; trailing columns' panel rows -> LDS
+      // rhs of the trailing rows: y_c -= sum_r U[r][c] y_r; trailing columns' panel rows -> LDS; the
+      // panel's U11, 1/U_jj and forward rhs for the W / z pass (wave 0)
       const bool trail = v && lane >= kCholNb;
       double s0 = 0.0;
 #pragma unroll
@@ -1140,37 +1186,26 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
 #pragma unroll
       for (int r = 0; r < kCholNb; ++r)
         if (r < w && trail) Wn(win, kb + r, c) = ca[r];
-      // back-substitution operands: W = U11^-1 U12 (trailing lanes) and z = U11^-1 y (diagonal lanes),
-      // so the back substitution is one mat-vec per panel, x_p = z_p - W_p x_rest, with no serial
-      // triangle.  U11 columns go through this wave's LDS copy (lane k writes column k).
-      double* u11 = u11w[wave];
-      if (lane < kCholNb) {
+      if (wave == 0) {
+        if (lane < kCholNb) {
 #pragma unroll
-        for (int r = 0; r < kCholNb; ++r) u11[lane * kCholNb + r] = ca[r];
+          for (int r = 0; r < kCholNb; ++r) u11w[buf][lane * kCholNb + r] = ca[r];
+        }
+        if (lane == 0) {
+#pragma unroll
+          for (int r = 0; r < kCholNb; ++r) ypan[buf][r] = yv[r];
+          if (bad) fail_sh = 1;
+        }
       }
-      double t[kCholNb];
-#pragma unroll
-      for (int r = 0; r < kCholNb; ++r) t[r] = lane < kCholNb ? yv[r] : ca[r];
-#pragma unroll
-      for (int k = kCholNb - 1; k >= 0; --k) {
-        t[k] *= pinv[wave][k];
-#pragma unroll
-        for (int r = 0; r < k; ++r) t[r] -= u11[k * kCholNb + r] * t[k];
-        asm volatile("" : "+v"(t[k]));
-      }
-#pragma unroll
-      for (int r = 0; r < kCholNb; ++r)
-        if (r < w && trail) d.S[(size_t)(kb + r) * n + c] = t[r];
-      if (wave == 0 && lane == 0) {
-#pragma unroll
-        for (int r = 0; r < kCholNb; ++r)
-          if (r < w) y[kb + r] = t[r];
-        if (bad) fail_sh = 1;
-      }
+    } else if (pk > 0 && wave < kPanelWaves + 2) {
+      // (a') the previous panel's back-substitution operands, off the critical path
+      const int pb = pk - 1;
+      chol_panel_w(win, u11w[buf ^ 1], pinv[buf ^ 1], ypan[buf ^ 1], pb * kCholNb, min(kCholNb, n - pb * kCholNb),
+                   jend_sh[pb], n, (wave - kPanelWaves) * 64 + lane, d.S, y);
     }
     lds_barrier();
     SG_STAMP_AT(2)
-    // (c) trailing update A22 -= U12^T U12 on the band, 16x16 MFMA tiles (upper tiles only), rhs update
+    // (b) trailing update A22 -= U12^T U12 on the band, 16x16 MFMA tiles (upper tiles only)
     const int m = jend - (kb + w);
     const int T = (m + 15) >> 4;
     const int ntiles = T * (T + 1) / 2;
@@ -1200,7 +1235,7 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
       }
     }
     SG_STAMP_AT(4)
-    // (e) slide the window: columns [kb + WS, kb + WS + w) replace the departed rows/columns.  Disjoint
+    // (c) slide the window: columns [kb + WS, kb + WS + w) replace the departed rows/columns.  Disjoint
     // from everything the trailing update touches (columns < jend <= kb + WS), so no barrier between.
 #pragma unroll
     for (int q = 0; q < kPf; ++q) {
@@ -1211,6 +1246,12 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
     if (tid < jn1 - jn0) yw[(jn0 + tid) & (kCholWS - 1)] = pfy;
     lds_barrier();
     SG_STAMP_AT(5)
+  }
+  // the last panel's operands
+  if (wave >= kPanelWaves && wave < kPanelWaves + 2) {
+    const int pb = npanel - 1;
+    chol_panel_w(win, u11w[pb & 1], pinv[pb & 1], ypan[pb & 1], pb * kCholNb, min(kCholNb, n - pb * kCholNb),
+                 jend_sh[pb], n, (wave - kPanelWaves) * 64 + lane, d.S, y);
   }
   __syncthreads();   // global W rows / z visible to every wave
   double* xs = win;  // the window is free now: the solution lives in LDS
