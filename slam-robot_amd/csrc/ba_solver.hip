@@ -5,14 +5,16 @@
 // decision, trust-region update and termination tests run on the device (k_decide), so a solve is a
 // stream of identical iterations the host only polls for completion.
 //
-//   k_linearize    [chunk of 128 points, 8 lanes/point]  residuals + analytic Jacobians (HBM sweep),
+//   k_linearize    [chunk of 128 points, 4 lanes/point]  residuals + analytic Jacobians (HBM sweep),
 //                  point blocks V,g; camera blocks U,g_c into an LDS window (co-visibility band)
 //   k_cam_reduce   deterministic reduce of per-chunk camera partials  -> xchg_cam   (all-reduced)
 //   k_cam_finalize FrameDistance terms, cost, gradient test, Jacobi scale (iteration 0), LM diagonal
-//   k_schur        [chunk, one wave per point, lanes over observation pairs] damped V^-1 and the Schur
-//                  complement contributions -J_c^T J_p V^-1 J_p^T J_c into an LDS window
-//   k_S_reduce     deterministic reduce of per-chunk Schur windows -> dense S, rhs  (all-reduced)
-//   k_cholesky     one workgroup: add U + damping, banded Cholesky, solve, candidate camera poses
+//   k_schur        [segment of <= 32 points] damped V^-1 (thread per point), P = J_p V^-1 (thread per
+//                  observation), Schur blocks -J_c^T P J_p^T J_c (thread per observation pair) into an
+//                  LDS window of the segment's camera blocks
+//   k_S_reduce     deterministic reduce of the segment windows + blockdiag(U), FrameDistance, damping
+//                  -> damped S and rhs (all-reduced across landmark shards)
+//   k_cholesky     one workgroup: banded Cholesky of S in an LDS window, back substitution, candidate poses
 //   k_point_update back-substitution, model cost change, candidate points, candidate cost
 //   k_upd_reduce   reduce of the per-chunk update scalars  -> xchg_upd              (all-reduced)
 //   k_decide       Ceres TrustRegionMinimizer / LevenbergMarquardtStrategy bookkeeping
@@ -735,36 +737,66 @@ __device__ __forceinline__ double assembly_term(const Dev& d, int I, int J, int 
   return v;
 }
 
-// k_S_reduce: grid (x: elements of block row I with J >= I, y: I; y == NB is the rhs row).  The
-// assembling rank also adds assembly_term and the S g_c part of the rhs, so S leaves here damped.
+// k_S_reduce: the assembling rank also adds assembly_term and the S g_c part of the rhs, so S leaves
+// here damped.
+// One wave per block pair (I <= J) of S, then one wave per rhs block: the wave loads up to 64 slab offsets
+// of its partial list at once and walks them in list order (deterministic), lanes 0..35 (0..5 for the rhs)
+// summing their element, so every partial's load is independent and in flight together.
 __global__ __launch_bounds__(256) void k_S_reduce(Dev d) {
   const LmState* st = d.st;
   if (st->done) return;
-  const int I = blockIdx.y;
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (I < d.NB) {
-    const int nJ = d.NB - I;
-    if (e >= nJ * 36) return;
-    const int Jb = I + e / 36, a = (e % 36) / 6, c = e % 6;
-    const size_t gi = (size_t)(6 * I + a) * d.n + 6 * Jb + c;
-    double s = d.S_wide[gi];
-    d.S_wide[gi] = 0.0;
+  const int lane = threadIdx.x & 63;
+  const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int npb = d.NB * (d.NB + 1) / 2;
+  if (wv >= npb + d.NB) return;
+  const bool is_rhs = wv >= npb;
+  int I = 0, Jb = 0, j0, j1;
+  const int32_t* lidx;
+  if (!is_rhs) {
+    int rem = wv;   // wave-uniform walk to (I, J)
+    while (rem >= d.NB - I) { rem -= d.NB - I; ++I; }
+    Jb = I + rem;
     const int pr = I * d.NB + Jb;
-    const int j0 = d.s_loff[pr], j1 = d.s_loff[pr + 1];
-    const int ac = a * 6 + c;
-#pragma unroll 4
-    for (int j = j0; j < j1; ++j) s += d.S_slab[d.s_lidx[j] + ac];
+    j0 = d.s_loff[pr];
+    j1 = d.s_loff[pr + 1];
+    lidx = d.s_lidx;
+  } else {
+    I = wv - npb;
+    j0 = d.r_loff[I];
+    j1 = d.r_loff[I + 1];
+    lidx = d.r_lidx;
+  }
+  const int ne = is_rhs ? 6 : 36;
+  const int el = lane < ne ? lane : 0;
+  double s = 0.0;
+  for (int base = j0; base < j1; base += 64) {
+    const int cnt = min(64, j1 - base);
+    const int myoff = lane < cnt ? lidx[base + lane] : 0;
+    for (int k = 0; k < cnt; k += 8) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {   // eight independent loads in flight, summed in list order
+        const int off = __builtin_amdgcn_readlane(myoff, min(k + u, 63));
+        v[u] = (k + u < cnt) ? d.S_slab[off + el] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (k + u < cnt) s += v[u];
+    }
+  }
+  if (lane >= ne) return;
+  if (!is_rhs) {
+    const int a = lane / 6, c = lane % 6;
+    const size_t gi = (size_t)(6 * I + a) * d.n + 6 * Jb + c;
+    s += d.S_wide[gi];
+    d.S_wide[gi] = 0.0;
     if (d.assemble) s += assembly_term(d, I, Jb, a, c, st->radius);
     d.S[gi] = s;
   } else {
-    if (e >= d.n) return;
-    const int b = e / 6, a = e % 6;
-    double s = d.rhs[e];   // wide-chunk atomics
-    const int j0 = d.r_loff[b], j1 = d.r_loff[b + 1];
-#pragma unroll 4
-    for (int j = j0; j < j1; ++j) s += d.S_slab[d.r_lidx[j] + a];
+    const int e = 6 * I + lane;
+    s += d.rhs[e];   // wide-segment atomics
     if (d.assemble) s += d.scale_c[e] * d.camg[e];   // y = rhs_sub + S g_c
-    d.xc[e] = s;       // local rhs partial (all-reduced with S); the wide-chunk accumulator is reset
+    d.xc[e] = s;       // local rhs partial (all-reduced with S); the wide accumulator is reset
     d.rhs[e] = 0.0;
   }
 }
@@ -2202,8 +2234,8 @@ void BaSolver::Iterate(int n) {
     hipLaunchKernelGGL(k_schur, dim3(std::max(nseg_, 1)), dim3(kSchurThreads), schur_lds_, stream_, d);
     TimedLaunchEnd(kKSchur);
     TimedLaunchBegin(kKSReduce);
-    const int maxrow = std::max(NB_ * 36, n_);
-    hipLaunchKernelGGL(k_S_reduce, dim3((maxrow + 255) / 256, NB_ + 1), dim3(256), 0, stream_, d);
+    const int nwv = NB_ * (NB_ + 1) / 2 + NB_;
+    hipLaunchKernelGGL(k_S_reduce, dim3(std::max((nwv + 3) / 4, 1)), dim3(256), 0, stream_, d);
     TimedLaunchEnd(kKSReduce);
     if (comm_ && comm_->nranks() > 1) {
       // the upper blocks of S and the rhs partial are summed over landmark shards
