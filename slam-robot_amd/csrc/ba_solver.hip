@@ -1076,7 +1076,10 @@ __device__ __forceinline__ void chol_panel_w(const double* win, const double* u1
   if (!(wi < nc || isz)) return;
   double t[kCholNb];
 #pragma unroll
-  for (int r = 0; r < kCholNb; ++r) t[r] = isz ? ypan[r] : (r < w ? Wn(const_cast<double*>(win), kb + r, c) : 0.0);
+  for (int r = 0; r < kCholNb; ++r) {
+    const double wv = Wn(const_cast<double*>(win), kb + r, c), yr = ypan[r];
+    t[r] = isz ? yr : (r < w ? wv : 0.0);
+  }
 #pragma unroll
   for (int k = kCholNb - 1; k >= 0; --k) {
     t[k] *= pinv[k];
@@ -1174,8 +1177,9 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
 #pragma unroll
       for (int r = 0; r < kCholNb; ++r) {
         const bool real = r < w;
-        ca[r] = (real && v && r <= slot) ? Wn(win, kb + r, c) : ((!real && slot == r) ? 1.0 : 0.0);
-        yv[r] = real ? yw[(kb + r) & (kCholWS - 1)] : 0.0;
+        const double wv = Wn(win, kb + r, c), yr = yw[(kb + r) & (kCholWS - 1)];   // unconditional loads
+        ca[r] = (real && v && r <= slot) ? wv : ((!real && slot == r) ? 1.0 : 0.0);
+        yv[r] = real ? yr : 0.0;
       }
       bool bad = false;
       SG_STAMP_AT(1)
@@ -1250,14 +1254,16 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
 #pragma unroll
       for (int qq = 0; qq < 4; ++qq) {
         const int row = i0 + lk + 4 * qq, col = j0 + li;
-        acc[qq] = (row < jend && col < jend && row <= col) ? Wn(win, row, col) : 0.0;
+        const double wv = Wn(win, row, col);   // ring index: always a valid address
+        acc[qq] = (row < jend && col < jend && row <= col) ? wv : 0.0;
       }
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4) {
         const int k = kb + 4 * s4 + lk;
         const bool kin = (4 * s4 + lk) < w;
-        const double av = (kin && i0 + li < jend) ? -Wn(win, k, i0 + li) : 0.0;
-        const double bv = (kin && j0 + li < jend) ? Wn(win, k, j0 + li) : 0.0;
+        const double wa = Wn(win, k, i0 + li), wb = Wn(win, k, j0 + li);
+        const double av = (kin && i0 + li < jend) ? -wa : 0.0;
+        const double bv = (kin && j0 + li < jend) ? wb : 0.0;
         acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
       }
 #pragma unroll
