@@ -20,11 +20,7 @@
 
 namespace sg {
 
-constexpr int kChunkPts = 128;      // points per chunk (one workgroup)
-constexpr int kLanesPerPt = 4;      // lanes per point in the observation sweeps
-constexpr int kSweepThreads = kChunkPts * kLanesPerPt;  // 512
 constexpr int kSchurThreads = 256;
-constexpr int kNbwMax = 24;         // max camera blocks in a chunk window (wider points go "wide")
 constexpr int kCamV = 27;           // per camera block: upper(Jc^T Jc) 21 + Jc^T r 6
 constexpr int kJStride = 24;
 constexpr int kNScal = 16;          // per-chunk scalar slots
@@ -41,14 +37,6 @@ enum CamX { kXCost = 0, kXFail, kXFixed, kXFixedFail, kXXnorm2, kXNum };
 enum UpdX { kUModel = 0, kUCandCost, kUCandFail, kUStep2, kUCandX2, kULinFail, kUNum };
 enum CholX { kCStep2 = 0, kCCandX2, kCModel, kCCandCost, kCFail, kCNum };
 
-struct Chunk {
-  int32_t p0, p1;     // point range [p0, p1) (device order)
-  int32_t b_lo, nb;   // camera-block window [b_lo, b_lo + nb)
-  int32_t cam_off;    // offset of this chunk's camera partials in cam_slab (doubles)
-  int32_t s_off;      // offset of this chunk's Schur window in S_slab (doubles)
-  int32_t wide;       // window too wide for LDS: accumulate with global atomics instead
-  int32_t pad;
-};
 
 // Schur work unit: up to kSegPts consecutive points (device order) sharing a window of <= kSegNbMax
 // camera blocks (or one "wide" point), with its slice of the observation-pair list.
@@ -61,6 +49,30 @@ struct SchurSeg {
   int32_t s_off;        // offset of the window partial in S_slab
   int32_t wide;         // global atomics instead of an LDS window
   int32_t pair_lo, pair_hi;
+};
+
+// k_linearize work decomposition: a chunk (one single-wave workgroup) is a run of consecutive points whose
+// camera blocks fit one window of <= kLinNbMax blocks, split into rounds of <= kLinObs observations and
+// <= kLinPts points that hold whole points (one observation per lane).  A point with more observations, or
+// spanning more blocks, is a "wide" chunk of its own: rounds are pieces of it and its camera terms go to
+// global atomics.
+constexpr int kLinThreads = 64;
+constexpr int kLinObs = 64;
+constexpr int kLinPts = 16;
+constexpr int kLinNbMax = 24;
+constexpr int kLinMaxRounds = 4;   // measured best at 130k and 1.6M observations
+struct LinRound {
+  int32_t o0, o1;     // observation range
+  int32_t p0, p1;     // points (whole points; every piece of a wide point names it)
+  int32_t lst;        // offset in lin_list (uint16): [nb + 1] per-block offsets, then local indices by block
+  int32_t pad;
+};
+struct LinChunk {
+  int32_t r0, r1;     // round range
+  int32_t b_lo, nb;   // camera window [b_lo, b_lo + nb) (nb = 0: no camera terms in LDS)
+  int32_t cam_off;    // offset of this chunk's camera partials in cam_slab (doubles)
+  int32_t wide;       // one point: camera terms by global atomics, point block reduced over the workgroup
+  int32_t p0, p1;
 };
 
 struct LmState {
@@ -122,8 +134,6 @@ struct Dev {
   double* camdiag;               // [n] diag(J^T J) camera columns, unscaled (obs + FD)
   double* camg;                  // [n] camera gradient, unscaled (obs + FD)
   // chunks and partials
-  const Chunk* chunks;
-  int32_t nchunks;
   const int32_t* cam_loff;       // [NB+1] CSR: per camera block, offsets of its partials in cam_slab
   const int32_t* cam_lidx;
   const int32_t* s_loff;         // [NB*NB+1] CSR: per block pair (I<=J), offsets of its partials in S_slab
@@ -132,7 +142,7 @@ struct Dev {
   const int32_t* r_lidx;
   double* cam_slab;
   double* S_slab;
-  double* chunk_scal;            // [nchunks][kNScal]
+  double* chunk_scal;            // [nlin][kNScal] k_point_update scalars
   double* cam_wide;              // [NB][27] (wide chunks, global atomics)
   double* S_wide;                // [n][n]   (wide chunks, global atomics)
   // exchange buffers (all-reduced across landmark shards)
@@ -148,6 +158,11 @@ struct Dev {
   int32_t assemble;              // this rank adds blockdiag(U) + FD + damping to S (rank 0 of a shard group)
   int32_t dbg;                   // development switches (SG_DBG), 0 in production
   const int32_t* obs_pnt;        // [M] point (device order) of each observation
+  const LinChunk* lchunks;       // [nlin] k_linearize workgroups
+  const LinRound* lrounds;
+  const uint16_t* llist;         // per round: window-block offsets + local observation indices by block
+  int32_t nlin;
+  double* lin_scal;              // [nlin][kNScal] k_linearize scalars (cost, failures, |x|^2, max |g|)
   const struct SchurSeg* segs;   // [nseg] Schur work units
   int32_t nseg;
   double* seg_fail;              // [nseg] point blocks whose damped inverse failed

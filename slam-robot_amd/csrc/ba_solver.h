@@ -59,10 +59,9 @@ class BaSolver {
 
  private:
   // host copies of the structure
-  int F_ = 0, P_ = 0, M_ = 0, NB_ = 0, n_ = 0, D_ = 0, nchunks_ = 0, max_nb_ = 0, ncam_ = 0;
+  int F_ = 0, P_ = 0, M_ = 0, NB_ = 0, n_ = 0, D_ = 0, ncam_ = 0;
   std::vector<int32_t> point_perm_;   // device order -> problem point
   std::vector<int32_t> obs_perm_;     // device order -> problem observation
-  std::vector<Chunk> chunks_;
   size_t schur_lds_ = 0;
   // device buffers
   DBuf<LmState> st_;
@@ -72,11 +71,15 @@ class BaSolver {
   DBuf<int32_t> frame_cam_, frame_block_, poff_, obs_frame_, fd_a_, fd_b_, fd_boff_, fd_bidx_, cam_loff_,
       cam_lidx_, s_loff_, s_lidx_, r_loff_, r_lidx_, mobs_frame_, mobs_point_, mframe_cam_;
   DBuf<uint8_t> rot_free_, trans_free_, pfree_, obs_fixed_;
-  DBuf<Chunk> chunks_d_;
   DBuf<int32_t> work_i_;   // Cholesky panel envelopes (panel_jmax)
   DBuf<int32_t> fd_pair_;
   DBuf<int32_t> obs_pnt_, pairs_;   // Schur work lists
   DBuf<SchurSeg> segs_;
+  DBuf<LinChunk> lchunks_d_;
+  DBuf<LinRound> lrounds_d_;
+  DBuf<uint16_t> llist_d_;
+  DBuf<double> lin_scal_;
+  int nlin_ = 0;
   DBuf<double> seg_fail_;
   int nseg_ = 0, max_seg_nb_ = 0, max_seg_obs_ = 0;  // FrameDistance cross-block lookup
   DBuf<double> rdg_;       // 1/U_jj of the factor

@@ -5,8 +5,8 @@
 // decision, trust-region update and termination tests run on the device (k_decide), so a solve is a
 // stream of identical iterations the host only polls for completion.
 //
-//   k_linearize    [chunk of 128 points, 4 lanes/point]  residuals + analytic Jacobians (HBM sweep),
-//                  point blocks V,g; camera blocks U,g_c into an LDS window (co-visibility band)
+//   k_linearize    [one wave: rounds of <= 64 observations, lane per observation]  residuals + analytic
+//                  Jacobians (HBM sweep), point blocks V,g; camera blocks U,g_c of the co-visibility window
 //   k_cam_reduce   deterministic reduce of per-chunk camera partials  -> xchg_cam   (all-reduced)
 //   k_cam_finalize FrameDistance terms, cost, gradient test, Jacobi scale (iteration 0), LM diagonal
 //   k_schur        [segment of <= 32 points] damped V^-1 (thread per point), P = J_p V^-1 (thread per
@@ -32,6 +32,10 @@
 #include "project_math.h"
 
 namespace sg {
+
+#ifndef SG_LIN_ATTR
+#define SG_LIN_ATTR
+#endif
 
 // ------------------------------------------------------------------------------------------------
 // small device helpers
@@ -61,6 +65,19 @@ __device__ __forceinline__ double wave_sum_full(double v) {
   v += dpp_d<0x141>(v);   // row_half_mirror
   v += dpp_d<0x140>(v);   // row_mirror: every lane holds its 16-lane row sum
   return (readlane_dd(v, 0) + readlane_dd(v, 16)) + (readlane_dd(v, 32) + readlane_dd(v, 48));
+}
+// LDS-only workgroup barrier: waits for this wave's LDS traffic, not for outstanding global loads or
+// stores (those may stay in flight across it).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+// Sum over aligned groups of 8 lanes by DPP (quad perms, then the half-row mirror pairs lane i with 7 - i):
+// every lane of the group gets the group sum, in the same order.  All 64 lanes must be active.
+__device__ __forceinline__ double sum8_dpp(double v) {
+  v += dpp_d<0xB1>(v);
+  v += dpp_d<0x4E>(v);
+  v += dpp_d<0x141>(v);
+  return v;
 }
 __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
@@ -185,44 +202,73 @@ __device__ __forceinline__ bool inv4_spd(const double* A, double* Ai) {
 __device__ __forceinline__ double sym4(const double* A, int a, int c) { return a <= c ? A[u4(a, c)] : A[u4(c, a)]; }
 
 // ------------------------------------------------------------------------------------------------
-// k_linearize: the Jacobian sweep.  One chunk (<=128 points) per workgroup, 8 lanes per point; each
-// lane walks its point's observations, evaluates project.h + its analytic Jacobian, the Cauchy
-// corrector, and stores the corrected block (24 doubles, one 192-byte record per observation).
-__global__ __launch_bounds__(kSweepThreads) void k_linearize(Dev d) {
+// k_linearize: the Jacobian sweep.  One LinChunk per single-wave workgroup (independent waves, no workgroup
+// barriers, so the chip interleaves one wave's projections with another's loads and stores), one
+// observation per lane: each lane evaluates project.h + its analytic Jacobian and the Cauchy corrector and
+// stores the corrected 24-double record (r~ 2 | Jc 12 | Jp 8 | cost | pad); its point-block terms
+// (V = Jp^T Jp, g = Jp^T r) and camera-block terms (upper Jc^T Jc, Jc^T r) go to LDS accumulators of the
+// round's points and of the chunk's camera window.  Only this wave touches its LDS, so the accumulation
+// order is fixed (program order, lanes serialised in hardware order).  The next round's observation inputs
+// are loaded before this round's projections.
+// Wave-local LDS ordering (single-wave workgroups): all of this wave's LDS operations are complete.
+__device__ __forceinline__ void lds_fence_wave() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+__global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_linearize(Dev d) {
   const LmState* st = d.st;
   if (st->done || !st->need_lin) return;
   const int cur = st->cur;
   const bool first = st->first != 0;
-  const Chunk ch = d.chunks[blockIdx.x];
-  __shared__ double cam[kNbwMax * kCamV];
-  __shared__ double red[kSweepThreads / 64];
-  const int ncv = ch.wide ? 0 : ch.nb * kCamV;
-  for (int i = threadIdx.x; i < ncv; i += blockDim.x) cam[i] = 0.0;
-  __syncthreads();
-
-  const int lp = threadIdx.x / kLanesPerPt, l8 = threadIdx.x % kLanesPerPt;
-  const int p = ch.p0 + lp;
+  const LinChunk ch = d.lchunks[blockIdx.x];
+  __shared__ double pacc[kLinPts * 14];         // point blocks of the round: V (10) | g (4)
+  __shared__ double camacc[kLinNbMax * kCamV];  // camera blocks of the window: upper Jc^T Jc (21) | Jc^T r (6)
+  const int lane = threadIdx.x;
+  const double4* X4 = reinterpret_cast<const double4*>(d.X[cur]);
+  const int ncv = ch.nb * kCamV;
+  for (int i = lane; i < ncv; i += kLinThreads) camacc[i] = 0.0;
+  for (int i = lane; i < kLinPts * 14; i += kLinThreads) pacc[i] = 0.0;
   double cost = 0.0, fail = 0.0, fixed = 0.0, ffail = 0.0, xn2 = 0.0, gmax = 0.0;
-  double V[10], g[4];
-#pragma unroll
-  for (int i = 0; i < 10; ++i) V[i] = 0.0;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) g[i] = 0.0;
-  bool pf = false;
-  if (p < ch.p1) {
-    pf = d.pfree[p] != 0;
-    const double4 Xv = reinterpret_cast<const double4*>(d.X[cur])[p];
-    const double X[4] = {Xv.x, Xv.y, Xv.z, Xv.w};
-    const int o1 = d.poff[p + 1];
-    for (int o = d.poff[p] + l8; o < o1; o += kLanesPerPt) {
-      const int f = d.obs_frame[o];
-      const double* q = d.q[cur] + 4 * f;
-      const double* t = d.t[cur] + 3 * f;
-      const double* k = d.k + 7 * d.frame_cam[f];
-      const bool fx = d.obs_fixed[o] != 0;
-      double r[2], Jc[12], Jp[8], c;
+  // per-observation inputs, software-pipelined one round ahead
+  LinRound R = d.lrounds[ch.r0];
+  int nobs = R.o1 - R.o0;
+  double2 n_uv = make_double2(0.0, 0.0);
+  int n_f = 0, n_p = 0, n_fx = 0;
+  if (lane < nobs) {
+    const int o = R.o0 + lane;
+    n_uv = reinterpret_cast<const double2*>(d.obs_pt)[o];
+    n_f = d.obs_frame[o];
+    n_p = d.obs_pnt[o];
+    n_fx = d.obs_fixed[o];
+  }
+  lds_fence_wave();
+  for (int r = ch.r0; r < ch.r1; ++r) {
+    const double2 uv = n_uv;
+    const int f = n_f, p = n_p;
+    const bool fx = n_fx != 0;
+    const LinRound Rc = R;
+    const int nc = nobs;
+    if (r + 1 < ch.r1) {
+      R = d.lrounds[r + 1];
+      nobs = R.o1 - R.o0;
+      if (lane < nobs) {
+        const int o = R.o0 + lane;
+        n_uv = reinterpret_cast<const double2*>(d.obs_pt)[o];
+        n_f = d.obs_frame[o];
+        n_p = d.obs_pnt[o];
+        n_fx = d.obs_fixed[o];
+      }
+    }
+    if (lane < nc) {
+      const int o = Rc.o0 + lane;
+      const bool pf = d.pfree[p] != 0;
+      const double4 Xv = X4[p];
+      const double X[4] = {Xv.x, Xv.y, Xv.z, Xv.w};
+      const double pt[2] = {uv.x, uv.y};
+      double rr[2], Jc[12], Jp[8], c;
+      const bool ok = LinearizeObservation(d.q[cur] + 4 * f, d.t[cur] + 3 * f, d.k + 7 * d.frame_cam[f], X, pt,
+                                           d.b, d.inv_b, rr, Jc, Jp, &c);
       double2* Jo = reinterpret_cast<double2*>(d.J + (size_t)o * kJStride);
-      const bool ok = LinearizeObservation(q, t, k, X, d.obs_pt + 2 * o, d.b, d.inv_b, r, Jc, Jp, &c);
       if (!ok || fx) {
         if (!ok) {
           if (fx) ffail += 1.0;
@@ -231,82 +277,98 @@ __global__ __launch_bounds__(kSweepThreads) void k_linearize(Dev d) {
           fixed += c;
         }
 #pragma unroll
-        for (int i = 0; i < 12; ++i) Jo[i] = make_double2(0.0, 0.0);
-        continue;
-      }
-      cost += c;
-      const int b = d.frame_block[f];
-      if (b < 0) {
-#pragma unroll
-        for (int i = 0; i < 12; ++i) Jc[i] = 0.0;
+        for (int i = 0; i < kJStride / 2; ++i) Jo[i] = make_double2(0.0, 0.0);
       } else {
-        if (!d.rot_free[f]) { Jc[0] = Jc[1] = Jc[2] = Jc[6] = Jc[7] = Jc[8] = 0.0; }
-        if (!d.trans_free[f]) { Jc[3] = Jc[4] = Jc[5] = Jc[9] = Jc[10] = Jc[11] = 0.0; }
-      }
-      if (!pf) {
+        cost += c;
+        const int b = d.frame_block[f];
+        if (b < 0) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) Jp[i] = 0.0;
-      }
-      Jo[0] = make_double2(r[0], r[1]);
-#pragma unroll
-      for (int i = 0; i < 6; ++i) Jo[1 + i] = make_double2(Jc[2 * i], Jc[2 * i + 1]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) Jo[7 + i] = make_double2(Jp[2 * i], Jp[2 * i + 1]);
-      Jo[11] = make_double2(c, 0.0);
-      if (pf) {
-#pragma unroll
-        for (int a = 0; a < 4; ++a) {
-          g[a] += Jp[a] * r[0] + Jp[4 + a] * r[1];
-#pragma unroll
-          for (int cc = 0; cc < 4; ++cc)
-            if (cc >= a) V[u4(a, cc)] += Jp[a] * Jp[cc] + Jp[4 + a] * Jp[4 + cc];
+          for (int i = 0; i < 12; ++i) Jc[i] = 0.0;
+        } else {
+          if (!d.rot_free[f]) { Jc[0] = Jc[1] = Jc[2] = Jc[6] = Jc[7] = Jc[8] = 0.0; }
+          if (!d.trans_free[f]) { Jc[3] = Jc[4] = Jc[5] = Jc[9] = Jc[10] = Jc[11] = 0.0; }
         }
-      }
-      if (b >= 0) {
-        double* dst = ch.wide ? d.cam_wide + (size_t)b * kCamV : cam + (b - ch.b_lo) * kCamV;
+        if (!pf) {
 #pragma unroll
-        for (int a = 0; a < 6; ++a) {
+          for (int i = 0; i < 8; ++i) Jp[i] = 0.0;
+        }
+        Jo[0] = make_double2(rr[0], rr[1]);
 #pragma unroll
-          for (int cc = 0; cc < 6; ++cc)
-            if (cc >= a) atomicAdd(dst + u6(a, cc), Jc[a] * Jc[cc] + Jc[6 + a] * Jc[6 + cc]);
-          atomicAdd(dst + 21 + a, Jc[a] * r[0] + Jc[6 + a] * r[1]);
+        for (int i = 0; i < 6; ++i) Jo[1 + i] = make_double2(Jc[2 * i], Jc[2 * i + 1]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) Jo[7 + i] = make_double2(Jp[2 * i], Jp[2 * i + 1]);
+        Jo[11] = make_double2(c, 0.0);
+        if (pf) {
+          double* pa = pacc + (p - Rc.p0) * 14;
+#pragma unroll
+          for (int a = 0; a < 4; ++a) {
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc)
+              if (cc >= a) atomicAdd(pa + u4(a, cc), Jp[a] * Jp[cc] + Jp[4 + a] * Jp[4 + cc]);
+            atomicAdd(pa + 10 + a, Jp[a] * rr[0] + Jp[4 + a] * rr[1]);
+          }
+        }
+        if (b >= 0) {
+          // separate paths: a pointer that may be LDS or global would make these flat atomics
+          auto add_cam = [&](double* dst) {
+#pragma unroll
+            for (int a = 0; a < 6; ++a) {
+#pragma unroll
+              for (int cc = 0; cc < 6; ++cc)
+                if (cc >= a) atomicAdd(dst + u6(a, cc), Jc[a] * Jc[cc] + Jc[6 + a] * Jc[6 + cc]);
+              atomicAdd(dst + 21 + a, Jc[a] * rr[0] + Jc[6 + a] * rr[1]);
+            }
+          };
+          if (ch.wide) add_cam(d.cam_wide + (size_t)b * kCamV);
+          else add_cam(camacc + (b - ch.b_lo) * kCamV);
         }
       }
     }
-    // reduce the point blocks across the 8 lanes of this point
+    // point blocks of the round's (whole) points; a wide chunk's one point after its last piece
+    if (!ch.wide || r + 1 == ch.r1) {
+      lds_fence_wave();
+      const int np = Rc.p1 - Rc.p0;
+      if (lane < np) {
+        const int pp = Rc.p0 + lane;
+        double* pa = pacc + lane * 14;
+        double V[10], g[4];
 #pragma unroll
-    for (int m = 1; m < kLanesPerPt; m <<= 1) {
+        for (int i = 0; i < 10; ++i) V[i] = pa[i];
 #pragma unroll
-      for (int i = 0; i < 10; ++i) V[i] += __shfl_xor(V[i], m);
+        for (int i = 0; i < 4; ++i) g[i] = pa[10 + i];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) g[i] += __shfl_xor(g[i], m);
-    }
-    if (l8 == 0) {
-      double* Vd = d.V + 10 * (size_t)p;
+        for (int i = 0; i < 14; ++i) pa[i] = 0.0;
+        const bool pf = d.pfree[pp] != 0;
+        double2* Vd = reinterpret_cast<double2*>(d.V + 10 * (size_t)pp);
 #pragma unroll
-      for (int i = 0; i < 10; ++i) Vd[i] = V[i];
-      reinterpret_cast<double4*>(d.g)[p] = make_double4(g[0], g[1], g[2], g[3]);
-      if (pf) {
-        gmax = fmax(fmax(fabs(g[0]), fabs(g[1])), fmax(fabs(g[2]), fabs(g[3])));
-        if (first) {
-          reinterpret_cast<double4*>(d.scale_p)[p] =
-              make_double4(1.0 / (1.0 + sqrt(V[0])), 1.0 / (1.0 + sqrt(V[4])), 1.0 / (1.0 + sqrt(V[7])),
-                           1.0 / (1.0 + sqrt(V[9])));
-          xn2 = X[0] * X[0] + X[1] * X[1] + X[2] * X[2] + X[3] * X[3];
+        for (int k = 0; k < 5; ++k) Vd[k] = make_double2(V[2 * k], V[2 * k + 1]);
+        reinterpret_cast<double4*>(d.g)[pp] = make_double4(g[0], g[1], g[2], g[3]);
+        if (pf) {
+          gmax = fmax(gmax, fmax(fmax(fabs(g[0]), fabs(g[1])), fmax(fabs(g[2]), fabs(g[3]))));
+          if (first) {
+            reinterpret_cast<double4*>(d.scale_p)[pp] =
+                make_double4(1.0 / (1.0 + sqrt(V[0])), 1.0 / (1.0 + sqrt(V[4])), 1.0 / (1.0 + sqrt(V[7])),
+                             1.0 / (1.0 + sqrt(V[9])));
+            const double4 Xv = X4[pp];
+            xn2 += Xv.x * Xv.x + Xv.y * Xv.y + Xv.z * Xv.z + Xv.w * Xv.w;
+          }
+        } else if (first) {
+          reinterpret_cast<double4*>(d.scale_p)[pp] = make_double4(1.0, 1.0, 1.0, 1.0);
         }
-      } else if (first) {
-        reinterpret_cast<double4*>(d.scale_p)[p] = make_double4(1.0, 1.0, 1.0, 1.0);
       }
+      lds_fence_wave();
     }
   }
-  cost = block_sum<kSweepThreads>(cost, red);
-  fail = block_sum<kSweepThreads>(fail, red);
-  fixed = block_sum<kSweepThreads>(fixed, red);
-  ffail = block_sum<kSweepThreads>(ffail, red);
-  xn2 = block_sum<kSweepThreads>(xn2, red);
-  gmax = block_max<kSweepThreads>(gmax, red);
-  double* sc = d.chunk_scal + (size_t)blockIdx.x * kNScal;
-  if (threadIdx.x == 0) {
+  lds_fence_wave();
+  for (int i = lane; i < ncv; i += kLinThreads) d.cam_slab[ch.cam_off + i] = camacc[i];
+  cost = wave_sum_full(cost);
+  fail = wave_sum_full(fail);
+  fixed = wave_sum_full(fixed);
+  ffail = wave_sum_full(ffail);
+  xn2 = wave_sum_full(xn2);
+  gmax = wave_max(gmax);
+  if (lane == 0) {
+    double* sc = d.lin_scal + (size_t)blockIdx.x * kNScal;
     sc[kCost] = cost;
     sc[kFail] = fail;
     sc[kFixed] = fixed;
@@ -314,48 +376,61 @@ __global__ __launch_bounds__(kSweepThreads) void k_linearize(Dev d) {
     sc[kXnorm2] = xn2;
     sc[kGmax] = gmax;
   }
-  __syncthreads();
-  for (int i = threadIdx.x; i < ncv; i += blockDim.x) d.cam_slab[ch.cam_off + i] = cam[i];
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_cam_reduce: deterministic sum of the per-chunk camera partials (+ wide-chunk atomics).
-__global__ __launch_bounds__(256) void k_cam_reduce(Dev d) {
+// k_cam_reduce: deterministic sum of the per-chunk camera partials (+ wide-chunk atomics).  One workgroup
+// per camera block: kCamSlices slices x 27 elements, each slice summing every kCamSlices-th partial of the
+// block's list, the slices combined in slice order; the last workgroup reduces the chunk scalars.
+constexpr int kCamSlices = 32;
+constexpr int kRedThreads = 1024;   // >= kCamSlices * kCamV
+__global__ __launch_bounds__(kRedThreads) void k_cam_reduce(Dev d) {
   const LmState* st = d.st;
   if (st->done || !st->need_lin) return;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int tid = threadIdx.x;
   const int nv = d.NB * kCamV;
-  if (i < nv) {
-    const int b = i / kCamV, e = i % kCamV;
-    double s = d.cam_wide[i];
-    d.cam_wide[i] = 0.0;
-    const int j0 = d.cam_loff[b], j1 = d.cam_loff[b + 1];
+  if ((int)blockIdx.x < d.NB) {
+    const int b = blockIdx.x;
+    __shared__ double part[kCamSlices][kCamV];
+    const int e = tid % kCamV, sl = tid / kCamV;
+    if (sl < kCamSlices) {
+      const int j0 = d.cam_loff[b], j1 = d.cam_loff[b + 1];
+      double acc = 0.0;
 #pragma unroll 4
-    for (int j = j0; j < j1; ++j) s += d.cam_slab[d.cam_lidx[j] + e];
-    d.xchg_cam[i] = s;
+      for (int j = j0 + sl; j < j1; j += kCamSlices) acc += d.cam_slab[d.cam_lidx[j] + e];
+      part[sl][e] = acc;
+    }
+    __syncthreads();
+    if (tid < kCamV) {
+      const int i = b * kCamV + tid;
+      double s = d.cam_wide[i];
+      d.cam_wide[i] = 0.0;
+#pragma unroll
+      for (int k = 0; k < kCamSlices; ++k) s += part[k][tid];
+      d.xchg_cam[i] = s;
+    }
+    return;
   }
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x < 64) {
-    // scalars: one wave, lane l sums chunks l, l+64, ... then a fixed-order tree
-    const int lane = threadIdx.x;
-    double v[kXNum] = {0, 0, 0, 0, 0};
-    double gm = 0.0;
-    for (int c = lane; c < d.nchunks; c += 64) {
-      const double* sc = d.chunk_scal + (size_t)c * kNScal;
-      v[kXCost] += sc[kCost];
-      v[kXFail] += sc[kFail];
-      v[kXFixed] += sc[kFixed];
-      v[kXFixedFail] += sc[kFixedFail];
-      v[kXXnorm2] += sc[kXnorm2];
-      gm = fmax(gm, sc[kGmax]);
-    }
+  // scalars: thread t sums chunks t, t + 1024, ..., then a fixed-order workgroup tree
+  __shared__ double red[kRedThreads / 64];
+  double v[kXNum] = {0, 0, 0, 0, 0};
+  double gm = 0.0;
+  for (int c = tid; c < d.nlin; c += kRedThreads) {
+    const double* sc = d.lin_scal + (size_t)c * kNScal;
+    v[kXCost] += sc[kCost];
+    v[kXFail] += sc[kFail];
+    v[kXFixed] += sc[kFixed];
+    v[kXFixedFail] += sc[kFixedFail];
+    v[kXXnorm2] += sc[kXnorm2];
+    gm = fmax(gm, sc[kGmax]);
+  }
 #pragma unroll
-    for (int j = 0; j < kXNum; ++j) v[j] = wave_sum(v[j]);
-    gm = wave_max(gm);
-    if (lane == 0) {
+  for (int j = 0; j < kXNum; ++j) v[j] = block_sum<kRedThreads>(v[j], red);
+  gm = block_max<kRedThreads>(gm, red);
+  if (tid == 0) {
 #pragma unroll
-      for (int j = 0; j < kXNum; ++j) d.xchg_cam[nv + j] = v[j];
-      d.xchg_max[0] = gm;
-    }
+    for (int j = 0; j < kXNum; ++j) d.xchg_cam[nv + j] = v[j];
+    d.xchg_max[0] = gm;
   }
 }
 
@@ -517,7 +592,7 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d) {
 //   2. thread per observation: P_o = J~p,o V~^-1 staged in LDS, and the rhs term -A_c,o^T (A_p,o t_p);
 //   3. thread per observation pair (s <= t) of a point, from a pair list built at load time: the 6x6 block
 //      -A_c,s^T (P_s A_p,t^T) A_c,t accumulated into the chunk's window of the reduced system (LDS atomics;
-//      windows wider than kNbwMax blocks go to global atomics).
+//      windows wider than kSegNbMax blocks go to global atomics).
 
 __device__ __forceinline__ void load_Jc_scaled(const Dev& d, int o, int b, double* Jc) {
   const double2* J2 = reinterpret_cast<const double2*>(d.J + (size_t)o * kJStride) + 1;   // skip r
@@ -833,11 +908,6 @@ __device__ __forceinline__ int opaque_lane() {
   return v;
 }
 
-// LDS-only workgroup barrier: waits for this wave's LDS traffic, not for outstanding global loads or
-// stores (those may stay in flight across it).
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
 
 // Unblocked factorisation of the w x w diagonal block held column-per-lane (lanes 0..w-1, col[r] =
 // A[r][lane] for r <= lane), broadcasts by v_readlane.  `bad` is set on a non-positive pivot.
@@ -1391,115 +1461,161 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_global(Dev d, const i
 // ------------------------------------------------------------------------------------------------
 // k_point_update: back-substitution x_p = V~^-1 (g~_p - A_p^T A_c x_c), model cost change
 // -(A s).(r + A s / 2), candidate point X+ = X - S_p x_p and the candidate reprojection cost.
-__global__ __launch_bounds__(kSweepThreads) void k_point_update(Dev d) {
+// Same work decomposition as k_linearize (one wave per LinChunk, one observation per lane, rounds of
+// whole points): each observation's record is read once; per round
+//   1. lane per observation: u = A_c x_c, and A_p^T u into the LDS accumulator of its point;
+//   2. lane per point: x_p, X+, |step|^2, |X+|^2;
+//   3. lane per observation: the model term and the candidate projection at X+ (project.h).
+// A wide chunk (one point over several rounds) runs pass 1 over all its pieces, then 2, then 3.
+struct PuObs {
+  double r[2], Jp[8], u[2];
+  int f, b;
+  bool on;   // a non-fixed observation of this round
+};
+
+// pacc == nullptr: the records only (a wide chunk's second walk).
+__device__ __forceinline__ void pu_pass1(const Dev& d, const LinRound& R, int lane, double* pacc, PuObs& ob) {
+  ob.on = false;
+  const int nc = R.o1 - R.o0;
+  if (lane >= nc) return;
+  const int o = R.o0 + lane;
+  if (d.obs_fixed[o]) return;
+  ob.on = true;
+  const int p = d.obs_pnt[o];
+  ob.f = d.obs_frame[o];
+  ob.b = d.frame_block[ob.f];
+  const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
+  const double sp[4] = {s4.x, s4.y, s4.z, s4.w};
+  double Jc[12];
+  load_scaled_J(d, o, ob.b, sp, ob.r, Jc, ob.Jp);
+  ob.u[0] = ob.u[1] = 0.0;
+  if (ob.b >= 0) {
+    const double* xc = d.xc + 6 * ob.b;
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+      ob.u[0] += Jc[c] * xc[c];
+      ob.u[1] += Jc[6 + c] * xc[c];
+    }
+    if (pacc && d.pfree[p]) {
+      double* pa = pacc + (p - R.p0) * 4;
+#pragma unroll
+      for (int a = 0; a < 4; ++a) atomicAdd(pa + a, ob.Jp[a] * ob.u[0] + ob.Jp[4 + a] * ob.u[1]);
+    }
+  }
+}
+
+__device__ __forceinline__ void pu_pass3(const Dev& d, const LinRound& R, int lane, int nxt, const double* xps,
+                                         const double* Xns, const PuObs& ob, double& model, double& candcost,
+                                         double& candfail) {
+  if (!ob.on) return;
+  const int o = R.o0 + lane;
+  const int lp = d.obs_pnt[o] - R.p0;
+  const double* xp = xps + 4 * lp;
+  double m0 = -ob.u[0], m1 = -ob.u[1];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    m0 -= ob.Jp[c] * xp[c];
+    m1 -= ob.Jp[4 + c] * xp[c];
+  }
+  model -= m0 * (ob.r[0] + 0.5 * m0) + m1 * (ob.r[1] + 0.5 * m1);
+  const double Xn[4] = {Xns[4 * lp], Xns[4 * lp + 1], Xns[4 * lp + 2], Xns[4 * lp + 3]};
+  double uv[2];
+  if (!Project(d.q[nxt] + 4 * ob.f, d.t[nxt] + 3 * ob.f, d.k + 7 * d.frame_cam[ob.f], Xn, uv)) {
+    candfail += 1.0;
+    return;
+  }
+  const double2 pt = reinterpret_cast<const double2*>(d.obs_pt)[o];
+  const double e0 = uv[0] - pt.x, e1 = uv[1] - pt.y;
+  double rho0, rho1;
+  Cauchy(e0 * e0 + e1 * e1, d.b, d.inv_b, &rho0, &rho1);
+  candcost += 0.5 * rho0;
+}
+
+// pass 2 for the points [p0, p1) of a round (lane per point): x_p, X+ into LDS and HBM.
+__device__ __forceinline__ void pu_pass2(const Dev& d, int p0, int p1, int lane, int cur, int nxt, double* pacc,
+                                         double* xps, double* Xns, double& step2, double& candx2) {
+  if (lane >= p1 - p0) return;
+  const int p = p0 + lane;
+  const bool pf = d.pfree[p] != 0;
+  const double4 Xv = reinterpret_cast<const double4*>(d.X[cur])[p];
+  const double X[4] = {Xv.x, Xv.y, Xv.z, Xv.w};
+  double* pa = pacc + 4 * lane;
+  double xp[4] = {0.0, 0.0, 0.0, 0.0}, Xn[4] = {X[0], X[1], X[2], X[3]};
+  if (pf) {
+    const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
+    const double sp[4] = {s4.x, s4.y, s4.z, s4.w};
+    const double4 g4 = reinterpret_cast<const double4*>(d.g)[p];
+    const double rhs[4] = {g4.x * sp[0] - pa[0], g4.y * sp[1] - pa[1], g4.z * sp[2] - pa[2], g4.w * sp[3] - pa[3]};
+    const double* Vi = d.Vinv + 10 * (size_t)p;
+    double Vl[10];
+#pragma unroll
+    for (int i = 0; i < 10; ++i) Vl[i] = Vi[i];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      double s = 0.0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) s += sym4(Vl, a, c) * rhs[c];
+      xp[a] = s;
+    }
+    // step s_p = -x_p (scaled); candidate X+ = X + S_p s_p
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      Xn[a] = X[a] + (-xp[a] * sp[a]);
+      step2 += (Xn[a] - X[a]) * (Xn[a] - X[a]);
+      candx2 += Xn[a] * Xn[a];
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    pa[a] = 0.0;
+    xps[4 * lane + a] = xp[a];
+    Xns[4 * lane + a] = Xn[a];
+  }
+  reinterpret_cast<double4*>(d.X[nxt])[p] = make_double4(Xn[0], Xn[1], Xn[2], Xn[3]);
+}
+
+__global__ __launch_bounds__(kLinThreads) void k_point_update(Dev d) {
   const LmState* st = d.st;
   if (st->done) return;
   const int cur = st->cur, nxt = cur ^ 1;
-  const Chunk ch = d.chunks[blockIdx.x];
-  __shared__ double red[kSweepThreads / 64];
-  const int lp = threadIdx.x / kLanesPerPt, l8 = threadIdx.x % kLanesPerPt;
-  const int p = ch.p0 + lp;
+  const LinChunk ch = d.lchunks[blockIdx.x];
+  __shared__ double pacc[kLinPts * 4], xps[kLinPts * 4], Xns[kLinPts * 4];
+  const int lane = threadIdx.x;
+  for (int i = lane; i < kLinPts * 4; i += kLinThreads) pacc[i] = 0.0;
+  lds_fence_wave();
   double model = 0.0, candcost = 0.0, candfail = 0.0, step2 = 0.0, candx2 = 0.0;
-  if (p < ch.p1) {
-    const bool pf = d.pfree[p] != 0;
-    const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
-    const double sp[4] = {s4.x, s4.y, s4.z, s4.w};
-    const double4 Xv = reinterpret_cast<const double4*>(d.X[cur])[p];
-    const double X[4] = {Xv.x, Xv.y, Xv.z, Xv.w};
-    const int o0 = d.poff[p], o1 = d.poff[p + 1];
-    double xp[4] = {0.0, 0.0, 0.0, 0.0};
-    if (pf) {
-      double acc[4] = {0.0, 0.0, 0.0, 0.0};
-      for (int o = o0 + l8; o < o1; o += kLanesPerPt) {
-        if (d.obs_fixed[o]) continue;
-        const int b = d.frame_block[d.obs_frame[o]];
-        if (b < 0) continue;
-        double r[2], Jc[12], Jp[8];
-        load_scaled_J(d, o, b, sp, r, Jc, Jp);
-        const double* xc = d.xc + 6 * b;
-        double u0 = 0.0, u1 = 0.0;
-#pragma unroll
-        for (int c = 0; c < 6; ++c) {
-          u0 += Jc[c] * xc[c];
-          u1 += Jc[6 + c] * xc[c];
-        }
-#pragma unroll
-        for (int a = 0; a < 4; ++a) acc[a] += Jp[a] * u0 + Jp[4 + a] * u1;
-      }
-#pragma unroll
-      for (int m = 1; m < kLanesPerPt; m <<= 1)
-#pragma unroll
-        for (int a = 0; a < 4; ++a) acc[a] += __shfl_xor(acc[a], m);
-      const double4 g4 = reinterpret_cast<const double4*>(d.g)[p];
-      const double rhs[4] = {g4.x * sp[0] - acc[0], g4.y * sp[1] - acc[1], g4.z * sp[2] - acc[2],
-                             g4.w * sp[3] - acc[3]};
-      const double* Vi = d.Vinv + 10 * (size_t)p;
-      double Vl[10];
-#pragma unroll
-      for (int i = 0; i < 10; ++i) Vl[i] = Vi[i];
-#pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        double s = 0.0;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) s += sym4(Vl, a, c) * rhs[c];
-        xp[a] = s;
-      }
+  if (!ch.wide) {
+    for (int r = ch.r0; r < ch.r1; ++r) {
+      const LinRound R = d.lrounds[r];
+      PuObs ob;
+      pu_pass1(d, R, lane, pacc, ob);
+      lds_fence_wave();
+      pu_pass2(d, R.p0, R.p1, lane, cur, nxt, pacc, xps, Xns, step2, candx2);
+      lds_fence_wave();
+      pu_pass3(d, R, lane, nxt, xps, Xns, ob, model, candcost, candfail);
+      lds_fence_wave();
     }
-    // step s_p = -x_p (scaled); candidate X+ = X + S_p s_p
-    double Xn[4];
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      const double dl = -xp[a] * sp[a];
-      Xn[a] = pf ? X[a] + dl : X[a];
+  } else {
+    for (int r = ch.r0; r < ch.r1; ++r) {
+      PuObs ob;
+      pu_pass1(d, d.lrounds[r], lane, pacc, ob);
     }
-    if (l8 == 0) {
-      reinterpret_cast<double4*>(d.X[nxt])[p] = make_double4(Xn[0], Xn[1], Xn[2], Xn[3]);
-      if (pf) {
-#pragma unroll
-        for (int a = 0; a < 4; ++a) {
-          step2 += (Xn[a] - X[a]) * (Xn[a] - X[a]);
-          candx2 += Xn[a] * Xn[a];
-        }
-      }
-    }
-    for (int o = o0 + l8; o < o1; o += kLanesPerPt) {
-      if (d.obs_fixed[o]) continue;
-      const int f = d.obs_frame[o];
-      const int b = d.frame_block[f];
-      double r[2], Jc[12], Jp[8];
-      load_scaled_J(d, o, b, sp, r, Jc, Jp);
-      double m0 = 0.0, m1 = 0.0;
-      if (b >= 0) {
-        const double* xc = d.xc + 6 * b;
-#pragma unroll
-        for (int c = 0; c < 6; ++c) {
-          m0 -= Jc[c] * xc[c];
-          m1 -= Jc[6 + c] * xc[c];
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        m0 -= Jp[c] * xp[c];
-        m1 -= Jp[4 + c] * xp[c];
-      }
-      model -= m0 * (r[0] + 0.5 * m0) + m1 * (r[1] + 0.5 * m1);
-      double uv[2];
-      if (!Project(d.q[nxt] + 4 * f, d.t[nxt] + 3 * f, d.k + 7 * d.frame_cam[f], Xn, uv)) {
-        candfail += 1.0;
-        continue;
-      }
-      const double e0 = uv[0] - d.obs_pt[2 * o], e1 = uv[1] - d.obs_pt[2 * o + 1];
-      double rho0, rho1;
-      Cauchy(e0 * e0 + e1 * e1, d.b, d.inv_b, &rho0, &rho1);
-      candcost += 0.5 * rho0;
+    lds_fence_wave();
+    pu_pass2(d, ch.p0, ch.p1, lane, cur, nxt, pacc, xps, Xns, step2, candx2);
+    lds_fence_wave();
+    for (int r = ch.r0; r < ch.r1; ++r) {
+      const LinRound R = d.lrounds[r];
+      PuObs ob;
+      pu_pass1(d, R, lane, nullptr, ob);
+      pu_pass3(d, R, lane, nxt, xps, Xns, ob, model, candcost, candfail);
     }
   }
-  model = block_sum<kSweepThreads>(model, red);
-  candcost = block_sum<kSweepThreads>(candcost, red);
-  candfail = block_sum<kSweepThreads>(candfail, red);
-  step2 = block_sum<kSweepThreads>(step2, red);
-  candx2 = block_sum<kSweepThreads>(candx2, red);
-  if (threadIdx.x == 0) {
+  model = wave_sum_full(model);
+  candcost = wave_sum_full(candcost);
+  candfail = wave_sum_full(candfail);
+  step2 = wave_sum_full(step2);
+  candx2 = wave_sum_full(candx2);
+  if (lane == 0) {
     double* sc = d.chunk_scal + (size_t)blockIdx.x * kNScal;
     sc[kModel] = model;
     sc[kCandCost] = candcost;
@@ -1509,12 +1625,13 @@ __global__ __launch_bounds__(kSweepThreads) void k_point_update(Dev d) {
   }
 }
 
-__global__ __launch_bounds__(64) void k_upd_reduce(Dev d) {
+__global__ __launch_bounds__(kRedThreads) void k_upd_reduce(Dev d) {
   const LmState* st = d.st;
   if (st->done) return;
-  const int lane = threadIdx.x;
+  __shared__ double red[kRedThreads / 64];
+  const int tid = threadIdx.x;
   double v[kUNum] = {0, 0, 0, 0, 0, 0};
-  for (int c = lane; c < d.nchunks; c += 64) {
+  for (int c = tid; c < d.nlin; c += kRedThreads) {
     const double* sc = d.chunk_scal + (size_t)c * kNScal;
     v[kUModel] += sc[kModel];
     v[kUCandCost] += sc[kCandCost];
@@ -1522,10 +1639,10 @@ __global__ __launch_bounds__(64) void k_upd_reduce(Dev d) {
     v[kUStep2] += sc[kStep2];
     v[kUCandX2] += sc[kCandX2];
   }
-  for (int g = lane; g < d.nseg; g += 64) v[kULinFail] += d.seg_fail[g];
+  for (int g = tid; g < d.nseg; g += kRedThreads) v[kULinFail] += d.seg_fail[g];
 #pragma unroll
-  for (int j = 0; j < kUNum; ++j) v[j] = wave_sum(v[j]);
-  if (lane == 0)
+  for (int j = 0; j < kUNum; ++j) v[j] = block_sum<kRedThreads>(v[j], red);
+  if (tid == 0)
 #pragma unroll
     for (int j = 0; j < kUNum; ++j) d.xchg_upd[j] = v[j];
 }
@@ -1775,46 +1892,85 @@ void BaSolver::Load(const sg_problem& p) {
     obs_frame[o] = p.obs_frame[src];
     obs_fixed[o] = frame_block[p.obs_frame[src]] < 0 && !p.point_free[p.obs_point[src]];
   }
-  // chunks: up to kChunkPts consecutive points whose camera blocks fit a window of kNbwMax blocks
-  chunks_.clear();
-  max_nb_ = 0;
-  int cam_off = 0;
-  for (int i = 0; i < P_;) {
-    const int pt0 = point_perm_[i];
-    const int lo = pfirst[pt0];
-    Chunk c{};
-    c.p0 = i;
-    int j = i + 1;
-    if (lo >= NB_) {              // points observed only by constant frames
-      while (j < P_ && j - i < kChunkPts) ++j;
-      c.b_lo = 0;
-      c.nb = 0;
-    } else if (plast[pt0] - lo + 1 > kNbwMax) {
-      c.wide = 1;                 // one point spanning more blocks than the LDS window: global atomics
-      c.b_lo = lo;
-      c.nb = 0;
-    } else {
-      int hi = plast[pt0];
-      while (j < P_ && j - i < kChunkPts) {
-        const int ptj = point_perm_[j];
-        if (pfirst[ptj] >= NB_) break;
-        const int h = std::max(hi, plast[ptj]);
-        if (h - lo + 1 > kNbwMax) break;
-        hi = h;
-        ++j;
+  // k_linearize decomposition (see LinChunk): rounds of whole points (<= kLinObs observations), up to
+  // maxr rounds per chunk sharing one camera window; fewer rounds per chunk on small problems so that the
+  // grid still fills the chip.
+  std::vector<LinRound> lrounds;
+  std::vector<LinChunk> lchunks;
+  std::vector<uint16_t> llist;
+  int lcam_off = 0;
+  {
+    int maxr = std::max(1, std::min(kLinMaxRounds, M_ / (kLinObs * 1024)));
+    if (getenv("SG_LIN_MAXR")) maxr = std::max(1, atoi(getenv("SG_LIN_MAXR")));   // tuning experiments
+    auto kobs = [&](int i) { return poff[i + 1] - poff[i]; };
+    auto constonly = [&](int i) { return pfirst[point_perm_[i]] >= NB_; };
+    auto pspan = [&](int i) { return constonly(i) ? 0 : plast[point_perm_[i]] - pfirst[point_perm_[i]] + 1; };
+    for (int i = 0; i < P_;) {
+      LinChunk c{};
+      c.p0 = i;
+      c.r0 = (int)lrounds.size();
+      if (kobs(i) > kLinObs || pspan(i) > kLinNbMax) {
+        c.wide = 1;
+        for (int o = poff[i]; o < poff[i + 1]; o += kLinObs)
+          lrounds.push_back(LinRound{o, std::min(o + kLinObs, poff[i + 1]), i, i + 1, 0, 0});
+        c.p1 = ++i;
+      } else {
+        const bool co = constonly(i);
+        int lo = co ? 0 : pfirst[point_perm_[i]], hi = co ? -1 : plast[point_perm_[i]];
+        int j = i, nr = 0;
+        LinRound R{poff[i], poff[i], i, i, 0, 0};
+        while (j < P_) {
+          if (kobs(j) > kLinObs || pspan(j) > kLinNbMax || constonly(j) != co) break;
+          int l2 = lo, h2 = hi;
+          if (!co) {
+            l2 = std::min(lo, pfirst[point_perm_[j]]);
+            h2 = std::max(hi, plast[point_perm_[j]]);
+            if (h2 - l2 + 1 > kLinNbMax) break;
+          }
+          if (R.o1 - R.o0 + kobs(j) > kLinObs || R.p1 - R.p0 >= kLinPts) {
+            if (nr + 1 >= maxr) break;
+            lrounds.push_back(R);
+            ++nr;
+            R = LinRound{poff[j], poff[j], j, j, 0, 0};
+          }
+          R.o1 += kobs(j);
+          R.p1 = j + 1;
+          lo = l2;
+          hi = h2;
+          ++j;
+        }
+        lrounds.push_back(R);
+        c.p1 = j;
+        c.b_lo = lo;
+        c.nb = co ? 0 : hi - lo + 1;
+        i = j;
       }
-      c.b_lo = lo;
-      c.nb = hi - lo + 1;
+      c.r1 = (int)lrounds.size();
+      c.cam_off = lcam_off;
+      lcam_off += c.nb * kCamV;
+      // per round: the window-block offsets and the round-local observation indices sorted by block
+      for (int r = c.r0; r < c.r1; ++r) {
+        LinRound& R = lrounds[r];
+        R.lst = (int)llist.size();
+        if (c.nb == 0) continue;
+        std::vector<int> cnt(c.nb + 1, 0);
+        for (int o = R.o0; o < R.o1; ++o) {
+          const int b = frame_block[obs_frame[o]];
+          if (b >= 0) cnt[b - c.b_lo + 1]++;
+        }
+        for (int k = 0; k < c.nb; ++k) cnt[k + 1] += cnt[k];
+        const size_t base = llist.size();
+        llist.resize(base + c.nb + 1 + cnt[c.nb]);
+        for (int k = 0; k <= c.nb; ++k) llist[base + k] = (uint16_t)cnt[k];
+        for (int o = R.o0; o < R.o1; ++o) {
+          const int b = frame_block[obs_frame[o]];
+          if (b >= 0) llist[base + c.nb + 1 + cnt[b - c.b_lo]++] = (uint16_t)(o - R.o0);
+        }
+      }
+      lchunks.push_back(c);
     }
-    c.p1 = j;
-    c.cam_off = cam_off;
-    c.s_off = 0;
-    cam_off += c.nb * kCamV;
-    max_nb_ = std::max(max_nb_, c.nb);
-    chunks_.push_back(c);
-    i = j;
   }
-  nchunks_ = (int)chunks_.size();
+  nlin_ = (int)lchunks.size();
   // Schur segments: runs of at most kSegPts consecutive points (device order) whose observations fit the
   // LDS stage and whose camera blocks fit a window of kSegNbMax blocks; one workgroup each, with its own
   // window partial in S_slab.  A point spanning more blocks is a "wide" segment of its own (global
@@ -1893,8 +2049,7 @@ void BaSolver::Load(const sg_problem& p) {
   {
     std::vector<std::vector<int32_t>> cl(NB_), rl(NB_);
     std::vector<std::vector<int32_t>> sl((size_t)NB_ * NB_);
-    for (int c = 0; c < nchunks_; ++c) {
-      const Chunk& ch = chunks_[c];
+    for (const LinChunk& ch : lchunks) {
       if (ch.wide || ch.nb == 0) continue;
       for (int i = 0; i < ch.nb; ++i) cl[ch.b_lo + i].push_back(ch.cam_off + i * kCamV);
     }
@@ -1999,7 +2154,10 @@ void BaSolver::Load(const sg_problem& p) {
   obs_pt_.Upload(obs_pt, s);
   obs_frame_.Upload(obs_frame, s);
   obs_fixed_.Upload(obs_fixed, s);
-  chunks_d_.Upload(chunks_, s);
+  lchunks_d_.Upload(lchunks, s);
+  lrounds_d_.Upload(lrounds, s);
+  if (llist.empty()) llist.push_back(0);
+  llist_d_.Upload(llist, s);
   obs_pnt_.Upload(obs_pnt.empty() ? std::vector<int32_t>{0} : obs_pnt, s);
   segs_.Upload(segs.empty() ? std::vector<SchurSeg>(1) : segs, s);
   pairs_.Upload(pairs_flat, s);
@@ -2038,9 +2196,11 @@ void BaSolver::Load(const sg_problem& p) {
   diag_c_.Resize(nn);
   camdiag_.Resize(nn);
   camg_.Resize(nn);
-  cam_slab_.Resize(std::max(cam_off, 1));
+  cam_slab_.Resize(std::max(lcam_off, 1));
+  lin_scal_.Resize((size_t)std::max(nlin_, 1) * kNScal);
+  lin_scal_.Zero(s);
   S_slab_.Resize(std::max(s_off, 1));
-  chunk_scal_.Resize((size_t)std::max(nchunks_, 1) * kNScal);
+  chunk_scal_.Resize((size_t)std::max(nlin_, 1) * kNScal);
   cam_wide_.Resize((size_t)std::max(NB_, 1) * kCamV);
   S_wide_.Resize(nn * nn);
   xchg_cam_.Resize((size_t)NB_ * kCamV + kXNum);
@@ -2128,8 +2288,6 @@ Dev BaSolver::MakeDev() {
   d.diag_c = diag_c_.ptr;
   d.camdiag = camdiag_.ptr;
   d.camg = camg_.ptr;
-  d.chunks = chunks_d_.ptr;
-  d.nchunks = nchunks_;
   d.cam_loff = cam_loff_.ptr;
   d.cam_lidx = cam_lidx_.ptr;
   d.s_loff = s_loff_.ptr;
@@ -2152,6 +2310,11 @@ Dev BaSolver::MakeDev() {
   d.stamps = stamp_on_ ? stamps_.ptr : nullptr;
   d.fd_pair = fd_pair_.ptr;
   d.obs_pnt = obs_pnt_.ptr;
+  d.lchunks = lchunks_d_.ptr;
+  d.lrounds = lrounds_d_.ptr;
+  d.llist = llist_d_.ptr;
+  d.nlin = nlin_;
+  d.lin_scal = lin_scal_.ptr;
   d.segs = segs_.ptr;
   d.nseg = nseg_;
   d.seg_fail = seg_fail_.ptr;
@@ -2222,14 +2385,13 @@ void BaSolver::Iterate(int n) {
   SG_REQUIRE(loaded_, SG_EINVAL, "no problem loaded");
   SG_HIP_CHECK(hipSetDevice(dev_.device));
   Dev d = MakeDev();
-  const int nc = std::max(nchunks_, 1);
   for (int it = 0; it < n; ++it) {
     TimedLaunchBegin(kKLin);
-    hipLaunchKernelGGL(k_linearize, dim3(nc), dim3(kSweepThreads), 0, stream_, d);
+    hipLaunchKernelGGL(k_linearize, dim3(std::max(nlin_, 1)), dim3(kLinThreads), 0, stream_, d);
     TimedLaunchEnd(kKLin);
     TimedLaunchBegin(kKCamReduce);
     const int nv = NB_ * kCamV;
-    hipLaunchKernelGGL(k_cam_reduce, dim3((nv + 255) / 256 + 1), dim3(256), 0, stream_, d);
+    hipLaunchKernelGGL(k_cam_reduce, dim3(NB_ + 1), dim3(kRedThreads), 0, stream_, d);
     TimedLaunchEnd(kKCamReduce);
     AllReduceSum(xchg_cam_.ptr, (size_t)nv + kXNum);
     AllReduceMax(xchg_max_.ptr, 1);
@@ -2260,10 +2422,10 @@ void BaSolver::Iterate(int n) {
                          (const int32_t*)work_i_.ptr, rdg_.ptr);
     TimedLaunchEnd(kKChol);
     TimedLaunchBegin(kKPointUpd);
-    hipLaunchKernelGGL(k_point_update, dim3(nc), dim3(kSweepThreads), 0, stream_, d);
+    hipLaunchKernelGGL(k_point_update, dim3(std::max(nlin_, 1)), dim3(kLinThreads), 0, stream_, d);
     TimedLaunchEnd(kKPointUpd);
     TimedLaunchBegin(kKUpdRed);
-    hipLaunchKernelGGL(k_upd_reduce, dim3(1), dim3(64), 0, stream_, d);
+    hipLaunchKernelGGL(k_upd_reduce, dim3(1), dim3(kRedThreads), 0, stream_, d);
     TimedLaunchEnd(kKUpdRed);
     AllReduceSum(xchg_upd_.ptr, kUNum);
     TimedLaunchBegin(kKDecide);
@@ -2284,11 +2446,10 @@ void BaSolver::Sweep(int n) {
   SG_REQUIRE(loaded_, SG_EINVAL, "no problem loaded");
   SG_HIP_CHECK(hipSetDevice(dev_.device));
   Dev d = MakeDev();
-  const int nc = std::max(nchunks_, 1);
   for (int it = 0; it < n; ++it) {
     hipLaunchKernelGGL(k_force_linearize, dim3(1), dim3(64), 0, stream_, st_.ptr);
     TimedLaunchBegin(kKLin);
-    hipLaunchKernelGGL(k_linearize, dim3(nc), dim3(kSweepThreads), 0, stream_, d);
+    hipLaunchKernelGGL(k_linearize, dim3(std::max(nlin_, 1)), dim3(kLinThreads), 0, stream_, d);
     TimedLaunchEnd(kKLin);
   }
   SG_HIP_CHECK(hipGetLastError());
