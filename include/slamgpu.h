@@ -290,6 +290,16 @@ int sg_hamming_results(sg_matcher* m, int32_t* best_idx, int32_t* best_dist, int
                        double* kernel_ms);
 int sg_slam_set_options(sg_slam* s, const sg_solver_options* o);
 
+/* LocalMap maintenance on the device, run on the residuals sg_slam_reproject_map wrote (main.cpp:584-599).
+ * A point's observation order (TrackedPoint::observations()) is ascending frame index, ties by map index
+ * (Frame::Commit, localmap.cpp:85-89). */
+/* LocalMap::Clean(error_threshold) (localmap.cpp:283-398): fixes X[4p+3], writes point_flags,
+ * point_uncertainty and obs_disabled; *result = the reference's bool (0 when observations were disabled). */
+int sg_map_clean(sg_slam* s, sg_map* map, double error_threshold, int32_t* result);
+/* LocalMap::ApplyEpipolarConstraint() (localmap.cpp:232-276): writes point_flags and obs_disabled;
+ * *num_violations = points whose |h2^T E h1| exceeded 0.15. */
+int sg_map_apply_epipolar(sg_slam* s, sg_map* map, int32_t* num_violations);
+
 #ifdef __cplusplus
 }
 #endif

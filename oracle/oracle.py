@@ -60,6 +60,10 @@ def lib():
         L.or_slam_solve_all_frames.argtypes = [C.POINTER(SgMap), C.c_double, C.c_int,
                                                C.POINTER(SgSolverOptions), C.c_int,
                                                C.POINTER(SgSolverSummary)]
+        L.orm_clean.restype = C.c_int
+        L.orm_clean.argtypes = [C.POINTER(SgMap), C.c_double]
+        L.orm_apply_epipolar.restype = C.c_int
+        L.orm_apply_epipolar.argtypes = [C.POINTER(SgMap)]
         _LIB = L
     return _LIB
 
@@ -152,6 +156,18 @@ def quat_plus(x, d):
 def reproject_map(m) -> float:
     s = m.struct()
     return lib().or_reproject_map(C.byref(s))
+
+
+def clean(m, error_threshold: float) -> bool:
+    """LocalMap::Clean (localmap.cpp:283-398) restated in oracle_map.cpp; mutates m."""
+    s = m.struct()
+    return bool(lib().orm_clean(C.byref(s), error_threshold))
+
+
+def apply_epipolar(m) -> int:
+    """LocalMap::ApplyEpipolarConstraint (localmap.cpp:232-276) restated in oracle_map.cpp; mutates m."""
+    s = m.struct()
+    return int(lib().orm_apply_epipolar(C.byref(s)))
 
 
 def slam_solve_frames(m, num_to_solve, num_to_present, range_=2.0, options=None, nthreads=1):

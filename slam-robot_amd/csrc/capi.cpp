@@ -8,6 +8,7 @@
 
 #include "ba_solver.h"
 #include "common.h"
+#include "map_ops.h"
 
 struct sg_ba {
   std::unique_ptr<sg::BaSolver> solver;
@@ -15,6 +16,8 @@ struct sg_ba {
 
 struct sg_slam {
   std::unique_ptr<sg::BaSolver> solver;
+  std::unique_ptr<sg::MapOps> mapops;   // created on first use
+  sg_device_options dev;
   sg_solver_options options;
   int32_t iterations = 0;    // Slam::iterations_ (slam.cpp:517)
   double error = 0.0;        // Slam::error_ (slam.cpp:518)
@@ -161,6 +164,7 @@ int sg_slam_create(sg_slam** out, const sg_device_options* dev) {
   if (dev) d = *dev;
   auto s = std::make_unique<sg_slam>();
   s->solver.reset(new sg::BaSolver(d));
+  s->dev = d;
   sg_solver_options_default(&s->options);
   *out = s.release();
   SG_CAPI_END
@@ -231,6 +235,25 @@ int sg_slam_reproject_map(sg_slam* s, sg_map* map, double* mean) {
   SG_CAPI_BEGIN
   SG_REQUIRE(s && map && mean, SG_EINVAL, "null argument");
   *mean = s->solver->ReprojectMap(map);
+  SG_CAPI_END
+}
+
+static sg::MapOps& MapOpsOf(sg_slam* s) {
+  if (!s->mapops) s->mapops.reset(new sg::MapOps(s->dev));
+  return *s->mapops;
+}
+
+int sg_map_clean(sg_slam* s, sg_map* map, double error_threshold, int32_t* result) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(s && map && result, SG_EINVAL, "null argument");
+  *result = MapOpsOf(s).Clean(map, error_threshold);
+  SG_CAPI_END
+}
+
+int sg_map_apply_epipolar(sg_slam* s, sg_map* map, int32_t* num_violations) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(s && map && num_violations, SG_EINVAL, "null argument");
+  *num_violations = MapOpsOf(s).ApplyEpipolarConstraint(map);
   SG_CAPI_END
 }
 

@@ -198,6 +198,22 @@ class Slam:
         check(self.lib.sg_slam_reproject_map(self.h, C.byref(ms), C.byref(mean)), "Slam::ReprojectMap")
         return mean.value
 
+    # LocalMap maintenance (localmap.cpp), on the device through the same handle.  These mirror
+    # LocalMap::Clean / LocalMap::ApplyEpipolarConstraint, which main.cpp calls after each solve.
+    def Clean(self, m: MapArrays, error_threshold: float) -> bool:
+        """LocalMap::Clean (localmap.cpp:283-398) on m's ReprojectMap residuals; mutates m in place."""
+        res = C.c_int32()
+        ms = m.struct()
+        check(self.lib.sg_map_clean(self.h, C.byref(ms), error_threshold, C.byref(res)), "LocalMap::Clean")
+        return bool(res.value)
+
+    def ApplyEpipolarConstraint(self, m: MapArrays) -> int:
+        """LocalMap::ApplyEpipolarConstraint (localmap.cpp:232-276); mutates m.  Returns the violation count."""
+        n = C.c_int32()
+        ms = m.struct()
+        check(self.lib.sg_map_apply_epipolar(self.h, C.byref(ms), C.byref(n)), "LocalMap::ApplyEpipolarConstraint")
+        return n.value
+
     def iterations(self) -> int:
         return int(self.lib.sg_slam_iterations(self.h))
 

@@ -253,6 +253,8 @@ SYMBOLS = {
     "sg_slam_solve_all_frames": (C.c_int, [C.c_void_p, C.POINTER(SgMap), C.c_double, C.c_int32,
                                            C.POINTER(C.c_int32)]),
     "sg_slam_reproject_map": (C.c_int, [C.c_void_p, C.POINTER(SgMap), _dp]),
+    "sg_map_clean": (C.c_int, [C.c_void_p, C.POINTER(SgMap), C.c_double, C.POINTER(C.c_int32)]),
+    "sg_map_apply_epipolar": (C.c_int, [C.c_void_p, C.POINTER(SgMap), C.POINTER(C.c_int32)]),
     "sg_slam_iterations": (C.c_int32, [C.c_void_p]),
     "sg_slam_error": (C.c_double, [C.c_void_p]),
     "sg_slam_last_summary": (C.c_int, [C.c_void_p, C.POINTER(SgSolverSummary)]),
