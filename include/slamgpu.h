@@ -267,6 +267,14 @@ int sg_tracker_load_features(sg_tracker* t, int32_t n, const float* from_xy, con
                              const int32_t* levels);
 int sg_tracker_run(sg_tracker* t, int32_t from, int32_t to, int32_t repeats);
 int sg_tracker_results(sg_tracker* t, float* to_xy, int32_t* accepted, int32_t* iterations);
+/* New-keyframe corner seeding of Matcher::Track (matcher.cpp:123-169, 214, 380-383) on the image of `slot`:
+ * grey = cvtColor(BGR, CV_RGB2GRAY); goodFeaturesToTrack(grey, max_corners = 120, quality = 0.01,
+ * min_distance = 20) (Shi-Tomasi, blockSize 3, strongest first, ties in row-major order); then
+ * AddNewFeatures' 30 x 30 grid: a corner is added unless its cell is within one cell of a match.
+ * corners_xy / added_xy hold up to max_corners points each (x, y). */
+int sg_tracker_seed_features(sg_tracker* t, int32_t slot, const float* match_xy, int32_t num_matches,
+                             int32_t max_corners, double quality, double min_distance, float* corners_xy,
+                             int32_t* num_corners, float* added_xy, int32_t* num_added);
 /* Kernel timing (HIP events on the tracker's stream) of the last sg_tracker_run: total ms of the
  * tracking kernels and of the pyramid kernels of the last sg_tracker_set_image. */
 int sg_tracker_kernel_ms(sg_tracker* t, double* track_ms, double* pyramid_ms);

@@ -205,8 +205,37 @@ def _trk():
         L.ort_mask.argtypes = [C.c_int, _fp]
         L.ort_track_fb.argtypes = [_fp, _fp, _i32p, C.c_int, C.c_int, C.c_int, _fp, _fp, _i32p, _i32p, _i32p,
                                    C.c_int]
+        L.ort_seed_features.restype = C.c_int
+        L.ort_seed_features.argtypes = [_u8p, C.c_int, C.c_int, C.c_int, _fp, C.c_int, C.c_int, C.c_double,
+                                        C.c_double, _fp, _i32p, _fp]
+        L.ort_min_eigen.argtypes = [_u8p, C.c_int, C.c_int, C.c_int, _fp]
         L._trk_ready = True
     return L
+
+
+def seed_features(bgr: np.ndarray, match_xy=None, max_corners=120, quality=0.01, min_distance=20.0):
+    """Matcher::Track's new-keyframe seeding (matcher.cpp:123-169): (corners[n,2], added[m,2])."""
+    bgr = np.ascontiguousarray(bgr, dtype=np.uint8)
+    h, w = bgr.shape[:2]
+    mxy = np.ascontiguousarray(np.zeros((0, 2)) if match_xy is None else match_xy, dtype=np.float32).reshape(-1, 2)
+    corners = np.zeros((max_corners, 2), np.float32)
+    added = np.zeros((max_corners, 2), np.float32)
+    nc = C.c_int32()
+    na = _trk().ort_seed_features(bgr.ctypes.data_as(_u8p), w, h, bgr.strides[0],
+                                  mxy.ctypes.data_as(_fp) if len(mxy) else None, len(mxy), max_corners, quality,
+                                  min_distance, corners.ctypes.data_as(_fp), C.byref(nc), added.ctypes.data_as(_fp))
+    if na < 0:
+        raise ValueError("a match lies outside the image (AddNewFeatures CHECK)")
+    return corners[:nc.value].copy(), added[:na].copy()
+
+
+def min_eigen(bgr: np.ndarray) -> np.ndarray:
+    """cornerMinEigenVal(cvtColor(bgr, RGB2GRAY), 3, 3)."""
+    bgr = np.ascontiguousarray(bgr, dtype=np.uint8)
+    h, w = bgr.shape[:2]
+    out = np.zeros((h, w), np.float32)
+    _trk().ort_min_eigen(bgr.ctypes.data_as(_u8p), w, h, bgr.strides[0], out.ctypes.data_as(_fp))
+    return out
 
 
 def pyramid_sizes(w, h, depth):

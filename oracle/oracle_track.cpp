@@ -443,3 +443,150 @@ extern "C" int ort_hamming_match(const uint64_t* q, int nq, const uint64_t* t, i
   }
   return 0;
 }
+
+// ------------------------------------------------------------------------------------------------
+// Corner seeding of a new keyframe (matcher.cpp:123-169, AddNewFeatures): cvtColor(img, grey,
+// CV_RGB2GRAY) (matcher.cpp:214) then goodFeaturesToTrack(grey, corners, 120, 0.01, 20) with OpenCV 2.4's
+// defaults (blockSize 3, Shi-Tomasi), then the 30 x 30 grid suppression around the existing matches.
+// OpenCV 2.4 imgproc restated: corner.cpp cornerEigenValsVecs / calcMinEigenVal (Sobel 3x3 scaled by
+// 1 / (4 * 3 * 255) on the smoothing tap, boxFilter 3x3 unnormalised, BORDER_REFLECT_101), featureselect.cpp
+// goodFeaturesToTrack (threshold at quality x max, 3x3 dilation = local maxima, strongest first, greedy
+// minimum distance on a cell grid).  OpenCV sorts with std::sort (order of exactly equal responses
+// implementation-defined); here ties go to the lower row-major index.  Float arithmetic in the order
+// written (this file is compiled with -ffp-contract=off).
+namespace oracle_trk {
+
+// cornerMinEigenVal(grey, eig, 3, 3).
+void MinEigen3(const uint8_t* g, int w, int h, float* eig) {
+  const float s = (float)(1.0 / (4.0 * 3.0 * 255.0));
+  const float k0 = 2.0f * s, k1 = s;   // scaled smoothing tap [s, 2s, s]
+  std::vector<float> dx((size_t)w * h), dy((size_t)w * h);
+  auto G = [&](int y, int x) { return (float)g[(size_t)Reflect101(y, h) * w + Reflect101(x, w)]; };
+  for (int y = 0; y < h; ++y)
+    for (int x = 0; x < w; ++x) {
+      float r[3], q[3];
+      for (int k = 0; k < 3; ++k) {
+        const int yy = y - 1 + k;
+        r[k] = G(yy, x + 1) - G(yy, x - 1);                     // derivative row tap [-1, 0, 1]
+        q[k] = G(yy, x) * k0 + (G(yy, x - 1) + G(yy, x + 1)) * k1;   // smoothing row tap
+      }
+      dx[(size_t)y * w + x] = r[1] * k0 + (r[0] + r[2]) * k1;   // smoothing column tap
+      dy[(size_t)y * w + x] = q[2] - q[0];                      // derivative column tap
+    }
+  std::vector<float> c0((size_t)w * h), c1((size_t)w * h), c2((size_t)w * h);
+  for (size_t i = 0; i < c0.size(); ++i) {
+    c0[i] = dx[i] * dx[i];
+    c1[i] = dx[i] * dy[i];
+    c2[i] = dy[i] * dy[i];
+  }
+  auto box = [&](const std::vector<float>& c, int y, int x) {
+    float col = 0.0f;
+    for (int k = 0; k < 3; ++k) {
+      const size_t row = (size_t)Reflect101(y - 1 + k, h) * w;
+      const float rs = (c[row + Reflect101(x - 1, w)] + c[row + x]) + c[row + Reflect101(x + 1, w)];
+      col = k == 0 ? rs : col + rs;
+    }
+    return col;
+  };
+  for (int y = 0; y < h; ++y)
+    for (int x = 0; x < w; ++x) {
+      const float a = box(c0, y, x) * 0.5f, b = box(c1, y, x), c = box(c2, y, x) * 0.5f;
+      eig[(size_t)y * w + x] = (a + c) - std::sqrt((a - c) * (a - c) + b * b);
+    }
+}
+
+// goodFeaturesToTrack(grey, corners, max_corners, quality, min_distance) with its default mask / block
+// size; corners as (x, y) pixel positions.
+int GoodFeatures(const uint8_t* g, int w, int h, int max_corners, double quality, double min_distance,
+                 std::vector<float>* corners) {
+  std::vector<float> eig((size_t)w * h);
+  MinEigen3(g, w, h, eig.data());
+  float maxv = 0.0f;
+  for (float v : eig) maxv = std::max(maxv, v);
+  const float thr = (float)(maxv * quality);
+  for (float& v : eig) v = v > thr ? v : 0.0f;   // THRESH_TOZERO
+  std::vector<int> cand;
+  for (int y = 1; y < h - 1; ++y)
+    for (int x = 1; x < w - 1; ++x) {
+      const float v = eig[(size_t)y * w + x];
+      float m = v;
+      for (int dy = -1; dy <= 1; ++dy)
+        for (int dx = -1; dx <= 1; ++dx) m = std::max(m, eig[(size_t)(y + dy) * w + x + dx]);
+      if (v != 0 && v == m) cand.push_back(y * w + x);
+    }
+  std::stable_sort(cand.begin(), cand.end(), [&](int a, int b) { return eig[a] > eig[b]; });
+  corners->clear();
+  const int cell = (int)std::lround(min_distance);
+  const int gw = (w + cell - 1) / cell, gh = (h + cell - 1) / cell;
+  std::vector<std::vector<std::pair<float, float>>> grid((size_t)gw * gh);
+  const double md2 = min_distance * min_distance;
+  int n = 0;
+  for (int idx : cand) {
+    const int y = idx / w, x = idx % w;
+    const int xc = x / cell, yc = y / cell;
+    bool good = true;
+    for (int yy = std::max(0, yc - 1); yy <= std::min(gh - 1, yc + 1) && good; ++yy)
+      for (int xx = std::max(0, xc - 1); xx <= std::min(gw - 1, xc + 1) && good; ++xx)
+        for (const auto& m : grid[(size_t)yy * gw + xx]) {
+          const float ddx = x - m.first, ddy = y - m.second;
+          if (ddx * ddx + ddy * ddy < md2) {
+            good = false;
+            break;
+          }
+        }
+    if (!good) continue;
+    grid[(size_t)yc * gw + xc].push_back({(float)x, (float)y});
+    corners->push_back((float)x);
+    corners->push_back((float)y);
+    if (max_corners > 0 && ++n == max_corners) break;
+  }
+  return n;
+}
+
+// AddNewFeatures' cell of a point: (pt / size) * 30 + 1 in float, truncated (matcher.cpp:135-137).
+inline int SeedCell(float v, int size) { return (int)(v / size * 30 + 1); }
+
+}  // namespace oracle_trk
+
+extern "C" {
+
+// Matcher::Track's new-keyframe seeding: grey from the BGR frame, goodFeaturesToTrack(120, 0.01, 20), and
+// AddNewFeatures' grid filter against the current matches.  corners_xy gets every corner (<= max_corners),
+// added_xy the ones kept; returns the number kept (*num_corners = corners found).
+int ort_seed_features(const uint8_t* bgr, int w, int h, int stride, const float* match_xy, int num_matches,
+                      int max_corners, double quality, double min_distance, float* corners_xy, int32_t* num_corners,
+                      float* added_xy) {
+  using namespace oracle_trk;
+  std::vector<uint8_t> grey((size_t)w * h);
+  RgbToGrayU8(bgr, w, h, stride, grey.data());
+  std::vector<float> corners;
+  const int n = GoodFeatures(grey.data(), w, h, max_corners, quality, min_distance, &corners);
+  *num_corners = n;
+  std::copy(corners.begin(), corners.end(), corners_xy);
+  int grid[32][32] = {};
+  for (int i = 0; i < num_matches; ++i) {
+    const int gx = SeedCell(match_xy[2 * i], w), gy = SeedCell(match_xy[2 * i + 1], h);
+    if (gx <= 0 || gy <= 0 || gx >= 31 || gy >= 31) return -1;   // the reference CHECKs 0 < g < size + 2
+    for (int a = -1; a <= 1; ++a)
+      for (int b = -1; b <= 1; ++b) grid[gx + a][gy + b] = 1;
+  }
+  int added = 0;
+  for (int i = 0; i < n; ++i) {
+    const int gx = SeedCell(corners[2 * i], w), gy = SeedCell(corners[2 * i + 1], h);
+    if (grid[gx][gy]) continue;
+    added_xy[2 * added] = corners[2 * i];
+    added_xy[2 * added + 1] = corners[2 * i + 1];
+    ++added;
+  }
+  return added;
+}
+
+// cornerMinEigenVal(grey(bgr), eig, 3, 3) alone (checker of the device response image).
+int ort_min_eigen(const uint8_t* bgr, int w, int h, int stride, float* eig) {
+  std::vector<uint8_t> grey((size_t)w * h);
+  oracle_trk::RgbToGrayU8(bgr, w, h, stride, grey.data());
+  oracle_trk::MinEigen3(grey.data(), w, h, eig);
+  return 0;
+}
+
+}  // extern "C"

@@ -13,6 +13,9 @@ namespace sg {
 
 constexpr int kTrkMaxDepth = 8;
 
+// BGR u8 -> grey u8 with CV_RGB2GRAY's fixed-point weights on BGR memory (corners.hip).
+__global__ void k_grey_u8(const uint8_t* bgr, int w, int h, int stride, uint8_t* grey);
+
 struct TrackParams {
   int window, max_iterations;
   float threshold, fb_max;
@@ -31,6 +34,9 @@ class Tracker {
   void LoadFeatures(int n, const float* from_xy, const float* to_xy, const int32_t* levels);
   void Run(int from, int to, int repeats);
   void Results(float* to_xy, int32_t* accepted, int32_t* iterations);
+  // Matcher::Track's new-keyframe seeding (goodFeaturesToTrack + AddNewFeatures, corners.hip).
+  void SeedFeatures(int slot, const float* match_xy, int nmatch, int max_corners, double quality, double min_distance,
+                    float* corners_xy, int* ncorners, float* added_xy, int* nadded);
   double track_ms() const { return track_ms_; }
   double pyramid_ms() const { return pyr_ms_; }
 
@@ -38,6 +44,7 @@ class Tracker {
   struct Slot {
     DBuf<float> pyr;
     DBuf<uint8_t> table;   // per-level {image, width, height} for the tracking kernel
+    DBuf<uint8_t> grey;    // level-0 grey u8 (cvtColor RGB2GRAY) for corner seeding
     std::vector<int> w, h;
     std::vector<size_t> off;
     bool valid = false;
@@ -51,6 +58,9 @@ class Tracker {
   DBuf<uint8_t> img_;
   DBuf<float> from_, init_, out_;
   DBuf<int32_t> levels_, acc_, its_;
+  DBuf<float> seed_dx_, seed_dy_, seed_eig_, seed_val_, seed_val2_;
+  DBuf<uint8_t> seed_flag_, seed_tmp_;
+  DBuf<int> seed_idx_, seed_idx2_, seed_misc_;
   int n_ = 0;
   bool ran_ = false;
   double track_ms_ = 0.0, pyr_ms_ = 0.0;

@@ -555,6 +555,8 @@ void Tracker::SetImage(int slot, const uint8_t* bgr, int w, int h, int stride) {
                        s.pyr.ptr + s.off[l]);
   }
   SG_HIP_CHECK(hipEventRecord(ev_[3], stream_));
+  s.grey.Resize((size_t)w * h);
+  hipLaunchKernelGGL(k_grey_u8, dim3((w + bx - 1) / bx, h), dim3(bx), 0, stream_, img_.ptr, w, h, stride, s.grey.ptr);
   SG_HIP_CHECK(hipGetLastError());
   // level table for the tracking kernel: {image, width, height} per level (scalar-loaded on the device)
   std::vector<uint8_t> tab(sizeof(LevelDev) * opt_.depth);

@@ -105,4 +105,16 @@ int sg_tracker_kernel_ms(sg_tracker* t, double* track_ms, double* pyramid_ms) {
   SG_CAPI_END
 }
 
+int sg_tracker_seed_features(sg_tracker* t, int32_t slot, const float* match_xy, int32_t num_matches,
+                             int32_t max_corners, double quality, double min_distance, float* corners_xy,
+                             int32_t* num_corners, float* added_xy, int32_t* num_added) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(t && corners_xy && num_corners && added_xy && num_added, SG_EINVAL, "null argument");
+  int nc = 0, na = 0;
+  t->t->SeedFeatures(slot, match_xy, num_matches, max_corners, quality, min_distance, corners_xy, &nc, added_xy, &na);
+  *num_corners = nc;
+  *num_added = na;
+  SG_CAPI_END
+}
+
 }  // extern "C"

@@ -239,6 +239,8 @@ SYMBOLS = {
     "sg_tracker_run": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32]),
     "sg_tracker_results": (C.c_int, [C.c_void_p, _fp, _ip, _ip]),
     "sg_tracker_kernel_ms": (C.c_int, [C.c_void_p, _dp, _dp]),
+    "sg_tracker_seed_features": (C.c_int, [C.c_void_p, C.c_int32, _fp, C.c_int32, C.c_int32, C.c_double, C.c_double,
+                                           _fp, _ip, _fp, _ip]),
     "sg_matcher_create": (C.c_int, [C.POINTER(C.c_void_p), C.POINTER(SgDeviceOptions)]),
     "sg_matcher_destroy": (None, [C.c_void_p]),
     "sg_hamming_match": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int32, C.POINTER(C.c_uint64), C.c_int32,

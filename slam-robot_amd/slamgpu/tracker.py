@@ -121,3 +121,18 @@ class HessianTracker:
         t, p = C.c_double(), C.c_double()
         check(self.lib.sg_tracker_kernel_ms(self.h, C.byref(t), C.byref(p)), "kernel_ms")
         return t.value, p.value
+
+    def SeedFeatures(self, slot: int, match_xy=None, max_corners: int = 120, quality: float = 0.01,
+                     min_distance: float = 20.0):
+        """Matcher::Track's new-keyframe seeding on the image of `slot` (matcher.cpp:123-169, AddNewFeatures):
+        goodFeaturesToTrack(grey, 120, 0.01, 20) then the 30 x 30 grid filter against the current matches.
+        Returns (corners[n, 2], added[m, 2])."""
+        mxy = np.ascontiguousarray(np.zeros((0, 2)) if match_xy is None else match_xy, dtype=np.float32).reshape(-1, 2)
+        corners = np.zeros((max_corners, 2), np.float32)
+        added = np.zeros((max_corners, 2), np.float32)
+        nc, na = C.c_int32(), C.c_int32()
+        check(self.lib.sg_tracker_seed_features(self.h, slot, mxy.ctypes.data_as(_fp) if len(mxy) else None, len(mxy),
+                                                max_corners, quality, min_distance, corners.ctypes.data_as(_fp),
+                                                C.byref(nc), added.ctypes.data_as(_fp), C.byref(na)),
+              "sg_tracker_seed_features")
+        return corners[:nc.value].copy(), added[:na.value].copy()
