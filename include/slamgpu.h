@@ -240,8 +240,12 @@ typedef struct sg_tracker_options {
   float fb_max;            /* forward/backward disagreement limit: 0.3 px (matcher.cpp:200) */
   int32_t retry_levels;    /* levels of the retry after a failed attempt: 6 (matcher.cpp:248); 0 = none */
   int32_t max_images;      /* pyramid slots held on the device */
-  int32_t reserved[5];
+  int32_t mode;            /* FeatureTracker implementation: SG_TRACKER_HESSIAN (the one Matcher uses,
+                              matcher.cpp:20), SG_TRACKER_KLT (klt.h), SG_TRACKER_BRUTE (brute.h) */
+  int32_t reserved[4];
 } sg_tracker_options;
+
+enum sg_tracker_mode { SG_TRACKER_HESSIAN = 0, SG_TRACKER_KLT = 1, SG_TRACKER_BRUTE = 2 };
 
 void sg_tracker_options_default(sg_tracker_options* o);
 int sg_tracker_create(sg_tracker** out, const sg_tracker_options* o, const sg_device_options* dev);
@@ -263,6 +267,13 @@ int sg_tracker_track(sg_tracker* t, int32_t from, int32_t to, int32_t n, const f
                      const int32_t* levels, int32_t* accepted, int32_t* iterations);
 /* Device-resident variant for throughput runs: load features once, run `repeats` asynchronous tracking
  * passes (each restarts from the loaded starting guesses), then fetch the last pass's results. */
+/* One-directional TrackFeature of the tracker's mode for n features (hessian.h:243-264, klt.h:403-424,
+ * brute.h:129-164): templates GetPatches(from slot, from_xy) (levels[i] of them in HESSIAN mode, NULL = all;
+ * every level in the other modes), then coarse-to-fine tracking in the `to` slot starting from to_xy, with
+ * threshold / max_iterations from the options.  to_xy is updated only where status is 0 (OK); 2 =
+ * OUT_OF_BOUNDS.  iterations (optional): Newton iterations run (0 in BRUTE mode). */
+int sg_tracker_track_feature(sg_tracker* t, int32_t from, int32_t to, int32_t n, const float* from_xy, float* to_xy,
+                             const int32_t* levels, int32_t* status, int32_t* iterations);
 int sg_tracker_load_features(sg_tracker* t, int32_t n, const float* from_xy, const float* to_xy,
                              const int32_t* levels);
 int sg_tracker_run(sg_tracker* t, int32_t from, int32_t to, int32_t repeats);

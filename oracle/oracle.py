@@ -209,6 +209,11 @@ def _trk():
         L.ort_seed_features.argtypes = [_u8p, C.c_int, C.c_int, C.c_int, _fp, C.c_int, C.c_int, C.c_double,
                                         C.c_double, _fp, _i32p, _fp]
         L.ort_min_eigen.argtypes = [_u8p, C.c_int, C.c_int, C.c_int, _fp]
+        L.ort_make_pyramid_mode.argtypes = [C.c_int, _u8p, C.c_int, C.c_int, C.c_int, C.c_int, _fp, _i32p]
+        L.ort_track_feature_mode.argtypes = [C.c_int, _fp, _fp, _i32p, C.c_int, C.c_int, C.c_int, _fp, _fp, _i32p,
+                                             C.c_float, C.c_int, _i32p, _i32p, C.c_int]
+        L.ort_brute_steps.restype = C.c_int
+        L.ort_brute_steps.argtypes = [C.c_float, C.c_float, _fp, C.c_int]
         L._trk_ready = True
     return L
 
@@ -227,6 +232,44 @@ def seed_features(bgr: np.ndarray, match_xy=None, max_corners=120, quality=0.01,
     if na < 0:
         raise ValueError("a match lies outside the image (AddNewFeatures CHECK)")
     return corners[:nc.value].copy(), added[:na].copy()
+
+
+def make_pyramid_mode(bgr: np.ndarray, depth: int = 6, mode: int = 0):
+    """MakePyramid of hessian.h (mode 0), klt.h (1) or brute.h (2): (flat levels, dims[depth, 2])."""
+    bgr = np.ascontiguousarray(bgr, dtype=np.uint8)
+    h, w = bgr.shape[:2]
+    dims = pyramid_sizes(w, h, depth)
+    out = np.zeros(sum(a * b for a, b in dims), np.float32)
+    d = np.zeros(2 * depth, np.int32)
+    _trk().ort_make_pyramid_mode(mode, bgr.ctypes.data_as(_u8p), w, h, bgr.strides[0], depth, out.ctypes.data_as(_fp),
+                                 d.ctypes.data_as(_i32p))
+    return out, d.reshape(depth, 2)
+
+
+def track_feature_mode(mode, pyr_from, pyr_to, dims, win, from_xy, to_xy, levels=None, threshold=0.001,
+                       max_iterations=10, nthreads=1):
+    """One-directional TrackFeature of hessian.h / klt.h / brute.h: (to_xy, status, iterations)."""
+    from_xy = np.ascontiguousarray(from_xy, dtype=np.float32).reshape(-1, 2)
+    out = np.ascontiguousarray(to_xy, dtype=np.float32).reshape(-1, 2).copy()
+    n = from_xy.shape[0]
+    lv = None if levels is None else np.ascontiguousarray(levels, dtype=np.int32)
+    st = np.zeros(n, np.int32)
+    it = np.zeros(n, np.int32)
+    d = np.ascontiguousarray(dims, dtype=np.int32).reshape(-1)
+    pf = np.ascontiguousarray(pyr_from, dtype=np.float32)
+    pt = np.ascontiguousarray(pyr_to, dtype=np.float32)
+    _trk().ort_track_feature_mode(mode, pf.ctypes.data_as(_fp), pt.ctypes.data_as(_fp), d.ctypes.data_as(_i32p),
+                                  len(d) // 2, win, n, from_xy.ctypes.data_as(_fp), out.ctypes.data_as(_fp),
+                                  None if lv is None else lv.ctypes.data_as(_i32p), threshold, max_iterations,
+                                  st.ctypes.data_as(_i32p), it.ctypes.data_as(_i32p), nthreads)
+    return out, st, it
+
+
+def brute_steps(window: float, res: float) -> np.ndarray:
+    """brute.h SearchBest's float-stepped offsets for one (window, res) pass."""
+    buf = np.zeros(4096, np.float32)
+    n = _trk().ort_brute_steps(window, res, buf.ctypes.data_as(_fp), len(buf))
+    return buf[:n].copy()
 
 
 def min_eigen(bgr: np.ndarray) -> np.ndarray:

@@ -590,3 +590,278 @@ int ort_min_eigen(const uint8_t* bgr, int w, int h, int stride, float* eig) {
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------------------------------------
+// The reference's two other FeatureTracker implementations.  Neither is
+// executed by the reference (Matcher typedefs HessianTracker, matcher.cpp:20), so their restatements below
+// are the specification of the device modes; they share the HessianTracker primitives above.
+namespace oracle_trk {
+
+// klt.h:105-135 / brute.h:60-80 MakePyramid: grey / 255, no blur at level 0; each further level pyrDown,
+// then (klt.h only) GaussianBlur 5x5 sigma 0.6.  klt.h's Scharr gradient images (105-106, 119-125) feed only
+// the LK matrices A, B, C, RS, VW of Track, whose result the reference overwrites with the BruteHessian
+// step (klt.h:333-359): they do not influence any output and are not computed here.
+void MakePyramidMode(int mode, const uint8_t* bgr, int w, int h, int stride, int depth, float* out, int32_t* dims) {
+  std::vector<uint8_t> grey((size_t)w * h);
+  RgbToGrayU8(bgr, w, h, stride, grey.data());
+  std::vector<float> cur((size_t)w * h);
+  const float sc = (float)(1. / 255.);
+  for (size_t i = 0; i < cur.size(); ++i) cur[i] = (float)grey[i] * sc;
+  int cw = w, ch = h;
+  size_t off = 0;
+  for (int l = 0; l < depth; ++l) {
+    if (l > 0) {
+      std::vector<float> nxt;
+      int nw, nh;
+      PyrDown(cur, cw, ch, nxt, &nw, &nh);
+      if (mode == 1) GaussianBlur5(nxt, nw, nh, 0.6);
+      cur.swap(nxt);
+      cw = nw;
+      ch = nh;
+    }
+    std::memcpy(out + off, cur.data(), cur.size() * sizeof(float));
+    dims[2 * l] = cw;
+    dims[2 * l + 1] = ch;
+    off += cur.size();
+  }
+}
+
+// klt.h / brute.h GetPatch: a plain W x W getRectSubPix (no edge shift).  `lane_sums` selects the patch-sum
+// order: the KLT mode uses the one-wave-per-feature lane-tree order, the brute mode (one device thread per
+// candidate) the sequential order of the reference's loop.
+Patch PlainPatch(const Tracker& T, const float* img, int w, int h, float px, float py, bool lane_sums) {
+  Patch p;
+  p.data.assign(T.len, 0.f);
+  GetRectSubPix(img, w, h, T.W, T.W, px, py, p.data.data(), T.W);
+  float sum = 0.f, sum_sq = 0.f;
+  if (lane_sums) {
+    std::vector<float> sq(T.len);
+    for (int i = 0; i < T.len; ++i) sq[i] = p.data[i] * p.data[i];
+    sum = LaneTreeSum(p.data.data(), T.len);
+    sum_sq = LaneTreeSum(sq.data(), T.len);
+  } else {
+    for (float d : p.data) {
+      sum += d;
+      sum_sq += d * d;
+    }
+  }
+  p.mean = sum / T.len;
+  p.sumsq = sum_sq / T.len;
+  return p;
+}
+
+// klt.h:139-149 SADPatches(template, probe): masked, not lighting-normalised.
+float KltScore(const Tracker& T, const Patch& p1, const Patch& p2) {
+  std::vector<float> term(T.len, 0.f);
+  for (int i = 0; i < T.len; ++i) {
+    if (p1.data[i] == 0 || p2.data[i] == 0) continue;
+    const float diff = p1.data[i] - p2.data[i];
+    term[i] = diff * diff * T.mask[i];
+  }
+  return LaneTreeSum(term.data(), T.len);
+}
+
+// klt.h:258-401 Track with the BruteHessian of 181-204 (forward differences, h = 0.01); margin 0.1, stop when
+// both steps are below threshold / 10.
+int KltTrack(const Tracker& T, const Level& L, const Patch& patch, float threshold, int max_iterations, float* px,
+             float* py, int* iters) {
+  float x = *px, y = *py;
+  const float margin = 0.1f;
+  int it = 0;
+  for (; it < max_iterations; ++it) {
+    if (x < margin || y < margin || (x + margin) > L.w || (y + margin) > L.h) {
+      if (iters) *iters += it;
+      return 2;
+    }
+    const double hh = 0.01;
+    auto S = [&](float qx, float qy) { return (double)KltScore(T, patch, PlainPatch(T, L.img, L.w, L.h, qx, qy, true)); };
+    const double sad0 = S(x, y);
+    const double sadx = S((float)(x + hh), y);
+    const double sady = S(x, (float)(y + hh));
+    const double sadxx = S((float)(x + 2 * hh), y);
+    const double sadyy = S(x, (float)(y + 2 * hh));
+    const double sadxy = S((float)(x + hh), (float)(y + hh));
+    const float mdx = (float)((sadx - sad0) / hh), mdy = (float)((sady - sad0) / hh);
+    const float mdxx = (float)(((sadxx - sadx) / hh - (sadx - sad0) / hh) / hh);
+    const float mdyy = (float)(((sadyy - sady) / hh - (sady - sad0) / hh) / hh);
+    const float mdxy = (float)(((sadxy - sady) / hh - (sadx - sad0) / hh) / hh);
+    const float mdyx = (float)(((sadxy - sadx) / hh - (sady - sad0) / hh) / hh);
+    const double H00 = mdxx, H01 = mdxy, H10 = mdyx, H11 = mdyy;
+    const double det = H00 * H11 - H10 * H01;
+    const double invdet = 1.0 / det;
+    const double i00 = H11 * invdet, i10 = -H10 * invdet, i01 = -H01 * invdet, i11 = H00 * invdet;
+    const double g0 = mdx, g1 = mdy;
+    const double jj0 = i00 * g0 + i01 * g1, jj1 = i10 * g0 + i11 * g1;
+    float dx = (float)-jj0, dy = (float)-jj1;
+    if ((dx * dx + dy * dy) > 1) {
+      dx /= std::sqrt(dx * dx + dy * dy);
+      dy /= std::sqrt(dx * dx + dy * dy);
+    }
+    const float cx = (dx < 1.f) ? dx : 1.f, cy = (dy < 1.f) ? dy : 1.f;
+    x += (-1.f < cx) ? cx : -1.f;
+    y += (-1.f < cy) ? cy : -1.f;
+    if (std::fabs(dx) < threshold / 10. && std::fabs(dy) < threshold / 10.) {
+      ++it;
+      break;
+    }
+  }
+  if (iters) *iters += it;
+  *px = x;
+  *py = y;
+  return 0;
+}
+
+// klt.h:403-424 TrackFeature: every pyramid level, threshold x 50 on the coarse levels.
+int KltTrackFeature(const Tracker& T, const std::vector<Level>& src, const std::vector<Level>& dst, float sx, float sy,
+                    float threshold, int max_iterations, float* px, float* py, int* iters) {
+  const int lvls = (int)dst.size();
+  std::vector<Patch> patches(lvls);
+  float tx = sx, ty = sy;
+  for (int i = 0; i < lvls; ++i) {
+    patches[i] = PlainPatch(T, src[i].img, src[i].w, src[i].h, tx, ty, true);
+    tx = (float)(tx * 0.5);
+    ty = (float)(ty * 0.5);
+  }
+  const double s = 1. / (1 << (lvls - 1));
+  float x = (float)(*px * s), y = (float)(*py * s);
+  for (int i = lvls - 1; i > 0; --i) {
+    const int st = KltTrack(T, dst[i], patches[i], threshold * 50, max_iterations, &x, &y, iters);
+    if (st) return st;
+    x = (float)(x * 2.);
+    y = (float)(y * 2.);
+  }
+  const int st = KltTrack(T, dst[0], patches[0], threshold, max_iterations, &x, &y, iters);
+  if (st) return st;
+  *px = x;
+  *py = y;
+  return 0;
+}
+
+// brute.h:82-94 SADPatches(template, candidate): lighting-normalised, unmasked, sequential sum.
+float BruteScore(const Tracker& T, const Patch& p1, const Patch& p2) {
+  const float alpha = std::sqrt(p1.sumsq / p2.sumsq);
+  const float beta = p1.mean - alpha * p2.mean;
+  float sum = 0.f;
+  for (int i = 0; i < T.len; ++i) {
+    if (p1.data[i] == 0 || p2.data[i] == 0) continue;
+    const float diff = p1.data[i] - p2.data[i] * alpha - beta;
+    sum += std::fabs(diff * diff);
+  }
+  return sum;
+}
+
+// The float-stepped offsets of `for (float x = -window; x <= window; x += res)` (brute.h:104-105).
+std::vector<float> BruteSteps(float window, float res) {
+  std::vector<float> v;
+  for (float x = -window; x <= window; x += res) v.push_back(x);
+  return v;
+}
+
+// brute.h:96-117 SearchBest: exhaustive grid, x outer, y inner; a candidate replaces the best unless its
+// score is larger (ties go to the later candidate).
+float BruteSearchBest(const Tracker& T, const Level& L, const Patch& patch, float window, float res, float* ptx,
+                      float* pty) {
+  const std::vector<float> st = BruteSteps(window, res);
+  const float p0x = *ptx, p0y = *pty;
+  float best = 1e6f;
+  for (float ox : st)
+    for (float oy : st) {
+      const float sad = BruteScore(T, patch, PlainPatch(T, L.img, L.w, L.h, p0x + ox, p0y + oy, false));
+      if (sad > best) continue;
+      *ptx = p0x + ox;
+      *pty = p0y + oy;
+      best = sad;
+    }
+  return best;
+}
+
+// brute.h:129-164 TrackFeature (threshold and max_iterations unused by the reference).
+int BruteTrackFeature(const Tracker& T, const std::vector<Level>& src, const std::vector<Level>& dst, float sx,
+                      float sy, float* px, float* py) {
+  const int lvls = (int)dst.size();
+  const float margin = 13;
+  if (*px < margin || *py < margin || (*px + margin) > dst[0].w || (*py + margin) > dst[0].h) return 2;
+  std::vector<Patch> patches(lvls);
+  float tx = sx, ty = sy;
+  for (int i = 0; i < lvls; ++i) {
+    patches[i] = PlainPatch(T, src[i].img, src[i].w, src[i].h, tx, ty, false);
+    tx = (float)(tx * 0.5);
+    ty = (float)(ty * 0.5);
+  }
+  const double s = 1. / (1 << (lvls - 1));
+  float x = (float)(*px * s), y = (float)(*py * s);
+  for (int i = lvls - 1; i > 0; --i) {
+    BruteSearchBest(T, dst[i], patches[i], 3, 1, &x, &y);
+    const float sad = BruteSearchBest(T, dst[i], patches[i], 1, 0.33333f, &x, &y);
+    if (sad > 100) return 2;
+    x = (float)(x * 2.);
+    y = (float)(y * 2.);
+  }
+  BruteSearchBest(T, dst[0], patches[0], 3, 1, &x, &y);
+  BruteSearchBest(T, dst[0], patches[0], 1, 0.3333f, &x, &y);
+  BruteSearchBest(T, dst[0], patches[0], 0.4f, 0.1f, &x, &y);
+  BruteSearchBest(T, dst[0], patches[0], 0.2f, 0.025f, &x, &y);
+  const float sad = BruteSearchBest(T, dst[0], patches[0], 8, 0.01f, &x, &y);
+  if (sad > 100) return 2;
+  *px = x;
+  *py = y;
+  return 0;
+}
+
+}  // namespace oracle_trk
+
+extern "C" {
+
+// MakePyramid of mode 0 (hessian.h), 1 (klt.h) or 2 (brute.h).
+int ort_make_pyramid_mode(int mode, const uint8_t* bgr, int w, int h, int stride, int depth, float* out,
+                          int32_t* dims) {
+  if (mode == 0) return ort_make_pyramid(bgr, w, h, stride, depth, out, dims);
+  oracle_trk::MakePyramidMode(mode, bgr, w, h, stride, depth, out, dims);
+  return 0;
+}
+
+// One-directional TrackFeature of the mode for n features: templates GetPatches(from, from_xy), tracking on
+// `to` from the initial guess in to_xy (updated only on success).  status: 0 OK, 2 OUT_OF_BOUNDS.  levels
+// (mode 0 only; NULL = all levels): HessianTracker::GetPatches' level count.
+int ort_track_feature_mode(int mode, const float* pyr_from, const float* pyr_to, const int32_t* dims, int depth, int win,
+                           int n, const float* from_xy, float* to_xy, const int32_t* levels, float threshold,
+                           int max_iterations, int32_t* status, int32_t* iters, int nthreads) {
+  using namespace oracle_trk;
+  std::vector<Level> from(depth), to(depth);
+  size_t off = 0;
+  for (int l = 0; l < depth; ++l) {
+    from[l] = Level{pyr_from + off, dims[2 * l], dims[2 * l + 1]};
+    to[l] = Level{pyr_to + off, dims[2 * l], dims[2 * l + 1]};
+    off += (size_t)dims[2 * l] * dims[2 * l + 1];
+  }
+  Tracker T(win);
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
+  for (int i = 0; i < n; ++i) {
+    int it = 0;
+    float x = to_xy[2 * i], y = to_xy[2 * i + 1];
+    int st;
+    if (mode == 0)
+      st = TrackFeature(T, from, to, from_xy[2 * i], from_xy[2 * i + 1], levels ? levels[i] : depth, threshold,
+                        max_iterations, &x, &y, &it);
+    else if (mode == 1)
+      st = KltTrackFeature(T, from, to, from_xy[2 * i], from_xy[2 * i + 1], threshold, max_iterations, &x, &y, &it);
+    else
+      st = BruteTrackFeature(T, from, to, from_xy[2 * i], from_xy[2 * i + 1], &x, &y);
+    status[i] = st;
+    if (iters) iters[i] = it;
+    if (st == 0) {
+      to_xy[2 * i] = x;
+      to_xy[2 * i + 1] = y;
+    }
+  }
+  return 0;
+}
+
+// brute.h SearchBest offsets of one (window, res) pass (checker of the device step tables).
+int ort_brute_steps(float window, float res, float* out, int cap) {
+  const std::vector<float> v = oracle_trk::BruteSteps(window, res);
+  for (int i = 0; i < (int)v.size() && i < cap; ++i) out[i] = v[i];
+  return (int)v.size();
+}
+
+}  // extern "C"

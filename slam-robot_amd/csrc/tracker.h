@@ -34,6 +34,9 @@ class Tracker {
   void LoadFeatures(int n, const float* from_xy, const float* to_xy, const int32_t* levels);
   void Run(int from, int to, int repeats);
   void Results(float* to_xy, int32_t* accepted, int32_t* iterations);
+  // One-directional TrackFeature of the configured FeatureTracker (hessian.h / klt.h / brute.h).
+  void TrackFeature(int from, int to, int n, const float* from_xy, float* to_xy, const int32_t* levels,
+                    int32_t* status, int32_t* iterations);
   // Matcher::Track's new-keyframe seeding (goodFeaturesToTrack + AddNewFeatures, corners.hip).
   void SeedFeatures(int slot, const float* match_xy, int nmatch, int max_corners, double quality, double min_distance,
                     float* corners_xy, int* ncorners, float* added_xy, int* nadded);
@@ -61,6 +64,9 @@ class Tracker {
   DBuf<float> seed_dx_, seed_dy_, seed_eig_, seed_val_, seed_val2_;
   DBuf<uint8_t> seed_flag_, seed_tmp_;
   DBuf<int> seed_idx_, seed_idx2_, seed_misc_;
+  DBuf<float> brute_steps_, brute_tmpl_, brute_sad_;
+  DBuf<int> brute_idx_;
+  DBuf<uint8_t> brute_state_;
   int n_ = 0;
   bool ran_ = false;
   double track_ms_ = 0.0, pyr_ms_ = 0.0;

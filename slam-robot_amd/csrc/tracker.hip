@@ -64,6 +64,15 @@ __global__ void k_gray_blur_row(const uint8_t* bgr, int w, int h, int stride, Bl
   out[(size_t)y * w + x] = c * k.k0 + (l1 + r1) * k.k1 + (l2 + r2) * k.k2;
 }
 
+// level 0 of the klt.h / brute.h pyramids (klt.h:104, brute.h:64): grey / 255, no blur
+__global__ void k_gray_scale(const uint8_t* bgr, int w, int h, int stride, float* out) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+  if (x >= w || y >= h) return;
+  const uint8_t* p = bgr + (size_t)y * stride + 3 * x;
+  const int v = (4899 * p[0] + 9617 * p[1] + 1868 * p[2] + (1 << 13)) >> 14;
+  out[(size_t)y * w + x] = (float)(uint8_t)v * (float)(1. / 255.);
+}
+
 __global__ void k_blur_row(const float* in, int w, int h, Blur5 k, float* out) {
   const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
   if (x >= w || y >= h) return;
@@ -120,18 +129,21 @@ struct Geo {
   float a11, a12, a21, a22, b1, b2;
 };
 
+// kShift: HessianTracker::GetPatch's zero-filled left / top edge (hessian.h:63-75); without it the plain
+// getRectSubPix of klt.h / brute.h GetPatch.
+template <bool kShift = true>
 __device__ __forceinline__ void make_geo(float px, float py, int W, int w, int h, Geo& g) {
   g.zx = 0;
   g.zy = 0;
   g.pw = W;
   g.ph = W;
-  if (px < 0.5 * W) {
+  if (kShift && px < 0.5 * W) {
     const int d = (int)((0.5 * W - px) + 0.9999);
     px = (float)(px + 0.5 * d);
     g.zx = d;
     g.pw = W - d;
   }
-  if (py < 0.5 * W) {
+  if (kShift && py < 0.5 * W) {
     const int d = (int)(0.5 * W - py);
     py = (float)(py + 0.5 * d);
     g.zy = d;
@@ -455,6 +467,351 @@ __global__ __launch_bounds__(64 * kTrackWaves) void k_get_patches(LevelDev L, in
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// One-directional TrackFeature of each FeatureTracker (sg_tracker_track_feature).
+
+__device__ __forceinline__ void init_ctx(TrackCtx& c, const TrackParams& prm, int lane) {
+  c.W = prm.window;
+  c.len = prm.window * prm.window;
+  c.max_it = prm.max_iterations;
+  c.threshold = prm.threshold;
+  c.lane = lane;
+#pragma unroll
+  for (int k = 0; k < kNP; ++k) {
+    const int p = lane + 64 * k;
+    const bool in = p < c.len;
+    c.mk[k] = in ? prm.mask[p] : 0.f;
+    c.pi[k] = in ? p / c.W : -1;
+    c.pj[k] = in ? p % c.W : 0;
+  }
+}
+
+// HessianTracker::TrackFeature (hessian.h:243-264) alone, one wave per feature.
+__global__ __launch_bounds__(64 * kTrackWaves) void k_track_one(const LevelDev* __restrict__ from_lv,
+                                                                const LevelDev* __restrict__ to_lv, int depth,
+                                                                TrackParams prm, int n, const float* from_xy,
+                                                                float* to_xy, const int32_t* levels,
+                                                                int32_t* status, int32_t* iterations) {
+  const int lane = threadIdx.x & 63;
+  const int f = blockIdx.x * kTrackWaves + (threadIdx.x >> 6);
+  if (f >= n) return;
+  TrackCtx c;
+  init_ctx(c, prm, lane);
+  const int lvls = min(depth, levels ? levels[f] : depth);
+  float qx = to_xy[2 * f], qy = to_xy[2 * f + 1];
+  int iters = 0;
+  const int st = track_pass(c, from_lv, to_lv, lvls, from_xy[2 * f], from_xy[2 * f + 1], &qx, &qy, &iters);
+  if (lane == 0) {
+    status[f] = st;
+    if (st == 0) {
+      to_xy[2 * f] = qx;
+      to_xy[2 * f + 1] = qy;
+    }
+    if (iterations) iterations[f] = iters;
+  }
+}
+
+// klt.h BruteHessian (181-204): forward differences (h = 0.01) of SADPatches(template, probe) (139-149), the
+// masked, not lighting-normalised SSD, on plain getRectSubPix probes; six probes sampled together.
+__device__ __forceinline__ void klt_hessian(const TrackCtx& c, const LevelDev& L, const Tmpl& tp, float x, float y,
+                                            float* mdx, float* mdy, float* mdxx, float* mdxy, float* mdyx,
+                                            float* mdyy) {
+  const double hh = 0.01;
+  float px[6], py[6];
+  px[0] = x;                   py[0] = y;                    // sad0
+  px[1] = (float)(x + hh);     py[1] = y;                    // sadx
+  px[2] = x;                   py[2] = (float)(y + hh);      // sady
+  px[3] = (float)(x + 2 * hh); py[3] = y;                    // sadxx
+  px[4] = x;                   py[4] = (float)(y + 2 * hh);  // sadyy
+  px[5] = (float)(x + hh);     py[5] = (float)(y + hh);      // sadxy
+  float sc[6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    Geo g;
+    make_geo<false>(px[r], py[r], c.W, L.w, L.h, g);
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < kNP; ++k) {
+      float term = 0.f;
+      if (c.pi[k] >= 0) {
+        const float a = tp.v[k], b = sample(L.img, L.w, g, c.pi[k], c.pj[k]);
+        if (!(a == 0 || b == 0)) {
+          const float diff = a - b;
+          term = diff * diff * c.mk[k];
+        }
+      }
+      acc += term;
+    }
+    sc[r] = acc;
+  }
+#pragma unroll
+  for (int r = 0; r < 6; ++r) sc[r] = wave_tree_sum(sc[r]);
+  const double sad0 = sc[0], sadx = sc[1], sady = sc[2], sadxx = sc[3], sadyy = sc[4], sadxy = sc[5];
+  *mdx = (float)((sadx - sad0) / hh);
+  *mdy = (float)((sady - sad0) / hh);
+  *mdxx = (float)(((sadxx - sadx) / hh - (sadx - sad0) / hh) / hh);
+  *mdyy = (float)(((sadyy - sady) / hh - (sady - sad0) / hh) / hh);
+  *mdxy = (float)(((sadxy - sady) / hh - (sadx - sad0) / hh) / hh);
+  *mdyx = (float)(((sadxy - sadx) / hh - (sady - sad0) / hh) / hh);
+}
+
+// klt.h:258-401 Track (the LK matrices A, B, C, RS, VW it accumulates are overwritten by the BruteHessian step
+// before use, so they are not formed): margin 0.1, stop when both steps are below threshold / 10.
+__device__ __forceinline__ int klt_track(const TrackCtx& c, const LevelDev& L, const Tmpl& tp, float threshold,
+                                         float* px, float* py, int* iters) {
+  float x = *px, y = *py;
+  const float margin = 0.1f;
+  int it = 0;
+  for (; it < c.max_it; ++it) {
+    if (x < margin || y < margin || (x + margin) > L.w || (y + margin) > L.h) {
+      *iters += it;
+      return 2;
+    }
+    float mdx, mdy, mdxx, mdxy, mdyx, mdyy;
+    klt_hessian(c, L, tp, x, y, &mdx, &mdy, &mdxx, &mdxy, &mdyx, &mdyy);
+    const double H00 = mdxx, H01 = mdxy, H10 = mdyx, H11 = mdyy;
+    const double det = H00 * H11 - H10 * H01;
+    const double invdet = 1.0 / det;
+    const double i00 = H11 * invdet, i10 = -H10 * invdet, i01 = -H01 * invdet, i11 = H00 * invdet;
+    const double g0 = mdx, g1 = mdy;
+    const double jj0 = i00 * g0 + i01 * g1, jj1 = i10 * g0 + i11 * g1;
+    float dx = (float)-jj0, dy = (float)-jj1;
+    if ((dx * dx + dy * dy) > 1) {
+      dx /= sqrtf(dx * dx + dy * dy);
+      dy /= sqrtf(dx * dx + dy * dy);
+    }
+    const float cx = (dx < 1.f) ? dx : 1.f, cy = (dy < 1.f) ? dy : 1.f;
+    x += (-1.f < cx) ? cx : -1.f;
+    y += (-1.f < cy) ? cy : -1.f;
+    if ((double)fabsf(dx) < threshold / 10. && (double)fabsf(dy) < threshold / 10.) {
+      ++it;
+      break;
+    }
+  }
+  *iters += it;
+  *px = x;
+  *py = y;
+  return 0;
+}
+
+// klt.h:403-424 TrackFeature, one wave per feature: every level, threshold x 50 on the coarse levels.
+__global__ __launch_bounds__(64 * kTrackWaves) void k_track_klt(const LevelDev* __restrict__ from_lv,
+                                                                const LevelDev* __restrict__ to_lv, int depth,
+                                                                TrackParams prm, int n, const float* from_xy,
+                                                                float* to_xy, int32_t* status, int32_t* iterations) {
+  const int lane = threadIdx.x & 63;
+  const int f = blockIdx.x * kTrackWaves + (threadIdx.x >> 6);
+  if (f >= n) return;
+  TrackCtx c;
+  init_ctx(c, prm, lane);
+  const float sx = from_xy[2 * f], sy = from_xy[2 * f + 1];
+  const double s = 1. / (1 << (depth - 1));
+  float x = (float)(to_xy[2 * f] * s), y = (float)(to_xy[2 * f + 1] * s);
+  int iters = 0, st = 0;
+  for (int i = depth - 1; i >= 0; --i) {
+    float tx = sx, ty = sy;
+    for (int k = 0; k < i; ++k) {
+      tx = (float)(tx * 0.5);
+      ty = (float)(ty * 0.5);
+    }
+    const LevelDev Ls = from_lv[i];
+    Geo g;
+    make_geo<false>(tx, ty, c.W, Ls.w, Ls.h, g);
+    Tmpl tp;
+#pragma unroll
+    for (int k = 0; k < kNP; ++k) tp.v[k] = c.pi[k] >= 0 ? sample(Ls.img, Ls.w, g, c.pi[k], c.pj[k]) : 0.f;
+    st = klt_track(c, to_lv[i], tp, i > 0 ? prm.threshold * 50 : prm.threshold, &x, &y, &iters);
+    if (st) break;
+    if (i > 0) {
+      x = (float)(x * 2.);
+      y = (float)(y * 2.);
+    }
+  }
+  if (lane == 0) {
+    status[f] = st;
+    if (st == 0) {
+      to_xy[2 * f] = x;
+      to_xy[2 * f + 1] = y;
+    }
+    if (iterations) iterations[f] = iters;
+  }
+}
+
+// ---- brute.h (one thread per search candidate) --------------------------------------------------
+constexpr int kBruteThreads = 256;
+
+struct BruteState {
+  float x, y;     // the search centre p (brute.h:143), at the current level's scale
+  float sad;      // SearchBest's return value of the last pass
+  int status;     // 0 tracking, 2 OUT_OF_BOUNDS
+};
+
+// GetPatch (brute.h:35-58: plain getRectSubPix, sequential sums) of one candidate and SADPatches(template,
+// candidate) (82-94: lighting-normalised, unmasked, sequential sum).  The patch is sampled twice (sums, then
+// the score) instead of being held in registers.
+__device__ __forceinline__ float brute_candidate(const LevelDev& L, int W, const float* tmpl, float tmean,
+                                                 float tsumsq, float px, float py) {
+  Geo g;
+  make_geo<false>(px, py, W, L.w, L.h, g);
+  const int len = W * W;
+  float sum = 0.f, sum_sq = 0.f;
+  for (int i = 0; i < W; ++i)
+    for (int j = 0; j < W; ++j) {
+      const float d = sample(L.img, L.w, g, i, j);
+      sum += d;
+      sum_sq += d * d;
+    }
+  const float mean = sum / len, sumsq = sum_sq / len;
+  const float alpha = sqrtf(tsumsq / sumsq);
+  const float beta = tmean - alpha * mean;
+  float acc = 0.f;
+  for (int i = 0; i < W; ++i)
+    for (int j = 0; j < W; ++j) {
+      const float a = tmpl[i * W + j], d = sample(L.img, L.w, g, i, j);
+      if (a == 0 || d == 0) continue;
+      const float diff = a - d * alpha - beta;
+      acc += fabsf(diff * diff);
+    }
+  return acc;
+}
+
+// Templates GetPatches(from, from_xy) (brute.h:120-127), thread per (feature, level); initial margin test and
+// search centre (brute.h:136-143), thread per feature.
+__global__ void k_brute_setup(const LevelDev* __restrict__ from_lv, const LevelDev* __restrict__ to_lv, int depth,
+                              int W, int n, const float* from_xy, const float* to_xy, float* tmpls, BruteState* stt) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n * depth) return;
+  const int f = t / depth, l = t % depth;
+  float tx = from_xy[2 * f], ty = from_xy[2 * f + 1];
+  for (int k = 0; k < l; ++k) {
+    tx = (float)(tx * 0.5);
+    ty = (float)(ty * 0.5);
+  }
+  const LevelDev L = from_lv[l];
+  Geo g;
+  make_geo<false>(tx, ty, W, L.w, L.h, g);
+  const int len = W * W;
+  float* o = tmpls + ((size_t)f * depth + l) * (len + 2);
+  float sum = 0.f, sum_sq = 0.f;
+  for (int i = 0; i < W; ++i)
+    for (int j = 0; j < W; ++j) {
+      const float d = sample(L.img, L.w, g, i, j);
+      o[i * W + j] = d;
+      sum += d;
+      sum_sq += d * d;
+    }
+  o[len] = sum / len;
+  o[len + 1] = sum_sq / len;
+  if (l == 0) {
+    const float px = to_xy[2 * f], py = to_xy[2 * f + 1];
+    const float margin = 13;
+    BruteState s;
+    s.status = (px < margin || py < margin || (px + margin) > to_lv[0].w || (py + margin) > to_lv[0].h) ? 2 : 0;
+    const double sc = 1. / (1 << (depth - 1));
+    s.x = (float)(px * sc);
+    s.y = (float)(py * sc);
+    s.sad = 0.f;
+    stt[f] = s;
+  }
+}
+
+// (sad, candidate) order of SearchBest (brute.h:104-113): a candidate wins unless its score is larger, so the
+// result is the last candidate with the smallest score.  NaN scores never win here.
+__device__ __forceinline__ bool brute_better(float sa, int ia, float sb, int ib) {
+  return sa < sb || (sa == sb && ia > ib);
+}
+
+// One SearchBest pass: every candidate of every live feature, one per thread; workgroup bests to bsad / bidx.
+__global__ __launch_bounds__(kBruteThreads) void k_brute_eval(const LevelDev* __restrict__ to_lv, int lvl, int W,
+                                                              int depth, const float* tmpls, const float* steps,
+                                                              int ns, const BruteState* stt, float* bsad, int* bidx,
+                                                              int nblk) {
+  __shared__ float rs[kBruteThreads / 64];
+  __shared__ int ri[kBruteThreads / 64];
+  const int f = blockIdx.y;
+  const BruteState s = stt[f];
+  float best = INFINITY;
+  int bi = -1;
+  const int c = blockIdx.x * kBruteThreads + threadIdx.x;
+  if (s.status == 0 && c < ns * ns) {
+    const float ox = steps[c / ns], oy = steps[c % ns];
+    const int len = W * W;
+    const float* t = tmpls + ((size_t)f * depth + lvl) * (len + 2);
+    const float sad = brute_candidate(to_lv[lvl], W, t, t[len], t[len + 1], s.x + ox, s.y + oy);
+    if (sad == sad) {
+      best = sad;
+      bi = c;
+    }
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    const float os = __shfl_xor(best, m);
+    const int oi = __shfl_xor(bi, m);
+    if (brute_better(os, oi, best, bi)) {
+      best = os;
+      bi = oi;
+    }
+  }
+  if ((threadIdx.x & 63) == 0) {
+    rs[threadIdx.x >> 6] = best;
+    ri[threadIdx.x >> 6] = bi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < kBruteThreads / 64; ++w)
+      if (brute_better(rs[w], ri[w], best, bi)) {
+        best = rs[w];
+        bi = ri[w];
+      }
+    bsad[(size_t)f * nblk + blockIdx.x] = best;
+    bidx[(size_t)f * nblk + blockIdx.x] = bi;
+  }
+}
+
+// The pass's winner per feature (one wave each): p moves to it when its score is <= SearchBest's initial 1e6;
+// check: sad > 100 -> OUT_OF_BOUNDS (brute.h:147-148, 158-159); scale: p *= 2 for the next level.
+__global__ void k_brute_pick(const float* steps, int ns, BruteState* stt, const float* bsad, const int* bidx,
+                             int nblk, int n, int check, int scale) {
+  const int lane = threadIdx.x & 63;
+  const int f = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (f >= n) return;
+  BruteState s = stt[f];
+  if (s.status != 0) return;
+  float best = INFINITY;
+  int bi = -1;
+  for (int b = lane; b < nblk; b += 64) {
+    const float sb = bsad[(size_t)f * nblk + b];
+    const int ib = bidx[(size_t)f * nblk + b];
+    if (brute_better(sb, ib, best, bi)) {
+      best = sb;
+      bi = ib;
+    }
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    const float os = __shfl_xor(best, m);
+    const int oi = __shfl_xor(bi, m);
+    if (brute_better(os, oi, best, bi)) {
+      best = os;
+      bi = oi;
+    }
+  }
+  if (lane != 0) return;
+  float sel = 1e6f;
+  if (bi >= 0 && !(best > 1e6f)) {
+    s.x = s.x + steps[bi / ns];
+    s.y = s.y + steps[bi % ns];
+    sel = best;
+  }
+  s.sad = sel;
+  if (check && sel > 100) s.status = 2;
+  else if (scale) {
+    s.x = (float)(s.x * 2.);
+    s.y = (float)(s.y * 2.);
+  }
+  stt[f] = s;
+}
+
 std::vector<float> GaussianKernel5(double sigma) {   // getGaussianKernel(5, sigma, CV_32F)
   std::vector<float> k(5);
   const double scale2X = -0.5 / (sigma * sigma);
@@ -484,6 +841,7 @@ Tracker::Tracker(const sg_tracker_options& o, const sg_device_options& d) : opt_
   SG_REQUIRE(o.depth >= 1 && o.depth <= kTrkMaxDepth, SG_EINVAL, "depth must be 1..8");
   SG_REQUIRE(o.max_images >= 1 && o.max_images <= 64, SG_EINVAL, "max_images must be 1..64");
   SG_REQUIRE(o.max_iterations >= 0, SG_EINVAL, "bad max_iterations");
+  SG_REQUIRE(o.mode >= SG_TRACKER_HESSIAN && o.mode <= SG_TRACKER_BRUTE, SG_EINVAL, "bad tracker mode");
   int ndev = 0;
   SG_HIP_CHECK(hipGetDeviceCount(&ndev));
   SG_REQUIRE(ndev > 0 && d.device >= 0 && d.device < ndev, SG_ENODEV, "no such HIP device");
@@ -539,16 +897,26 @@ void Tracker::SetImage(int slot, const uint8_t* bgr, int w, int h, int stride) {
   tmp2_.Resize((size_t)w * h);
   img_.Resize((size_t)stride * h);
   SG_HIP_CHECK(hipMemcpyAsync(img_.ptr, bgr, (size_t)stride * h, hipMemcpyHostToDevice, stream_));
-  const Blur5 b0 = MakeBlur(1.1), b1 = MakeBlur(0.8);
+  // hessian.h:95-126: blur 1.1 at level 0, pyrDown + blur 0.8 per level; klt.h:100-130: no blur at level 0,
+  // pyrDown + blur 0.6; brute.h:60-80: no blur at all
+  const int mode = opt_.mode;
+  const Blur5 b0 = MakeBlur(1.1), b1 = MakeBlur(mode == SG_TRACKER_KLT ? 0.6 : 0.8);
   SG_HIP_CHECK(hipEventRecord(ev_[2], stream_));
   const int bx = 256;
-  hipLaunchKernelGGL(k_gray_blur_row, dim3((w + bx - 1) / bx, h), dim3(bx), 0, stream_, img_.ptr, w, h, stride, b0,
-                     tmp_.ptr);
-  hipLaunchKernelGGL(k_blur_col, dim3((w + bx - 1) / bx, h), dim3(bx), 0, stream_, tmp_.ptr, w, h, b0, s.pyr.ptr);
+  if (mode == SG_TRACKER_HESSIAN) {
+    hipLaunchKernelGGL(k_gray_blur_row, dim3((w + bx - 1) / bx, h), dim3(bx), 0, stream_, img_.ptr, w, h, stride, b0,
+                       tmp_.ptr);
+    hipLaunchKernelGGL(k_blur_col, dim3((w + bx - 1) / bx, h), dim3(bx), 0, stream_, tmp_.ptr, w, h, b0, s.pyr.ptr);
+  } else {
+    hipLaunchKernelGGL(k_gray_scale, dim3((w + bx - 1) / bx, h), dim3(bx), 0, stream_, img_.ptr, w, h, stride,
+                       s.pyr.ptr);
+  }
   for (int l = 1; l < opt_.depth; ++l) {
     const int pw = s.w[l - 1], ph = s.h[l - 1], ow = s.w[l], oh = s.h[l];
+    const bool blur = mode != SG_TRACKER_BRUTE;
     hipLaunchKernelGGL(k_pyrdown, dim3((ow + bx - 1) / bx, oh), dim3(bx), 0, stream_, s.pyr.ptr + s.off[l - 1], pw,
-                       ph, tmp_.ptr, ow, oh);
+                       ph, blur ? tmp_.ptr : s.pyr.ptr + s.off[l], ow, oh);
+    if (!blur) continue;
     hipLaunchKernelGGL(k_blur_row, dim3((ow + bx - 1) / bx, oh), dim3(bx), 0, stream_, tmp_.ptr, ow, oh, b1,
                        tmp2_.ptr);
     hipLaunchKernelGGL(k_blur_col, dim3((ow + bx - 1) / bx, oh), dim3(bx), 0, stream_, tmp2_.ptr, ow, oh, b1,
@@ -659,4 +1027,104 @@ void Tracker::Results(float* to_xy, int32_t* accepted, int32_t* iterations) {
   track_ms_ = ms;
 }
 
+// One-directional TrackFeature of the configured FeatureTracker for n features (sg_tracker_track_feature).
+void Tracker::TrackFeature(int from, int to, int n, const float* from_xy, float* to_xy, const int32_t* levels,
+                           int32_t* status, int32_t* iterations) {
+  SG_REQUIRE(from >= 0 && from < (int)slots_.size() && slots_[from].valid, SG_EINVAL, "empty 'from' slot");
+  SG_REQUIRE(to >= 0 && to < (int)slots_.size() && slots_[to].valid, SG_EINVAL, "empty 'to' slot");
+  SG_REQUIRE(n >= 0 && (n == 0 || (from_xy && to_xy && status)), SG_EINVAL, "bad features");
+  const Slot& a = slots_[from];
+  const Slot& b = slots_[to];
+  SG_REQUIRE(a.w == b.w && a.h == b.h, SG_EINVAL, "pyramids of different sizes");
+  if (n == 0) return;
+  SG_HIP_CHECK(hipSetDevice(dev_.device));
+  hipStream_t st = stream_;
+  const int depth = opt_.depth, W = opt_.window;
+  from_.Upload(std::vector<float>(from_xy, from_xy + 2 * (size_t)n), st);
+  out_.Upload(std::vector<float>(to_xy, to_xy + 2 * (size_t)n), st);
+  if (levels) {
+    for (int i = 0; i < n; ++i) SG_REQUIRE(levels[i] >= 1, SG_EINVAL, "levels must be >= 1");
+    levels_.Upload(std::vector<int32_t>(levels, levels + n), st);
+  }
+  acc_.Resize(n);
+  its_.Resize(n);
+  its_.Zero(st);
+  TrackParams prm{W, opt_.max_iterations, opt_.threshold, opt_.fb_max, opt_.retry_levels, mask_.ptr};
+  const LevelDev* la = (const LevelDev*)a.table.ptr;
+  const LevelDev* lb = (const LevelDev*)b.table.ptr;
+  const dim3 grid((n + kTrackWaves - 1) / kTrackWaves), block(64 * kTrackWaves);
+  if (opt_.mode == SG_TRACKER_HESSIAN) {
+    hipLaunchKernelGGL(k_track_one, grid, block, 0, st, la, lb, depth, prm, n, from_.ptr, out_.ptr,
+                       levels ? (const int32_t*)levels_.ptr : nullptr, acc_.ptr, its_.ptr);
+  } else if (opt_.mode == SG_TRACKER_KLT) {
+    hipLaunchKernelGGL(k_track_klt, grid, block, 0, st, la, lb, depth, prm, n, from_.ptr, out_.ptr, acc_.ptr,
+                       its_.ptr);
+  } else {
+    SG_REQUIRE(n <= 65535, SG_EINVAL, "at most 65535 features per brute-force call");
+    // brute.h:129-164: two passes per coarse level, five at level 0, each an exhaustive SearchBest grid
+    struct Pass {
+      float window, res;
+      int lvl, check, scale;
+    };
+    std::vector<Pass> passes;
+    for (int l = depth - 1; l > 0; --l) {
+      passes.push_back({3.f, 1.f, l, 0, 0});
+      passes.push_back({1.f, 0.33333f, l, 1, 1});
+    }
+    passes.push_back({3.f, 1.f, 0, 0, 0});
+    passes.push_back({1.f, 0.3333f, 0, 0, 0});
+    passes.push_back({0.4f, 0.1f, 0, 0, 0});
+    passes.push_back({0.2f, 0.025f, 0, 0, 0});
+    passes.push_back({8.f, 0.01f, 0, 1, 0});
+    std::vector<float> steps;
+    std::vector<int> soff, sn;
+    int max_nblk = 1;
+    for (const Pass& p : passes) {
+      soff.push_back((int)steps.size());
+      int cnt = 0;
+      for (float x = -p.window; x <= p.window; x += p.res) {   // the reference's float stepping
+        steps.push_back(x);
+        ++cnt;
+      }
+      sn.push_back(cnt);
+      max_nblk = std::max(max_nblk, (cnt * cnt + kBruteThreads - 1) / kBruteThreads);
+    }
+    brute_steps_.Upload(steps, st);
+    brute_tmpl_.Resize((size_t)n * depth * (W * W + 2));
+    brute_state_.Resize(sizeof(BruteState) * (size_t)n);
+    brute_sad_.Resize((size_t)n * max_nblk);
+    brute_idx_.Resize((size_t)n * max_nblk);
+    BruteState* stt = reinterpret_cast<BruteState*>(brute_state_.ptr);
+    hipLaunchKernelGGL(k_brute_setup, dim3((n * depth + 255) / 256), dim3(256), 0, st, la, lb, depth, W, n,
+                       from_.ptr, out_.ptr, brute_tmpl_.ptr, stt);
+    for (size_t k = 0; k < passes.size(); ++k) {
+      const int ns = sn[k], nblk = (ns * ns + kBruteThreads - 1) / kBruteThreads;
+      hipLaunchKernelGGL(k_brute_eval, dim3(nblk, n), dim3(kBruteThreads), 0, st, lb, passes[k].lvl, W, depth,
+                         brute_tmpl_.ptr, brute_steps_.ptr + soff[k], ns, stt, brute_sad_.ptr, brute_idx_.ptr, nblk);
+      hipLaunchKernelGGL(k_brute_pick, dim3((n + 3) / 4), dim3(256), 0, st, brute_steps_.ptr + soff[k], ns, stt,
+                         brute_sad_.ptr, brute_idx_.ptr, nblk, n, passes[k].check, passes[k].scale);
+    }
+    SG_HIP_CHECK(hipGetLastError());
+    std::vector<BruteState> hs(n);
+    SG_HIP_CHECK(hipMemcpyAsync(hs.data(), stt, sizeof(BruteState) * (size_t)n, hipMemcpyDeviceToHost, st));
+    SG_HIP_CHECK(hipStreamSynchronize(st));
+    for (int i = 0; i < n; ++i) {
+      status[i] = hs[i].status;
+      if (hs[i].status == 0) {
+        to_xy[2 * i] = hs[i].x;
+        to_xy[2 * i + 1] = hs[i].y;
+      }
+      if (iterations) iterations[i] = 0;
+    }
+    return;
+  }
+  SG_HIP_CHECK(hipGetLastError());
+  SG_HIP_CHECK(hipMemcpyAsync(to_xy, out_.ptr, sizeof(float) * 2 * (size_t)n, hipMemcpyDeviceToHost, st));
+  SG_HIP_CHECK(hipMemcpyAsync(status, acc_.ptr, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost, st));
+  if (iterations)
+    SG_HIP_CHECK(hipMemcpyAsync(iterations, its_.ptr, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost, st));
+  SG_HIP_CHECK(hipStreamSynchronize(st));
+}
+
 }  // namespace sg
+

@@ -117,4 +117,12 @@ int sg_tracker_seed_features(sg_tracker* t, int32_t slot, const float* match_xy,
   SG_CAPI_END
 }
 
+int sg_tracker_track_feature(sg_tracker* t, int32_t from, int32_t to, int32_t n, const float* from_xy, float* to_xy,
+                             const int32_t* levels, int32_t* status, int32_t* iterations) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(t, SG_EINVAL, "null handle");
+  t->t->TrackFeature(from, to, n, from_xy, to_xy, levels, status, iterations);
+  SG_CAPI_END
+}
+
 }  // extern "C"

@@ -193,7 +193,7 @@ _LIB = None
 class SgTrackerOptions(C.Structure):
     _fields_ = [("window", C.c_int32), ("depth", C.c_int32), ("max_iterations", C.c_int32),
                 ("threshold", C.c_float), ("fb_max", C.c_float), ("retry_levels", C.c_int32),
-                ("max_images", C.c_int32), ("reserved", C.c_int32 * 5)]
+                ("max_images", C.c_int32), ("mode", C.c_int32), ("reserved", C.c_int32 * 4)]
 
 
 _fp = C.POINTER(C.c_float)
@@ -239,6 +239,7 @@ SYMBOLS = {
     "sg_tracker_run": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32]),
     "sg_tracker_results": (C.c_int, [C.c_void_p, _fp, _ip, _ip]),
     "sg_tracker_kernel_ms": (C.c_int, [C.c_void_p, _dp, _dp]),
+    "sg_tracker_track_feature": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, _fp, _fp, _ip, _ip, _ip]),
     "sg_tracker_seed_features": (C.c_int, [C.c_void_p, C.c_int32, _fp, C.c_int32, C.c_int32, C.c_double, C.c_double,
                                            _fp, _ip, _fp, _ip]),
     "sg_matcher_create": (C.c_int, [C.POINTER(C.c_void_p), C.POINTER(SgDeviceOptions)]),

@@ -122,6 +122,22 @@ class HessianTracker:
         check(self.lib.sg_tracker_kernel_ms(self.h, C.byref(t), C.byref(p)), "kernel_ms")
         return t.value, p.value
 
+    def TrackFeature(self, from_slot: int, to_slot: int, from_xy, to_xy=None, levels=None):
+        """One-directional TrackFeature of this tracker's mode (hessian.h:243-264 / klt.h:403-424 /
+        brute.h:129-164) for many features: GetPatches(from_slot, from_xy), then tracking in to_slot from to_xy.
+        Returns (to_xy, status (0 OK, 2 OUT_OF_BOUNDS), iterations); failed features keep their guess."""
+        from_xy = np.ascontiguousarray(from_xy, dtype=np.float32).reshape(-1, 2)
+        n = from_xy.shape[0]
+        out = (from_xy.copy() if to_xy is None else np.ascontiguousarray(to_xy, dtype=np.float32).reshape(-1, 2).copy())
+        lv = None if levels is None else np.ascontiguousarray(levels, dtype=np.int32)
+        st = np.zeros(n, np.int32)
+        its = np.zeros(n, np.int32)
+        check(self.lib.sg_tracker_track_feature(self.h, from_slot, to_slot, n, from_xy.ctypes.data_as(_fp),
+                                                out.ctypes.data_as(_fp), None if lv is None else lv.ctypes.data_as(_ip),
+                                                st.ctypes.data_as(_ip), its.ctypes.data_as(_ip)),
+              "sg_tracker_track_feature")
+        return out, st, its
+
     def SeedFeatures(self, slot: int, match_xy=None, max_corners: int = 120, quality: float = 0.01,
                      min_distance: float = 20.0):
         """Matcher::Track's new-keyframe seeding on the image of `slot` (matcher.cpp:123-169, AddNewFeatures):
@@ -136,3 +152,19 @@ class HessianTracker:
                                                 C.byref(nc), added.ctypes.data_as(_fp), C.byref(na)),
               "sg_tracker_seed_features")
         return corners[:nc.value].copy(), added[:na.value].copy()
+
+
+class KLTTracker(HessianTracker):
+    """klt.h's KLTTracker on the device (sg_tracker_options.mode = SG_TRACKER_KLT): MakePyramid and
+    TrackFeature with klt.h's pyramid, masked SSD and forward-difference Newton step."""
+
+    def __init__(self, window: int = 13, depth: int = 6, device: int = 0, max_images: int = 8, **kw):
+        super().__init__(window=window, depth=depth, device=device, max_images=max_images, mode=1, **kw)
+
+
+class BruteTracker(HessianTracker):
+    """brute.h's BruteTracker on the device (sg_tracker_options.mode = SG_TRACKER_BRUTE): exhaustive
+    float-stepped SearchBest grids, one candidate per thread."""
+
+    def __init__(self, window: int = 13, depth: int = 6, device: int = 0, max_images: int = 8, **kw):
+        super().__init__(window=window, depth=depth, device=device, max_images=max_images, mode=2, **kw)
