@@ -108,6 +108,26 @@ __device__ __forceinline__ double block_max(double v, double* red) {
   return s;
 }
 
+// Fixed-order workgroup sums of NV values at once: DPP wave sums, one LDS exchange, one barrier; every
+// thread gets the totals.  red: LDS of NV * NT / 64 doubles.
+template <int NT, int NV>
+__device__ __forceinline__ void block_sum_multi(double (&v)[NV], double* red) {
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) v[j] = wave_sum_full(v[j]);
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int j = 0; j < NV; ++j) red[w * NV + j] = v[j];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    double t = 0.0;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) t += red[i * NV + j];
+    v[j] = t;
+  }
+}
+
 // packed upper-triangle index of a 6x6 block (a <= c)
 __device__ __forceinline__ int u6(int a, int c) { return a * (11 - a) / 2 + c; }
 // packed upper-triangle index of a 4x4 block (a <= c)
@@ -396,8 +416,18 @@ __global__ __launch_bounds__(kRedThreads) void k_cam_reduce(Dev d) {
     if (sl < kCamSlices) {
       const int j0 = d.cam_loff[b], j1 = d.cam_loff[b + 1];
       double acc = 0.0;
-#pragma unroll 4
-      for (int j = j0 + sl; j < j1; j += kCamSlices) acc += d.cam_slab[d.cam_lidx[j] + e];
+      constexpr int kU = 8;   // offsets, then partials, kU at a time in flight
+      for (int jb = j0 + sl; jb < j1; jb += kU * kCamSlices) {
+        int ix[kU];
+        double v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) ix[u] = jb + u * kCamSlices < j1 ? d.cam_lidx[jb + u * kCamSlices] : 0;
+#pragma unroll
+        for (int u = 0; u < kU; ++u) v[u] = d.cam_slab[ix[u] + e];
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+          if (jb + u * kCamSlices < j1) acc += v[u];
+      }
       part[sl][e] = acc;
     }
     __syncthreads();
@@ -411,22 +441,35 @@ __global__ __launch_bounds__(kRedThreads) void k_cam_reduce(Dev d) {
     }
     return;
   }
-  // scalars: thread t sums chunks t, t + 1024, ..., then a fixed-order workgroup tree
-  __shared__ double red[kRedThreads / 64];
+  // scalars: thread t sums chunks t, t + 1024, ... (two chunks' loads in flight), then a fixed-order
+  // workgroup tree
+  __shared__ double red[kRedThreads / 64 * kXNum];
+  __shared__ double redm[kRedThreads / 64];
   double v[kXNum] = {0, 0, 0, 0, 0};
   double gm = 0.0;
-  for (int c = tid; c < d.nlin; c += kRedThreads) {
-    const double* sc = d.lin_scal + (size_t)c * kNScal;
-    v[kXCost] += sc[kCost];
-    v[kXFail] += sc[kFail];
-    v[kXFixed] += sc[kFixed];
-    v[kXFixedFail] += sc[kFixedFail];
-    v[kXXnorm2] += sc[kXnorm2];
-    gm = fmax(gm, sc[kGmax]);
-  }
+  for (int c0 = tid; c0 < d.nlin; c0 += 2 * kRedThreads) {
+    double t[2][kXNum + 1];
 #pragma unroll
-  for (int j = 0; j < kXNum; ++j) v[j] = block_sum<kRedThreads>(v[j], red);
-  gm = block_max<kRedThreads>(gm, red);
+    for (int u = 0; u < 2; ++u) {
+      const int c = c0 + u * kRedThreads;
+      const double* sc = d.lin_scal + (size_t)(c < d.nlin ? c : 0) * kNScal;
+      t[u][kXCost] = sc[kCost];
+      t[u][kXFail] = sc[kFail];
+      t[u][kXFixed] = sc[kFixed];
+      t[u][kXFixedFail] = sc[kFixedFail];
+      t[u][kXXnorm2] = sc[kXnorm2];
+      t[u][kXNum] = sc[kGmax];
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      if (c0 + u * kRedThreads < d.nlin) {
+#pragma unroll
+        for (int j = 0; j < kXNum; ++j) v[j] += t[u][j];
+        gm = fmax(gm, t[u][kXNum]);
+      }
+  }
+  block_sum_multi<kRedThreads, kXNum>(v, red);
+  gm = block_max<kRedThreads>(gm, redm);
   if (tid == 0) {
 #pragma unroll
     for (int j = 0; j < kXNum; ++j) d.xchg_cam[nv + j] = v[j];
@@ -843,21 +886,22 @@ __global__ __launch_bounds__(256) void k_S_reduce(Dev d) {
   }
   const int ne = is_rhs ? 6 : 36;
   const int el = lane < ne ? lane : 0;
+  // partials in list order; the next 64 offsets and kSR partial loads are in flight at a time
+  constexpr int kSR = 32;
   double s = 0.0;
+  int myoff = (j0 + lane < j1) ? lidx[j0 + lane] : 0;
   for (int base = j0; base < j1; base += 64) {
     const int cnt = min(64, j1 - base);
-    const int myoff = lane < cnt ? lidx[base + lane] : 0;
-    for (int k = 0; k < cnt; k += 8) {
-      double v[8];
+    const int nxt = (base + 64 + lane < j1) ? lidx[base + 64 + lane] : 0;
+    for (int k = 0; k < cnt; k += kSR) {
+      double v[kSR];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {   // eight independent loads in flight, summed in list order
-        const int off = __builtin_amdgcn_readlane(myoff, min(k + u, 63));
-        v[u] = (k + u < cnt) ? d.S_slab[off + el] : 0.0;
-      }
+      for (int u = 0; u < kSR; ++u) v[u] = d.S_slab[__builtin_amdgcn_readlane(myoff, min(k + u, 63)) + el];
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
+      for (int u = 0; u < kSR; ++u)
         if (k + u < cnt) s += v[u];
     }
+    myoff = nxt;
   }
   if (lane >= ne) return;
   if (!is_rhs) {
@@ -1073,60 +1117,71 @@ __device__ __forceinline__ void chol_candidates(const Dev& d, const double* y, i
   }
 
 // Back substitution of the window path from x_p = z_p - W_p x_rest (W = U11^-1 U12 and z = U11^-1 y per
-// panel, stored over the U rows of A and over y): one mat-vec per panel, two rows per wave, the next
-// panel's W loads in flight during the current panel's reduction.
+// panel, stored over the U rows of A and over y): one mat-vec per panel, two rows per wave.  The operands of
+// the next kBsDepth panels are in flight in registers (a ring, statically indexed by an unrolled loop), so
+// a panel step waits on LDS and the DPP reduction, not on a global load.
+constexpr int kBsDepth = 8;
+struct BsOps {
+  double w[2][2], z[2];
+  int jend;
+};
+__device__ __forceinline__ void chol_bs_load(const double* Wm, const double* z, int n, const int* jend_sh, int pk,
+                                             int wave, int lane, BsOps& o) {
+  if (pk < 0) {
+    o.jend = 0;
+    return;
+  }
+  const int kb = pk * kCholNb;
+  o.jend = jend_sh[pk];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int r = kb + 2 * wave + h;
+    const bool rin = r < n;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int c = kb + kCholNb + lane + 64 * q;
+      o.w[h][q] = (rin && c < o.jend) ? Wm[(size_t)r * n + c] : 0.0;
+    }
+    o.z[h] = rin ? z[r] : 0.0;
+  }
+}
+
 __device__ __forceinline__ void chol_backsub_w(const double* Wm, const double* z, double* xs, int n,
                                                const int* jend_sh, const int32_t* panel_jend) {
+  (void)panel_jend;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   static_assert(kCholThreads / 64 * 2 == kCholNb, "two panel rows per wave");
   const int npanel = (n + kCholNb - 1) / kCholNb;
-  auto load = [&](int pk, double (&wv)[2][2], double (&zv)[2], int& jend) {
-    const int kb = pk * kCholNb;
-    jend = jend_sh[pk];
+  BsOps ring[kBsDepth];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int r = kb + 2 * wave + h;
-      const bool rin = r < n;
+  for (int s = 0; s < kBsDepth; ++s) chol_bs_load(Wm, z, n, jend_sh, npanel - 1 - s, wave, lane, ring[s]);
+  for (int base = npanel - 1; base >= 0; base -= kBsDepth) {
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int c = kb + kCholNb + lane + 64 * q;
-        wv[h][q] = (rin && c < jend) ? Wm[(size_t)r * n + c] : 0.0;
+    for (int s = 0; s < kBsDepth; ++s) {
+      const int pk = base - s;   // workgroup-uniform
+      if (pk >= 0) {
+        const BsOps cur = ring[s];
+        chol_bs_load(Wm, z, n, jend_sh, pk - kBsDepth, wave, lane, ring[s]);
+        const int kb = pk * kCholNb;
+        double sv[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          double acc = 0.0;
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const int c = kb + kCholNb + lane + 64 * q;
+            acc += cur.w[h][q] * (c < cur.jend ? xs[c] : 0.0);
+          }
+          sv[h] = wave_sum_full(acc);
+        }
+        if (lane == 0) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            if (kb + 2 * wave + h < n) xs[kb + 2 * wave + h] = cur.z[h] - sv[h];
+        }
+        lds_barrier();
       }
-      zv[h] = rin ? z[r] : 0.0;
     }
-  };
-  double wv[2][2], zv[2];
-  int jend;
-  load(npanel - 1, wv, zv, jend);
-  for (int pk = npanel - 1; pk >= 0; --pk) {
-    const int kb = pk * kCholNb;
-    double wn[2][2] = {{0.0, 0.0}, {0.0, 0.0}}, zn[2] = {0.0, 0.0};
-    int jn = 0;
-    if (pk > 0) load(pk - 1, wn, zn, jn);
-    double sv[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      double acc = 0.0;
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int c = kb + kCholNb + lane + 64 * q;
-        acc += wv[h][q] * (c < jend ? xs[c] : 0.0);
-      }
-      sv[h] = wave_sum_full(acc);
-    }
-    if (lane == 0) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-        if (kb + 2 * wave + h < n) xs[kb + 2 * wave + h] = zv[h] - sv[h];
-    }
-    lds_barrier();
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      zv[h] = zn[h];
-#pragma unroll
-      for (int q = 0; q < 2; ++q) wv[h][q] = wn[h][q];
-    }
-    jend = jn;
   }
 }
 
@@ -1625,33 +1680,55 @@ __global__ __launch_bounds__(kLinThreads) void k_point_update(Dev d) {
   }
 }
 
-__global__ __launch_bounds__(kRedThreads) void k_upd_reduce(Dev d) {
+__device__ void decide_step(const Dev& d);
+
+// fuse: single rank, no all-reduce in between: thread 0 also runs k_decide's step (one launch less).
+__global__ __launch_bounds__(kRedThreads) void k_upd_reduce(Dev d, int fuse) {
   const LmState* st = d.st;
   if (st->done) return;
-  __shared__ double red[kRedThreads / 64];
+  __shared__ double red[kRedThreads / 64 * kUNum];
   const int tid = threadIdx.x;
   double v[kUNum] = {0, 0, 0, 0, 0, 0};
-  for (int c = tid; c < d.nlin; c += kRedThreads) {
-    const double* sc = d.chunk_scal + (size_t)c * kNScal;
-    v[kUModel] += sc[kModel];
-    v[kUCandCost] += sc[kCandCost];
-    v[kUCandFail] += sc[kCandFail];
-    v[kUStep2] += sc[kStep2];
-    v[kUCandX2] += sc[kCandX2];
+  for (int c0 = tid; c0 < d.nlin; c0 += 4 * kRedThreads) {
+    double t[4][5];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int c = c0 + u * kRedThreads;
+      const double* sc = d.chunk_scal + (size_t)(c < d.nlin ? c : 0) * kNScal;
+      t[u][0] = sc[kModel];
+      t[u][1] = sc[kCandCost];
+      t[u][2] = sc[kCandFail];
+      t[u][3] = sc[kStep2];
+      t[u][4] = sc[kCandX2];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (c0 + u * kRedThreads < d.nlin) {
+        v[kUModel] += t[u][0];
+        v[kUCandCost] += t[u][1];
+        v[kUCandFail] += t[u][2];
+        v[kUStep2] += t[u][3];
+        v[kUCandX2] += t[u][4];
+      }
   }
   for (int g = tid; g < d.nseg; g += kRedThreads) v[kULinFail] += d.seg_fail[g];
-#pragma unroll
-  for (int j = 0; j < kUNum; ++j) v[j] = block_sum<kRedThreads>(v[j], red);
-  if (tid == 0)
+  block_sum_multi<kRedThreads, kUNum>(v, red);
+  if (tid == 0) {
 #pragma unroll
     for (int j = 0; j < kUNum; ++j) d.xchg_upd[j] = v[j];
+    if (fuse) decide_step(d);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
 // k_decide: TrustRegionMinimizer + LevenbergMarquardtStrategy step bookkeeping (Ceres 1.8 semantics).
 __global__ void k_decide(Dev d) {
+  if (threadIdx.x == 0) decide_step(d);
+}
+
+__device__ void decide_step(const Dev& d) {
   LmState* st = d.st;
-  if (threadIdx.x != 0 || st->done) return;
+  if (st->done) return;
   const double* u = d.xchg_upd;
   const double* c = d.xchg_chol;
   const double model = u[kUModel] + c[kCModel];
@@ -2424,13 +2501,16 @@ void BaSolver::Iterate(int n) {
     TimedLaunchBegin(kKPointUpd);
     hipLaunchKernelGGL(k_point_update, dim3(std::max(nlin_, 1)), dim3(kLinThreads), 0, stream_, d);
     TimedLaunchEnd(kKPointUpd);
+    const bool multi = comm_ && comm_->nranks() > 1;
     TimedLaunchBegin(kKUpdRed);
-    hipLaunchKernelGGL(k_upd_reduce, dim3(1), dim3(kRedThreads), 0, stream_, d);
+    hipLaunchKernelGGL(k_upd_reduce, dim3(1), dim3(kRedThreads), 0, stream_, d, multi ? 0 : 1);
     TimedLaunchEnd(kKUpdRed);
-    AllReduceSum(xchg_upd_.ptr, kUNum);
-    TimedLaunchBegin(kKDecide);
-    hipLaunchKernelGGL(k_decide, dim3(1), dim3(64), 0, stream_, d);
-    TimedLaunchEnd(kKDecide);
+    if (multi) {
+      AllReduceSum(xchg_upd_.ptr, kUNum);
+      TimedLaunchBegin(kKDecide);
+      hipLaunchKernelGGL(k_decide, dim3(1), dim3(64), 0, stream_, d);
+      TimedLaunchEnd(kKDecide);
+    }
   }
   SG_HIP_CHECK(hipGetLastError());
 }
