@@ -1297,66 +1297,67 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
       const int slot = lane < kCholNb ? lane : kCholNb + (64 - kCholNb) * wave + (lane - kCholNb);
       const int c = kb + slot;
       const bool v = slot < kCholWS && c < jend;
+      const bool isy = slot == kCholWS;   // the rhs rides as an augmented column in an otherwise idle lane
       double* prw = prow[wave];
-      double ca[kCholNb], yv[kCholNb];
+      double ca[kCholNb];
 #pragma unroll
       for (int r = 0; r < kCholNb; ++r) {
         const bool real = r < w;
         const double wv = Wn(win, kb + r, c), yr = yw[(kb + r) & (kCholWS - 1)];   // unconditional loads
-        ca[r] = (real && v && r <= slot) ? wv : ((!real && slot == r) ? 1.0 : 0.0);
-        yv[r] = real ? yr : 0.0;
+        ca[r] = isy ? (real ? yr : 0.0)
+                    : ((real && v && r <= slot) ? wv : ((!real && slot == r) ? 1.0 : 0.0));
       }
       bool bad = false;
       SG_STAMP_AT(1)
+      // Right-looking steps: row j is scaled by 1/U_jj and every column entry below it updated with
+      // A[r][c] -= U[j][r] U[j][c] = A[j][r] (U[j][c] / U_jj) (one FMA per entry).  The pivot-row broadcast is
+      // software-pipelined: step j updates row j+1 first and posts it to the LDS row, then applies the rest
+      // of its updates while that write / read round trip is in flight.
+      double u[kCholNb];
+      if (lane < kCholNb) prw[lane] = ca[0];
+#pragma unroll
+      for (int r = 0; r < kCholNb; ++r) u[r] = prw[r];
 #pragma unroll
       for (int j = 0; j < kCholNb; ++j) {
-        if (lane < kCholNb) prw[lane] = ca[j];
-        double u[kCholNb];
-#pragma unroll
-        for (int r = j; r < kCholNb; ++r) u[r] = prw[r];
         const double piv = u[j];
         bad |= !(piv > 0.0);
         double inv = __builtin_amdgcn_rsq(piv);
         inv = inv * (1.5 - 0.5 * piv * inv * inv);   // two Newton steps: full fp64 1/sqrt
         inv = inv * (1.5 - 0.5 * piv * inv * inv);
         ca[j] *= inv;
-        yv[j] *= inv;
+        const double t = ca[j] * inv;
         if (wave == 0 && lane == 0) pinv[buf][j] = inv;
-#pragma unroll
-        for (int r = j + 1; r < kCholNb; ++r) {
-          const double ur = u[r] * inv;   // U[j][r], rounded exactly as lane r rounds its own ca[j]
-          ca[r] -= ur * ca[j];
-          yv[r] -= ur * yv[j];
+        if (j + 1 < kCholNb) {
+          ca[j + 1] = fma(-u[j + 1], t, ca[j + 1]);
+          if (lane < kCholNb) prw[lane] = ca[j + 1];   // the next pivot row
         }
-        // materialise this step's updates here (otherwise they are sunk into later steps and the
-        // deferred multipliers spill)
 #pragma unroll
-        for (int r = j; r < kCholNb; ++r) {
-          asm volatile("" : "+v"(ca[r]));
-          asm volatile("" : "+v"(yv[r]));
+        for (int r = j + 2; r < kCholNb; ++r) ca[r] = fma(-u[r], t, ca[r]);
+        // materialise this step's updates here (otherwise they are sunk into later steps and spill)
+#pragma unroll
+        for (int r = j; r < kCholNb; ++r) asm volatile("" : "+v"(ca[r]));
+        if (j + 1 < kCholNb) {
+#pragma unroll
+          for (int r = j + 1; r < kCholNb; ++r) u[r] = prw[r];
         }
       }
       SG_STAMP_AT(3)
-      // rhs of the trailing rows: y_c -= sum_r U[r][c] y_r; trailing columns' panel rows -> LDS; the
-      // panel's U11, 1/U_jj and forward rhs for the W / z pass (wave 0)
+      // trailing columns' panel rows -> LDS; the panel's U11 and 1/U_jj (wave 0) and forward-substituted rhs
+      // (the rhs lane) for the W / z pass and the trailing rhs update
       const bool trail = v && lane >= kCholNb;
-      double s0 = 0.0;
-#pragma unroll
-      for (int r = 0; r < kCholNb; ++r) s0 += ca[r] * yv[r];
-      if (trail) yw[c & (kCholWS - 1)] -= s0;
 #pragma unroll
       for (int r = 0; r < kCholNb; ++r)
         if (r < w && trail) Wn(win, kb + r, c) = ca[r];
+      if (isy) {
+#pragma unroll
+        for (int r = 0; r < kCholNb; ++r) ypan[buf][r] = ca[r];
+      }
       if (wave == 0) {
         if (lane < kCholNb) {
 #pragma unroll
           for (int r = 0; r < kCholNb; ++r) u11w[buf][lane * kCholNb + r] = ca[r];
         }
-        if (lane == 0) {
-#pragma unroll
-          for (int r = 0; r < kCholNb; ++r) ypan[buf][r] = yv[r];
-          if (bad) fail_sh = 1;
-        }
+        if (lane == 0 && bad) fail_sh = 1;
       }
     } else if (pk > 0 && wave < kPanelWaves + 2) {
       // (a') the previous panel's back-substitution operands, off the critical path
@@ -1366,7 +1367,17 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
     }
     lds_barrier();
     SG_STAMP_AT(2)
-    // (b) trailing update A22 -= U12^T U12 on the band, 16x16 MFMA tiles (upper tiles only)
+    // (b) rhs of the trailing rows, y_c -= sum_r U[r][c] ytilde_r (one thread per band column), and the
+    // trailing update A22 -= U12^T U12 on the band, 16x16 MFMA tiles (upper tiles only)
+    if (tid < kCholWS - kCholNb) {
+      const int c = kb + kCholNb + tid;
+      if (c < jend) {
+        double s0 = 0.0;
+#pragma unroll
+        for (int r = 0; r < kCholNb; ++r) s0 += (r < w ? Wn(win, kb + r, c) : 0.0) * ypan[buf][r];
+        yw[c & (kCholWS - 1)] -= s0;
+      }
+    }
     const int m = jend - (kb + w);
     const int T = (m + 15) >> 4;
     const int ntiles = T * (T + 1) / 2;
