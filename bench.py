@@ -50,6 +50,21 @@ FP32_PEAK_TFLOPS = 157.3     # MI355X FP32 vector peak
 INT_PEAK_TOPS = 78.6         # 32-bit integer VALU lane-ops/s: 256 CU x 4 SIMD x 32 lanes/clk x 2.4 GHz
 
 
+def pmc_traffic(kernel, largest_grid=False):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes
+    (tools/pmc_traffic.sh -> profiles/<round>_pmc_traffic.json, newest file wins).  Among several launch
+    shapes of one kernel the smallest grid is the config-2 / bench launch, the largest the scaled sweep."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    if not files:
+        return None
+    groups = [g for g in json.load(open(files[-1]))["kernels"].values() if g["kernel"] == kernel]
+    if not groups:
+        return None
+    g = (max if largest_grid else min)(groups, key=lambda g: g["grid_size"])
+    return g["traffic_bytes"]
+
+
 def bench_tracker(local, cpu_seconds):
     """BASELINE config 3: 640x480 synthetic video, 2000 tracks, 3-level pyramid, 7x7 window, forward/backward
     TrackFeature (matcher.cpp:173-206).  Inputs resident on the device; value = tracks / kernel time."""
@@ -77,7 +92,7 @@ def bench_tracker(local, cpu_seconds):
            "tracks_per_s_with_pyramid": len(pts) / ((ms + pyr_ms) * 1e-3),
            "accepted_frac": float(acc.mean()), "newton_iterations": int(its.sum()),
            "roofline": {"bound": "valu", "achieved": ach, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                        "frac": ach / FP32_PEAK_TFLOPS, "traffic": None, "kernel": "k_track_fb",
+                        "frac": ach / FP32_PEAK_TFLOPS, "traffic": pmc_traffic("k_track_fb"), "kernel": "k_track_fb",
                         "note": "108*W^2 flops per Newton iteration (6 probes of bilinear sampling, moments, "
                                 "score); one wave per feature"}}
     if cpu_seconds > 0:
@@ -116,7 +131,8 @@ def bench_hamming(local, cpu_seconds):
            "unit": "rows/s", "pairs_per_s": pairs / (ms * 1e-3), "ms": ms,
            "recall_of_true_matches": float((bi[truth >= 0] == truth[truth >= 0]).mean()),
            "roofline": {"bound": "valu-int", "achieved": ach, "peak": INT_PEAK_TOPS, "unit": "Tops/s",
-                        "frac": ach / INT_PEAK_TOPS, "traffic": None, "kernel": "k_hamming_slices"}}
+                        "frac": ach / INT_PEAK_TOPS, "traffic": pmc_traffic("k_hamming_slices"),
+                        "kernel": "k_hamming_slices"}}
     if cpu_seconds > 0:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
@@ -217,13 +233,13 @@ def main():
     if dom_flops > 0 and dominant in ("cholesky",):
         ach = dom_flops / (dom_ms * 1e-3) / 1e12
         roof = {"bound": "mfma", "achieved": ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": ach / FP64_PEAK_TFLOPS, "traffic": None, "kernel": dominant,
+                "frac": ach / FP64_PEAK_TFLOPS, "traffic": pmc_traffic("k_cholesky_window"), "kernel": dominant,
                 "note": "single-workgroup dense banded Cholesky of the reduced camera system (n=%d)"
                         % (6 * (args.frames - 2))}
     else:
         ach = dom_bytes / (dom_ms * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": ach / HBM_PEAK_GBS, "traffic": None, "kernel": dominant}
+                "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic("k_" + dominant), "kernel": dominant}
     # Jacobian/Hessian sweep (north-star kernel): bytes per linearization / mean active launch time.
     lin_total_ms = ktimes["linearize"][0] * ktimes["linearize"][1]
     sweep = None
@@ -231,6 +247,7 @@ def main():
         ach = work["linearize"][0] * n_lin / (lin_total_ms * 1e-3) / 1e9
         sweep = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                  "frac": ach / HBM_PEAK_GBS, "bytes_per_launch": work["linearize"][0],
+                 "traffic": pmc_traffic("k_linearize"),
                  "active_launches": n_lin, "launches": ktimes["linearize"][1]}
 
     # scaled sweep: the same kernel on a problem large enough to amortise launch latency
@@ -252,7 +269,8 @@ def main():
         ach = wb / (kt[0] * 1e-3) / 1e9
         sweep_scaled = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": ach / HBM_PEAK_GBS, "obs": bp.num_obs, "points": bp.num_points,
-                        "ms_per_launch": kt[0], "bytes_per_launch": wb}
+                        "ms_per_launch": kt[0], "bytes_per_launch": wb,
+                        "traffic": pmc_traffic("k_linearize", largest_grid=True)}
         bs.close()
 
     # CPU baseline: the oracle (C++ restatement of the same LM) on the host cores, bounded sample
@@ -306,6 +324,8 @@ def main():
         "speedup_vs_cpu": (value / cpu["value"]) if cpu else None,
         "lm_state": {"final_cost": summary_after["final_cost"], "radius": summary_after["trust_region_radius"]},
         "frontend": frontend,
+        "traffic_source": "HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes "
+                          "(tools/pmc_traffic.sh, profiles/*_pmc_traffic.json; FETCH_SIZE doubled on gfx950)",
     }
     print(json.dumps(line), flush=True)
     if dist is not None:
