@@ -319,6 +319,54 @@ int sg_map_clean(sg_slam* s, sg_map* map, double error_threshold, int32_t* resul
  * *num_violations = points whose |h2^T E h1| exceeded 0.15. */
 int sg_map_apply_epipolar(sg_slam* s, sg_map* map, int32_t* num_violations);
 
+/* ------------------------------------------------------------------------------------------------
+ * Matcher::Track (matcher.h:20-26, matcher.cpp:301-405): the per-frame front end with its bookkeeping —
+ * live features (ordered by TrackedPoint id), up to four keyframe views whose pyramids stay resident on the
+ * device, FindMatches (matcher.cpp:210-271) batched over features on the device, the keyframe decision
+ * (< 40 matches), corner seeding of new points (AddNewFeatures + Unproject at 2000) and view expiry.
+ * The LocalMap stays the caller's: the library reads and grows it through these callbacks, which stand in
+ * for the reference's direct member access (each cites what it replaces).  Callbacks return 0 on success;
+ * a non-zero return aborts the call with SG_EINVAL.
+ */
+typedef struct sg_map_callbacks {
+  void* user;
+  /* Frame::rotation().coeffs() [x,y,z,w], translation(), camera()->k (localmap.h:129-132,159-160,30) */
+  int32_t (*frame_pose)(void* user, int32_t frame, double* q4, double* t3, double* k7);
+  /* TrackedPoint::location(), uncertainty(), feature_usable() (localmap.h:194-195,251,249) */
+  int32_t (*point_state)(void* user, int32_t point, double* X4, double* uncertainty, int32_t* feature_usable);
+  /* LocalMap::AddPoint(id, location) (localmap.cpp:103-109): NO_OBSERVATIONS | NO_BASELINE flags,
+   * uncertainty 1e8.  Writes the new point's handle to *point. */
+  int32_t (*add_point)(void* user, int32_t id, const double* X4, int32_t* point);
+  /* Frame::AddObservation(pt, point) (localmap.h:138-143) */
+  int32_t (*add_observation)(void* user, int32_t frame, double x, double y, int32_t point);
+  /* frame->is_keyframe_ = true (matcher.cpp:357) */
+  int32_t (*set_keyframe)(void* user, int32_t frame);
+  /* Matcher::Track's update_frames argument (may be NULL): *updated = its bool result */
+  int32_t (*update_frames)(void* user, int32_t* updated);
+} sg_map_callbacks;
+
+typedef struct sg_frontend_stats {
+  int32_t matches_first;   /* "Started with %d" (matcher.cpp:341) */
+  int32_t matches;         /* "grew to %d" */
+  int32_t keyframe;        /* 1 when the frame became a keyframe */
+  int32_t corners;         /* goodFeaturesToTrack corners on a keyframe */
+  int32_t added;           /* new features / points ("Added %d new features") */
+  int32_t features;        /* live features after the call */
+  int32_t views;           /* keyframe views after the call */
+  int32_t track_batches;   /* device tracking launches (FindMatches rounds x source views) */
+} sg_frontend_stats;
+
+typedef struct sg_frontend sg_frontend;
+/* o: tracker options (window 13, depth 6 for the reference's Matcher; NULL = defaults). */
+int sg_frontend_create(sg_frontend** out, const sg_tracker_options* o, const sg_device_options* dev);
+void sg_frontend_destroy(sg_frontend* f);
+/* Matcher::Track(img, frame, camera, map, update_frames): *result = the reference's bool (always 1). */
+int sg_frontend_track(sg_frontend* f, const uint8_t* bgr, int32_t width, int32_t height, int32_t stride,
+                      int32_t frame, int32_t camera, const sg_map_callbacks* cb, int32_t* result,
+                      sg_frontend_stats* stats);
+/* Live features: point handles and TrackedPoint ids in set order (ids ascending); n in/out = capacity/count. */
+int sg_frontend_features(sg_frontend* f, int32_t* points, int32_t* ids, int32_t* n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -199,6 +199,29 @@ class SgTrackerOptions(C.Structure):
 _fp = C.POINTER(C.c_float)
 _u8p = C.POINTER(C.c_uint8)
 
+# sg_map_callbacks (slamgpu.h): the LocalMap accessors Matcher::Track uses.
+FRAME_POSE_CB = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int32, _dp, _dp, _dp)
+POINT_STATE_CB = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int32, _dp, _dp, C.POINTER(C.c_int32))
+ADD_POINT_CB = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int32, _dp, C.POINTER(C.c_int32))
+ADD_OBS_CB = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int32, C.c_double, C.c_double, C.c_int32)
+SET_KEYFRAME_CB = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int32)
+UPDATE_FRAMES_CB = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.POINTER(C.c_int32))
+
+
+class SgMapCallbacks(C.Structure):
+    _fields_ = [("user", C.c_void_p), ("frame_pose", FRAME_POSE_CB), ("point_state", POINT_STATE_CB),
+                ("add_point", ADD_POINT_CB), ("add_observation", ADD_OBS_CB), ("set_keyframe", SET_KEYFRAME_CB),
+                ("update_frames", UPDATE_FRAMES_CB)]
+
+
+class SgFrontendStats(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("matches_first", "matches", "keyframe", "corners", "added", "features",
+                                         "views", "track_batches")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
 SYMBOLS = {
     "sg_version": (C.c_char_p, []),
     "sg_last_error": (C.c_char_p, []),
@@ -262,6 +285,11 @@ SYMBOLS = {
     "sg_slam_error": (C.c_double, [C.c_void_p]),
     "sg_slam_last_summary": (C.c_int, [C.c_void_p, C.POINTER(SgSolverSummary)]),
     "sg_slam_set_options": (C.c_int, [C.c_void_p, C.POINTER(SgSolverOptions)]),
+    "sg_frontend_create": (C.c_int, [C.POINTER(C.c_void_p), C.POINTER(SgTrackerOptions), C.POINTER(SgDeviceOptions)]),
+    "sg_frontend_destroy": (None, [C.c_void_p]),
+    "sg_frontend_track": (C.c_int, [C.c_void_p, _u8p, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                    C.POINTER(SgMapCallbacks), C.POINTER(C.c_int32), C.POINTER(SgFrontendStats)]),
+    "sg_frontend_features": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
 }
 
 

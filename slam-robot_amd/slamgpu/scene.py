@@ -105,6 +105,7 @@ class MapArrays:
     obs_point: np.ndarray      # [M] int32
     obs_disabled: np.ndarray   # [M] int32
     obs_error: np.ndarray      # [M*2]
+    frame_keyframe: np.ndarray = None   # [F] int32 Frame::is_keyframe_ (set by Matcher::Track)
     # ground truth (not part of the map)
     q_true: np.ndarray = None
     t_true: np.ndarray = None
