@@ -10,7 +10,8 @@
 //   V[P][10], g[P][4]              point normal-equation blocks (upper 4x4) and gradient
 //   Vinv[P][10], tp[P][4]          damped, scaled inverse and V^-1 g~ (per LM iteration)
 //   cam_slab / S_slab              per-chunk partial camera blocks / Schur window (deterministic reduce)
-//   S[n][n]                        dense reduced camera system (upper blocks), n = 6 * free frames
+//   S[n][n], xc[n]                 dense reduced camera system (upper blocks), n = 6 * free frames, and
+//                                  its rhs, contiguous (one all-reduce over landmark shards)
 #ifndef SG_BA_KERNELS_H_
 #define SG_BA_KERNELS_H_
 
@@ -146,8 +147,8 @@ struct Dev {
   double* cam_wide;              // [NB][27] (wide chunks, global atomics)
   double* S_wide;                // [n][n]   (wide chunks, global atomics)
   // exchange buffers (all-reduced across landmark shards)
-  double* xchg_cam;              // [NB*27 + kXNum]
-  double* xchg_max;              // [1]
+  double* xchg_cam;              // [NB*27 + kXNum + nranks]: camera blocks, scalars, per-rank max |g| slots
+  int32_t rank, nranks;          // landmark shard of this solver
   double* S;                     // [n][n] reduced system (upper blocks), then its factor
   double* rhs;                   // [n]
   double* xchg_upd;              // [kUNum]

@@ -42,6 +42,7 @@ class BaSolver {
   double ReprojectMap(sg_map* m);
 
   hipStream_t stream() const { return stream_; }
+  int nranks() const;
 
  private:
   sg_device_options dev_;
@@ -66,8 +67,8 @@ class BaSolver {
   // device buffers
   DBuf<LmState> st_;
   DBuf<double> k_, q_, t_, X_, obs_pt_, J_, V_, g_, scale_p_, diag_p_, Vinv_, tp_, scale_c_, diag_c_, camdiag_,
-      camg_, cam_slab_, S_slab_, chunk_scal_, cam_wide_, S_wide_, xchg_cam_, xchg_max_, S_, rhs_, xchg_upd_,
-      xchg_chol_, xc_, work_, fd_r_, fd_J_, fd_D_, fd_X_, red_;
+      camg_, cam_slab_, S_slab_, chunk_scal_, cam_wide_, S_wide_, xchg_cam_, S_, rhs_, xchg_upd_,
+      xchg_chol_, work_, fd_r_, fd_J_, fd_D_, fd_X_, red_;
   DBuf<int32_t> frame_cam_, frame_block_, poff_, obs_frame_, fd_a_, fd_b_, fd_boff_, fd_bidx_, cam_loff_,
       cam_lidx_, s_loff_, s_lidx_, r_loff_, r_lidx_, mobs_frame_, mobs_point_, mframe_cam_;
   DBuf<uint8_t> rot_free_, trans_free_, pfree_, obs_fixed_;
@@ -99,7 +100,6 @@ class BaSolver {
   void CollectTimes();
   Dev MakeDev();
   void AllReduceSum(double* buf, size_t n);
-  void AllReduceMax(double* buf, size_t n);
 };
 
 }  // namespace sg

@@ -473,7 +473,8 @@ __global__ __launch_bounds__(kRedThreads) void k_cam_reduce(Dev d) {
   if (tid == 0) {
 #pragma unroll
     for (int j = 0; j < kXNum; ++j) d.xchg_cam[nv + j] = v[j];
-    d.xchg_max[0] = gm;
+    // max |g| travels in the same sum all-reduce: one slot per rank, zeros in the others' slots
+    for (int r = 0; r < d.nranks; ++r) d.xchg_cam[nv + kXNum + r] = (r == d.rank) ? gm : 0.0;
   }
 }
 
@@ -569,7 +570,8 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d) {
       for (int i = 0; i < (int)blockDim.x; ++i) fd += fdcost[i];
       const double* xs = d.xchg_cam + nv;
       const double cost = xs[kXCost] + fd;
-      const double gmax = fmax(gm, d.xchg_max[0]);
+      double gmax = gm;
+      for (int r = 0; r < d.nranks; ++r) gmax = fmax(gmax, xs[kXNum + r]);
       if (st->first) {
         st->fixed_cost = xs[kXFixed];
         if (xs[kXFixedFail] > 0.0) {
@@ -1907,17 +1909,17 @@ BaSolver::~BaSolver() {
 void BaSolver::UniqueId(void* id128) { Comm::UniqueId(id128); }
 
 void BaSolver::CommInit(const void* id128, int nranks, int rank) {
+  SG_REQUIRE(!loaded_, SG_EINVAL, "sg_ba_comm_init must precede sg_ba_load (exchange buffers are sized by it)");
   SG_HIP_CHECK(hipSetDevice(dev_.device));
   comm_.reset(new Comm(id128, nranks, rank));
   dev_.nranks = nranks;
   dev_.rank = rank;
 }
 
+int BaSolver::nranks() const { return comm_ ? comm_->nranks() : 1; }
+
 void BaSolver::AllReduceSum(double* buf, size_t n) {
   if (comm_ && comm_->nranks() > 1) comm_->AllReduceSum(buf, n, stream_);
-}
-void BaSolver::AllReduceMax(double* buf, size_t n) {
-  if (comm_ && comm_->nranks() > 1) comm_->AllReduceMax(buf, n, stream_);
 }
 
 void BaSolver::Load(const sg_problem& p) {
@@ -2291,13 +2293,11 @@ void BaSolver::Load(const sg_problem& p) {
   chunk_scal_.Resize((size_t)std::max(nlin_, 1) * kNScal);
   cam_wide_.Resize((size_t)std::max(NB_, 1) * kCamV);
   S_wide_.Resize(nn * nn);
-  xchg_cam_.Resize((size_t)NB_ * kCamV + kXNum);
-  xchg_max_.Resize(1);
-  S_.Resize(nn * nn);
+  xchg_cam_.Resize((size_t)NB_ * kCamV + kXNum + nranks());
+  S_.Resize(nn * nn + nn);   // S, then the rhs partial xc: one all-reduce covers both
   rhs_.Resize(nn);
   xchg_upd_.Resize(kUNum);
   xchg_chol_.Resize(kCNum);
-  xc_.Resize(nn);
   work_.Resize(nn);
   fd_r_.Resize(std::max(D_, 1));
   fd_J_.Resize(6 * (size_t)std::max(D_, 1));
@@ -2388,12 +2388,13 @@ Dev BaSolver::MakeDev() {
   d.cam_wide = cam_wide_.ptr;
   d.S_wide = S_wide_.ptr;
   d.xchg_cam = xchg_cam_.ptr;
-  d.xchg_max = xchg_max_.ptr;
+  d.rank = comm_ ? comm_->rank() : 0;
+  d.nranks = nranks();
   d.S = S_.ptr;
   d.rhs = rhs_.ptr;
   d.xchg_upd = xchg_upd_.ptr;
   d.xchg_chol = xchg_chol_.ptr;
-  d.xc = xc_.ptr;
+  d.xc = S_.ptr + (size_t)n_ * n_;
   d.work = work_.ptr;
   d.stamps = stamp_on_ ? stamps_.ptr : nullptr;
   d.fd_pair = fd_pair_.ptr;
@@ -2481,8 +2482,7 @@ void BaSolver::Iterate(int n) {
     const int nv = NB_ * kCamV;
     hipLaunchKernelGGL(k_cam_reduce, dim3(NB_ + 1), dim3(kRedThreads), 0, stream_, d);
     TimedLaunchEnd(kKCamReduce);
-    AllReduceSum(xchg_cam_.ptr, (size_t)nv + kXNum);
-    AllReduceMax(xchg_max_.ptr, 1);
+    AllReduceSum(xchg_cam_.ptr, (size_t)nv + kXNum + nranks());
     TimedLaunchBegin(kKCamFinal);
     hipLaunchKernelGGL(k_cam_finalize, dim3(1), dim3(256), 0, stream_, d);
     TimedLaunchEnd(kKCamFinal);
@@ -2495,8 +2495,7 @@ void BaSolver::Iterate(int n) {
     TimedLaunchEnd(kKSReduce);
     if (comm_ && comm_->nranks() > 1) {
       // the upper blocks of S and the rhs partial are summed over landmark shards
-      AllReduceSum(S_.ptr, (size_t)n_ * n_);
-      AllReduceSum(xc_.ptr, (size_t)n_);
+      AllReduceSum(S_.ptr, (size_t)n_ * n_ + n_);
     }
     TimedLaunchBegin(kKChol);
     if (chol_window_ && d.stamps)
