@@ -939,6 +939,15 @@ __device__ __forceinline__ double& Wn(double* win, int i, int j) {
   return win[(i & (kCholWS - 1)) * kCholLd + (j & (kCholWS - 1))];
 }
 
+// 1/sqrt(x): v_rsq_f64 and one Newton step in FMA form, y (1.5 - x y^2 / 2) (relative error ~1e-14, far
+// inside the solver's parity tolerances; the pivot chain of the panel factorisation runs through it).
+__device__ __forceinline__ double rsq_nr1(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  const double h = 0.5 * x;
+  const double e = fma(-(h * y), y, 0.5);
+  return fma(y, e, y);
+}
+
 // Wave-uniform broadcast of lane `l`'s double (v_readlane pair: no LDS round trip).
 __device__ __forceinline__ double readlane_d(double v, int l) {
   const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
@@ -1129,22 +1138,22 @@ struct BsOps {
 };
 __device__ __forceinline__ void chol_bs_load(const double* Wm, const double* z, int n, const int* jend_sh, int pk,
                                              int wave, int lane, BsOps& o) {
-  if (pk < 0) {
-    o.jend = 0;
-    return;
-  }
-  const int kb = pk * kCholNb;
-  o.jend = jend_sh[pk];
+  // Branch-free: every call issues the same six global loads (clamped addresses; entries outside the band
+  // are masked at the use), so the compiler's vmcnt accounting stays exact and a panel step waits only on
+  // the loads issued kBsDepth steps earlier.
+  const bool pv = pk >= 0;
+  const int kb = (pv ? pk : 0) * kCholNb;
+  o.jend = pv ? jend_sh[pv ? pk : 0] : 0;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int r = kb + 2 * wave + h;
-    const bool rin = r < n;
+    const bool rin = pv && r < n;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int c = kb + kCholNb + lane + 64 * q;
-      o.w[h][q] = (rin && c < o.jend) ? Wm[(size_t)r * n + c] : 0.0;
+      o.w[h][q] = Wm[(rin && c < n) ? (size_t)r * n + c : 0];
     }
-    o.z[h] = rin ? z[r] : 0.0;
+    o.z[h] = z[rin ? r : 0];
   }
 }
 
@@ -1161,18 +1170,22 @@ __device__ __forceinline__ void chol_backsub_w(const double* Wm, const double* z
 #pragma unroll
     for (int s = 0; s < kBsDepth; ++s) {
       const int pk = base - s;   // workgroup-uniform
+      const BsOps cur = ring[s];
+      chol_bs_load(Wm, z, n, jend_sh, pk - kBsDepth, wave, lane, ring[s]);   // unconditional: exact vmcnt
       if (pk >= 0) {
-        const BsOps cur = ring[s];
-        chol_bs_load(Wm, z, n, jend_sh, pk - kBsDepth, wave, lane, ring[s]);
         const int kb = pk * kCholNb;
         double sv[2];
+        double xv[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) xv[q] = xs[kb + kCholNb + lane + 64 * q];   // in the LDS window: valid
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           double acc = 0.0;
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
             const int c = kb + kCholNb + lane + 64 * q;
-            acc += cur.w[h][q] * (c < cur.jend ? xs[c] : 0.0);
+            const bool in = c < cur.jend;
+            acc += (in ? cur.w[h][q] : 0.0) * (in ? xv[q] : 0.0);
           }
           sv[h] = wave_sum_full(acc);
         }
@@ -1202,16 +1215,35 @@ __device__ __forceinline__ void chol_panel_w(const double* win, const double* u1
   const int c = kb + kCholNb + wi;
   if (!(wi < nc || isz)) return;
   double t[kCholNb];
+  // unconditional loads from a lane-selected address (window column or the panel rhs), all in flight
+  // together: per-lane branches here serialise 16 LDS round trips on the critical path of phase (a)
+  const double* base = isz ? ypan : win + (c & (kCholWS - 1));
 #pragma unroll
-  for (int r = 0; r < kCholNb; ++r) {
-    const double wv = Wn(const_cast<double*>(win), kb + r, c), yr = ypan[r];
-    t[r] = isz ? yr : (r < w ? wv : 0.0);
+  for (int r = 0; r < kCholNb; ++r) t[r] = base[isz ? r : ((kb + r) & (kCholWS - 1)) * kCholLd];
+  // U11 columns (rows above the diagonal) and 1/U_kk stream through a 3-deep register ring, column k-2
+  // issued before step k's FMAs (scheduling barriers keep the loads ahead of their use)
+  double cb[3][kCholNb], pb[3];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int k = kCholNb - 1 - q;
+#pragma unroll
+    for (int r = 0; r < k; ++r) cb[k % 3][r] = u11[k * kCholNb + r];
+    pb[k % 3] = pinv[k];
   }
 #pragma unroll
-  for (int k = kCholNb - 1; k >= 0; --k) {
-    t[k] *= pinv[k];
+  for (int r = 0; r < kCholNb; ++r) t[r] = (isz || r < w) ? t[r] : 0.0;
 #pragma unroll
-    for (int r = 0; r < k; ++r) t[r] -= u11[k * kCholNb + r] * t[k];
+  for (int k = kCholNb - 1; k >= 0; --k) {
+    if (k >= 2) {
+#pragma unroll
+      for (int r = 0; r < k - 2; ++r) cb[(k - 2) % 3][r] = u11[(k - 2) * kCholNb + r];
+      pb[(k - 2) % 3] = pinv[k - 2];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    t[k] *= pb[k % 3];
+#pragma unroll
+    for (int r = 0; r < k; ++r) t[r] = fma(-cb[k % 3][r], t[k], t[r]);
+    __builtin_amdgcn_sched_barrier(0);
   }
   if (isz) {
 #pragma unroll
@@ -1238,7 +1270,7 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
   if (st->done) return;
   extern __shared__ double win[];
   __shared__ double yw[kCholWS];
-  __shared__ double prow[kPanelWaves][kCholNb];
+  __shared__ double prow[kPanelWaves][2 * kCholNb];   // per panel wave: the next two pivot rows
   __shared__ double pinv[2][kCholNb];                 // 1/U_jj of the current / previous panel
   __shared__ double u11w[2][kCholNb * kCholNb];       // U11 columns of the current / previous panel
   __shared__ double ypan[2][kCholNb];                 // forward-substituted rhs of the panel rows
@@ -1302,45 +1334,81 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
       const bool isy = slot == kCholWS;   // the rhs rides as an augmented column in an otherwise idle lane
       double* prw = prow[wave];
       double ca[kCholNb];
+      // one unconditional LDS load per row from a lane-selected address (window column or rhs ring), all
+      // issued before the first use: per-lane branches here would serialise 16 LDS round trips
+      const double* col0 = isy ? &yw[0] : &Wn(win, 0, c);
+      const int rstride = isy ? 1 : kCholLd;
+#pragma unroll
+      for (int r = 0; r < kCholNb; ++r) ca[r] = col0[((kb + r) & (kCholWS - 1)) * rstride];
+#pragma unroll
+      for (int r = 0; r < kCholNb; ++r) asm volatile("" : "+v"(ca[r]));
 #pragma unroll
       for (int r = 0; r < kCholNb; ++r) {
         const bool real = r < w;
-        const double wv = Wn(win, kb + r, c), yr = yw[(kb + r) & (kCholWS - 1)];   // unconditional loads
-        ca[r] = isy ? (real ? yr : 0.0)
-                    : ((real && v && r <= slot) ? wv : ((!real && slot == r) ? 1.0 : 0.0));
+        ca[r] = isy ? (real ? ca[r] : 0.0)
+                    : ((real && v && r <= slot) ? ca[r] : ((!real && slot == r) ? 1.0 : 0.0));
       }
       bool bad = false;
       SG_STAMP_AT(1)
-      // Right-looking steps: row j is scaled by 1/U_jj and every column entry below it updated with
-      // A[r][c] -= U[j][r] U[j][c] = A[j][r] (U[j][c] / U_jj) (one FMA per entry).  The pivot-row broadcast is
-      // software-pipelined: step j updates row j+1 first and posts it to the LDS row, then applies the rest
-      // of its updates while that write / read round trip is in flight.
-      double u[kCholNb];
-      if (lane < kCholNb) prw[lane] = ca[0];
+      // Right-looking steps, two pivots per LDS broadcast: rows j and j+1 of the diagonal block arrive
+      // together; every lane derives row j+1 after pivot j itself (wave-uniform values, 14 FMAs) instead of
+      // waiting for a second round trip.  Pivot j scales row j by 1/U_jj and updates every entry below with
+      // A[r][c] -= A[j][r] (A[j][c] / A_jj) (one FMA per entry); pivot j+1 likewise.  Rows j+2 and j+3 are
+      // updated first and posted while the remaining updates run.
+      double u0[kCholNb], u1[kCholNb];
+      double* prw2 = prw + kCholNb;
+      if (lane < kCholNb) {
+        prw[lane] = ca[0];
+        prw2[lane] = ca[1];
+      }
 #pragma unroll
-      for (int r = 0; r < kCholNb; ++r) u[r] = prw[r];
+      for (int r = 0; r < kCholNb; ++r) {
+        u0[r] = prw[r];
+        u1[r] = prw2[r];
+      }
 #pragma unroll
-      for (int j = 0; j < kCholNb; ++j) {
-        const double piv = u[j];
-        bad |= !(piv > 0.0);
-        double inv = __builtin_amdgcn_rsq(piv);
-        inv = inv * (1.5 - 0.5 * piv * inv * inv);   // two Newton steps: full fp64 1/sqrt
-        inv = inv * (1.5 - 0.5 * piv * inv * inv);
-        ca[j] *= inv;
-        const double t = ca[j] * inv;
-        if (wave == 0 && lane == 0) pinv[buf][j] = inv;
-        if (j + 1 < kCholNb) {
-          ca[j + 1] = fma(-u[j + 1], t, ca[j + 1]);
-          if (lane < kCholNb) prw[lane] = ca[j + 1];   // the next pivot row
+      for (int j = 0; j < kCholNb; j += 2) {
+        const double p0 = u0[j];
+        bad |= !(p0 > 0.0);
+        const double i0 = rsq_nr1(p0);
+        const double r0 = i0 * i0;                       // 1 / A_jj
+        const double w1 = u0[j + 1] * r0;
+        double v1[kCholNb];                              // row j+1 after pivot j
+#pragma unroll
+        for (int r = j + 1; r < kCholNb; ++r) v1[r] = fma(-w1, u0[r], u1[r]);
+        const double p1 = v1[j + 1];
+        bad |= !(p1 > 0.0);
+        const double i1 = rsq_nr1(p1);
+        const double r1 = i1 * i1;
+        const double aj = ca[j];
+        const double t0 = aj * r0;
+        ca[j] = aj * i0;
+        const double aj1 = fma(-u0[j + 1], t0, ca[j + 1]);
+        const double t1 = aj1 * r1;
+        ca[j + 1] = aj1 * i1;
+        if (wave == 0 && lane == 0) {
+          pinv[buf][j] = i0;
+          pinv[buf][j + 1] = i1;
+        }
+        if (j + 2 < kCholNb) {
+          ca[j + 2] = fma(-v1[j + 2], t1, fma(-u0[j + 2], t0, ca[j + 2]));
+          ca[j + 3] = fma(-v1[j + 3], t1, fma(-u0[j + 3], t0, ca[j + 3]));
+          if (lane < kCholNb) {                          // the next two pivot rows
+            prw[lane] = ca[j + 2];
+            prw2[lane] = ca[j + 3];
+          }
         }
 #pragma unroll
-        for (int r = j + 2; r < kCholNb; ++r) ca[r] = fma(-u[r], t, ca[r]);
+        for (int r = j + 4; r < kCholNb; ++r) ca[r] = fma(-v1[r], t1, fma(-u0[r], t0, ca[r]));
         // materialise this step's updates here (otherwise they are sunk into later steps and spill)
 #pragma unroll
         for (int r = j; r < kCholNb; ++r) asm volatile("" : "+v"(ca[r]));
-        if (j + 1 < kCholNb) {
+        if (j + 2 < kCholNb) {
 #pragma unroll
-          for (int r = j + 1; r < kCholNb; ++r) u[r] = prw[r];
+          for (int r = j + 2; r < kCholNb; ++r) {
+            u0[r] = prw[r];
+            u1[r] = prw2[r];
+          }
         }
       }
       SG_STAMP_AT(3)
@@ -2206,6 +2274,19 @@ void BaSolver::Load(const sg_problem& p) {
         lo_blk[hi3] = std::min(lo_blk[hi3], lo3);
       }
     }
+  }
+  // Landmark shards: S is summed over every rank's points, so each rank must factor it with the envelope of
+  // the whole problem (the union of the shards' envelopes), not of its own points.  One max all-reduce of
+  // -lo(J) at load time.
+  if (comm_ && comm_->nranks() > 1 && NB_ > 0) {
+    std::vector<double> neg(NB_);
+    for (int b = 0; b < NB_; ++b) neg[b] = -(double)lo_blk[b];
+    DBuf<double> env;
+    env.Upload(neg, stream_);
+    comm_->AllReduceMax(env.ptr, (size_t)NB_, stream_);
+    SG_HIP_CHECK(hipMemcpyAsync(neg.data(), env.ptr, NB_ * sizeof(double), hipMemcpyDeviceToHost, stream_));
+    SG_HIP_CHECK(hipStreamSynchronize(stream_));
+    for (int b = 0; b < NB_; ++b) lo_blk[b] = (int)(-neg[b]);
   }
   const int npanel = (n_ + kCholNb - 1) / kCholNb;
   std::vector<int32_t> panel_jmax(std::max(npanel, 1), 0);
