@@ -1124,7 +1124,7 @@ __device__ __forceinline__ void chol_candidates(const Dev& d, const double* y, i
   }
 #define SG_STAMP_FLUSH()                                                         \
   if (kStamp && threadIdx.x == 0) {                                               \
-    for (int s_ = 0; s_ < 8; ++s_) d.stamps[s_] += stamp_acc[s_];                 \
+    for (int s_ = 0; s_ < 12; ++s_) d.stamps[s_] += stamp_acc[s_];                 \
   }
 
 // Back substitution of the window path from x_p = z_p - W_p x_rest (W = U11^-1 U12 and z = U11^-1 y per
@@ -1265,7 +1265,7 @@ __device__ __forceinline__ void chol_panel_w(const double* win, const double* u1
 template <bool kStamp>
 __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const int32_t* panel_jend, double* rdg) {
   unsigned long long last_stamp = kStamp ? __builtin_amdgcn_s_memtime() : 0ull;
-  unsigned long long stamp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long stamp_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   LmState* st = d.st;
   if (st->done) return;
   extern __shared__ double win[];
@@ -1497,9 +1497,12 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
     chol_panel_w(win, u11w[pb & 1], pinv[pb & 1], ypan[pb & 1], pb * kCholNb, min(kCholNb, n - pb * kCholNb),
                  jend_sh[pb], n, (wave - kPanelWaves) * 64 + lane, d.S, y);
   }
+  SG_STAMP_AT(8)
   __syncthreads();   // global W rows / z visible to every wave
+  SG_STAMP_AT(9)
   double* xs = win;  // the window is free now: the solution lives in LDS
   chol_backsub_w(d.S, y, xs, n, jend_sh, panel_jend);
+  SG_STAMP_AT(10)
   for (int i = tid; i < n; i += kCholThreads) {
     d.xc[i] = xs[i];
     y[i] = xs[i];

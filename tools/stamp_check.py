@@ -17,8 +17,9 @@ g.iterate(N); g.sync()
 buf = (C.c_ulonglong * 64)()
 g.lib.sg_ba_debug_stamps.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
 g.lib.sg_ba_debug_stamps(g.h, buf, 64)
-names = ["initial window load", "prefetch+panel load", "panel stores+barrier", "panel factor loop", "trailing update", "slide", "backsub", "candidates"]
-tot = sum(buf[i] for i in range(8))
+names = ["initial window load", "prefetch+panel load", "panel stores+barrier", "panel factor loop", "trailing update",
+         "slide", "xc/y stores+sync", "candidates", "last W pass", "W sync", "backsub loop"]
+tot = sum(buf[i] for i in range(len(names)))
 for i, n in enumerate(names):
     print("%-18s %10.0f cycles/iter  (%4.1f%%)" % (n, buf[i] / N, 100.0 * buf[i] / max(tot, 1)))
 print("total %.0f cycles/iter" % (tot / N))
