@@ -1124,41 +1124,45 @@ __device__ __forceinline__ void chol_candidates(const Dev& d, const double* y, i
   }
 #define SG_STAMP_FLUSH()                                                         \
   if (kStamp && threadIdx.x == 0) {                                               \
-    for (int s_ = 0; s_ < 12; ++s_) d.stamps[s_] += stamp_acc[s_];                 \
+    for (int s_ = 0; s_ < 16; ++s_) d.stamps[s_] += stamp_acc[s_];                 \
   }
 
 // Back substitution of the window path from x_p = z_p - W_p x_rest (W = U11^-1 U12 and z = U11^-1 y per
 // panel, stored over the U rows of A and over y): one mat-vec per panel, two rows per wave.  The operands of
 // the next kBsDepth panels are in flight in registers (a ring, statically indexed by an unrolled loop), so
 // a panel step waits on LDS and the DPP reduction, not on a global load.
-constexpr int kBsDepth = 8;
+#ifndef SG_BS_DEPTH
+#define SG_BS_DEPTH 4   // measured best of 4 / 8 / 12 (fewer loads queued per wave)
+#endif
+constexpr int kBsDepth = SG_BS_DEPTH;
 struct BsOps {
-  double w[2][2], z[2];
+  double2 w[2];   // rows kb + 2 wave + h, columns kb + 16 + 2 lane + {0, 1}
+  double2 z;      // z of the two rows
   int jend;
 };
 __device__ __forceinline__ void chol_bs_load(const double* Wm, const double* z, int n, const int* jend_sh, int pk,
                                              int wave, int lane, BsOps& o) {
-  // Branch-free: every call issues the same six global loads (clamped addresses; entries outside the band
-  // are masked at the use), so the compiler's vmcnt accounting stays exact and a panel step waits only on
-  // the loads issued kBsDepth steps earlier.
+  // Branch-free 16-byte loads: every call issues the same three global loads (clamped addresses; entries
+  // outside the band are masked at the use), so the compiler's vmcnt accounting stays exact and a panel
+  // step waits only on the loads issued kBsDepth steps earlier.  n = 6 x blocks and kb are even, so a
+  // column pair never straddles n or the (16-aligned) band end.
   const bool pv = pk >= 0;
   const int kb = (pv ? pk : 0) * kCholNb;
   o.jend = pv ? jend_sh[pv ? pk : 0] : 0;
+  const int r0 = kb + 2 * wave;
+  const int c = kb + kCholNb + 2 * lane;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    const int r = kb + 2 * wave + h;
-    const bool rin = pv && r < n;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int c = kb + kCholNb + lane + 64 * q;
-      o.w[h][q] = Wm[(rin && c < n) ? (size_t)r * n + c : 0];
-    }
-    o.z[h] = z[rin ? r : 0];
+    const bool rin = pv && r0 + h < n;
+    o.w[h] = *reinterpret_cast<const double2*>(Wm + ((rin && c < n) ? (size_t)(r0 + h) * n + c : 0));
   }
+  o.z = *reinterpret_cast<const double2*>(z + ((pv && r0 < n) ? r0 : 0));
 }
 
+template <bool kStamp>
 __device__ __forceinline__ void chol_backsub_w(const double* Wm, const double* z, double* xs, int n,
-                                               const int* jend_sh, const int32_t* panel_jend) {
+                                               const int* jend_sh, const int32_t* panel_jend,
+                                               unsigned long long (&stamp_acc)[16], unsigned long long& last_stamp) {
   (void)panel_jend;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   static_assert(kCholThreads / 64 * 2 == kCholNb, "two panel rows per wave");
@@ -1174,27 +1178,24 @@ __device__ __forceinline__ void chol_backsub_w(const double* Wm, const double* z
       chol_bs_load(Wm, z, n, jend_sh, pk - kBsDepth, wave, lane, ring[s]);   // unconditional: exact vmcnt
       if (pk >= 0) {
         const int kb = pk * kCholNb;
+        const int c = kb + kCholNb + 2 * lane;
+        const double2 xv = *reinterpret_cast<const double2*>(xs + c);   // inside the LDS window
+        const bool in = c < cur.jend;
         double sv[2];
-        double xv[2];
-#pragma unroll
-        for (int q = 0; q < 2; ++q) xv[q] = xs[kb + kCholNb + lane + 64 * q];   // in the LDS window: valid
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          double acc = 0.0;
-#pragma unroll
-          for (int q = 0; q < 2; ++q) {
-            const int c = kb + kCholNb + lane + 64 * q;
-            const bool in = c < cur.jend;
-            acc += (in ? cur.w[h][q] : 0.0) * (in ? xv[q] : 0.0);
-          }
+          const double acc = (in ? cur.w[h].x : 0.0) * (in ? xv.x : 0.0) + (in ? cur.w[h].y : 0.0) * (in ? xv.y : 0.0);
+          if (h == 0) { SG_STAMP_AT(11) }
           sv[h] = wave_sum_full(acc);
         }
+        SG_STAMP_AT(12)
         if (lane == 0) {
-#pragma unroll
-          for (int h = 0; h < 2; ++h)
-            if (kb + 2 * wave + h < n) xs[kb + 2 * wave + h] = cur.z[h] - sv[h];
+          const int r0 = kb + 2 * wave;
+          if (r0 < n) xs[r0] = cur.z.x - sv[0];
+          if (r0 + 1 < n) xs[r0 + 1] = cur.z.y - sv[1];
         }
         lds_barrier();
+        SG_STAMP_AT(13)
       }
     }
   }
@@ -1265,7 +1266,7 @@ __device__ __forceinline__ void chol_panel_w(const double* win, const double* u1
 template <bool kStamp>
 __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const int32_t* panel_jend, double* rdg) {
   unsigned long long last_stamp = kStamp ? __builtin_amdgcn_s_memtime() : 0ull;
-  unsigned long long stamp_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long stamp_acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   LmState* st = d.st;
   if (st->done) return;
   extern __shared__ double win[];
@@ -1320,6 +1321,7 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
       pf[q] = d.S[in ? (size_t)i * n + j : 0];   // branch-free: the loads stay in flight across phases
     }
     const double pfy = d.xc[min(jn0 + tid, n - 1)];   // rhs entries of the incoming rows (unmodified yet)
+    SG_STAMP_AT(14)
     // (a) panel factorisation by kPanelWaves waves: rows kb..kb+15 of the band.  Every panel wave holds
     // the 16 diagonal-block columns in lanes 0..15 (factored redundantly, so no cross-wave sync) and 48
     // off-diagonal columns in lanes 16..63; the diagonal block, the TRSM of the off-diagonal columns and
@@ -1342,6 +1344,7 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
       for (int r = 0; r < kCholNb; ++r) ca[r] = col0[((kb + r) & (kCholWS - 1)) * rstride];
 #pragma unroll
       for (int r = 0; r < kCholNb; ++r) asm volatile("" : "+v"(ca[r]));
+      SG_STAMP_AT(15)
 #pragma unroll
       for (int r = 0; r < kCholNb; ++r) {
         const bool real = r < w;
@@ -1501,7 +1504,7 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
   __syncthreads();   // global W rows / z visible to every wave
   SG_STAMP_AT(9)
   double* xs = win;  // the window is free now: the solution lives in LDS
-  chol_backsub_w(d.S, y, xs, n, jend_sh, panel_jend);
+  chol_backsub_w<kStamp>(d.S, y, xs, n, jend_sh, panel_jend, stamp_acc, last_stamp);
   SG_STAMP_AT(10)
   for (int i = tid; i < n; i += kCholThreads) {
     d.xc[i] = xs[i];

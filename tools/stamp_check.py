@@ -18,7 +18,8 @@ buf = (C.c_ulonglong * 64)()
 g.lib.sg_ba_debug_stamps.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
 g.lib.sg_ba_debug_stamps(g.h, buf, 64)
 names = ["initial window load", "prefetch+panel load", "panel stores+barrier", "panel factor loop", "trailing update",
-         "slide", "xc/y stores+sync", "candidates", "last W pass", "W sync", "backsub loop"]
+         "slide", "xc/y stores+sync", "candidates", "last W pass", "W sync", "backsub loop rest",
+         "bs load wait+fma", "bs dpp reduce", "bs store+barrier", "loop head+prefetch issue", "panel column loads"]
 tot = sum(buf[i] for i in range(len(names)))
 for i, n in enumerate(names):
     print("%-18s %10.0f cycles/iter  (%4.1f%%)" % (n, buf[i] / N, 100.0 * buf[i] / max(tot, 1)))
