@@ -1345,11 +1345,24 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
 #pragma unroll
       for (int r = 0; r < kCholNb; ++r) asm volatile("" : "+v"(ca[r]));
       SG_STAMP_AT(15)
+      // Row selection as per-lane bit sets (bit r: keep row r / identity-pad row r), applied with opaque
+      // v_bfe_i32 masks: written as selects, the compiler turns this into 16 divergent branches (~2k cycles).
+      {
+        const unsigned real_rows = (w >= kCholNb) ? 0xFFFFu : ((1u << w) - 1u);
+        const unsigned upto = slot >= kCholNb - 1 ? 0xFFFFu : ((2u << slot) - 1u);   // rows r <= slot
+        unsigned keepbits = isy ? real_rows : (v ? (real_rows & upto) : 0u);
+        unsigned onebits = (!isy && slot < kCholNb && slot >= w) ? (1u << slot) : 0u;
+        asm volatile("" : "+v"(keepbits), "+v"(onebits));
+        const unsigned long long kOneBits = 0x3FF0000000000000ull;
 #pragma unroll
-      for (int r = 0; r < kCholNb; ++r) {
-        const bool real = r < w;
-        ca[r] = isy ? (real ? ca[r] : 0.0)
-                    : ((real && v && r <= slot) ? ca[r] : ((!real && slot == r) ? 1.0 : 0.0));
+        for (int r = 0; r < kCholNb; ++r) {
+          int km, om;
+          asm volatile("v_bfe_i32 %0, %1, %2, 1" : "=v"(km) : "v"(keepbits), "n"(r));
+          asm volatile("v_bfe_i32 %0, %1, %2, 1" : "=v"(om) : "v"(onebits), "n"(r));
+          const unsigned long long b = (unsigned long long)__double_as_longlong(ca[r]);
+          ca[r] = __longlong_as_double((long long)((b & (unsigned long long)(long long)km) |
+                                                   (kOneBits & (unsigned long long)(long long)om)));
+        }
       }
       bool bad = false;
       SG_STAMP_AT(1)
