@@ -1430,10 +1430,13 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
       SG_STAMP_AT(3)
       // trailing columns' panel rows -> LDS; the panel's U11 and 1/U_jj (wave 0) and forward-substituted rhs
       // (the rhs lane) for the W / z pass and the trailing rhs update
+      // (one divergent region per destination; rows r >= w of the last panel land in ring slots of retired
+      // rows below the previous panel, which nothing reads again)
       const bool trail = v && lane >= kCholNb;
+      if (trail) {
 #pragma unroll
-      for (int r = 0; r < kCholNb; ++r)
-        if (r < w && trail) Wn(win, kb + r, c) = ca[r];
+        for (int r = 0; r < kCholNb; ++r) Wn(win, kb + r, c) = ca[r];
+      }
       if (isy) {
 #pragma unroll
         for (int r = 0; r < kCholNb; ++r) ypan[buf][r] = ca[r];
