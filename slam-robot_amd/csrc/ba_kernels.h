@@ -41,9 +41,15 @@ enum CholX { kCStep2 = 0, kCCandX2, kCModel, kCCandCost, kCFail, kCNum };
 
 // Schur work unit: up to kSegPts consecutive points (device order) sharing a window of <= kSegNbMax
 // camera blocks (or one "wide" point), with its slice of the observation-pair list.
-constexpr int kSegPts = 32;
-constexpr int kSegObsCap = 256;
-constexpr int kSegNbMax = 20;
+#ifndef SG_SEG_NB
+#define SG_SEG_NB 24   // cap of the per-load window width (the widest point, see BaSolver::Load)
+#endif
+#ifndef SG_SEG_PTS
+#define SG_SEG_PTS 32
+#endif
+constexpr int kSegPts = SG_SEG_PTS;
+constexpr int kSegObsCap = 8 * SG_SEG_PTS;
+constexpr int kSegNbMax = SG_SEG_NB;
 struct SchurSeg {
   int32_t p0, p1;       // point range
   int32_t b_lo, nb;     // window [b_lo, b_lo + nb)
