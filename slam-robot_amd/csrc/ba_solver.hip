@@ -837,27 +837,8 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d) {
 // The camera-camera terms of the damped reduced system that do not come from the Schur complement:
 // blockdiag(U) (observation Jacobians) + FrameDistance diagonal and cross blocks + D^2 = diag/radius,
 // all Jacobi-scaled, for element (6I+a, 6J+c), J >= I.
-__device__ __forceinline__ double assembly_term(const Dev& d, int I, int J, int a, int c, double radius) {
-  const int i = 6 * I + a, j = 6 * J + c;
-  double v = 0.0;
-  if (I == J) {
-    if (c < a) return 0.0;   // lower triangle of a diagonal block is never read
-    v = d.xchg_cam[(size_t)I * kCamV + u6(a, c)];
-    if (a >= 3) v += d.fd_D[9 * I + 3 * (a - 3) + (c - 3)];
-    v *= d.scale_c[i] * d.scale_c[j];
-    if (a == c) v += d.diag_c[i] / radius;
-  } else if (a >= 3 && c >= 3) {
-    const int dd = d.fd_pair[I * d.NB + J];
-    if (dd >= 0) {
-      const double* Xd = d.fd_X + 9 * dd;   // J_a J_b^T, rows: frame a's translation
-      const bool a_is_i = d.frame_block[d.fd_a[dd]] == I;
-      v = (a_is_i ? Xd[3 * (a - 3) + (c - 3)] : Xd[3 * (c - 3) + (a - 3)]) * d.scale_c[i] * d.scale_c[j];
-    }
-  }
-  return v;
-}
 
-// k_S_reduce: the assembling rank also adds assembly_term and the S g_c part of the rhs, so S leaves
+// k_S_reduce: the assembling rank also adds the camera-only terms and the S g_c part of the rhs, so S leaves
 // here damped.
 // One wave per block pair (I <= J) of S, then one wave per rhs block: the wave loads up to 64 slab offsets
 // of its partial list at once and walks them in list order (deterministic), lanes 0..35 (0..5 for the rhs)
@@ -866,7 +847,8 @@ __global__ __launch_bounds__(256) void k_S_reduce(Dev d) {
   const LmState* st = d.st;
   if (st->done) return;
   const int lane = threadIdx.x & 63;
-  const int wv = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int part = threadIdx.x >> 6;   // the four waves of a workgroup split one block's partial list
+  const int wv = blockIdx.x;
   const int npb = d.NB * (d.NB + 1) / 2;
   if (wv >= npb + d.NB) return;
   const bool is_rhs = wv >= npb;
@@ -888,13 +870,46 @@ __global__ __launch_bounds__(256) void k_S_reduce(Dev d) {
   }
   const int ne = is_rhs ? 6 : 36;
   const int el = lane < ne ? lane : 0;
-  // partials in list order; the next 64 offsets and kSR partial loads are in flight at a time
+  // Epilogue operands first (independent of the partials), so their round trips overlap the walk below:
+  // the wide-segment accumulator, and on the assembling rank blockdiag(U) + FrameDistance + damping (the
+  // assembly of slam.cpp's camera-only terms, Jacobi-scaled) or the S g_c part of the rhs.
+  const int a = el / 6, c = el % 6;
+  const int ei = is_rhs ? 6 * I + el : 6 * I + a, ej = 6 * Jb + c;
+  const size_t gi = (size_t)ei * d.n + ej;
+  const double radius = st->radius;
+  const double e_acc = is_rhs ? d.rhs[ei] : d.S_wide[gi];
+  double e_si = 0.0, e_sj = 0.0, e_u = 0.0, e_fd = 0.0, e_dg = 0.0, e_g = 0.0, e_x0 = 0.0, e_x1 = 0.0;
+  int e_dd = -1, e_blk = -1;
+  if (d.assemble) {
+    e_si = d.scale_c[ei];
+    if (is_rhs) {
+      e_g = d.camg[ei];
+    } else {
+      e_sj = d.scale_c[ej];
+      if (I == Jb) {
+        e_u = d.xchg_cam[(size_t)I * kCamV + u6(min(a, c), max(a, c))];
+        e_fd = (a >= 3 && c >= 3) ? d.fd_D[9 * I + 3 * (a - 3) + (c - 3)] : 0.0;
+        e_dg = d.diag_c[ei];
+      } else if (a >= 3 && c >= 3) {
+        e_dd = d.fd_pair[I * d.NB + Jb];
+        if (e_dd >= 0) {
+          const double* Xd = d.fd_X + 9 * e_dd;   // J_a J_b^T, rows: frame a's translation
+          e_x0 = Xd[3 * (a - 3) + (c - 3)];
+          e_x1 = Xd[3 * (c - 3) + (a - 3)];
+          e_blk = d.frame_block[d.fd_a[e_dd]];
+        }
+      }
+    }
+  }
+  // Wave `part` sums every fourth 64-entry chunk of the list (in list order), kSR partial loads in flight;
+  // the four wave sums are combined in wave order (deterministic).
   constexpr int kSR = 32;
+  __shared__ double wsum[4][36];
   double s = 0.0;
-  int myoff = (j0 + lane < j1) ? lidx[j0 + lane] : 0;
-  for (int base = j0; base < j1; base += 64) {
+  int myoff = lidx[(j0 + 64 * part + lane < j1) ? j0 + 64 * part + lane : 0];
+  for (int base = j0 + 64 * part; base < j1; base += 256) {
     const int cnt = min(64, j1 - base);
-    const int nxt = (base + 64 + lane < j1) ? lidx[base + 64 + lane] : 0;
+    const int nxt = lidx[(base + 256 + lane < j1) ? base + 256 + lane : 0];
     for (int k = 0; k < cnt; k += kSR) {
       double v[kSR];
 #pragma unroll
@@ -905,20 +920,30 @@ __global__ __launch_bounds__(256) void k_S_reduce(Dev d) {
     }
     myoff = nxt;
   }
-  if (lane >= ne) return;
+  if (lane < ne) wsum[part][lane] = s;
+  __syncthreads();
+  if (part != 0 || lane >= ne) return;
+  s = ((wsum[0][lane] + wsum[1][lane]) + wsum[2][lane]) + wsum[3][lane];
+  s += e_acc;
   if (!is_rhs) {
-    const int a = lane / 6, c = lane % 6;
-    const size_t gi = (size_t)(6 * I + a) * d.n + 6 * Jb + c;
-    s += d.S_wide[gi];
     d.S_wide[gi] = 0.0;
-    if (d.assemble) s += assembly_term(d, I, Jb, a, c, st->radius);
+    if (d.assemble) {   // assembly_term, from the prefetched operands
+      double v = 0.0;
+      if (I == Jb) {
+        if (c >= a) {
+          v = (e_u + e_fd) * (e_si * e_sj);
+          if (a == c) v += e_dg / radius;
+        }
+      } else if (e_dd >= 0) {
+        v = (e_blk == I ? e_x0 : e_x1) * e_si * e_sj;
+      }
+      s += v;
+    }
     d.S[gi] = s;
   } else {
-    const int e = 6 * I + lane;
-    s += d.rhs[e];   // wide-segment atomics
-    if (d.assemble) s += d.scale_c[e] * d.camg[e];   // y = rhs_sub + S g_c
-    d.xc[e] = s;       // local rhs partial (all-reduced with S); the wide accumulator is reset
-    d.rhs[e] = 0.0;
+    if (d.assemble) s += e_si * e_g;   // y = rhs_sub + S g_c
+    d.xc[ei] = s;       // local rhs partial (all-reduced with S); the wide accumulator is reset
+    d.rhs[ei] = 0.0;
   }
 }
 
@@ -2600,7 +2625,7 @@ void BaSolver::Iterate(int n) {
     TimedLaunchEnd(kKSchur);
     TimedLaunchBegin(kKSReduce);
     const int nwv = NB_ * (NB_ + 1) / 2 + NB_;
-    hipLaunchKernelGGL(k_S_reduce, dim3(std::max((nwv + 3) / 4, 1)), dim3(256), 0, stream_, d);
+    hipLaunchKernelGGL(k_S_reduce, dim3(std::max(nwv, 1)), dim3(256), 0, stream_, d);
     TimedLaunchEnd(kKSReduce);
     if (comm_ && comm_->nranks() > 1) {
       // the upper blocks of S and the rhs partial are summed over landmark shards
