@@ -149,7 +149,7 @@ struct Dev {
   const int32_t* r_lidx;
   double* cam_slab;
   double* S_slab;
-  double* chunk_scal;            // [nlin][kNScal] k_point_update scalars
+  double* chunk_scal;            // [npu][kNScal] k_point_update scalars (per work unit)
   double* cam_wide;              // [NB][27] (wide chunks, global atomics)
   double* S_wide;                // [n][n]   (wide chunks, global atomics)
   // exchange buffers (all-reduced across landmark shards)
@@ -170,6 +170,8 @@ struct Dev {
   const uint16_t* llist;         // per round: window-block offsets + local observation indices by block
   int32_t nlin;
   double* lin_scal;              // [nlin][kNScal] k_linearize scalars (cost, failures, |x|^2, max |g|)
+  const int32_t* pu_units;       // [npu] k_point_update work units: round index, or -(chunk + 1) (wide chunk)
+  int32_t npu;
   const struct SchurSeg* segs;   // [nseg] Schur work units
   int32_t nseg;
   double* seg_fail;              // [nseg] point blocks whose damped inverse failed

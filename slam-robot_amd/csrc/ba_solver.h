@@ -74,6 +74,7 @@ class BaSolver {
   DBuf<uint8_t> rot_free_, trans_free_, pfree_, obs_fixed_;
   DBuf<int32_t> work_i_;   // Cholesky panel envelopes (panel_jmax)
   DBuf<int32_t> fd_pair_;
+  DBuf<int32_t> pu_units_;   // k_point_update work units
   DBuf<int32_t> obs_pnt_, pairs_;   // Schur work lists
   DBuf<SchurSeg> segs_;
   DBuf<LinChunk> lchunks_d_;
@@ -81,6 +82,7 @@ class BaSolver {
   DBuf<uint16_t> llist_d_;
   DBuf<double> lin_scal_;
   int nlin_ = 0;
+  int npu_ = 0;
   DBuf<double> seg_fail_;
   int nseg_ = 0, max_seg_nb_ = 0, max_seg_obs_ = 0;  // FrameDistance cross-block lookup
   DBuf<double> rdg_;       // 1/U_jj of the factor

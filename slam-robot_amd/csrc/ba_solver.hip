@@ -388,13 +388,14 @@ __global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_linearize(Dev d) {
   xn2 = wave_sum_full(xn2);
   gmax = wave_max(gmax);
   if (lane == 0) {
-    double* sc = d.lin_scal + (size_t)blockIdx.x * kNScal;
-    sc[kCost] = cost;
-    sc[kFail] = fail;
-    sc[kFixed] = fixed;
-    sc[kFixedFail] = ffail;
-    sc[kXnorm2] = xn2;
-    sc[kGmax] = gmax;
+    double* sc = d.lin_scal + blockIdx.x;   // structure of arrays: slot j at [j * nlin + chunk]
+    const size_t ns = d.nlin;
+    sc[kCost * ns] = cost;
+    sc[kFail * ns] = fail;
+    sc[kFixed * ns] = fixed;
+    sc[kFixedFail * ns] = ffail;
+    sc[kXnorm2 * ns] = xn2;
+    sc[kGmax * ns] = gmax;
   }
 }
 
@@ -452,13 +453,14 @@ __global__ __launch_bounds__(kRedThreads) void k_cam_reduce(Dev d) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int c = c0 + u * kRedThreads;
-      const double* sc = d.lin_scal + (size_t)(c < d.nlin ? c : 0) * kNScal;
-      t[u][kXCost] = sc[kCost];
-      t[u][kXFail] = sc[kFail];
-      t[u][kXFixed] = sc[kFixed];
-      t[u][kXFixedFail] = sc[kFixedFail];
-      t[u][kXXnorm2] = sc[kXnorm2];
-      t[u][kXNum] = sc[kGmax];
+      const double* sc = d.lin_scal + (c < d.nlin ? c : 0);   // coalesced: slot j at [j * nlin + chunk]
+      const size_t ns = d.nlin;
+      t[u][kXCost] = sc[kCost * ns];
+      t[u][kXFail] = sc[kFail * ns];
+      t[u][kXFixed] = sc[kFixed * ns];
+      t[u][kXFixedFail] = sc[kFixedFail * ns];
+      t[u][kXXnorm2] = sc[kXnorm2 * ns];
+      t[u][kXNum] = sc[kGmax * ns];
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u)
@@ -1761,7 +1763,17 @@ __global__ __launch_bounds__(kLinThreads) void k_point_update(Dev d) {
   const LmState* st = d.st;
   if (st->done) return;
   const int cur = st->cur, nxt = cur ^ 1;
-  const LinChunk ch = d.lchunks[blockIdx.x];
+  // work unit: one round of a regular chunk (rounds are independent here: the camera step is known), or a
+  // whole wide chunk (one point split over rounds)
+  const int unit = d.pu_units[blockIdx.x];
+  LinChunk ch;
+  if (unit >= 0) {
+    ch.r0 = unit;
+    ch.r1 = unit + 1;
+    ch.wide = 0;
+  } else {
+    ch = d.lchunks[-unit - 1];
+  }
   __shared__ double pacc[kLinPts * 4], xps[kLinPts * 4], Xns[kLinPts * 4];
   const int lane = threadIdx.x;
   for (int i = lane; i < kLinPts * 4; i += kLinThreads) pacc[i] = 0.0;
@@ -1799,16 +1811,17 @@ __global__ __launch_bounds__(kLinThreads) void k_point_update(Dev d) {
   step2 = wave_sum_full(step2);
   candx2 = wave_sum_full(candx2);
   if (lane == 0) {
-    double* sc = d.chunk_scal + (size_t)blockIdx.x * kNScal;
-    sc[kModel] = model;
-    sc[kCandCost] = candcost;
-    sc[kCandFail] = candfail;
-    sc[kStep2] = step2;
-    sc[kCandX2] = candx2;
+    double* sc = d.chunk_scal + blockIdx.x;   // structure of arrays: slot j at [j * npu + unit]
+    const size_t ns = d.npu;
+    sc[kModel * ns] = model;
+    sc[kCandCost * ns] = candcost;
+    sc[kCandFail * ns] = candfail;
+    sc[kStep2 * ns] = step2;
+    sc[kCandX2 * ns] = candx2;
   }
 }
 
-__device__ void decide_step(const Dev& d);
+__device__ void decide_step(LmState& s, const double* u, const double* c);
 
 // fuse: single rank, no all-reduce in between: thread 0 also runs k_decide's step (one launch less).
 __global__ __launch_bounds__(kRedThreads) void k_upd_reduce(Dev d, int fuse) {
@@ -1816,22 +1829,31 @@ __global__ __launch_bounds__(kRedThreads) void k_upd_reduce(Dev d, int fuse) {
   if (st->done) return;
   __shared__ double red[kRedThreads / 64 * kUNum];
   const int tid = threadIdx.x;
+  // the decision's inputs are loaded up front (one round trip overlapping the reduction, not a chain of
+  // dependent ones after it)
+  LmState s;
+  double cc[kCNum];
+  if (fuse && tid == 0) {
+    s = *st;
+    for (int j = 0; j < kCNum; ++j) cc[j] = d.xchg_chol[j];
+  }
   double v[kUNum] = {0, 0, 0, 0, 0, 0};
-  for (int c0 = tid; c0 < d.nlin; c0 += 4 * kRedThreads) {
+  for (int c0 = tid; c0 < d.npu; c0 += 4 * kRedThreads) {
     double t[4][5];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int c = c0 + u * kRedThreads;
-      const double* sc = d.chunk_scal + (size_t)(c < d.nlin ? c : 0) * kNScal;
-      t[u][0] = sc[kModel];
-      t[u][1] = sc[kCandCost];
-      t[u][2] = sc[kCandFail];
-      t[u][3] = sc[kStep2];
-      t[u][4] = sc[kCandX2];
+      const double* sc = d.chunk_scal + (c < d.npu ? c : 0);   // coalesced: slot j at [j * npu + unit]
+      const size_t ns = d.npu;
+      t[u][0] = sc[kModel * ns];
+      t[u][1] = sc[kCandCost * ns];
+      t[u][2] = sc[kCandFail * ns];
+      t[u][3] = sc[kStep2 * ns];
+      t[u][4] = sc[kCandX2 * ns];
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u)
-      if (c0 + u * kRedThreads < d.nlin) {
+      if (c0 + u * kRedThreads < d.npu) {
         v[kUModel] += t[u][0];
         v[kUCandCost] += t[u][1];
         v[kUCandFail] += t[u][2];
@@ -1844,78 +1866,85 @@ __global__ __launch_bounds__(kRedThreads) void k_upd_reduce(Dev d, int fuse) {
   if (tid == 0) {
 #pragma unroll
     for (int j = 0; j < kUNum; ++j) d.xchg_upd[j] = v[j];
-    if (fuse) decide_step(d);
+    if (fuse) {
+      decide_step(s, v, cc);
+      *d.st = s;
+    }
   }
 }
 
 // ------------------------------------------------------------------------------------------------
 // k_decide: TrustRegionMinimizer + LevenbergMarquardtStrategy step bookkeeping (Ceres 1.8 semantics).
 __global__ void k_decide(Dev d) {
-  if (threadIdx.x == 0) decide_step(d);
+  if (threadIdx.x == 0) {
+    LmState s = *d.st;
+    double u[kUNum], c[kCNum];
+    for (int j = 0; j < kUNum; ++j) u[j] = d.xchg_upd[j];
+    for (int j = 0; j < kCNum; ++j) c[j] = d.xchg_chol[j];
+    decide_step(s, u, c);
+    *d.st = s;
+  }
 }
 
-__device__ void decide_step(const Dev& d) {
-  LmState* st = d.st;
-  if (st->done) return;
-  const double* u = d.xchg_upd;
-  const double* c = d.xchg_chol;
+__device__ void decide_step(LmState& s, const double* u, const double* c) {
+  if (s.done) return;
   const double model = u[kUModel] + c[kCModel];
   const double step2 = u[kUStep2] + c[kCStep2];
   const bool solved = u[kULinFail] == 0.0 && c[kCFail] == 0.0 && isfinite(step2) && isfinite(model);
   const bool valid = solved && !(model < 0.0);
   bool success = false;
-  st->last_model = model;
+  s.last_model = model;
   if (!valid) {
-    st->n_invalid += 1;
-    st->consecutive_invalid += 1;
-    if (!st->disable_term && st->consecutive_invalid >= st->max_invalid) {
-      st->done = 1; st->ok = 0; st->termination = SG_NUMERICAL_FAILURE;
+    s.n_invalid += 1;
+    s.consecutive_invalid += 1;
+    if (!s.disable_term && s.consecutive_invalid >= s.max_invalid) {
+      s.done = 1; s.ok = 0; s.termination = SG_NUMERICAL_FAILURE;
       return;
     }
   } else {
-    st->consecutive_invalid = 0;
+    s.consecutive_invalid = 0;
     const double new_cost = u[kUCandFail] > 0.0 ? DBL_MAX : u[kUCandCost] + c[kCCandCost];
     const double step_norm = sqrt(step2);
-    st->last_new_cost = new_cost;
-    st->last_step_norm = step_norm;
-    if (!st->disable_term && step_norm <= st->ptol * (st->x_norm + st->ptol)) {
-      st->done = 1; st->ok = 1; st->termination = SG_PARAMETER_TOLERANCE;
+    s.last_new_cost = new_cost;
+    s.last_step_norm = step_norm;
+    if (!s.disable_term && step_norm <= s.ptol * (s.x_norm + s.ptol)) {
+      s.done = 1; s.ok = 1; s.termination = SG_PARAMETER_TOLERANCE;
       return;
     }
-    const double cost_change = st->cost - new_cost;
-    if (!st->disable_term && fabs(cost_change) < st->ftol * st->cost) {
-      st->done = 1; st->ok = 1; st->termination = SG_FUNCTION_TOLERANCE;
+    const double cost_change = s.cost - new_cost;
+    if (!s.disable_term && fabs(cost_change) < s.ftol * s.cost) {
+      s.done = 1; s.ok = 1; s.termination = SG_FUNCTION_TOLERANCE;
       return;
     }
     const double rel = cost_change / model;
-    st->last_rel_decrease = rel;
-    success = rel > st->min_rel_dec;
+    s.last_rel_decrease = rel;
+    success = rel > s.min_rel_dec;
     if (success) {
-      st->n_succ += 1;
+      s.n_succ += 1;
       const double t = 2.0 * rel - 1.0;
-      st->radius = st->radius / fmax(1.0 / 3.0, 1.0 - t * t * t);
-      st->radius = fmin(st->max_radius, st->radius);
-      st->decrease_factor = 2.0;
-      st->reuse_diag = 0;
-      st->cur ^= 1;
-      st->x_norm = sqrt(u[kUCandX2] + c[kCCandX2]);
-      st->cost = new_cost;
-      st->need_lin = 1;   // the iteration is pushed after the gradient test in k_cam_finalize
+      s.radius = s.radius / fmax(1.0 / 3.0, 1.0 - t * t * t);
+      s.radius = fmin(s.max_radius, s.radius);
+      s.decrease_factor = 2.0;
+      s.reuse_diag = 0;
+      s.cur ^= 1;
+      s.x_norm = sqrt(u[kUCandX2] + c[kCCandX2]);
+      s.cost = new_cost;
+      s.need_lin = 1;   // the iteration is pushed after the gradient test in k_cam_finalize
       return;
     }
   }
   // rejected (StepRejected) or invalid (StepIsInvalid == StepRejected(0))
-  if (valid) st->n_unsucc += 1;
-  else st->n_unsucc += 1;
-  st->radius = st->radius / st->decrease_factor;
-  st->decrease_factor *= 2.0;
-  st->reuse_diag = 1;
-  if (!st->disable_term && st->radius < st->min_radius) {
-    st->done = 1; st->ok = 1; st->termination = SG_PARAMETER_TOLERANCE;
+  if (valid) s.n_unsucc += 1;
+  else s.n_unsucc += 1;
+  s.radius = s.radius / s.decrease_factor;
+  s.decrease_factor *= 2.0;
+  s.reuse_diag = 1;
+  if (!s.disable_term && s.radius < s.min_radius) {
+    s.done = 1; s.ok = 1; s.termination = SG_PARAMETER_TOLERANCE;
     return;
   }
-  st->pushed += 1;
-  st->min_pushed_cost = fmin(st->min_pushed_cost, st->cost);
+  s.pushed += 1;
+  s.min_pushed_cost = fmin(s.min_pushed_cost, s.cost);
 }
 
 // Zero the S accumulation target before k_S_reduce writes the new system (upper blocks only are
@@ -2176,6 +2205,15 @@ void BaSolver::Load(const sg_problem& p) {
     }
   }
   nlin_ = (int)lchunks.size();
+  std::vector<int32_t> pu_units;   // k_point_update work units: a round index, or -(chunk + 1) for wide chunks
+  for (int c = 0; c < nlin_; ++c) {
+    if (lchunks[c].wide)
+      pu_units.push_back(-(c + 1));
+    else
+      for (int r = lchunks[c].r0; r < lchunks[c].r1; ++r) pu_units.push_back(r);
+  }
+  npu_ = (int)pu_units.size();
+  if (pu_units.empty()) pu_units.push_back(0);
   // Schur segments: runs of at most kSegPts consecutive points (device order) whose observations fit the
   // LDS stage and whose camera blocks fit a window of kSegNbMax blocks; one workgroup each, with its own
   // window partial in S_slab.  A point spanning more blocks is a "wide" segment of its own (global
@@ -2424,7 +2462,8 @@ void BaSolver::Load(const sg_problem& p) {
   lin_scal_.Resize((size_t)std::max(nlin_, 1) * kNScal);
   lin_scal_.Zero(s);
   S_slab_.Resize(std::max(s_off, 1));
-  chunk_scal_.Resize((size_t)std::max(nlin_, 1) * kNScal);
+  chunk_scal_.Resize((size_t)std::max(npu_, 1) * kNScal);
+  pu_units_.Upload(pu_units, s);
   cam_wide_.Resize((size_t)std::max(NB_, 1) * kCamV);
   S_wide_.Resize(nn * nn);
   xchg_cam_.Resize((size_t)NB_ * kCamV + kXNum + nranks());
@@ -2537,6 +2576,8 @@ Dev BaSolver::MakeDev() {
   d.lrounds = lrounds_d_.ptr;
   d.llist = llist_d_.ptr;
   d.nlin = nlin_;
+  d.npu = npu_;
+  d.pu_units = pu_units_.ptr;
   d.lin_scal = lin_scal_.ptr;
   d.segs = segs_.ptr;
   d.nseg = nseg_;
@@ -2643,7 +2684,7 @@ void BaSolver::Iterate(int n) {
                          (const int32_t*)work_i_.ptr, rdg_.ptr);
     TimedLaunchEnd(kKChol);
     TimedLaunchBegin(kKPointUpd);
-    hipLaunchKernelGGL(k_point_update, dim3(std::max(nlin_, 1)), dim3(kLinThreads), 0, stream_, d);
+    hipLaunchKernelGGL(k_point_update, dim3(std::max(npu_, 1)), dim3(kLinThreads), 0, stream_, d);
     TimedLaunchEnd(kKPointUpd);
     const bool multi = comm_ && comm_->nranks() > 1;
     TimedLaunchBegin(kKUpdRed);
