@@ -178,18 +178,25 @@ __device__ __forceinline__ void make_geo(float px, float py, int W, int w, int h
 
 // Patch pixel (i, j) of the W x W patch.
 __device__ __forceinline__ float sample(const float* img, int w, const Geo& g, int i, int j) {
-  if (g.pw <= 0 || g.ph <= 0 || j < g.zx || i < g.zy) return 0.f;
+  // Branch-free form of getRectSubPix's three cases (left edge column, interior bilinear, right edge
+  // column) and the zero-filled border: the four loads are unconditional (clamped to index 0 when the
+  // pixel is zero) so a wave's samples are all in flight together; each case's arithmetic is the
+  // reference expression, evaluated as written (FMA contraction is off in this file).
+  const bool zero = g.pw <= 0 || g.ph <= 0 || j < g.zx || i < g.zy;
   const int ii = i - g.zy, jj = j - g.zx;
   const bool same = (ii < g.ry || ii >= g.rh);
   const int row = g.base_row + max(0, min(ii, g.rh) - g.ry);
-  const float* s1 = img + (size_t)row * w;
-  const float* s2 = same ? s1 : s1 + w;
-  if (jj < g.rx) return s1[g.col0 + g.rx] * g.b1 + s2[g.col0 + g.rx] * g.b2;
-  if (jj < g.rw) {
-    const int c = g.col0 + jj;
-    return s1[c] * g.a11 + s1[c + 1] * g.a12 + s2[c] * g.a21 + s2[c + 1] * g.a22;
-  }
-  return s1[g.col0 + g.rw] * g.b1 + s2[g.col0 + g.rw] * g.b2;
+  const bool left = jj < g.rx, right = !left && jj >= g.rw;
+  const bool edge = left || right;
+  const int ce = g.col0 + (left ? g.rx : g.rw);
+  const int c0 = zero ? 0 : (edge ? ce : g.col0 + jj);
+  const int c1 = zero ? 0 : (edge ? ce : g.col0 + jj + 1);
+  const size_t r1 = zero ? 0 : (size_t)row * w;
+  const size_t r2 = (zero || same) ? r1 : r1 + w;
+  const float v11 = img[r1 + c0], v12 = img[r1 + c1], v21 = img[r2 + c0], v22 = img[r2 + c1];
+  const float re = v11 * g.b1 + v21 * g.b2;
+  const float rb = v11 * g.a11 + v12 * g.a12 + v21 * g.a21 + v22 * g.a22;
+  return zero ? 0.f : (edge ? re : rb);
 }
 
 template <int kCtrl>
@@ -221,8 +228,8 @@ __device__ __forceinline__ void get_patch(const LevelDev& L, float px, float py,
 #pragma unroll
   for (int k = 0; k < kNP; ++k) {
     const int p = lane + 64 * k;
-    float v = 0.f;
-    if (p < len) v = sample(L.img, L.w, g, p / W, p % W);
+    const float sv = sample(L.img, L.w, g, p / W, p % W);   // unconditional: loads in flight together
+    const float v = (p < len) ? sv : 0.f;
     t.v[k] = v;
     s += v;
     q += v * v;
@@ -247,8 +254,7 @@ __device__ __forceinline__ void get_patch_ctx(const TrackCtx& c, const LevelDev&
   float s = 0.f, q = 0.f;
 #pragma unroll
   for (int k = 0; k < kNP; ++k) {
-    float v = 0.f;
-    if (c.pi[k] >= 0) v = sample(L.img, L.w, g, c.pi[k], c.pj[k]);
+    const float v = sample(L.img, L.w, g, c.pi[k], c.pj[k]);   // 0 past the patch (pi = -1 < zy)
     t.v[k] = v;
     s += v;
     q += v * v;
@@ -279,8 +285,7 @@ __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev&
     float s = 0.f, q = 0.f;
 #pragma unroll
     for (int k = 0; k < kNP; ++k) {
-      float v = 0.f;
-      if (c.pi[k] >= 0) v = sample(L.img, L.w, g, c.pi[k], c.pj[k]);
+      const float v = sample(L.img, L.w, g, c.pi[k], c.pj[k]);   // 0 past the patch (pi = -1 < zy)
       pv[r][k] = v;
       s += v;
       q += v * v;
