@@ -242,6 +242,7 @@ __device__ __forceinline__ void get_patch(const LevelDev& L, float px, float py,
 
 struct TrackCtx {
   int W, len, max_it;
+  int nk;              // patch pixels per lane actually used: ceil(len / 64) <= kNP
   float threshold;
   int lane;
   float mk[kNP];       // this lane's mask values
@@ -254,7 +255,7 @@ __device__ __forceinline__ void get_patch_ctx(const TrackCtx& c, const LevelDev&
   float s = 0.f, q = 0.f;
 #pragma unroll
   for (int k = 0; k < kNP; ++k) {
-    const float v = sample(L.img, L.w, g, c.pi[k], c.pj[k]);   // 0 past the patch (pi = -1 < zy)
+    const float v = k < c.nk ? sample(L.img, L.w, g, c.pi[k], c.pj[k]) : 0.f;   // 0 past the patch
     t.v[k] = v;
     s += v;
     q += v * v;
@@ -285,7 +286,7 @@ __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev&
     float s = 0.f, q = 0.f;
 #pragma unroll
     for (int k = 0; k < kNP; ++k) {
-      const float v = sample(L.img, L.w, g, c.pi[k], c.pj[k]);   // 0 past the patch (pi = -1 < zy)
+      const float v = k < c.nk ? sample(L.img, L.w, g, c.pi[k], c.pj[k]) : 0.f;   // 0 past the patch
       pv[r][k] = v;
       s += v;
       q += v * v;
@@ -400,6 +401,7 @@ __global__ __launch_bounds__(64 * kTrackWaves) void k_track_fb(const LevelDev* _
   TrackCtx c;
   c.W = prm.window;
   c.len = prm.window * prm.window;
+  c.nk = (c.len + 63) / 64;
   c.max_it = prm.max_iterations;
   c.threshold = prm.threshold;
   c.lane = lane;
@@ -478,6 +480,7 @@ __global__ __launch_bounds__(64 * kTrackWaves) void k_get_patches(LevelDev L, in
 __device__ __forceinline__ void init_ctx(TrackCtx& c, const TrackParams& prm, int lane) {
   c.W = prm.window;
   c.len = prm.window * prm.window;
+  c.nk = (c.len + 63) / 64;
   c.max_it = prm.max_iterations;
   c.threshold = prm.threshold;
   c.lane = lane;
