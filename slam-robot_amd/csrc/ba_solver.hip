@@ -20,6 +20,9 @@
 //   k_decide       Ceres TrustRegionMinimizer / LevenbergMarquardtStrategy bookkeeping
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+#include <string>
+
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
@@ -2067,6 +2070,17 @@ void BaSolver::AllReduceSum(double* buf, size_t n) {
 }
 
 void BaSolver::Load(const sg_problem& p) {
+  static const bool host_timing = getenv("SG_HOST_TIMING") != nullptr;   // development aid: phase times
+  auto lt0 = std::chrono::steady_clock::now();
+  std::string lap_log;
+  auto lap = [&](const char* what) {
+    if (!host_timing) return;
+    const auto t = std::chrono::steady_clock::now();
+    char buf[96];
+    snprintf(buf, sizeof(buf), " %s %.2f", what, std::chrono::duration<double, std::milli>(t - lt0).count());
+    lap_log += buf;
+    lt0 = t;
+  };
   ValidateProblem(&p);
   SG_REQUIRE(!p.cameras_free, SG_EINVAL,
              "free intrinsics (SolveAllFrames(..., solve_cameras=true)) are not supported by the device solver yet");
@@ -2085,6 +2099,7 @@ void BaSolver::Load(const sg_problem& p) {
   for (int f = 0; f < F_; ++f)
     if (p.frame_rot_free[f] || p.frame_trans_free[f]) frame_block[f] = NB_++;
   n_ = 6 * NB_;
+  lap("blocks");
   // point order: by first free block (points without free-frame observations last)
   std::vector<int32_t> pfirst(P_, NB_), plast(P_, -1), pcount(P_, 0);
   for (int o = 0; o < M_; ++o) {
@@ -2101,6 +2116,7 @@ void BaSolver::Load(const sg_problem& p) {
                    [&](int a, int b) { return pfirst[a] < pfirst[b]; });
   std::vector<int32_t> inv_perm(P_);
   for (int i = 0; i < P_; ++i) inv_perm[point_perm_[i]] = i;
+  lap("point-order");
   // observations: CSR by device point order (stable in problem order)
   std::vector<int32_t> poff(P_ + 1, 0);
   for (int o = 0; o < M_; ++o) poff[inv_perm[p.obs_point[o]] + 1]++;
@@ -2126,6 +2142,7 @@ void BaSolver::Load(const sg_problem& p) {
     obs_frame[o] = p.obs_frame[src];
     obs_fixed[o] = frame_block[p.obs_frame[src]] < 0 && !p.point_free[p.obs_point[src]];
   }
+  lap("obs-csr");
   // k_linearize decomposition (see LinChunk): rounds of whole points (<= kLinObs observations), up to
   // maxr rounds per chunk sharing one camera window; fewer rounds per chunk on small problems so that the
   // grid still fills the chip.
@@ -2214,6 +2231,7 @@ void BaSolver::Load(const sg_problem& p) {
   }
   npu_ = (int)pu_units.size();
   if (pu_units.empty()) pu_units.push_back(0);
+  lap("lin-lists");
   // Schur segments: runs of at most kSegPts consecutive points (device order) whose observations fit the
   // LDS stage and whose camera blocks fit a window of kSegNbMax blocks; one workgroup each, with its own
   // window partial in S_slab.  A point spanning more blocks is a "wide" segment of its own (global
@@ -2291,6 +2309,7 @@ void BaSolver::Load(const sg_problem& p) {
   nseg_ = (int)segs.size();
   SG_REQUIRE(NB_ < 65536, SG_EINVAL, "too many camera blocks");
   if (pairs_flat.empty()) pairs_flat.assign(2, 0);
+  lap("segments");
   // deterministic reduction lists: for every camera block / block pair, the slab offsets of the chunk
   // partials that cover it (fixed chunk order)
   std::vector<int32_t> cam_loff(NB_ + 1, 0), cam_lidx, r_loff(NB_ + 1, 0), r_lidx;
@@ -2328,6 +2347,7 @@ void BaSolver::Load(const sg_problem& p) {
     if (r_lidx.empty()) r_lidx.push_back(0);
     if (s_lidx.empty()) s_lidx.push_back(0);
   }
+  lap("reduce-lists");
   // FrameDistance
   std::vector<int32_t> fd_a(p.dist_frame, p.dist_frame + D_), fd_b(p.dist_prev, p.dist_prev + D_);
   std::vector<int32_t> fd_boff(NB_ + 1, 0), fd_bidx;
@@ -2343,6 +2363,7 @@ void BaSolver::Load(const sg_problem& p) {
       fd_bidx.insert(fd_bidx.end(), lists[b].begin(), lists[b].end());
     }
   }
+  lap("fd");
   // Cholesky panel envelopes: block column J's first nonzero block row lo(J)
   std::vector<int32_t> lo_blk(NB_);
   for (int b = 0; b < NB_; ++b) lo_blk[b] = b;
@@ -2394,6 +2415,7 @@ void BaSolver::Load(const sg_problem& p) {
   chol_window_ = npanel <= kJendSh;   // band ends cached in LDS
   for (int pk = 0; pk < npanel; ++pk)
     if (panel_jmax[pk] - pk * kCholNb > kCholWS) chol_window_ = false;
+  lap("envelope");
   // device uploads
   hipStream_t s = stream_;
   k_.Upload(std::vector<double>(p.k, p.k + 7 * ncam_), s);
@@ -2496,6 +2518,12 @@ void BaSolver::Load(const sg_problem& p) {
     stamps_.Zero(s);
   }
   SG_HIP_CHECK(hipStreamSynchronize(s));
+  lap("uploads");
+  if (host_timing) {
+    SG_HIP_CHECK(hipStreamSynchronize(stream_));
+    lap("sync");
+    fprintf(stderr, "[sg] Load phases (ms):%s\n", lap_log.c_str());
+  }
   loaded_ = true;
   began_ = false;
 }

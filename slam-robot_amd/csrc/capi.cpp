@@ -3,6 +3,8 @@
 // sg_ba_*   : the device solver (Ceres 1.8 LM + SPARSE_SCHUR restated on MI355X, slam.cpp:482-521)
 // sg_slam_* : the Slam object of slam.h:21-65 — SolveFrames / SolveAllFrames / ReprojectMap with
 //             iterations() and error() bookkeeping — on top of sg_problem_* and sg_ba_*.
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 
@@ -180,10 +182,19 @@ int sg_slam_set_options(sg_slam* s, const sg_solver_options* o) {
 }
 
 static void RunProblem(sg_slam* s, sg_problem* p, sg_map* map, const sg_solver_options& o, int32_t* solved) {
+  static const bool timing = getenv("SG_HOST_TIMING") != nullptr;   // development aid: phase times to stderr
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  const auto t0 = now();
   s->solver->Load(*p);
+  const auto t1 = now();
   sg_solver_summary sum{};
   s->solver->Solve(o, p, &sum);
+  const auto t2 = now();
   if (sg_problem_write_back(p, map) != SG_OK) throw sg::Error(SG_EINVAL, sg_last_error());
+  if (timing) {
+    const auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    fprintf(stderr, "[sg] load %.2f ms, solve %.2f ms, write-back %.2f ms\n", ms(t0, t1), ms(t1, t2), ms(t2, now()));
+  }
   s->iterations += sum.num_iterations;   // iterations_ += summary.iterations.size()
   s->error = sum.final_cost;             // error_ = summary.final_cost
   s->last = sum;
