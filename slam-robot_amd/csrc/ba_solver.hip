@@ -425,7 +425,7 @@ __global__ __launch_bounds__(kRedThreads) void k_cam_reduce(Dev d) {
         int ix[kU];
         double v[kU];
 #pragma unroll
-        for (int u = 0; u < kU; ++u) ix[u] = jb + u * kCamSlices < j1 ? d.cam_lidx[jb + u * kCamSlices] : 0;
+        for (int u = 0; u < kU; ++u) ix[u] = d.cam_lidx[jb + u * kCamSlices < j1 ? jb + u * kCamSlices : 0];   // unconditional
 #pragma unroll
         for (int u = 0; u < kU; ++u) v[u] = d.cam_slab[ix[u] + e];
 #pragma unroll
