@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <memory>
 #include <string>
 #include <vector>
@@ -51,6 +52,8 @@ class BaSolver {
   bool loaded_ = false;
   bool began_ = false;
   bool chol_window_ = true;
+  bool pack_force_ = getenv("SG_PACK_S") != nullptr;   // pack/unpack S on one rank too (tests the path)
+  size_t npack_ = 0;                                      // band of S + rhs, doubles (all-reduce size)
   bool stamp_on_ = false;
   DBuf<unsigned long long> stamps_;
 
@@ -75,6 +78,8 @@ class BaSolver {
   DBuf<int32_t> work_i_;   // Cholesky panel envelopes (panel_jmax)
   DBuf<int32_t> fd_pair_;
   DBuf<int32_t> pu_units_;   // k_point_update work units
+  DBuf<int32_t> pack_off_;   // per panel offset of its band rows in the packed all-reduce buffer
+  DBuf<double> Spk_;         // packed band of S + rhs (landmark shards)
   DBuf<int32_t> obs_pnt_, pairs_;   // Schur work lists
   DBuf<SchurSeg> segs_;
   DBuf<LinChunk> lchunks_d_;

@@ -953,6 +953,33 @@ __global__ __launch_bounds__(256) void k_S_reduce(Dev d) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// Landmark shards: the part of S the Cholesky reads (per 16-row panel, columns kb .. band end, row-major)
+// and the rhs, packed into one contiguous buffer for the all-reduce and unpacked after it.  Outside the
+// band every rank's S holds exact zeros (k_S_reduce writes every block pair), so only the band travels.
+// Block (pk, y) of the grid copies panel pk (pk == npanel: the rhs).
+__global__ __launch_bounds__(256) void k_S_pack(double* S, int n, const int32_t* panel_jend, const int32_t* off,
+                                                int npanel, double* buf, int unpack) {
+  const int pk = blockIdx.x;
+  const int stride = 256 * gridDim.y;
+  if (pk == npanel) {
+    double* xc = S + (size_t)n * n;
+    for (int i = blockIdx.y * 256 + threadIdx.x; i < n; i += stride) {
+      if (unpack) xc[i] = buf[off[npanel] + i];
+      else buf[off[npanel] + i] = xc[i];
+    }
+    return;
+  }
+  const int kb = pk * kCholNb, w = min(kCholNb, n - kb), width = panel_jend[pk] - kb;
+  const int cnt = w * width;
+  for (int e = blockIdx.y * 256 + threadIdx.x; e < cnt; e += stride) {
+    const int r = e / width, c = e - r * width;
+    const size_t gi = (size_t)(kb + r) * n + kb + c;
+    if (unpack) S[gi] = buf[off[pk] + e];
+    else buf[off[pk] + e] = S[gi];
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Reduced camera system solve (the SPARSE_SCHUR + CHOLMOD step behind slam.cpp:489, restated): one
 // workgroup factors the damped, banded Schur complement A = U^T U (right-looking, 16-wide panels, the
 // rhs carried as an augmented column), then back-substitutes.  The band (co-visibility of the sliding
@@ -2412,6 +2439,14 @@ void BaSolver::Load(const sg_problem& p) {
     jmax = std::min(jmax, n_);
     panel_jmax[pk] = std::min(n_, (jmax + kCholNb - 1) / kCholNb * kCholNb);   // band end, 16-aligned
   }
+  {
+    std::vector<int32_t> off(npanel + 1, 0);
+    for (int pk = 0; pk < npanel; ++pk)
+      off[pk + 1] = off[pk] + std::min(kCholNb, n_ - pk * kCholNb) * (panel_jmax[pk] - pk * kCholNb);
+    npack_ = (size_t)off[npanel] + n_;
+    pack_off_.Upload(off, stream_);
+    Spk_.Resize(std::max<size_t>(npack_, 1));
+  }
   chol_window_ = npanel <= kJendSh;   // band ends cached in LDS
   for (int pk = 0; pk < npanel; ++pk)
     if (panel_jmax[pk] - pk * kCholNb > kCholWS) chol_window_ = false;
@@ -2696,9 +2731,15 @@ void BaSolver::Iterate(int n) {
     const int nwv = NB_ * (NB_ + 1) / 2 + NB_;
     hipLaunchKernelGGL(k_S_reduce, dim3(std::max(nwv, 1)), dim3(256), 0, stream_, d);
     TimedLaunchEnd(kKSReduce);
-    if (comm_ && comm_->nranks() > 1) {
-      // the upper blocks of S and the rhs partial are summed over landmark shards
-      AllReduceSum(S_.ptr, (size_t)n_ * n_ + n_);
+    if ((comm_ && comm_->nranks() > 1) || pack_force_) {
+      // the band of S and the rhs partial are summed over landmark shards (packed: the band only)
+      const int npanel = (n_ + kCholNb - 1) / kCholNb;
+      const dim3 pg(npanel + 1, 4);
+      hipLaunchKernelGGL(k_S_pack, pg, dim3(256), 0, stream_, S_.ptr, n_, (const int32_t*)work_i_.ptr,
+                         (const int32_t*)pack_off_.ptr, npanel, Spk_.ptr, 0);
+      AllReduceSum(Spk_.ptr, npack_);
+      hipLaunchKernelGGL(k_S_pack, pg, dim3(256), 0, stream_, S_.ptr, n_, (const int32_t*)work_i_.ptr,
+                         (const int32_t*)pack_off_.ptr, npanel, Spk_.ptr, 1);
     }
     TimedLaunchBegin(kKChol);
     if (chol_window_ && d.stamps)

@@ -213,3 +213,29 @@ def test_slam_too_few_frames_returns_false(gpu_lib):
     slam = ba.Slam()
     assert slam.SolveFrames(m, 1, 1, 2.0) is False
     assert slam.iterations() == 0
+
+
+def test_packed_band_exchange_is_exact(gpu_lib, monkeypatch):
+    """The landmark-shard exchange packs the band of S (per panel: rows of the panel, columns up to its band
+    end) and the rhs into one buffer for the all-reduce and unpacks it afterwards.  Forced on
+    one GPU (SG_PACK_S), the pack/unpack round trip must leave the solve unchanged.  k_schur accumulates the
+    window blocks with LDS atomics, so two runs agree to rounding only (cost rel 1e-12), not bit for bit."""
+    m = make_config("C2")
+    pa = ba.problem_from_map_frames(m, m.num_frames - 2, m.num_frames, 2.0)
+    out = []
+    for force in (False, True):
+        if force:
+            monkeypatch.setenv("SG_PACK_S", "1")
+        p = pa.copy()
+        g = ba.BundleAdjuster()
+        g.load(p)
+        s = g.solve(default_solver_options(max_num_iterations=6))
+        out.append((s, p))
+        g.close()
+    (s0, p0), (s1, p1) = out
+    assert s0["num_iterations"] == s1["num_iterations"]
+    assert s0["num_successful_steps"] == s1["num_successful_steps"]
+    assert abs(s0["final_cost"] - s1["final_cost"]) <= 1e-12 * s0["final_cost"]
+    np.testing.assert_allclose(p0.q, p1.q, rtol=0, atol=1e-12)
+    np.testing.assert_allclose(p0.t, p1.t, rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(p0.X, p1.X, rtol=1e-9, atol=1e-12)
