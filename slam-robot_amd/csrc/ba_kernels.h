@@ -33,6 +33,14 @@ enum ScalSlot {
   kCandX2
 };
 
+// Packed per-observation facts (device order), so that a sweep lane's loads depend only on its own
+// observation record: camera block + 1 (0: frame not free) in bits 0-15, camera in bits 16-23, then the
+// frame's rotation / translation freedom, the point's freedom and the fixed flag (all blocks constant).
+constexpr int kMetaCamShift = 16;
+constexpr int kMetaRot = 1 << 24, kMetaTrans = 1 << 25, kMetaPfree = 1 << 26, kMetaFixed = 1 << 27;
+__host__ __device__ __forceinline__ int meta_block(int m) { return (m & 0xffff) - 1; }
+__host__ __device__ __forceinline__ int meta_cam(int m) { return (m >> kMetaCamShift) & 0xff; }
+
 // Exchange-buffer scalar slots appended after the camera blocks.
 enum CamX { kXCost = 0, kXFail, kXFixed, kXFixedFail, kXXnorm2, kXNum };
 enum UpdX { kUModel = 0, kUCandCost, kUCandFail, kUStep2, kUCandX2, kULinFail, kUNum };
@@ -165,6 +173,7 @@ struct Dev {
   int32_t assemble;              // this rank adds blockdiag(U) + FD + damping to S (rank 0 of a shard group)
   int32_t dbg;                   // development switches (SG_DBG), 0 in production
   const int32_t* obs_pnt;        // [M] point (device order) of each observation
+  const int32_t* obs_meta;       // [M] packed block / camera / freedom flags (kMeta*)
   const LinChunk* lchunks;       // [nlin] k_linearize workgroups
   const LinRound* lrounds;
   const uint16_t* llist;         // per round: window-block offsets + local observation indices by block

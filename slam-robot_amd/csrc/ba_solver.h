@@ -81,6 +81,7 @@ class BaSolver {
   DBuf<int32_t> pack_off_;   // per panel offset of its band rows in the packed all-reduce buffer
   DBuf<double> Spk_;         // packed band of S + rhs (landmark shards)
   DBuf<int32_t> obs_pnt_, pairs_;   // Schur work lists
+  DBuf<int32_t> obs_meta_;         // packed per-observation facts (kMeta*)
   DBuf<SchurSeg> segs_;
   DBuf<LinChunk> lchunks_d_;
   DBuf<LinRound> lrounds_d_;

@@ -256,19 +256,19 @@ __global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_linearize(Dev d) {
   LinRound R = d.lrounds[ch.r0];
   int nobs = R.o1 - R.o0;
   double2 n_uv = make_double2(0.0, 0.0);
-  int n_f = 0, n_p = 0, n_fx = 0;
+  int n_f = 0, n_p = 0, n_m = 0;
   if (lane < nobs) {
     const int o = R.o0 + lane;
     n_uv = reinterpret_cast<const double2*>(d.obs_pt)[o];
     n_f = d.obs_frame[o];
     n_p = d.obs_pnt[o];
-    n_fx = d.obs_fixed[o];
+    n_m = d.obs_meta[o];
   }
   lds_fence_wave();
   for (int r = ch.r0; r < ch.r1; ++r) {
     const double2 uv = n_uv;
-    const int f = n_f, p = n_p;
-    const bool fx = n_fx != 0;
+    const int f = n_f, p = n_p, m = n_m;
+    const bool fx = (m & kMetaFixed) != 0;
     const LinRound Rc = R;
     const int nc = nobs;
     if (r + 1 < ch.r1) {
@@ -279,17 +279,17 @@ __global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_linearize(Dev d) {
         n_uv = reinterpret_cast<const double2*>(d.obs_pt)[o];
         n_f = d.obs_frame[o];
         n_p = d.obs_pnt[o];
-        n_fx = d.obs_fixed[o];
+        n_m = d.obs_meta[o];
       }
     }
     if (lane < nc) {
       const int o = Rc.o0 + lane;
-      const bool pf = d.pfree[p] != 0;
+      const bool pf = (m & kMetaPfree) != 0;
       const double4 Xv = X4[p];
       const double X[4] = {Xv.x, Xv.y, Xv.z, Xv.w};
       const double pt[2] = {uv.x, uv.y};
       double rr[2], Jc[12], Jp[8], c;
-      const bool ok = LinearizeObservation(d.q[cur] + 4 * f, d.t[cur] + 3 * f, d.k + 7 * d.frame_cam[f], X, pt,
+      const bool ok = LinearizeObservation(d.q[cur] + 4 * f, d.t[cur] + 3 * f, d.k + 7 * meta_cam(m), X, pt,
                                            d.b, d.inv_b, rr, Jc, Jp, &c);
       double2* Jo = reinterpret_cast<double2*>(d.J + (size_t)o * kJStride);
       if (!ok || fx) {
@@ -303,13 +303,13 @@ __global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_linearize(Dev d) {
         for (int i = 0; i < kJStride / 2; ++i) Jo[i] = make_double2(0.0, 0.0);
       } else {
         cost += c;
-        const int b = d.frame_block[f];
+        const int b = meta_block(m);
         if (b < 0) {
 #pragma unroll
           for (int i = 0; i < 12; ++i) Jc[i] = 0.0;
         } else {
-          if (!d.rot_free[f]) { Jc[0] = Jc[1] = Jc[2] = Jc[6] = Jc[7] = Jc[8] = 0.0; }
-          if (!d.trans_free[f]) { Jc[3] = Jc[4] = Jc[5] = Jc[9] = Jc[10] = Jc[11] = 0.0; }
+          if (!(m & kMetaRot)) { Jc[0] = Jc[1] = Jc[2] = Jc[6] = Jc[7] = Jc[8] = 0.0; }
+          if (!(m & kMetaTrans)) { Jc[3] = Jc[4] = Jc[5] = Jc[9] = Jc[10] = Jc[11] = 0.0; }
         }
         if (!pf) {
 #pragma unroll
@@ -1684,7 +1684,7 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_global(Dev d, const i
 // A wide chunk (one point over several rounds) runs pass 1 over all its pieces, then 2, then 3.
 struct PuObs {
   double r[2], Jp[8], u[2];
-  int f, b;
+  int f, b, cam;
   bool on;   // a non-fixed observation of this round
 };
 
@@ -1694,11 +1694,13 @@ __device__ __forceinline__ void pu_pass1(const Dev& d, const LinRound& R, int la
   const int nc = R.o1 - R.o0;
   if (lane >= nc) return;
   const int o = R.o0 + lane;
-  if (d.obs_fixed[o]) return;
-  ob.on = true;
+  const int m = d.obs_meta[o];
   const int p = d.obs_pnt[o];
   ob.f = d.obs_frame[o];
-  ob.b = d.frame_block[ob.f];
+  if (m & kMetaFixed) return;
+  ob.on = true;
+  ob.b = meta_block(m);
+  ob.cam = meta_cam(m);
   const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
   const double sp[4] = {s4.x, s4.y, s4.z, s4.w};
   double Jc[12];
@@ -1711,7 +1713,7 @@ __device__ __forceinline__ void pu_pass1(const Dev& d, const LinRound& R, int la
       ob.u[0] += Jc[c] * xc[c];
       ob.u[1] += Jc[6 + c] * xc[c];
     }
-    if (pacc && d.pfree[p]) {
+    if (pacc && (m & kMetaPfree)) {
       double* pa = pacc + (p - R.p0) * 4;
 #pragma unroll
       for (int a = 0; a < 4; ++a) atomicAdd(pa + a, ob.Jp[a] * ob.u[0] + ob.Jp[4 + a] * ob.u[1]);
@@ -1735,7 +1737,7 @@ __device__ __forceinline__ void pu_pass3(const Dev& d, const LinRound& R, int la
   model -= m0 * (ob.r[0] + 0.5 * m0) + m1 * (ob.r[1] + 0.5 * m1);
   const double Xn[4] = {Xns[4 * lp], Xns[4 * lp + 1], Xns[4 * lp + 2], Xns[4 * lp + 3]};
   double uv[2];
-  if (!Project(d.q[nxt] + 4 * ob.f, d.t[nxt] + 3 * ob.f, d.k + 7 * d.frame_cam[ob.f], Xn, uv)) {
+  if (!Project(d.q[nxt] + 4 * ob.f, d.t[nxt] + 3 * ob.f, d.k + 7 * ob.cam, Xn, uv)) {
     candfail += 1.0;
     return;
   }
@@ -2169,6 +2171,14 @@ void BaSolver::Load(const sg_problem& p) {
     obs_frame[o] = p.obs_frame[src];
     obs_fixed[o] = frame_block[p.obs_frame[src]] < 0 && !p.point_free[p.obs_point[src]];
   }
+  SG_REQUIRE(NB_ < 0xffff && ncam_ <= 0xff, SG_EINVAL, "too many free frames or cameras for the device solver");
+  std::vector<int32_t> obs_meta(M_);
+  for (int o = 0; o < M_; ++o) {
+    const int src = obs_perm_[o], f = p.obs_frame[src];
+    obs_meta[o] = (frame_block[f] + 1) | (p.frame_camera[f] << kMetaCamShift) |
+                  (p.frame_rot_free[f] ? kMetaRot : 0) | (p.frame_trans_free[f] ? kMetaTrans : 0) |
+                  (p.point_free[p.obs_point[src]] ? kMetaPfree : 0) | (obs_fixed[o] ? kMetaFixed : 0);
+  }
   lap("obs-csr");
   // k_linearize decomposition (see LinChunk): rounds of whole points (<= kLinObs observations), up to
   // maxr rounds per chunk sharing one camera window; fewer rounds per chunk on small problems so that the
@@ -2473,6 +2483,7 @@ void BaSolver::Load(const sg_problem& p) {
   obs_pt_.Upload(obs_pt, s);
   obs_frame_.Upload(obs_frame, s);
   obs_fixed_.Upload(obs_fixed, s);
+  obs_meta_.Upload(obs_meta.empty() ? std::vector<int32_t>{0} : obs_meta, s);
   lchunks_d_.Upload(lchunks, s);
   lrounds_d_.Upload(lrounds, s);
   if (llist.empty()) llist.push_back(0);
@@ -2587,6 +2598,7 @@ Dev BaSolver::MakeDev() {
   d.obs_pt = obs_pt_.ptr;
   d.obs_frame = obs_frame_.ptr;
   d.obs_fixed = obs_fixed_.ptr;
+  d.obs_meta = obs_meta_.ptr;
   d.b = range_b_;
   d.inv_b = 1.0 / range_b_;
   d.D = D_;
