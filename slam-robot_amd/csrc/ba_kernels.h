@@ -108,7 +108,7 @@ struct LmState {
 struct Dev {
   LmState* st;
   // cameras / frames
-  const double* k;
+  double* k[2];                  // intrinsics [ncam][7], two slots (current / candidate) like q, t, X
   double* q[2];
   double* t[2];
   const int32_t* frame_cam;
@@ -186,7 +186,15 @@ struct Dev {
   double* seg_fail;              // [nseg] point blocks whose damped inverse failed
   const int2* pairs;             // {(s << 16) | t local observation indices, (b_s << 16) | b_t}
   unsigned long long* stamps;    // diagnostic builds only: per-phase cycle counters (nullptr otherwise)
+  // free intrinsics (SolveAllFrames(..., solve_cameras = true), slam.cpp:447-480): 7 columns per camera after
+  // the 6 NB frame columns of S (nk = 0 when the intrinsics are constant)
+  int32_t nk, kc0, ncam;         // nk = 7 ncam, kc0 = 6 NB
+  double* Jk;                    // [M][14] corrected, unscaled d(uv)/dk of each observation
+  double* KU;                    // [n][nk] intrinsics columns of J^T J, unscaled (frame rows, then the k block)
+  double* kst;                   // [ncam][56] CameraStabilization corrected residual (7) and Jacobian (7x7)
+  double stab_b, stab_inv_b;     // CauchyLoss(stab_range): b = stab_range^2
 };
+constexpr int kMaxIntrCams = 4;  // cameras whose intrinsics the device solver can free at once
 
 }  // namespace sg
 

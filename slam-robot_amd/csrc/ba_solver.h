@@ -82,6 +82,9 @@ class BaSolver {
   DBuf<double> Spk_;         // packed band of S + rhs (landmark shards)
   DBuf<int32_t> obs_pnt_, pairs_;   // Schur work lists
   DBuf<int32_t> obs_meta_;         // packed per-observation facts (kMeta*)
+  DBuf<double> Jk_, KU_, kst_;     // free intrinsics (nk_ > 0)
+  int nk_ = 0;                     // 7 * cameras when the intrinsics are free
+  double stab_b_ = 25.0;
   DBuf<SchurSeg> segs_;
   DBuf<LinChunk> lchunks_d_;
   DBuf<LinRound> lrounds_d_;

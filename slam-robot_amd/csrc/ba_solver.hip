@@ -289,7 +289,7 @@ __global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_linearize(Dev d) {
       const double X[4] = {Xv.x, Xv.y, Xv.z, Xv.w};
       const double pt[2] = {uv.x, uv.y};
       double rr[2], Jc[12], Jp[8], c;
-      const bool ok = LinearizeObservation(d.q[cur] + 4 * f, d.t[cur] + 3 * f, d.k + 7 * meta_cam(m), X, pt,
+      const bool ok = LinearizeObservation(d.q[cur] + 4 * f, d.t[cur] + 3 * f, d.k[cur] + 7 * meta_cam(m), X, pt,
                                            d.b, d.inv_b, rr, Jc, Jp, &c);
       double2* Jo = reinterpret_cast<double2*>(d.J + (size_t)o * kJStride);
       if (!ok || fx) {
@@ -976,6 +976,280 @@ __global__ __launch_bounds__(256) void k_S_pack(double* S, int n, const int32_t*
     const size_t gi = (size_t)(kb + r) * n + kb + c;
     if (unpack) S[gi] = buf[off[pk] + e];
     else buf[off[pk] + e] = S[gi];
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Free intrinsics (SolveAllFrames(..., solve_cameras = true), slam.cpp:447-480; the oracle's k_col_ layout).
+// Each camera's 7 intrinsics are 7 more columns of the reduced system, after the 6 NB frame columns:
+// S = [[S_ff, S_fk], [., S_kk]], still eliminated over the points.  Few columns, coupled to every frame
+// and point of the camera, so these kernels are plain thread-per-item passes with global atomics (not on
+// the SolveFrames hot path); the k columns make S dense, so the Cholesky runs its global-memory variant.
+//   k_intr_zero / k_intr_lin / k_intr_fin (after an accepted step): J_k per observation, the k columns
+//     of J^T J (KU), the k gradient and diagonal, CameraStabilization (slam.cpp:107-124) on camera c;
+//   k_intr_assemble + k_intr_schur (every iteration): the k columns of the damped, scaled S and rhs:
+//     KU + damping, minus sum_p W_kp V~p^-1 [W_fp W_kp]^T;
+//   k_intr_step (after the solve): candidate intrinsics k+ = k - S x_k, step norms, stabilization
+//     model term and candidate cost.  The observation model terms take A_k x_k in k_point_update.
+
+__global__ __launch_bounds__(256) void k_intr_zero(Dev d) {
+  const LmState* st = d.st;
+  if (st->done || !st->need_lin) return;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < d.n * d.nk) d.KU[i] = 0.0;
+  if (i < d.nk) {
+    d.camg[d.kc0 + i] = 0.0;
+    d.camdiag[d.kc0 + i] = 0.0;
+  }
+}
+
+// One thread per observation: J_k (the same corrected projection Jacobian as k_linearize) and its
+// J^T J / J^T r terms.
+__global__ __launch_bounds__(256) void k_intr_lin(Dev d) {
+  const LmState* st = d.st;
+  if (st->done || !st->need_lin) return;
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= d.M) return;
+  const int cur = st->cur;
+  const int m = d.obs_meta[o], f = d.obs_frame[o], p = d.obs_pnt[o], cam = meta_cam(m);
+  double* Jko = d.Jk + 14 * (size_t)o;
+  const double4 Xv = reinterpret_cast<const double4*>(d.X[cur])[p];
+  const double X[4] = {Xv.x, Xv.y, Xv.z, Xv.w};
+  const double pt[2] = {d.obs_pt[2 * o], d.obs_pt[2 * o + 1]};
+  double rr[2], Jc[12], Jp[8], Jk[14], c;
+  if ((m & kMetaFixed) || !LinearizeObservation(d.q[cur] + 4 * f, d.t[cur] + 3 * f, d.k[cur] + 7 * cam, X, pt,
+                                                d.b, d.inv_b, rr, Jc, Jp, &c, Jk)) {
+    for (int i = 0; i < 14; ++i) Jko[i] = 0.0;   // a failed projection fails the linearization (k_linearize)
+    return;
+  }
+  for (int i = 0; i < 14; ++i) Jko[i] = Jk[i];
+  const int kc = 7 * cam, nk = d.nk;
+  double* Kk = d.KU + (size_t)(d.kc0 + kc) * nk;
+  for (int a = 0; a < 7; ++a) {
+    for (int j = a; j < 7; ++j) atomicAdd(Kk + (size_t)a * nk + kc + j, Jk[a] * Jk[j] + Jk[7 + a] * Jk[7 + j]);
+    atomicAdd(d.camg + d.kc0 + kc + a, Jk[a] * rr[0] + Jk[7 + a] * rr[1]);
+    atomicAdd(d.camdiag + d.kc0 + kc + a, Jk[a] * Jk[a] + Jk[7 + a] * Jk[7 + a]);
+  }
+  const int b = meta_block(m);
+  if (b < 0) return;
+  if (!(m & kMetaRot)) { Jc[0] = Jc[1] = Jc[2] = Jc[6] = Jc[7] = Jc[8] = 0.0; }
+  if (!(m & kMetaTrans)) { Jc[3] = Jc[4] = Jc[5] = Jc[9] = Jc[10] = Jc[11] = 0.0; }
+  double* Kf = d.KU + (size_t)(6 * b) * nk + kc;
+  for (int a = 0; a < 6; ++a)
+    for (int j = 0; j < 7; ++j) atomicAdd(Kf + (size_t)a * nk + j, Jc[a] * Jk[j] + Jc[6 + a] * Jk[7 + j]);
+}
+
+// CameraStabilization residual of camera c (slam.cpp:107-124) and its exact Jacobian.
+__device__ __forceinline__ void stab_residual(const double* k, double* res, double* J) {
+  res[0] = 1000.0 * k[0] * k[0];
+  res[1] = 1000.0 * k[1] * k[1];
+  res[2] = 1000.0 * k[2] * k[2];
+  res[3] = 0.1 * (k[3] - 416.0) * (k[3] - 416.0);
+  res[4] = 0.1 * (k[4] + k[3]) * (k[4] + k[3]);
+  res[5] = 0.01 * (k[5] - 320.0) * (k[5] - 320.0);
+  res[6] = 0.01 * (k[6] - 240.0) * (k[6] - 240.0);
+  if (!J) return;
+  for (int i = 0; i < 49; ++i) J[i] = 0.0;
+  J[0] = 2000.0 * k[0];
+  J[8] = 2000.0 * k[1];
+  J[16] = 2000.0 * k[2];
+  J[24] = 0.2 * (k[3] - 416.0);
+  J[31] = J[32] = 0.2 * (k[4] + k[3]);
+  J[40] = 0.02 * (k[5] - 320.0);
+  J[48] = 0.02 * (k[6] - 240.0);
+}
+
+// One wave: stabilization terms of every camera (lane = camera), then the cost, |g|_inf of the k columns
+// and |k|^2 into the exchange slots k_cam_finalize reads.
+__global__ __launch_bounds__(64) void k_intr_fin(Dev d) {
+  LmState* st = d.st;
+  if (st->done || !st->need_lin) return;
+  const int lane = threadIdx.x, cur = st->cur, nk = d.nk;
+  double cost = 0.0, xn2 = 0.0;
+  if (lane < d.ncam) {
+    const double* k = d.k[cur] + 7 * lane;
+    double res[7], J[49];
+    stab_residual(k, res, J);
+    double sq = 0.0;
+    for (int i = 0; i < 7; ++i) sq += res[i] * res[i];
+    double rho0, rho1;
+    Cauchy(sq, d.stab_b, d.stab_inv_b, &rho0, &rho1);
+    cost = 0.5 * rho0;
+    const double sr = sqrt(rho1);
+    double* ks = d.kst + 56 * lane;
+    for (int i = 0; i < 7; ++i) ks[i] = sr * res[i];
+    for (int i = 0; i < 49; ++i) ks[7 + i] = sr * J[i];
+    const int kc = 7 * lane;
+    double* Kk = d.KU + (size_t)(d.kc0 + kc) * nk;
+    for (int a = 0; a < 7; ++a) {
+      double g = 0.0, dg = 0.0;
+      for (int i = 0; i < 7; ++i) {
+        g += ks[7 + 7 * i + a] * ks[i];
+        dg += ks[7 + 7 * i + a] * ks[7 + 7 * i + a];
+      }
+      d.camg[d.kc0 + kc + a] += g;
+      d.camdiag[d.kc0 + kc + a] += dg;
+      for (int j = a; j < 7; ++j) {
+        double v = 0.0;
+        for (int i = 0; i < 7; ++i) v += ks[7 + 7 * i + a] * ks[7 + 7 * i + j];
+        Kk[(size_t)a * nk + kc + j] += v;
+      }
+    }
+    for (int i = 0; i < 7; ++i) xn2 += k[i] * k[i];
+  }
+  __syncthreads();
+  double gm = 0.0;
+  for (int i = lane; i < nk; i += 64) gm = fmax(gm, fabs(d.camg[d.kc0 + i]));
+  gm = wave_max(gm);
+  cost = wave_sum_full(cost);
+  xn2 = wave_sum_full(xn2);
+  if (lane == 0) {
+    double* xs = d.xchg_cam + (size_t)d.NB * kCamV;
+    xs[kXCost] += cost;
+    xs[kXNum] = fmax(xs[kXNum], gm);   // single rank (Load rejects shards with free intrinsics)
+    if (st->first) xs[kXXnorm2] += xn2;
+  }
+}
+
+// The k columns of the damped, scaled S (upper triangle) and the k part of the rhs y = s g, before the
+// point-elimination terms of k_intr_schur.  Thread per (row, k column).
+__global__ __launch_bounds__(256) void k_intr_assemble(Dev d) {
+  const LmState* st = d.st;
+  if (st->done) return;
+  const int id = blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= d.n * d.nk) return;
+  const int i = id / d.nk, j = id - i * d.nk, col = d.kc0 + j;
+  if (i <= col) {
+    double v = d.KU[id] * d.scale_c[i] * d.scale_c[col];
+    if (i == col) v += d.diag_c[col] / st->radius;
+    d.S[(size_t)i * d.n + col] = v;
+  }
+  if (i == 0) d.xc[col] = d.scale_c[col] * d.camg[col];
+}
+
+// Thread per free point p: W_kp = A_k^T A_p over its observations of camera c (scaled), Y = W_kp V~p^-1, then
+// S_kk -= Y W_kp'^T, rhs_k -= W_kp t_p, and for each observation (frame block b) S_bk -= A_c^T (A_p Y^T).
+__global__ __launch_bounds__(128) void k_intr_schur(Dev d) {
+  const LmState* st = d.st;
+  if (st->done) return;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= d.P || !d.pfree[p]) return;
+  const int o0 = d.poff[p], o1 = d.poff[p + 1], n = d.n;
+  const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
+  const double sp[4] = {s4.x, s4.y, s4.z, s4.w};
+  double Vi[10];
+  for (int i = 0; i < 10; ++i) Vi[i] = d.Vinv[10 * (size_t)p + i];
+  const double4 t4 = reinterpret_cast<const double4*>(d.tp)[p];
+  const double tpv[4] = {t4.x, t4.y, t4.z, t4.w};
+  // W of camera c (7x4, row-major), accumulated over the point's observations of that camera
+  auto build_W = [&](int c, double* W) -> bool {
+    for (int i = 0; i < 28; ++i) W[i] = 0.0;
+    bool any = false;
+    for (int o = o0; o < o1; ++o) {
+      const int m = d.obs_meta[o];
+      if ((m & kMetaFixed) || meta_cam(m) != c) continue;
+      any = true;
+      const double* Jk = d.Jk + 14 * (size_t)o;
+      const double* Jr = d.J + (size_t)o * kJStride + 14;   // corrected Jp (2x4)
+      for (int j = 0; j < 7; ++j) {
+        const double k0 = Jk[j] * d.scale_c[d.kc0 + 7 * c + j], k1 = Jk[7 + j] * d.scale_c[d.kc0 + 7 * c + j];
+        for (int a = 0; a < 4; ++a) W[4 * j + a] += (k0 * Jr[a] + k1 * Jr[4 + a]) * sp[a];
+      }
+    }
+    return any;
+  };
+  for (int c = 0; c < d.ncam; ++c) {
+    double W[28], Y[28];
+    if (!build_W(c, W)) continue;
+    const int kc = d.kc0 + 7 * c;
+    for (int j = 0; j < 7; ++j) {
+      double r = 0.0;
+      for (int a = 0; a < 4; ++a) {
+        double y = 0.0;
+        for (int e = 0; e < 4; ++e) y += W[4 * j + e] * sym4(Vi, e, a);
+        Y[4 * j + a] = y;
+        r += W[4 * j + a] * tpv[a];
+      }
+      atomicAdd(d.xc + kc + j, -r);
+    }
+    // S_kk blocks (c, c2 >= c), upper triangle
+    for (int c2 = c; c2 < d.ncam; ++c2) {
+      double W2[28];
+      if (c2 == c) {
+        for (int i = 0; i < 28; ++i) W2[i] = W[i];
+      } else if (!build_W(c2, W2)) {
+        continue;
+      }
+      const int kc2 = d.kc0 + 7 * c2;
+      for (int j = 0; j < 7; ++j)
+        for (int j2 = (c2 == c ? j : 0); j2 < 7; ++j2) {
+          double v = 0.0;
+          for (int a = 0; a < 4; ++a) v += Y[4 * j + a] * W2[4 * j2 + a];
+          atomicAdd(d.S + (size_t)(kc + j) * n + kc2 + j2, -v);
+        }
+    }
+    // S_fk: every observation of the point in a free frame block
+    for (int o = o0; o < o1; ++o) {
+      const int m = d.obs_meta[o], b = meta_block(m);
+      if ((m & kMetaFixed) || b < 0) continue;
+      double r[2], Jc[12], Jp[8];
+      load_scaled_J(d, o, b, sp, r, Jc, Jp);
+      double Mx[14];   // A_p Y^T (2x7)
+      for (int rr = 0; rr < 2; ++rr)
+        for (int j = 0; j < 7; ++j) {
+          double v = 0.0;
+          for (int a = 0; a < 4; ++a) v += Jp[4 * rr + a] * Y[4 * j + a];
+          Mx[7 * rr + j] = v;
+        }
+      for (int a = 0; a < 6; ++a)
+        for (int j = 0; j < 7; ++j)
+          atomicAdd(d.S + (size_t)(6 * b + a) * n + kc + j, -(Jc[a] * Mx[j] + Jc[6 + a] * Mx[7 + j]));
+    }
+  }
+}
+
+// Candidate intrinsics k+ = k - S x_k (Euclidean, the oracle's Plus), their step / norm terms, and the
+// stabilization model term and candidate cost.  Runs after the Cholesky kernel, adds to its slots.
+__global__ __launch_bounds__(64) void k_intr_step(Dev d) {
+  const LmState* st = d.st;
+  if (st->done) return;
+  const int lane = threadIdx.x, cur = st->cur, nxt = cur ^ 1;
+  double step2 = 0.0, candx2 = 0.0, model = 0.0, candcost = 0.0;
+  if (lane < d.ncam) {
+    const double* k = d.k[cur] + 7 * lane;
+    double* kn = d.k[nxt] + 7 * lane;
+    const int kc = d.kc0 + 7 * lane;
+    double dl[7], knv[7];
+    for (int j = 0; j < 7; ++j) {
+      dl[j] = -d.xc[kc + j] * d.scale_c[kc + j];
+      knv[j] = k[j] + dl[j];
+      kn[j] = knv[j];
+      step2 += (knv[j] - k[j]) * (knv[j] - k[j]);
+      candx2 += knv[j] * knv[j];
+    }
+    const double* ks = d.kst + 56 * lane;
+    for (int i = 0; i < 7; ++i) {
+      double mi = 0.0;
+      for (int j = 0; j < 7; ++j) mi += ks[7 + 7 * i + j] * dl[j];
+      model -= mi * (ks[i] + 0.5 * mi);
+    }
+    double res[7];
+    stab_residual(knv, res, nullptr);
+    double sq = 0.0;
+    for (int i = 0; i < 7; ++i) sq += res[i] * res[i];
+    double rho0, rho1;
+    Cauchy(sq, d.stab_b, d.stab_inv_b, &rho0, &rho1);
+    candcost = 0.5 * rho0;
+  }
+  step2 = wave_sum_full(step2);
+  candx2 = wave_sum_full(candx2);
+  model = wave_sum_full(model);
+  candcost = wave_sum_full(candcost);
+  if (lane == 0) {
+    d.xchg_chol[kCStep2] += step2;
+    d.xchg_chol[kCCandX2] += candx2;
+    d.xchg_chol[kCModel] += model;
+    d.xchg_chol[kCCandCost] += candcost;
   }
 }
 
@@ -1713,6 +1987,17 @@ __device__ __forceinline__ void pu_pass1(const Dev& d, const LinRound& R, int la
       ob.u[0] += Jc[c] * xc[c];
       ob.u[1] += Jc[6 + c] * xc[c];
     }
+  }
+  if (d.nk) {   // free intrinsics: u += A_k x_k
+    const double* Jk = d.Jk + 14 * (size_t)o;
+    const int kc = d.kc0 + 7 * ob.cam;
+    for (int c = 0; c < 7; ++c) {
+      const double xs = d.xc[kc + c] * d.scale_c[kc + c];
+      ob.u[0] += Jk[c] * xs;
+      ob.u[1] += Jk[7 + c] * xs;
+    }
+  }
+  if (ob.b >= 0 || d.nk) {
     if (pacc && (m & kMetaPfree)) {
       double* pa = pacc + (p - R.p0) * 4;
 #pragma unroll
@@ -1737,7 +2022,7 @@ __device__ __forceinline__ void pu_pass3(const Dev& d, const LinRound& R, int la
   model -= m0 * (ob.r[0] + 0.5 * m0) + m1 * (ob.r[1] + 0.5 * m1);
   const double Xn[4] = {Xns[4 * lp], Xns[4 * lp + 1], Xns[4 * lp + 2], Xns[4 * lp + 3]};
   double uv[2];
-  if (!Project(d.q[nxt] + 4 * ob.f, d.t[nxt] + 3 * ob.f, d.k + 7 * ob.cam, Xn, uv)) {
+  if (!Project(d.q[nxt] + 4 * ob.f, d.t[nxt] + 3 * ob.f, d.k[nxt] + 7 * ob.cam, Xn, uv)) {
     candfail += 1.0;
     return;
   }
@@ -1995,7 +2280,7 @@ __global__ void k_evaluate(Dev d, double* resid, double* cost_out, int32_t* nfai
   }
   const int p = lo, f = d.obs_frame[o];
   double uv[2];
-  if (!Project(d.q[cur] + 4 * f, d.t[cur] + 3 * f, d.k + 7 * d.frame_cam[f], d.X[cur] + 4 * p, uv)) {
+  if (!Project(d.q[cur] + 4 * f, d.t[cur] + 3 * f, d.k[cur] + 7 * d.frame_cam[f], d.X[cur] + 4 * p, uv)) {
     resid[2 * o] = 0.0;
     resid[2 * o + 1] = 0.0;
     atomicAdd(nfail, 1);
@@ -2111,8 +2396,8 @@ void BaSolver::Load(const sg_problem& p) {
     lt0 = t;
   };
   ValidateProblem(&p);
-  SG_REQUIRE(!p.cameras_free, SG_EINVAL,
-             "free intrinsics (SolveAllFrames(..., solve_cameras=true)) are not supported by the device solver yet");
+  SG_REQUIRE(!p.cameras_free || (p.num_cameras <= kMaxIntrCams && nranks() == 1), SG_EINVAL,
+             "free intrinsics: at most 4 cameras, on one rank (landmark shards keep the intrinsics constant)");
   SG_HIP_CHECK(hipSetDevice(dev_.device));
   F_ = p.num_frames;
   P_ = p.num_points;
@@ -2127,7 +2412,9 @@ void BaSolver::Load(const sg_problem& p) {
   NB_ = 0;
   for (int f = 0; f < F_; ++f)
     if (p.frame_rot_free[f] || p.frame_trans_free[f]) frame_block[f] = NB_++;
-  n_ = 6 * NB_;
+  nk_ = p.cameras_free ? 7 * ncam_ : 0;
+  n_ = 6 * NB_ + nk_;   // frame columns, then the free intrinsics
+  stab_b_ = p.stab_range * p.stab_range;
   lap("blocks");
   // point order: by first free block (points without free-frame observations last)
   std::vector<int32_t> pfirst(P_, NB_), plast(P_, -1), pcount(P_, 0);
@@ -2169,7 +2456,7 @@ void BaSolver::Load(const sg_problem& p) {
     obs_pt[2 * o] = p.obs_pt[2 * src];
     obs_pt[2 * o + 1] = p.obs_pt[2 * src + 1];
     obs_frame[o] = p.obs_frame[src];
-    obs_fixed[o] = frame_block[p.obs_frame[src]] < 0 && !p.point_free[p.obs_point[src]];
+    obs_fixed[o] = frame_block[p.obs_frame[src]] < 0 && !p.point_free[p.obs_point[src]] && !p.cameras_free;
   }
   SG_REQUIRE(NB_ < 0xffff && ncam_ <= 0xff, SG_EINVAL, "too many free frames or cameras for the device solver");
   std::vector<int32_t> obs_meta(M_);
@@ -2448,6 +2735,7 @@ void BaSolver::Load(const sg_problem& p) {
       if (lo_blk[b] <= blk_hi) jmax = std::max(jmax, 6 * b + 6);
     jmax = std::min(jmax, n_);
     panel_jmax[pk] = std::min(n_, (jmax + kCholNb - 1) / kCholNb * kCholNb);   // band end, 16-aligned
+    if (nk_) panel_jmax[pk] = n_;   // the intrinsics columns couple every frame: S is dense
   }
   {
     std::vector<int32_t> off(npanel + 1, 0);
@@ -2463,7 +2751,12 @@ void BaSolver::Load(const sg_problem& p) {
   lap("envelope");
   // device uploads
   hipStream_t s = stream_;
-  k_.Upload(std::vector<double>(p.k, p.k + 7 * ncam_), s);
+  {
+    std::vector<double> k2(14 * (size_t)ncam_);
+    std::copy(p.k, p.k + 7 * ncam_, k2.begin());
+    std::copy(p.k, p.k + 7 * ncam_, k2.begin() + 7 * ncam_);
+    k_.Upload(k2.empty() ? std::vector<double>{0.0} : k2, s);
+  }
   std::vector<double> q2(8 * (size_t)F_), t2(6 * (size_t)F_), X2(8 * (size_t)P_);
   std::copy(p.q, p.q + 4 * F_, q2.begin());
   std::copy(p.q, p.q + 4 * F_, q2.begin() + 4 * F_);
@@ -2544,6 +2837,11 @@ void BaSolver::Load(const sg_problem& p) {
   fd_J_.Resize(6 * (size_t)std::max(D_, 1));
   fd_D_.Resize(9 * (size_t)std::max(NB_, 1));
   fd_X_.Resize(9 * (size_t)std::max(D_, 1));
+  if (nk_) {
+    Jk_.Resize(14 * (size_t)std::max(M_, 1));
+    KU_.Resize(nn * nk_);
+    kst_.Resize(56 * (size_t)ncam_);
+  }
   st_.Zero(s);          // LmState: slot 0 current, nothing pending (evaluate() may run before begin())
   cam_wide_.Zero(s);
   S_wide_.Zero(s);
@@ -2577,7 +2875,16 @@ void BaSolver::Load(const sg_problem& p) {
 Dev BaSolver::MakeDev() {
   Dev d{};
   d.st = st_.ptr;
-  d.k = k_.ptr;
+  d.k[0] = k_.ptr;
+  d.k[1] = k_.ptr + 7 * (size_t)ncam_;
+  d.nk = nk_;
+  d.kc0 = 6 * NB_;
+  d.ncam = ncam_;
+  d.Jk = Jk_.ptr;
+  d.KU = KU_.ptr;
+  d.kst = kst_.ptr;
+  d.stab_b = stab_b_;
+  d.stab_inv_b = 1.0 / stab_b_;
   d.q[0] = q_.ptr;
   d.q[1] = q_.ptr + 4 * (size_t)F_;
   d.t[0] = t_.ptr;
@@ -2675,6 +2982,9 @@ void BaSolver::Begin(const sg_solver_options& o) {
       SG_HIP_CHECK(hipMemcpyAsync(q_.ptr, q_.ptr + 4 * (size_t)F_, 4 * (size_t)F_ * 8, hipMemcpyDeviceToDevice, stream_));
       SG_HIP_CHECK(hipMemcpyAsync(t_.ptr, t_.ptr + 3 * (size_t)F_, 3 * (size_t)F_ * 8, hipMemcpyDeviceToDevice, stream_));
       SG_HIP_CHECK(hipMemcpyAsync(X_.ptr, X_.ptr + 4 * (size_t)P_, 4 * (size_t)P_ * 8, hipMemcpyDeviceToDevice, stream_));
+      if (ncam_ > 0)
+        SG_HIP_CHECK(hipMemcpyAsync(k_.ptr, k_.ptr + 7 * (size_t)ncam_, 7 * (size_t)ncam_ * 8, hipMemcpyDeviceToDevice,
+                                    stream_));
     }
     began_ = true;
   }
@@ -2733,6 +3043,11 @@ void BaSolver::Iterate(int n) {
     hipLaunchKernelGGL(k_cam_reduce, dim3(NB_ + 1), dim3(kRedThreads), 0, stream_, d);
     TimedLaunchEnd(kKCamReduce);
     AllReduceSum(xchg_cam_.ptr, (size_t)nv + kXNum + nranks());
+    if (nk_) {
+      hipLaunchKernelGGL(k_intr_zero, dim3((n_ * nk_ + 255) / 256), dim3(256), 0, stream_, d);
+      hipLaunchKernelGGL(k_intr_lin, dim3((std::max(M_, 1) + 255) / 256), dim3(256), 0, stream_, d);
+      hipLaunchKernelGGL(k_intr_fin, dim3(1), dim3(64), 0, stream_, d);
+    }
     TimedLaunchBegin(kKCamFinal);
     hipLaunchKernelGGL(k_cam_finalize, dim3(1), dim3(256), 0, stream_, d);
     TimedLaunchEnd(kKCamFinal);
@@ -2743,6 +3058,10 @@ void BaSolver::Iterate(int n) {
     const int nwv = NB_ * (NB_ + 1) / 2 + NB_;
     hipLaunchKernelGGL(k_S_reduce, dim3(std::max(nwv, 1)), dim3(256), 0, stream_, d);
     TimedLaunchEnd(kKSReduce);
+    if (nk_) {
+      hipLaunchKernelGGL(k_intr_assemble, dim3((n_ * nk_ + 255) / 256), dim3(256), 0, stream_, d);
+      hipLaunchKernelGGL(k_intr_schur, dim3((std::max(P_, 1) + 127) / 128), dim3(128), 0, stream_, d);
+    }
     if ((comm_ && comm_->nranks() > 1) || pack_force_) {
       // the band of S and the rhs partial are summed over landmark shards (packed: the band only)
       const int npanel = (n_ + kCholNb - 1) / kCholNb;
@@ -2764,6 +3083,7 @@ void BaSolver::Iterate(int n) {
       hipLaunchKernelGGL(k_cholesky_global, dim3(1), dim3(kCholThreads), (size_t)std::max(n_, 1) * 8, stream_, d,
                          (const int32_t*)work_i_.ptr, rdg_.ptr);
     TimedLaunchEnd(kKChol);
+    if (nk_) hipLaunchKernelGGL(k_intr_step, dim3(1), dim3(64), 0, stream_, d);
     TimedLaunchBegin(kKPointUpd);
     hipLaunchKernelGGL(k_point_update, dim3(std::max(npu_, 1)), dim3(kLinThreads), 0, stream_, d);
     TimedLaunchEnd(kKPointUpd);
@@ -2840,6 +3160,11 @@ void BaSolver::Download(sg_problem* p) {
   SG_HIP_CHECK(hipStreamSynchronize(stream_));
   std::copy(q.begin(), q.end(), p->q);
   std::copy(t.begin(), t.end(), p->t);
+  if (nk_) {
+    SG_HIP_CHECK(hipMemcpyAsync(p->k, k_.ptr + 7 * (size_t)ncam_ * h.cur, 7 * (size_t)ncam_ * 8,
+                                hipMemcpyDeviceToHost, stream_));
+    SG_HIP_CHECK(hipStreamSynchronize(stream_));
+  }
   for (int i = 0; i < P_; ++i) {
     const int pt = point_perm_[i];
     for (int a = 0; a < 4; ++a) p->X[4 * pt + a] = X[4 * i + a];

@@ -239,3 +239,63 @@ def test_packed_band_exchange_is_exact(gpu_lib, monkeypatch):
     np.testing.assert_allclose(p0.q, p1.q, rtol=0, atol=1e-12)
     np.testing.assert_allclose(p0.t, p1.t, rtol=1e-9, atol=1e-9)
     np.testing.assert_allclose(p0.X, p1.X, rtol=1e-9, atol=1e-12)
+
+
+def _intrinsics_scene(seed=1):
+    """C1-sized scene whose intrinsics start off the generating camera (focal +0.4 %, principal point +1.5 px,
+    a little radial distortion), so SolveAllFrames(..., solve_cameras=true) has intrinsics to recover."""
+    m = make_scene(num_frames=10, num_points=500, seed=seed, run_max=14)
+    for c in range(len(m.k) // 7):
+        k = m.k[7 * c:7 * c + 7]
+        k[0] += 2e-3
+        k[3] *= 1.004
+        k[4] *= 1.004
+        k[5] += 1.5
+        k[6] -= 1.5
+    return m
+
+
+def test_free_intrinsics_first_steps_match_oracle(gpu_lib, oracle_lib):
+    """Two LM iterations with the intrinsics free (slam.cpp:447-480): the k columns of the reduced system
+    (J_k terms, CameraStabilization, their point elimination) and the candidate intrinsics match the
+    oracle's dense solve."""
+    m = _intrinsics_scene()
+    pa = ba.problem_from_map_all(m, 2.0, solve_cameras=True)
+    assert pa.cameras_free == 1
+    o = default_solver_options(max_num_iterations=2, function_tolerance=1e-9)
+    pg, sg, po, so = _solve_both(oracle_lib, pa, o)
+    assert sg["ok"] == so["ok"] == 1
+    assert abs(sg["initial_cost"] - so["initial_cost"]) <= 1e-10 * so["initial_cost"]
+    assert sg["num_successful_steps"] == so["num_successful_steps"]
+    assert abs(sg["final_cost"] - so["final_cost"]) <= 1e-8 * so["final_cost"]
+    np.testing.assert_allclose(pg.k, po.k, rtol=1e-7, atol=1e-9)
+    np.testing.assert_allclose(pg.t, po.t, atol=1e-5)
+
+
+def test_free_intrinsics_solve_matches_oracle(gpu_lib, oracle_lib):
+    """A full SolveAllFrames(..., true) solve (fine tolerance 1e-9): same minimum as the oracle.  All frames are
+    free here (7-DoF gauge), so poses are compared through the residuals; the intrinsics are gauge-invariant."""
+    m = _intrinsics_scene(seed=3)
+    pa = ba.problem_from_map_all(m, 2.0, solve_cameras=True)
+    o = default_solver_options(function_tolerance=1e-9)
+    pg, sg, po, so = _solve_both(oracle_lib, pa, o)
+    assert sg["ok"] == so["ok"] == 1
+    assert abs(sg["final_cost"] - so["final_cost"]) <= 1e-6 * so["final_cost"]
+    rg, _, fg = oracle_lib.evaluate(pg)
+    ro, _, fo = oracle_lib.evaluate(po)
+    assert fg == fo == 0
+    assert abs(np.sqrt((rg ** 2).mean()) - np.sqrt((ro ** 2).mean())) <= 1e-4
+    np.testing.assert_allclose(pg.k, po.k, rtol=1e-5, atol=1e-6)
+
+
+def test_slam_solve_all_frames_with_cameras(gpu_lib, oracle_lib):
+    """Slam::SolveAllFrames(map, 2.0, true) through the facade writes the solved intrinsics back to the map."""
+    m = _intrinsics_scene(seed=4)
+    mg, mo = m.copy(), m.copy()
+    slam = ba.Slam()
+    ok_g = slam.SolveAllFrames(mg, 2.0, True)
+    ok_o, so = oracle_lib.slam_solve_all_frames(mo, 2.0, True)
+    assert ok_g == ok_o is True
+    assert abs(slam.error() - so["final_cost"]) <= 1e-6 * so["final_cost"]
+    np.testing.assert_allclose(mg.k, mo.k, rtol=1e-5, atol=1e-6)
+    assert not np.allclose(mg.k, m.k)
