@@ -187,6 +187,10 @@ int sg_comm_unique_id(void* id128);
 int sg_ba_comm_init(sg_ba* h, const void* id128, int32_t nranks, int32_t rank);
 /* Upload a problem (the problem's q/t/X are read now and written back by sg_ba_download). */
 int sg_ba_load(sg_ba* h, const sg_problem* p);
+/* Incremental problem update (replaces the per-call rebuild of slam.cpp:257-414): a
+ * load whose structure equals the previous load's (frames, cameras, freedom flags, observation incidence,
+ * FrameDistance pairs) re-uploads the values only.  Counts of full and value-only loads on this handle. */
+int sg_ba_load_counts(const sg_ba* h, int32_t* full_loads, int32_t* value_loads);
 /* Run the LM solve on the device; writes the solved blocks back into p. */
 int sg_ba_solve(sg_ba* h, const sg_solver_options* o, sg_problem* p, sg_solver_summary* s);
 /* Benchmark entry: (re)initialise from the uploaded state, then enqueue exactly n LM iterations without
@@ -223,6 +227,7 @@ int sg_slam_solve_all_frames(sg_slam* s, sg_map* map, double range, int32_t solv
 int sg_slam_reproject_map(sg_slam* s, sg_map* map, double* mean);               /* slam.cpp:523-548 */
 int32_t sg_slam_iterations(const sg_slam* s);                                    /* slam.h:49 */
 double sg_slam_error(const sg_slam* s);                                          /* slam.h:50 */
+int sg_slam_load_counts(const sg_slam* s, int32_t* full_loads, int32_t* value_loads);   /* see sg_ba_load_counts */
 int sg_slam_last_summary(const sg_slam* s, sg_solver_summary* out);
 
 /* ------------------------------------------------------------------------------------------------

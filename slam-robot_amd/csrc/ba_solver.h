@@ -67,6 +67,29 @@ class BaSolver {
   std::vector<int32_t> point_perm_;   // device order -> problem point
   std::vector<int32_t> obs_perm_;     // device order -> problem observation
   size_t schur_lds_ = 0;
+  // Incremental problem update (replacing the per-call rebuild of slam.cpp:257-414):
+  // the structure of the last Load.  A Load with the same structure (frames, cameras, freedom flags,
+  // observation -> frame / point incidence, FrameDistance pairs) keeps the point order, the CSR, the sweep
+  // chunks, Schur segments, pair and reduction lists and the Cholesky envelope, and uploads the values only.
+  struct StructKey {
+    int32_t ncam = -1, cams_free = 0, F = -1, P = -1, M = -1, D = -1;
+    std::vector<int32_t> frame_camera, obs_frame, obs_point, dist_frame, dist_prev;
+    std::vector<uint8_t> rot_free, trans_free, point_free;
+  } skey_;
+  int32_t full_loads_ = 0, value_loads_ = 0;
+  bool SameStructure(const sg_problem& p) const;
+  void SaveStructure(const sg_problem& p);
+  void LoadValues(const sg_problem& p);
+  void ResetState(hipStream_t s);
+
+ public:
+  // loads that rebuilt the structure / loads that re-uploaded values only
+  void LoadCounts(int32_t* full, int32_t* values) const {
+    *full = full_loads_;
+    *values = value_loads_;
+  }
+
+ private:
   // device buffers
   DBuf<LmState> st_;
   DBuf<double> k_, q_, t_, X_, obs_pt_, J_, V_, g_, scale_p_, diag_p_, Vinv_, tp_, scale_c_, diag_c_, camdiag_,

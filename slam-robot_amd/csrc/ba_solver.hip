@@ -2399,6 +2399,23 @@ void BaSolver::Load(const sg_problem& p) {
   SG_REQUIRE(!p.cameras_free || (p.num_cameras <= kMaxIntrCams && nranks() == 1), SG_EINVAL,
              "free intrinsics: at most 4 cameras, on one rank (landmark shards keep the intrinsics constant)");
   SG_HIP_CHECK(hipSetDevice(dev_.device));
+  {
+    // incremental update: every rank must take the same path (the full path has a load-time all-reduce)
+    double changed = (loaded_ && !getenv("SG_NO_REUSE") && SameStructure(p)) ? 0.0 : 1.0;
+    if (comm_ && comm_->nranks() > 1) {
+      DBuf<double> flag;
+      flag.Upload(std::vector<double>{changed}, stream_);
+      comm_->AllReduceMax(flag.ptr, 1, stream_);
+      SG_HIP_CHECK(hipMemcpyAsync(&changed, flag.ptr, sizeof(double), hipMemcpyDeviceToHost, stream_));
+      SG_HIP_CHECK(hipStreamSynchronize(stream_));
+    }
+    if (changed == 0.0) {
+      LoadValues(p);
+      lap("values");
+      if (host_timing) fprintf(stderr, "[sg] Load phases (ms):%s\n", lap_log.c_str());
+      return;
+    }
+  }
   F_ = p.num_frames;
   P_ = p.num_points;
   M_ = p.num_obs;
@@ -2785,7 +2802,6 @@ void BaSolver::Load(const sg_problem& p) {
   segs_.Upload(segs.empty() ? std::vector<SchurSeg>(1) : segs, s);
   pairs_.Upload(pairs_flat, s);
   seg_fail_.Resize(std::max(nseg_, 1));
-  seg_fail_.Zero(s);
   cam_loff_.Upload(cam_loff, s);
   cam_lidx_.Upload(cam_lidx, s);
   s_loff_.Upload(s_loff, s);
@@ -2821,7 +2837,6 @@ void BaSolver::Load(const sg_problem& p) {
   camg_.Resize(nn);
   cam_slab_.Resize(std::max(lcam_off, 1));
   lin_scal_.Resize((size_t)std::max(nlin_, 1) * kNScal);
-  lin_scal_.Zero(s);
   S_slab_.Resize(std::max(s_off, 1));
   chunk_scal_.Resize((size_t)std::max(npu_, 1) * kNScal);
   pu_units_.Upload(pu_units, s);
@@ -2842,12 +2857,9 @@ void BaSolver::Load(const sg_problem& p) {
     KU_.Resize(nn * nk_);
     kst_.Resize(56 * (size_t)ncam_);
   }
-  st_.Zero(s);          // LmState: slot 0 current, nothing pending (evaluate() may run before begin())
-  cam_wide_.Zero(s);
-  S_wide_.Zero(s);
-  rhs_.Zero(s);
-  chunk_scal_.Zero(s);
-  S_.Zero(s);
+  stamp_on_ = getenv("SG_STAMP") && getenv("SG_STAMP")[0] == '1';
+  if (stamp_on_) stamps_.Resize(64);
+  ResetState(s);
   schur_lds_ = sizeof(double) * ((size_t)max_seg_nb_ * (max_seg_nb_ + 1) / 2 * kWinLd + max_seg_nb_ * 6 +
                                   (size_t)kSegPts * 14 + (size_t)std::max(max_seg_obs_, 1) * 8);
   SG_HIP_CHECK(hipFuncSetAttribute((const void*)k_schur, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2856,18 +2868,94 @@ void BaSolver::Load(const sg_problem& p) {
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCholLds));
   SG_HIP_CHECK(hipFuncSetAttribute((const void*)k_cholesky_window<true>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCholLds));
-  stamp_on_ = getenv("SG_STAMP") && getenv("SG_STAMP")[0] == '1';
-  if (stamp_on_) {
-    stamps_.Resize(64);
-    stamps_.Zero(s);
-  }
   SG_HIP_CHECK(hipStreamSynchronize(s));
   lap("uploads");
+  SaveStructure(p);
+  full_loads_++;
   if (host_timing) {
     SG_HIP_CHECK(hipStreamSynchronize(stream_));
     lap("sync");
     fprintf(stderr, "[sg] Load phases (ms):%s\n", lap_log.c_str());
   }
+  loaded_ = true;
+  began_ = false;
+}
+
+bool BaSolver::SameStructure(const sg_problem& p) const {
+  const StructKey& k = skey_;
+  if (p.num_cameras != k.ncam || (p.cameras_free != 0) != (k.cams_free != 0) || p.num_frames != k.F ||
+      p.num_points != k.P || p.num_obs != k.M || p.num_dist != k.D)
+    return false;
+  auto same = [](const auto* a, const auto& v) {
+    return v.empty() || std::memcmp(a, v.data(), v.size() * sizeof(v[0])) == 0;
+  };
+  return same(p.frame_camera, k.frame_camera) && same(p.frame_rot_free, k.rot_free) &&
+         same(p.frame_trans_free, k.trans_free) && same(p.point_free, k.point_free) &&
+         same(p.obs_frame, k.obs_frame) && same(p.obs_point, k.obs_point) && same(p.dist_frame, k.dist_frame) &&
+         same(p.dist_prev, k.dist_prev);
+}
+
+void BaSolver::SaveStructure(const sg_problem& p) {
+  StructKey& k = skey_;
+  k.ncam = p.num_cameras;
+  k.cams_free = p.cameras_free != 0;
+  k.F = p.num_frames;
+  k.P = p.num_points;
+  k.M = p.num_obs;
+  k.D = p.num_dist;
+  k.frame_camera.assign(p.frame_camera, p.frame_camera + k.F);
+  k.rot_free.assign(p.frame_rot_free, p.frame_rot_free + k.F);
+  k.trans_free.assign(p.frame_trans_free, p.frame_trans_free + k.F);
+  k.point_free.assign(p.point_free, p.point_free + k.P);
+  k.obs_frame.assign(p.obs_frame, p.obs_frame + k.M);
+  k.obs_point.assign(p.obs_point, p.obs_point + k.M);
+  k.dist_frame.assign(p.dist_frame, p.dist_frame + k.D);
+  k.dist_prev.assign(p.dist_prev, p.dist_prev + k.D);
+}
+
+// LM state and accumulators a fresh solve starts from (zeroed on every Load)
+void BaSolver::ResetState(hipStream_t s) {
+  st_.Zero(s);          // LmState: slot 0 current, nothing pending (evaluate() may run before begin())
+  lin_scal_.Zero(s);
+  seg_fail_.Zero(s);
+  cam_wide_.Zero(s);
+  S_wide_.Zero(s);
+  rhs_.Zero(s);
+  chunk_scal_.Zero(s);
+  S_.Zero(s);
+  if (stamp_on_) stamps_.Zero(s);
+}
+
+// Same structure as the last Load: new values (poses, intrinsics, points, observed pixels, loss ranges) in
+// the device order of that Load; every index list and the Cholesky envelope stay.
+void BaSolver::LoadValues(const sg_problem& p) {
+  range_b_ = p.range * p.range;
+  fd_target_ = p.dist_target;
+  fd_b2_ = p.dist_range * p.dist_range;
+  stab_b_ = p.stab_range * p.stab_range;
+  hipStream_t s = stream_;
+  std::vector<double> k2(14 * (size_t)ncam_), q2(8 * (size_t)F_), t2(6 * (size_t)F_), X2(8 * (size_t)P_),
+      obs_pt(2 * (size_t)M_);
+  for (int c = 0; c < 7 * ncam_; ++c) k2[c] = k2[c + 7 * ncam_] = p.k[c];
+  for (int i = 0; i < 4 * F_; ++i) q2[i] = q2[i + 4 * F_] = p.q[i];
+  for (int i = 0; i < 3 * F_; ++i) t2[i] = t2[i + 3 * F_] = p.t[i];
+  for (int i = 0; i < P_; ++i) {
+    const int pt = point_perm_[i];
+    for (int a = 0; a < 4; ++a) X2[4 * i + a] = X2[4 * (i + P_) + a] = p.X[4 * pt + a];
+  }
+  for (int o = 0; o < M_; ++o) {
+    const int src = obs_perm_[o];
+    obs_pt[2 * o] = p.obs_pt[2 * src];
+    obs_pt[2 * o + 1] = p.obs_pt[2 * src + 1];
+  }
+  k_.Upload(k2.empty() ? std::vector<double>{0.0} : k2, s);
+  q_.Upload(q2, s);
+  t_.Upload(t2, s);
+  X_.Upload(X2, s);
+  obs_pt_.Upload(obs_pt, s);
+  ResetState(s);
+  SG_HIP_CHECK(hipStreamSynchronize(s));
+  value_loads_++;
   loaded_ = true;
   began_ = false;
 }

@@ -63,6 +63,13 @@ int sg_ba_load(sg_ba* h, const sg_problem* p) {
   SG_CAPI_END
 }
 
+int sg_ba_load_counts(const sg_ba* h, int32_t* full_loads, int32_t* value_loads) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(h && full_loads && value_loads, SG_EINVAL, "null argument");
+  h->solver->LoadCounts(full_loads, value_loads);
+  SG_CAPI_END
+}
+
 int sg_ba_solve(sg_ba* h, const sg_solver_options* o, sg_problem* p, sg_solver_summary* s) {
   SG_CAPI_BEGIN
   SG_REQUIRE(h && p && s, SG_EINVAL, "null argument");
@@ -270,6 +277,14 @@ int sg_map_apply_epipolar(sg_slam* s, sg_map* map, int32_t* num_violations) {
 
 int32_t sg_slam_iterations(const sg_slam* s) { return s ? s->iterations : 0; }
 double sg_slam_error(const sg_slam* s) { return s ? s->error : 0.0; }
+
+int sg_slam_load_counts(const sg_slam* s, int32_t* full_loads, int32_t* value_loads) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(s && full_loads && value_loads, SG_EINVAL, "null argument");
+  *full_loads = *value_loads = 0;
+  if (s->solver) s->solver->LoadCounts(full_loads, value_loads);
+  SG_CAPI_END
+}
 
 int sg_slam_last_summary(const sg_slam* s, sg_solver_summary* out) {
   SG_CAPI_BEGIN

@@ -96,6 +96,12 @@ class BundleAdjuster:
         ps = pa.struct()
         check(self.lib.sg_ba_load(self.h, C.byref(ps)), "sg_ba_load")
 
+    def load_counts(self) -> tuple:
+        """(full loads, value-only loads): a load with the previous load's structure reuses its index lists."""
+        full, vals = C.c_int32(0), C.c_int32(0)
+        check(self.lib.sg_ba_load_counts(self.h, C.byref(full), C.byref(vals)), "sg_ba_load_counts")
+        return full.value, vals.value
+
     def solve(self, options: SgSolverOptions = None) -> dict:
         o = options or default_solver_options()
         s = SgSolverSummary()
@@ -216,6 +222,12 @@ class Slam:
 
     def iterations(self) -> int:
         return int(self.lib.sg_slam_iterations(self.h))
+
+    def load_counts(self) -> tuple:
+        """(full loads, value-only loads) of SolveFrames / SolveAllFrames calls on this object."""
+        full, vals = C.c_int32(0), C.c_int32(0)
+        check(self.lib.sg_slam_load_counts(self.h, C.byref(full), C.byref(vals)), "sg_slam_load_counts")
+        return full.value, vals.value
 
     def error(self) -> float:
         return float(self.lib.sg_slam_error(self.h))

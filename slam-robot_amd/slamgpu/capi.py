@@ -239,6 +239,7 @@ SYMBOLS = {
     "sg_comm_unique_id": (C.c_int, [C.c_void_p]),
     "sg_ba_comm_init": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32]),
     "sg_ba_load": (C.c_int, [C.c_void_p, C.POINTER(SgProblem)]),
+    "sg_ba_load_counts": (C.c_int, [C.c_void_p, _ip, _ip]),
     "sg_ba_solve": (C.c_int, [C.c_void_p, C.POINTER(SgSolverOptions), C.POINTER(SgProblem),
                               C.POINTER(SgSolverSummary)]),
     "sg_ba_begin": (C.c_int, [C.c_void_p, C.POINTER(SgSolverOptions)]),
@@ -282,6 +283,7 @@ SYMBOLS = {
     "sg_map_clean": (C.c_int, [C.c_void_p, C.POINTER(SgMap), C.c_double, C.POINTER(C.c_int32)]),
     "sg_map_apply_epipolar": (C.c_int, [C.c_void_p, C.POINTER(SgMap), C.POINTER(C.c_int32)]),
     "sg_slam_iterations": (C.c_int32, [C.c_void_p]),
+    "sg_slam_load_counts": (C.c_int, [C.c_void_p, _ip, _ip]),
     "sg_slam_error": (C.c_double, [C.c_void_p]),
     "sg_slam_last_summary": (C.c_int, [C.c_void_p, C.POINTER(SgSolverSummary)]),
     "sg_slam_set_options": (C.c_int, [C.c_void_p, C.POINTER(SgSolverOptions)]),
