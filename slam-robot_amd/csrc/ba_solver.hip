@@ -2443,12 +2443,19 @@ void BaSolver::Load(const sg_problem& p) {
       plast[pt] = std::max(plast[pt], b);
     }
   }
+  // stable counting sort on the key pfirst in [0, NB]
   point_perm_.resize(P_);
-  std::iota(point_perm_.begin(), point_perm_.end(), 0);
-  std::stable_sort(point_perm_.begin(), point_perm_.end(),
-                   [&](int a, int b) { return pfirst[a] < pfirst[b]; });
   std::vector<int32_t> inv_perm(P_);
-  for (int i = 0; i < P_; ++i) inv_perm[point_perm_[i]] = i;
+  {
+    std::vector<int32_t> bstart(NB_ + 2, 0);
+    for (int i = 0; i < P_; ++i) bstart[pfirst[i] + 1]++;
+    for (int b = 0; b <= NB_; ++b) bstart[b + 1] += bstart[b];
+    for (int i = 0; i < P_; ++i) {
+      const int pos = bstart[pfirst[i]]++;
+      point_perm_[pos] = i;
+      inv_perm[i] = pos;
+    }
+  }
   lap("point-order");
   // observations: CSR by device point order (stable in problem order)
   std::vector<int32_t> poff(P_ + 1, 0);
@@ -2468,20 +2475,23 @@ void BaSolver::Load(const sg_problem& p) {
     pfree[i] = p.point_free[pt];
     for (int a = 0; a < 4; ++a) X[4 * i + a] = p.X[4 * pt + a];
   }
-  for (int o = 0; o < M_; ++o) {
-    const int src = obs_perm_[o];
-    obs_pt[2 * o] = p.obs_pt[2 * src];
-    obs_pt[2 * o + 1] = p.obs_pt[2 * src + 1];
-    obs_frame[o] = p.obs_frame[src];
-    obs_fixed[o] = frame_block[p.obs_frame[src]] < 0 && !p.point_free[p.obs_point[src]] && !p.cameras_free;
-  }
   SG_REQUIRE(NB_ < 0xffff && ncam_ <= 0xff, SG_EINVAL, "too many free frames or cameras for the device solver");
   std::vector<int32_t> obs_meta(M_);
-  for (int o = 0; o < M_; ++o) {
-    const int src = obs_perm_[o], f = p.obs_frame[src];
-    obs_meta[o] = (frame_block[f] + 1) | (p.frame_camera[f] << kMetaCamShift) |
-                  (p.frame_rot_free[f] ? kMetaRot : 0) | (p.frame_trans_free[f] ? kMetaTrans : 0) |
-                  (p.point_free[p.obs_point[src]] ? kMetaPfree : 0) | (obs_fixed[o] ? kMetaFixed : 0);
+  {
+    // per frame: the frame part of the packed observation word
+    std::vector<int32_t> fmeta(F_);
+    for (int f = 0; f < F_; ++f)
+      fmeta[f] = (frame_block[f] + 1) | (p.frame_camera[f] << kMetaCamShift) | (p.frame_rot_free[f] ? kMetaRot : 0) |
+                 (p.frame_trans_free[f] ? kMetaTrans : 0);
+    for (int o = 0; o < M_; ++o) {
+      const int src = obs_perm_[o], f = p.obs_frame[src];
+      const bool pf = p.point_free[p.obs_point[src]] != 0;
+      obs_pt[2 * o] = p.obs_pt[2 * src];
+      obs_pt[2 * o + 1] = p.obs_pt[2 * src + 1];
+      obs_frame[o] = f;
+      obs_fixed[o] = frame_block[f] < 0 && !pf && !p.cameras_free;
+      obs_meta[o] = fmeta[f] | (pf ? kMetaPfree : 0) | (obs_fixed[o] ? kMetaFixed : 0);
+    }
   }
   lap("obs-csr");
   // k_linearize decomposition (see LinChunk): rounds of whole points (<= kLinObs observations), up to
@@ -2582,6 +2592,19 @@ void BaSolver::Load(const sg_problem& p) {
     for (int o = poff[i]; o < poff[i + 1]; ++o) obs_pnt[o] = i;
   std::vector<SchurSeg> segs;
   std::vector<int32_t> pairs_flat;   // int2 per pair
+  std::vector<int32_t> obs_blk(M_);
+  {
+    size_t npairs = 0;
+    for (int i = 0; i < P_; ++i) {
+      size_t kb = 0;
+      for (int o = poff[i]; o < poff[i + 1]; ++o) {
+        obs_blk[o] = frame_block[obs_frame[o]];
+        kb += obs_blk[o] >= 0;
+      }
+      if (pfree[i]) npairs += kb * (kb + 1) / 2;
+    }
+    pairs_flat.reserve(2 * npairs + 2);
+  }
   int s_off = 0;
   max_seg_nb_ = 0;
   {
@@ -2632,10 +2655,10 @@ void BaSolver::Load(const sg_problem& p) {
       for (int pt = i; pt < j; ++pt) {
         if (!pfree[pt]) continue;
         for (int os = poff[pt]; os < poff[pt + 1]; ++os) {
-          const int bs = frame_block[obs_frame[os]];
+          const int bs = obs_blk[os];
           if (bs < 0) continue;
           for (int ot = os; ot < poff[pt + 1]; ++ot) {
-            const int bt = frame_block[obs_frame[ot]];
+            const int bt = obs_blk[ot];
             if (bt < 0) continue;
             pairs_flat.push_back(((os - obs_lo) << 16) | (ot - obs_lo));
             pairs_flat.push_back((bs << 16) | bt);
