@@ -193,7 +193,9 @@ __device__ __forceinline__ float sample(const float* img, int w, const Geo& g, i
   const int c1 = zero ? 0 : (edge ? ce : g.col0 + jj + 1);
   const size_t r1 = zero ? 0 : (size_t)row * w;
   const size_t r2 = (zero || same) ? r1 : r1 + w;
-  const float v11 = img[r1 + c0], v12 = img[r1 + c1], v21 = img[r2 + c0], v22 = img[r2 + c1];
+  // image levels live in device global memory: global (not flat) loads, so the waits count vmcnt only
+  const __attribute__((address_space(1))) float* gi = (const __attribute__((address_space(1))) float*)img;
+  const float v11 = gi[r1 + c0], v12 = gi[r1 + c1], v21 = gi[r2 + c0], v22 = gi[r2 + c1];
   const float re = v11 * g.b1 + v21 * g.b2;
   const float rb = v11 * g.a11 + v12 * g.a12 + v21 * g.a21 + v22 * g.a22;
   return zero ? 0.f : (edge ? re : rb);
