@@ -91,6 +91,10 @@ def bench_tracker(local, cpu_seconds):
            "value": value, "unit": "tracks/s", "ms_per_frame_tracking": ms, "ms_pyramid": pyr_ms,
            "tracks_per_s_with_pyramid": len(pts) / ((ms + pyr_ms) * 1e-3),
            "accepted_frac": float(acc.mean()), "newton_iterations": int(its.sum()),
+           # one wave per track and ~2 waves per SIMD: the launch lasts as long as its longest serial
+           # Newton chain, so the per-iteration latency of that chain is the number that bounds the kernel
+           "newton_iterations_max_track": int(its.max()),
+           "us_per_newton_iteration_on_longest_track": ms * 1e3 / max(int(its.max()), 1),
            "roofline": {"bound": "valu", "achieved": ach, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                         "frac": ach / FP32_PEAK_TFLOPS, "traffic": pmc_traffic("k_track_fb"), "kernel": "k_track_fb",
                         "note": "108*W^2 flops per Newton iteration (6 probes of bilinear sampling, moments, "
