@@ -40,4 +40,7 @@ def test_null_arguments_return_einval():
     lib = load_library()
     assert lib.sg_ba_load(None, None) == -22
     assert lib.sg_problem_write_back(None, None) == -22
+    full, vals = C.c_int32(7), C.c_int32(7)
+    assert lib.sg_ba_load_counts(None, C.byref(full), C.byref(vals)) == -22
+    assert lib.sg_slam_load_counts(None, C.byref(full), C.byref(vals)) == -22
     assert lib.sg_last_error()
