@@ -52,6 +52,9 @@ class BaSolver {
   bool loaded_ = false;
   bool began_ = false;
   bool chol_window_ = true;
+  bool chol_tiles_ = false;    // tiled register-resident band Cholesky (k_chol_tiles)
+  size_t tile_lds_ = 0;        // its dynamic LDS
+  DBuf<double> Wg_;            // its back-substitution tiles W_KJ = U_KK^-1 U_KJ
   bool pack_force_ = getenv("SG_PACK_S") != nullptr;   // pack/unpack S on one rank too (tests the path)
   size_t npack_ = 0;                                      // band of S + rhs, doubles (all-reduce size)
   bool stamp_on_ = false;

@@ -1377,9 +1377,10 @@ __device__ __noinline__ void chol_backsub(const double* A, const double* rdg, do
 }
 
 // Candidate camera poses x+ = Plus(x, -S x_c) for every frame, FrameDistance model / candidate terms.
+template <int NT>
 __device__ __forceinline__ void chol_candidates(const Dev& d, const double* y, int fail) {
   const LmState* st = d.st;
-  __shared__ double red[kCholThreads / 64];
+  __shared__ double red[4 * NT / 64];
   const int tid = threadIdx.x;
   const int cur = st->cur, nxt = cur ^ 1;
   double step2 = 0.0, candx2 = 0.0, model = 0.0, candcost = 0.0;
@@ -1430,10 +1431,12 @@ __device__ __forceinline__ void chol_candidates(const Dev& d, const double* y, i
     Cauchy(r * r, d.fd_b2, d.fd_inv_b2, &rho0, &rho1);
     candcost += 0.5 * rho0;
   }
-  step2 = block_sum<kCholThreads>(step2, red);
-  candx2 = block_sum<kCholThreads>(candx2, red);
-  model = block_sum<kCholThreads>(model, red);
-  candcost = block_sum<kCholThreads>(candcost, red);
+  double sums[4] = {step2, candx2, model, candcost};
+  block_sum_multi<NT, 4>(sums, red);
+  step2 = sums[0];
+  candx2 = sums[1];
+  model = sums[2];
+  candcost = sums[3];
   if (tid == 0) {
     d.xchg_chol[kCStep2] = step2;
     d.xchg_chol[kCCandX2] = candx2;
@@ -1859,7 +1862,7 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
   }
   __syncthreads();
   SG_STAMP_AT(6)
-  chol_candidates(d, xs, fail_sh);
+  chol_candidates<kCholThreads>(d, xs, fail_sh);
   SG_STAMP_AT(7)
   SG_STAMP_FLUSH()
 }
@@ -1944,8 +1947,402 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_global(Dev d, const i
   chol_backsub(A, rdg, y, xs, n, panel_jend);
   for (int i = tid; i < n; i += kCholThreads) d.xc[i] = xs[i];
   __syncthreads();
-  chol_candidates(d, y, fail_sh);
+  chol_candidates<kCholThreads>(d, y, fail_sh);
 }
+
+// ------------------------------------------------------------------------------------------------
+// Tiled band Cholesky — the default reduced-camera solve (SPARSE_SCHUR + CHOLMOD behind slam.cpp:489,
+// restated as a dense banded factorisation S = U^T U of 16 x 16 tiles, right-looking, with the band of tile
+// columns resident in registers as MFMA accumulators).
+//   * 8 waves; wave w owns tile column J = w (mod 8): its tiles (I, J), J - 7 <= I <= J, live in slot I & 7
+//     of f64x4 acc[8] (v_mfma_f64_16x16x4f64 C/D layout: lane l holds rows (l >> 4) + 4 q of column l & 15).
+//     A column retires when it becomes the diagonal; its wave then loads column J + 8 from S.
+//   * One phase (one LDS barrier) per tile row K; every wave, in order:
+//       (0) the trailing update of its column by row K-1, A_IJ -= U_{K-1,I}^T U_{K-1,J} (four MFMAs a tile,
+//           U_{K-1,I} from LDS), row K first;
+//       (1) the TRSM of its row-K tile, U_KJ = Z_K A_KJ (MFMA with Z_K = U_KK^-T), posted to LDS for (0) of
+//           the next phase, and its rhs term y_J -= U_KJ^T z_K (per-lane partials);
+//       (2) the owner of column K+1 applies row K to D_{K+1} and factors it on the spot with the identity
+//           and y_{K+1} as augmented columns (right-looking, two pivots per LDS broadcast), posting Z_{K+1},
+//           z_{K+1} = Z_{K+1} y_{K+1} and Z_{K+1}^T z_{K+1} — the critical path of the phase, overlapping
+//           every other wave's trailing update;
+//       (3) W_KJ = Z_K^T U_KJ (= U_KK^-1 U_KJ) to global memory for the back substitution;
+//       (4) the owner reloads.
+//   * Back substitution x_K = Z_K^T z_K - sum_d W_{K,K+d} x_{K+d}: wave w forms the d = w + 1 term (W tiles
+//     prefetched four rows ahead), one barrier per tile row, every wave sums the partials in the same order.
+// Requires a band of at most 8 tiles per tile row (the sliding window's co-visibility band at the configured
+// window sizes); wider bands take k_cholesky_global.
+constexpr int kTB = 8;                         // band width in tiles = waves
+constexpr int kTileThreads = kTB * 64;
+constexpr int kTLd = 17;                       // LDS pitch of a 16 x 16 tile
+constexpr int kTileMaxNT = 400;                // dynamic LDS: x, z' (16 NT doubles each) + band ends
+struct TileShared {
+  double Zs[4][16 * kTLd];     // Z_K = U_KK^-T (lower triangular), row-major; 4 deep: the previous owner
+  double zK[4][16];            // reads Z_K one phase late.  z_K = Z_K y_K
+  double Ur[2][kTB - 1][256];  // row K: U_{K,K+d}, d = 1..7, acc layout
+  double Dw[16 * kTLd];        // the owner's diagonal tile (one owner per phase)
+  double Yw[16];
+  double prw[2 * kCholNb];     // the owner's next two pivot rows
+  double bsp[2][kTB][16];      // back-substitution partials
+  int fail;
+};
+
+__device__ __forceinline__ f64x4 mfma_f64_k16(const double (&a)[4], const f64x4& b, f64x4 c) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) c = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b[s], c, 0, 0, 0);
+  return c;
+}
+
+// Sum over the four 16-lane rows (lanes l, l^16, l^32, l^48) by gfx950 permlane swaps; every lane gets
+// (v0 + v2) + (v1 + v3), the same bits in each (addition commutes).
+__device__ __forceinline__ double sum_rows4(double v) {
+  auto a = __builtin_amdgcn_permlane32_swap(__double2loint(v), __double2loint(v), false, false);
+  auto b = __builtin_amdgcn_permlane32_swap(__double2hiint(v), __double2hiint(v), false, false);
+  const double w = __hiloint2double(b[0], a[0]) + __hiloint2double(b[1], a[1]);
+  auto c = __builtin_amdgcn_permlane16_swap(__double2loint(w), __double2loint(w), false, false);
+  auto e = __builtin_amdgcn_permlane16_swap(__double2hiint(w), __double2hiint(w), false, false);
+  return __hiloint2double(e[0], c[0]) + __hiloint2double(e[1], c[1]);
+}
+
+// Row-sum inside each 16-lane row (row_ror butterflies); lane-dependent association, so one fixed lane
+// per row consumes it.
+__device__ __forceinline__ double row_sum16(double v) {
+  v += dpp_d<0x128>(v);   // row_ror:8
+  v += dpp_d<0x124>(v);   // row_ror:4
+  v += dpp_d<0x122>(v);   // row_ror:2
+  v += dpp_d<0x121>(v);   // row_ror:1
+  return v;
+}
+
+// Tile (I, J) of S in acc layout (entries below the diagonal of a diagonal tile are whatever S holds: the
+// factorisation masks them); the identity beyond n (padding rows of the last tile) and zeros for I < 0 come
+// from the constants {0, 1} stored after S and its rhs (S[n n + n], S[n n + n + 1]).  The index is selected,
+// not the value, so the loads stay in flight until the tile is first used.
+__device__ __forceinline__ f64x4 tile_load(const double* __restrict__ S, int n, int I, int J, int li, int lk) {
+  f64x4 t;
+  const int cz = n * n + n;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int gi = 16 * I + lk + 4 * q, gj = 16 * J + li;
+    const bool in = (unsigned)gi < (unsigned)n && gj < n;
+    t[q] = S[in ? gi * n + gj : cz + (gi == gj ? 1 : 0)];
+  }
+  return t;
+}
+
+__device__ __forceinline__ void tile_col_load(f64x4 (&acc)[kTB], double& ypart, const Dev& d, int J, int li,
+                                              int lk) {
+#pragma unroll
+  for (int u = 0; u < kTB; ++u) acc[u] = tile_load(d.S, d.n, J - ((J - u) & 7), J, li, lk);
+  const int gj = 16 * J + li, n = d.n;
+  ypart = d.S[(lk == 0 && gj < n) ? n * n + gj : n * n + n];
+}
+
+// Factor one 16x16 diagonal tile D (upper triangle, pitch kTLd) with the identity (lanes 16-31) and the rhs
+// (lane 32) as augmented columns; lanes 0-15 hold the columns of D.  Right-looking, two pivots per LDS
+// broadcast (every lane derives pivot row j+1 after pivot j itself).  On return lanes 16-31 hold the columns
+// of Z = U^-T and lane 32 holds z = U^-T y.  Returns true on a non-positive pivot.
+__device__ __forceinline__ bool tile_factor(const double* D, const double* Yk, double* prw, double (&ca)[16]) {
+  const int lane = opaque_lane();
+  const int c = lane & 15;
+  const bool isy = lane == 32;
+  const double* b0 = isy ? Yk : D + c;
+  const int rs = isy ? 1 : kTLd;
+#pragma unroll
+  for (int r = 0; r < kCholNb; ++r) ca[r] = b0[r * rs];
+  {
+    // rows kept (the upper part of D's columns, all of y) and the identity's ones, as opaque bit masks
+    unsigned keepbits = lane < 16 ? ((2u << c) - 1u) : (isy ? 0xFFFFu : 0u);
+    unsigned onebits = (lane >= 16 && lane < 32) ? (1u << c) : 0u;
+    asm volatile("" : "+v"(keepbits), "+v"(onebits));
+    const unsigned long long kOneBits = 0x3FF0000000000000ull;
+#pragma unroll
+    for (int r = 0; r < kCholNb; ++r) {
+      int km, om;
+      asm volatile("v_bfe_i32 %0, %1, %2, 1" : "=v"(km) : "v"(keepbits), "n"(r));
+      asm volatile("v_bfe_i32 %0, %1, %2, 1" : "=v"(om) : "v"(onebits), "n"(r));
+      const unsigned long long b = (unsigned long long)__double_as_longlong(ca[r]);
+      ca[r] = __longlong_as_double((long long)((b & (unsigned long long)(long long)km) |
+                                               (kOneBits & (unsigned long long)(long long)om)));
+    }
+  }
+  bool bad = false;
+  double u0[kCholNb], u1[kCholNb];
+  double* prw2 = prw + kCholNb;
+  if (lane < kCholNb) {
+    prw[lane] = ca[0];
+    prw2[lane] = ca[1];
+  }
+#pragma unroll
+  for (int r = 0; r < kCholNb; ++r) {
+    u0[r] = prw[r];
+    u1[r] = prw2[r];
+  }
+#pragma unroll
+  for (int j = 0; j < kCholNb; j += 2) {
+    const double p0 = u0[j];
+    bad |= !(p0 > 0.0);
+    const double i0 = rsq_nr1(p0);
+    const double r0 = i0 * i0;
+    const double w1 = u0[j + 1] * r0;
+    double v1[kCholNb];
+#pragma unroll
+    for (int r = j + 1; r < kCholNb; ++r) v1[r] = fma(-w1, u0[r], u1[r]);
+    const double p1 = v1[j + 1];
+    bad |= !(p1 > 0.0);
+    const double i1 = rsq_nr1(p1);
+    const double r1 = i1 * i1;
+    const double aj = ca[j];
+    const double t0 = aj * r0;
+    ca[j] = aj * i0;
+    const double aj1 = fma(-u0[j + 1], t0, ca[j + 1]);
+    const double t1 = aj1 * r1;
+    ca[j + 1] = aj1 * i1;
+    if (j + 2 < kCholNb) {
+      ca[j + 2] = fma(-v1[j + 2], t1, fma(-u0[j + 2], t0, ca[j + 2]));
+      ca[j + 3] = fma(-v1[j + 3], t1, fma(-u0[j + 3], t0, ca[j + 3]));
+      if (lane < kCholNb) {
+        prw[lane] = ca[j + 2];
+        prw2[lane] = ca[j + 3];
+      }
+    }
+#pragma unroll
+    for (int r = j + 4; r < kCholNb; ++r) ca[r] = fma(-v1[r], t1, fma(-u0[r], t0, ca[r]));
+#pragma unroll
+    for (int r = j; r < kCholNb; ++r) asm volatile("" : "+v"(ca[r]));
+    if (j + 2 < kCholNb) {
+#pragma unroll
+      for (int r = j + 2; r < kCholNb; ++r) {
+        u0[r] = prw[r];
+        u1[r] = prw2[r];
+      }
+    }
+  }
+  return bad;
+}
+
+// The owner of the next diagonal: D (acc layout) and its rhs partials -> Z, z and Z^T z of tile row K.
+__device__ __forceinline__ bool tile_diag(const f64x4& D, double ypart, TileShared& sh, double* zp, int K,
+                                          int lane, int li, int lk) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) sh.Dw[(lk + 4 * q) * kTLd + li] = D[q];
+  const double ys = sum_rows4(ypart);
+  if (lk == 0) sh.Yw[li] = ys;
+  double ca[kCholNb];
+  const bool bad = tile_factor(sh.Dw, sh.Yw, sh.prw, ca);
+  double* Zs = sh.Zs[K & 3];
+  double* zk = sh.zK[K & 3];
+  if (lane >= 16 && lane < 32) {
+#pragma unroll
+    for (int r = 0; r < kCholNb; ++r) Zs[r * kTLd + (lane - 16)] = ca[r];
+  }
+  if (lane == 32) {
+#pragma unroll
+    for (int r = 0; r < kCholNb; ++r) zk[r] = ca[r];
+  }
+  if (lane >= 16 && lane < 32) {
+    double s = 0.0;
+#pragma unroll
+    for (int r = 0; r < kCholNb; ++r) s = fma(ca[r], zk[r], s);
+    zp[16 * K + lane - 16] = s;
+  }
+  return bad;
+}
+
+// Diagnostic stamps (SG_STAMP=1): lane 0 of every wave accumulates s_memtime deltas per phase; waves 0 and 1
+// report (tools/tile_stamps.py).
+#define SG_TSTAMP(slot)                                                                  \
+  if (kStamp && lane == 0) {                                                             \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime();                       \
+    tacc[slot] += now_ - tlast;                                                          \
+    tlast = now_;                                                                        \
+  }
+
+// W_KJ = Z_K^T U_KJ (= U_KK^-1 U_KJ) of one row-K tile, and its store to global memory for the back
+// substitution (kept apart so that loads issued in between do not reuse the stores' data registers, which
+// would wait for the stores).
+__device__ __forceinline__ f64x4 tile_w(const f64x4& U, const double* Zs, int li, int lk) {
+  const f64x4 zero = {0.0, 0.0, 0.0, 0.0};
+  double zt[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) zt[s] = Zs[(4 * s + lk) * kTLd + li];
+  return mfma_f64_k16(zt, U, zero);
+}
+__device__ __forceinline__ void tile_w_store(const f64x4& Wt, double* __restrict__ Wg, int K, int J, int lane) {
+  double* wg = Wg + ((size_t)K * kTB + (J - K)) * 256 + lane;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) wg[q * 64] = Wt[q];
+}
+
+// One phase (tile row K) of a wave; kU = K & 7.  `late`: this wave owned the diagonal of the previous phase
+// and still owes that phase's W tile and its column reload (it has no other work in this phase).
+template <int kU, bool kStamp>
+__device__ __forceinline__ void tile_phase(f64x4 (&acc)[kTB], double& ypart, int& J, bool& late, bool& bad,
+                                           TileShared& sh, const Dev& d, double* __restrict__ Wg, double* zp,
+                                           const int* tend, int K, int NT, int lane, int li, int lk,
+                                           unsigned long long (&tacc)[16], unsigned long long& tlast) {
+  constexpr int um = (kU + kTB - 1) & (kTB - 1), v = (kU + 1) & (kTB - 1);
+  if (late) {
+    // the previous phase's owner (column J = K): its row K-1 tile (slot um) -> W, then column J + 8, which
+    // row K + 1 touches first
+    const bool hasw = J < tend[K - 1];
+    f64x4 Wt = {0.0, 0.0, 0.0, 0.0};
+    if (hasw) Wt = tile_w(acc[um], sh.Zs[um & 3], li, lk);
+    const int Jw = J;
+    J += kTB;
+    tile_col_load(acc, ypart, d, J, li, lk);
+    if (hasw) tile_w_store(Wt, Wg, K - 1, Jw, lane);
+    late = false;
+    SG_TSTAMP(13)
+    return;
+  }
+  // (0) trailing update by row K-1
+  if (K >= 1 && J < tend[K - 1]) {
+    const double* Ub = sh.Ur[um & 1][0];
+#pragma unroll
+    for (int dd = 1; dd < kTB; ++dd) {
+      if (K - 1 + dd <= J) {
+        double a[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) a[s] = -Ub[(dd - 1) * 256 + s * 64 + lane];
+        acc[(um + dd) & (kTB - 1)] = mfma_f64_k16(a, acc[um], acc[(um + dd) & (kTB - 1)]);
+      }
+    }
+  }
+  SG_TSTAMP(8)
+  // (1) TRSM of row K's tile
+  const int te = tend[K];
+  const bool act = J < te;
+  const double* Zs = sh.Zs[kU & 3];
+  if (act) {
+    const f64x4 zero = {0.0, 0.0, 0.0, 0.0};
+    double za[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) za[s] = Zs[li * kTLd + 4 * s + lk];
+    const f64x4 U = mfma_f64_k16(za, acc[kU], zero);
+    acc[kU] = U;
+    double* ur = sh.Ur[kU & 1][J - K - 1];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ur[q * 64 + lane] = U[q];
+    const double* zk = sh.zK[kU & 3];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ypart = fma(-U[q], zk[lk + 4 * q], ypart);
+  }
+  SG_TSTAMP(9)
+  if (J == K + 1) {
+    // (2) the next diagonal: apply row K, factor, post; its W tile and the reload follow next phase
+    if (act) {
+      double a[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) a[s] = -acc[kU][s];
+      acc[v] = mfma_f64_k16(a, acc[kU], acc[v]);
+    }
+    SG_TSTAMP(10)
+    if (K + 1 < NT) bad |= tile_diag(acc[v], ypart, sh, zp, K + 1, lane, li, lk);
+    late = true;
+    SG_TSTAMP(11)
+  } else if (act) {
+    // (3) back-substitution tile
+    tile_w_store(tile_w(acc[kU], Zs, li, lk), Wg, K, J, lane);
+    SG_TSTAMP(12)
+  }
+}
+
+template <bool kStamp>
+__global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_t* panel_jend,
+                                                             double* __restrict__ Wg) {
+  const LmState* st = d.st;
+  if (st->done) return;
+  unsigned long long tlast = kStamp ? __builtin_amdgcn_s_memtime() : 0ull, tacc[16] = {};
+  __shared__ TileShared sh;
+  extern __shared__ double tdyn[];
+  const int n = d.n, tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 15, lk = lane >> 4;
+  const int NT = (n + 15) >> 4;
+  double* xs = tdyn;              // [16 NT] back-substitution solution
+  double* zp = tdyn + 16 * NT;    // [16 NT] Z_K^T z_K
+  int* tend = reinterpret_cast<int*>(tdyn + 32 * NT);   // [NT] band end (tiles, exclusive) per tile row
+  for (int k = tid; k < NT; k += kTileThreads) tend[k] = (panel_jend[k] + 15) >> 4;
+  if (tid == 0) sh.fail = 0;
+  bool bad = false;
+  {
+    f64x4 acc[kTB];
+    double ypart = 0.0;
+    int J = wave;
+    bool late = false;
+    tile_col_load(acc, ypart, d, J, li, lk);
+    if (J == 0) {   // D_0 has no updates: factor it and take column 8
+      bad |= tile_diag(acc[0], ypart, sh, zp, 0, lane, li, lk);
+      J = kTB;
+      tile_col_load(acc, ypart, d, J, li, lk);
+    }
+    SG_TSTAMP(0)
+    __syncthreads();
+    SG_TSTAMP(1)
+    for (int K0 = 0; K0 < NT; K0 += kTB) {
+#define SG_TILE_PHASE(U)                                                                  \
+      if (K0 + (U) < NT) {                                                                \
+        tile_phase<U, kStamp>(acc, ypart, J, late, bad, sh, d, Wg, zp, tend, K0 + (U), NT, lane, li, lk, tacc, tlast); \
+        SG_TSTAMP(2)                                                                      \
+        lds_barrier();                                                                    \
+        SG_TSTAMP(3)                                                                      \
+      }
+      SG_TILE_PHASE(0) SG_TILE_PHASE(1) SG_TILE_PHASE(2) SG_TILE_PHASE(3)
+      SG_TILE_PHASE(4) SG_TILE_PHASE(5) SG_TILE_PHASE(6) SG_TILE_PHASE(7)
+#undef SG_TILE_PHASE
+    }
+  }
+  if (bad && lane == 0) sh.fail = 1;
+  __syncthreads();   // W tiles (global) and z' visible to every wave
+  SG_TSTAMP(4)
+  {
+    // back substitution, rows K = NT-1 .. 0: wave w < 7 forms the partial W_{K,K+1+w} x_{K+1+w}, every wave
+    // sums the seven partials in wave order (the same bits everywhere) into x_K, wave 0 stores it.  The W tile
+    // is loaded one row ahead.
+    const bool hasd = wave < kTB - 1;
+    const double* wbase = Wg + (size_t)(wave + 1) * 256 + lane;
+    double wc[4], wn[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) wc[q] = wbase[(size_t)(NT - 1) * kTB * 256 + q * 64];
+    for (int K = NT - 1; K >= 0; --K) {
+      const double* src = wbase + (size_t)(K > 0 ? K - 1 : 0) * kTB * 256;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) wn[q] = src[q * 64];
+      const int Jt = K + 1 + wave;
+      const bool in = hasd && Jt < tend[K];
+      const double xr = xs[16 * (in ? Jt : K) + li];   // unconditional (a valid row either way)
+      const double xv = in ? xr : 0.0;
+      double t[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) t[q] = row_sum16((in ? wc[q] : 0.0) * xv);
+      const double tv = li == 0 ? t[0] : (li == 1 ? t[1] : (li == 2 ? t[2] : t[3]));
+      if (li < 4) sh.bsp[K & 1][wave][lk + 4 * li] = tv;
+      lds_barrier();
+      const double* bp = &sh.bsp[K & 1][0][li];
+      double sum = 0.0;
+#pragma unroll
+      for (int w = 0; w < kTB - 1; ++w) sum += bp[16 * w];
+      const double xk = zp[16 * K + li] - sum;
+      if (wave == 0 && lk == 0) xs[16 * K + li] = xk;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) wc[q] = wn[q];
+    }
+  }
+  SG_TSTAMP(5)
+  __syncthreads();
+  double* y = d.work;
+  for (int i = tid; i < n; i += kTileThreads) {
+    d.xc[i] = xs[i];
+    y[i] = xs[i];
+  }
+  __syncthreads();
+  chol_candidates<kTileThreads>(d, xs, sh.fail);
+  SG_TSTAMP(6)
+  if (kStamp && lane == 0 && wave < 2)
+    for (int s_ = 0; s_ < 16; ++s_) d.stamps[16 * wave + s_] += tacc[s_];
+}
+#undef SG_TSTAMP
 
 // ------------------------------------------------------------------------------------------------
 // k_point_update: back-substitution x_p = V~^-1 (g~_p - A_p^T A_c x_c), model cost change
@@ -2788,6 +3185,16 @@ void BaSolver::Load(const sg_problem& p) {
   chol_window_ = npanel <= kJendSh;   // band ends cached in LDS
   for (int pk = 0; pk < npanel; ++pk)
     if (panel_jmax[pk] - pk * kCholNb > kCholWS) chol_window_ = false;
+  // tiled band Cholesky: every tile row's band within kTB tiles, x and z' of the whole system in LDS
+  chol_tiles_ = n_ > 0 && nk_ == 0 && npanel <= kTileMaxNT && !getenv("SG_CHOL_WINDOW");
+  for (int pk = 0; pk < npanel; ++pk)
+    if ((panel_jmax[pk] + kCholNb - 1) / kCholNb - pk > kTB) chol_tiles_ = false;
+  if (chol_tiles_) {
+    std::vector<double> wz((size_t)npanel * kTB * 256 + 2, 0.0);   // W tiles, then the constants {0, 1}
+    wz.back() = 1.0;
+    Wg_.Upload(wz, stream_);
+    tile_lds_ = (size_t)npanel * 32 * sizeof(double) + (size_t)npanel * sizeof(int32_t);
+  }
   lap("envelope");
   // device uploads
   hipStream_t s = stream_;
@@ -2866,7 +3273,7 @@ void BaSolver::Load(const sg_problem& p) {
   cam_wide_.Resize((size_t)std::max(NB_, 1) * kCamV);
   S_wide_.Resize(nn * nn);
   xchg_cam_.Resize((size_t)NB_ * kCamV + kXNum + nranks());
-  S_.Resize(nn * nn + nn);   // S, then the rhs partial xc: one all-reduce covers both
+  S_.Resize(nn * nn + nn + 2);   // S, then the rhs partial xc (one all-reduce covers both), then {0, 1}
   rhs_.Resize(nn);
   xchg_upd_.Resize(kUNum);
   xchg_chol_.Resize(kCNum);
@@ -2887,6 +3294,9 @@ void BaSolver::Load(const sg_problem& p) {
                                   (size_t)kSegPts * 14 + (size_t)std::max(max_seg_obs_, 1) * 8);
   SG_HIP_CHECK(hipFuncSetAttribute((const void*)k_schur, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)schur_lds_));
+  if (chol_tiles_)
+    for (const void* f : {(const void*)k_chol_tiles<false>, (const void*)k_chol_tiles<true>})
+      SG_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tile_lds_));
   SG_HIP_CHECK(hipFuncSetAttribute((const void*)k_cholesky_window<false>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCholLds));
   SG_HIP_CHECK(hipFuncSetAttribute((const void*)k_cholesky_window<true>,
@@ -2946,6 +3356,10 @@ void BaSolver::ResetState(hipStream_t s) {
   rhs_.Zero(s);
   chunk_scal_.Zero(s);
   S_.Zero(s);
+  {
+    static const double kConst01[2] = {0.0, 1.0};   // k_chol_tiles: padding entries of the last tile
+    SG_HIP_CHECK(hipMemcpyAsync(S_.ptr + S_.size - 2, kConst01, sizeof(kConst01), hipMemcpyHostToDevice, s));
+  }
   if (stamp_on_) stamps_.Zero(s);
 }
 
@@ -3184,7 +3598,13 @@ void BaSolver::Iterate(int n) {
                          (const int32_t*)pack_off_.ptr, npanel, Spk_.ptr, 1);
     }
     TimedLaunchBegin(kKChol);
-    if (chol_window_ && d.stamps)
+    if (chol_tiles_ && d.stamps)
+      hipLaunchKernelGGL(k_chol_tiles<true>, dim3(1), dim3(kTileThreads), tile_lds_, stream_, d,
+                         (const int32_t*)work_i_.ptr, Wg_.ptr);
+    else if (chol_tiles_)
+      hipLaunchKernelGGL(k_chol_tiles<false>, dim3(1), dim3(kTileThreads), tile_lds_, stream_, d,
+                         (const int32_t*)work_i_.ptr, Wg_.ptr);
+    else if (chol_window_ && d.stamps)
       hipLaunchKernelGGL(k_cholesky_window<true>, dim3(1), dim3(kCholThreads), kCholLds, stream_, d,
                          (const int32_t*)work_i_.ptr, rdg_.ptr);
     else if (chol_window_)

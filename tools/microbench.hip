@@ -126,7 +126,59 @@ __global__ __launch_bounds__(512) void k_lat(const double* g, double* out, unsig
   if (tid == 0) t[8] = (t1 - t0) / iters;
   const double chk = wave_sum_full((double)lane);   // all lanes active; 2016 expected
   if (tid == 0) t[9] = (unsigned long long)chk;
-  out[tid] = acc + x + y + z + r + w + q;
+  // 10. dependent v_mfma_f64_16x16x4f64 chain (one wave)
+  typedef double f64x4 __attribute__((ext_vector_type(4)));
+  f64x4 m = {acc, acc, acc, acc};
+  const double ma = acc * 1e-9 + 1e-12, mb = acc + 1e-3;
+  __syncthreads();
+  t0 = __builtin_amdgcn_s_memtime();
+  if (tid < 64) {
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) m = __builtin_amdgcn_mfma_f64_16x16x4f64(ma, mb, m, 0, 0, 0);
+    }
+  }
+  t1 = __builtin_amdgcn_s_memtime();
+  if (tid == 0) t[10] = (t1 - t0) / (8 * iters);
+  // 11. same chain, all 8 waves (two per SIMD) at once
+  __syncthreads();
+  t0 = __builtin_amdgcn_s_memtime();
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m = __builtin_amdgcn_mfma_f64_16x16x4f64(ma, mb, m, 0, 0, 0);
+  }
+  t1 = __builtin_amdgcn_s_memtime();
+  if (tid == 0) t[11] = (t1 - t0) / (8 * iters);
+  // 12. four independent accumulators, one wave (issue rate)
+  f64x4 m1 = m, m2 = m, m3 = m;
+  __syncthreads();
+  t0 = __builtin_amdgcn_s_memtime();
+  if (tid < 64) {
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        m = __builtin_amdgcn_mfma_f64_16x16x4f64(ma, mb, m, 0, 0, 0);
+        m1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ma, mb, m1, 0, 0, 0);
+        m2 = __builtin_amdgcn_mfma_f64_16x16x4f64(ma, mb, m2, 0, 0, 0);
+        m3 = __builtin_amdgcn_mfma_f64_16x16x4f64(ma, mb, m3, 0, 0, 0);
+      }
+    }
+  }
+  t1 = __builtin_amdgcn_s_memtime();
+  if (tid == 0) t[12] = (t1 - t0) / (8 * iters);
+  // 13. LDS write then dependent 4 x ds_read_b64 (lane-dependent addresses) + use
+  double v13 = acc;
+  __syncthreads();
+  t0 = __builtin_amdgcn_s_memtime();
+  if (tid < 64) {
+    for (int i = 0; i < iters; ++i) {
+      sh[lane] = v13;
+      v13 = (sh[(lane * 5) & 63] + sh[(lane * 7) & 63]) * 0.5 + (sh[(lane * 3) & 63] + sh[(lane * 11) & 63]) * 1e-9;
+    }
+  }
+  t1 = __builtin_amdgcn_s_memtime();
+  if (tid == 0) t[13] = (t1 - t0) / iters;
+  out[tid] = acc + x + y + z + r + w + q + m[0] + m[1] + m[2] + m[3] + m1[0] + m2[1] + m3[2] + v13;
 }
 
 int main() {
@@ -145,7 +197,9 @@ int main() {
   const char* names[] = {"LDS write->read round trip", "8-wave LDS barrier", "global load (dependent)",
                          "fp64 FMA (dependent)", "readlane pair + FMA", "wave_sum (shfl_xor)",
                          "rsq + 2 Newton", "LDS write + 16 broadcast reads + adds",
-                         "wave_sum_full (DPP)", "check: sum of lane ids (2016)"};
-  for (int i = 0; i < 10; ++i) printf("%-40s %6llu cycles\n", names[i], h[i]);
+                         "wave_sum_full (DPP)", "check: sum of lane ids (2016)",
+                         "f64 MFMA 16x16x4 dependent (1 wave)", "f64 MFMA dependent (8 waves)",
+                         "f64 MFMA 4 independent (1 wave)", "LDS write + 4 reads + use"};
+  for (int i = 0; i < 14; ++i) printf("%-40s %6llu cycles\n", names[i], h[i]);
   return 0;
 }
