@@ -5,13 +5,20 @@ One "step" = one Levenberg-Marquardt iteration of the reference's local BA (slam
 LM + SPARSE_SCHUR restated on the GPU): linearize (if the previous step was accepted), damp + Schur
 complement, reduced camera Cholesky, back-substitution, candidate cost, accept/reject — all on device.
 
-Workload (N = 1): BASELINE config 2 — 50 keyframes / ~20k landmarks / ~130k observations, synthetic
-scene (slamgpu/scene.py, seed 2), SolveFrames(map, 48, 50, 2.0).  fp64 arithmetic (the reference's own
-precision).  Termination is disabled inside the timed region so that exactly K iterations run.
+Workloads (synthetic scenes, slamgpu/scene.py; fp64 arithmetic, the reference's own precision):
+  --config C2 (default): BASELINE config 2 — 50 keyframes / ~19.4k landmarks / ~148k observations (seed 2),
+      SolveFrames(map, 48, 50, 2.0).  N > 1 (torchrun, one rank per GPU): weak scaling — 50 keyframes and
+      N x 20k landmarks sharded over the ranks (sg_problem_shard), RCCL all-reduce of the camera system per
+      iteration; value = N * K / time (the unit is one LM iteration's worth of config-2 work).
+  --config C5: BASELINE config 5 — 200 keyframes / ~194k landmarks / ~1.95M observations (seed 5),
+      SolveFrames(map, 198, 200, 2.0); N > 1: strong scaling, the same problem's landmarks sharded over the
+      ranks; value = K / time.
+The default run also measures the other workload (C5 next to a C2 headline: strong over the same N ranks).
 
-N > 1 (torchrun, one rank per GPU): weak scaling — 50 keyframes and N x 20k landmarks sharded over the
-ranks by first observing frame (sg_problem_shard), RCCL all-reduce of the camera system per iteration;
-value = N * K / time, i.e. the unit is one LM iteration's worth of config-2 work (20k landmarks).
+The timed region is K LM iterations with termination disabled, after W warm-up iterations: past
+convergence, so about half the steps are rejected (a rejected step skips the linearization, as in Ceres).
+`accepted_frac` reports that share, and `solve_from_start` times complete solves from the perturbed start
+(Slam::SolveFrames semantics, termination on, mostly accepted steps): iterations / wall time.
 
 Prints ONE JSON line on rank 0.
 """
@@ -37,7 +44,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--points", type=int, default=20000, help="landmarks per GPU")
     ap.add_argument("--frames", type=int, default=50)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample (0: skip)")
+    ap.add_argument("--config", choices=("C2", "C5"), default="C2", help="headline workload")
+    ap.add_argument("--other", type=int, default=1, help="also measure the other BA workload (C5 / C2)")
+    ap.add_argument("--cpu-runs", type=int, default=20, help="CPU-baseline timed runs per leg (0: skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=4.0, help="front-end CPU-baseline sample (0: skip)")
     ap.add_argument("--sweep-obs", type=int, default=2_000_000,
                     help="observations in the scaled Jacobian-sweep measurement (0: skip)")
     ap.add_argument("--frontend", type=int, default=1,
@@ -159,13 +169,193 @@ def dist_env():
     return ws, rank, local
 
 
+def cpu_legs(full, runs, ba_iters_note):
+    """CPU baseline of one LM iteration (oracle/oracle_ba.cpp, the Ceres-1.8 LM + SPARSE_SCHUR restatement):
+    each run solves the config from its perturbed start with max_num_iterations = 1 (iteration 0's
+    residual pass + one LM iteration: linearize, Schur, Cholesky, candidate), 3 warm-up runs, median of
+    `runs` timed runs.  Legs: 1 thread (the reference's Ceres num_threads default, slam.cpp:504), 1 thread
+    with -ffast-math (the reference's Makefile:4 flags), and this process's CPU share on OpenMP."""
+    import statistics
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    from slamgpu.capi import default_solver_options
+    nproc = os.cpu_count() or 1
+    share = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else nproc
+    share = min(share, int(os.environ.get("OMP_NUM_THREADS", share)))
+    o1 = default_solver_options(max_num_iterations=1)
+    legs = []
+    for name, nt, fm in (("1 thread, -O3", 1, False), ("1 thread, -O3 -ffast-math", 1, True),
+                         ("%d threads (OpenMP), -O3" % share, share, False)):
+        ts = []
+        for r in range(3 + runs):
+            po = full.copy()
+            t0 = time.perf_counter()
+            oracle.solve(po, o1, nthreads=nt, fastmath=fm)
+            if r >= 3:
+                ts.append(time.perf_counter() - t0)
+        med = statistics.median(ts)
+        legs.append({"leg": name, "threads": nt, "fastmath": fm, "value": 1.0 / med, "unit": "iters/s",
+                     "median_s_per_iteration": med, "runs": len(ts)})
+    best = max(legs, key=lambda l: l["value"])
+    return {"value": best["value"], "unit": "iters/s", "cores": best["threads"], "kind": "port",
+            "sample": "median of %d runs per leg: SolveFrames(%s) from the perturbed start, max_num_iterations=1 "
+                      "(oracle/oracle_ba.cpp, dual-number Jacobians); nproc=%d, CPU share %d"
+                      % (runs, ba_iters_note, nproc, share),
+            "legs": legs}
+
+
+def make_workload(cfg, n_gpus, rank, points_per_gpu, frames):
+    """(full problem, this rank's shard, description) of a BA workload."""
+    from slamgpu import ba
+    from slamgpu.scene import make_config, make_scene
+    if cfg == "C2":
+        scene = make_scene(num_frames=frames, num_points=points_per_gpu * n_gpus, seed=2, run_max=14, run_min=4)
+        full = ba.problem_from_map_frames(scene, frames - 2, frames, 2.0)
+        desc = "config 2: SolveFrames(%d of %d KF) local BA, LM iteration" % (frames - 2, frames)
+    else:
+        scene = make_config("C5")
+        full = ba.problem_from_map_frames(scene, scene.num_frames - 2, scene.num_frames, 2.0)
+        desc = "config 5: SolveFrames(198 of 200 KF) local BA, LM iteration"
+    prob = ba.shard_problem(full, rank, n_gpus) if n_gpus > 1 else full
+    return full, prob, desc
+
+
+class Runner:
+    """One BA workload on this rank: its solver (and RCCL communicator for N > 1)."""
+
+    def __init__(self, prob, local, rank, n_gpus, dist):
+        import torch
+        from slamgpu import ba
+        self.prob, self.dist, self.local, self.rank, self.n = prob, dist, local, rank, n_gpus
+        self.solver = ba.BundleAdjuster(device=local)
+        if n_gpus > 1:
+            uid = ba.BundleAdjuster.unique_id() if rank == 0 else bytes(128)
+            t = torch.tensor(list(uid), dtype=torch.uint8, device=f"cuda:{local}")
+            dist.broadcast(t, 0)
+            self.solver.comm_init(bytes(t.cpu().tolist()), n_gpus, rank)
+        self.initial = prob.copy()
+        self.solver.load(prob)
+
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
+
+    def max_over_ranks(self, x):
+        if self.dist is None:
+            return x
+        import torch
+        e = torch.tensor([x], dtype=torch.float64, device=f"cuda:{self.local}")
+        self.dist.all_reduce(e, op=self.dist.ReduceOp.MAX)
+        return float(e.item())
+
+    def timed(self, steps, warmup):
+        """W warm-up then exactly K LM iterations (termination disabled), barrier + synchronize on both
+        sides, max over ranks; then the same K with per-kernel HIP-event timing."""
+        import torch
+        from slamgpu.capi import default_solver_options
+        g = self.solver
+        g.begin(default_solver_options(max_num_iterations=warmup + 2 * steps + 16, disable_termination=1))
+        g.iterate(warmup)
+        g.sync()
+        s0 = g.summary()
+        self.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        g.iterate(steps)
+        g.sync()
+        torch.cuda.synchronize()
+        self.barrier()
+        elapsed = self.max_over_ranks(time.perf_counter() - t0)
+        s1 = g.summary()
+        g.set_timing(True)
+        g.iterate(steps)
+        g.sync()
+        kt = g.kernel_times()
+        g.set_timing(False)
+        s2 = g.summary()
+        return {"elapsed": elapsed, "accepted": s1["num_successful_steps"] - s0["num_successful_steps"],
+                "kt": kt, "work": g.kernel_work(), "lin_active": s2["num_successful_steps"] - s1["num_successful_steps"],
+                "summary": s1}
+
+    def solve_from_start(self):
+        """Complete solves from the perturbed start (termination on): iterations over wall time (includes
+        the host's completion polls every 8 iterations and the result download), and the per-kernel
+        device time per iteration from HIP events."""
+        g = self.solver
+        p = self.initial.copy()
+        g.load(p)            # same structure: value-only reload of the perturbed start
+        self.barrier()
+        t0 = time.perf_counter()
+        s = g.solve()
+        wall = self.max_over_ranks(time.perf_counter() - t0)
+        p = self.initial.copy()
+        g.load(p)
+        g.set_timing(True)
+        g.solve()
+        kt = g.kernel_times()
+        g.set_timing(False)
+        dev_ms = sum(v[0] * v[1] for v in kt.values())
+        its = s["num_lm_iterations"]
+        return {"lm_iterations": its, "accepted": s["num_successful_steps"], "termination": s["termination"],
+                "final_cost": s["final_cost"], "wall_ms": 1e3 * wall, "iters_per_s_wall": its / wall if wall else None,
+                "device_kernel_ms": dev_ms, "iters_per_s_device": its / (dev_ms * 1e-3) if dev_ms else None}
+
+
+def kernel_report(res, steps, n_text):
+    """Per-iteration kernel times, the dominant kernel's roofline and the sweep roofline."""
+    kt, work = res["kt"], res["work"]
+    per_iter_ms = {k: v[0] * v[1] / max(steps, 1) for k, v in kt.items()}
+    dominant = max(per_iter_ms, key=per_iter_ms.get)
+    dom_ms = kt[dominant][0]
+    dom_bytes, dom_flops = work[dominant]
+    if dom_flops > 0 and dominant == "cholesky":
+        ach = dom_flops / (dom_ms * 1e-3) / 1e12
+        roof = {"bound": "mfma", "achieved": ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": ach / FP64_PEAK_TFLOPS, "traffic": pmc_traffic("k_chol_tiles"), "kernel": dominant,
+                "us_per_launch": 1e3 * dom_ms,
+                "note": "single-workgroup tiled band Cholesky of the reduced camera system (%s), n^3/3 flops "
+                        "over its mean HIP-event launch time" % n_text}
+    else:
+        ach = dom_bytes / (dom_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic("k_" + dominant), "kernel": dominant,
+                "us_per_launch": 1e3 * dom_ms}
+    sweep = None
+    n_lin = res["lin_active"]
+    if n_lin > 0:
+        lin_total_ms = kt["linearize"][0] * kt["linearize"][1]
+        ach = work["linearize"][0] * n_lin / (lin_total_ms * 1e-3) / 1e9
+        sweep = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                 "frac": ach / HBM_PEAK_GBS, "bytes_per_launch": work["linearize"][0],
+                 "traffic": pmc_traffic("k_linearize"), "active_launches": n_lin, "launches": kt["linearize"][1]}
+    return {k: round(v, 5) for k, v in per_iter_ms.items()}, roof, sweep
+
+
+def run_workload(cfg, args, n_gpus, rank, local, dist, steps, warmup):
+    full, prob, desc = make_workload(cfg, n_gpus, rank, args.points, args.frames)
+    r = Runner(prob, local, rank, n_gpus, dist)
+    res = r.timed(steps, warmup)
+    info = r.solver.info()
+    start = r.solve_from_start()
+    # shard balance: every rank's observations / pairs, gathered
+    bal = None
+    if dist is not None:
+        import torch
+        v = torch.tensor([prob.num_points, prob.num_obs, info["num_pairs"]], dtype=torch.float64,
+                         device=f"cuda:{local}")
+        allv = [torch.zeros_like(v) for _ in range(n_gpus)]
+        dist.all_gather(allv, v)
+        rows = [[int(x) for x in t.cpu().tolist()] for t in allv]
+        bal = {"points": [x[0] for x in rows], "obs": [x[1] for x in rows], "schur_pairs": [x[2] for x in rows]}
+        bal["pairs_max_over_mean"] = max(bal["schur_pairs"]) / (sum(bal["schur_pairs"]) / n_gpus)
+    r.solver.close()
+    return full, prob, desc, res, info, start, bal
+
+
 def main():
     args = parse()
     ws, rank, local = dist_env()
     import torch
-    from slamgpu import ba
-    from slamgpu.capi import default_solver_options
-    from slamgpu.scene import make_scene
 
     dist = None
     if ws > 1:
@@ -174,54 +364,25 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", rank=rank, world_size=ws)
     n_gpus = ws
+    strong = args.config == "C5"
 
-    # ---- workload: config 2 per GPU (weak scaling over landmarks)
-    scene = make_scene(num_frames=args.frames, num_points=args.points * n_gpus, seed=2, run_max=14)
-    full = ba.problem_from_map_frames(scene, args.frames - 2, args.frames, 2.0)
-    prob = ba.shard_problem(full, rank, n_gpus) if n_gpus > 1 else full
-
-    solver = ba.BundleAdjuster(device=local)
-    if n_gpus > 1:
-        uid = ba.BundleAdjuster.unique_id() if rank == 0 else bytes(128)
-        t = torch.tensor(list(uid), dtype=torch.uint8, device=f"cuda:{local}")
-        dist.broadcast(t, 0)
-        solver.comm_init(bytes(t.cpu().tolist()), n_gpus, rank)
-    solver.load(prob)
-    total_iters = args.warmup + 2 * args.steps + 16
-    opts = default_solver_options(max_num_iterations=total_iters, disable_termination=1)
-    solver.begin(opts)
-    solver.iterate(args.warmup)
-    solver.sync()
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
-    # ---- timed region: exactly K LM iterations
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    solver.iterate(args.steps)
-    solver.sync()
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
-    summary_after = solver.summary()
-
-    # ---- per-kernel HIP-event timing over a second timed region of the same workload
-    s0 = solver.summary()
-    solver.set_timing(True)
-    solver.iterate(args.steps)
-    solver.sync()
-    ktimes = solver.kernel_times()
-    solver.set_timing(False)
-    s1 = solver.summary()
-    n_lin = s1["num_successful_steps"] - s0["num_successful_steps"]
-    work = solver.kernel_work()
+    full, prob, desc, res, info, start, bal = run_workload(args.config, args, n_gpus, rank, local, dist,
+                                                           args.steps, args.warmup)
+    other = None
+    if args.other:
+        ocfg = "C2" if strong else "C5"
+        k2 = min(args.steps, 50)
+        f2, p2, d2, r2, i2, st2, b2 = run_workload(ocfg, args, n_gpus, rank, local, dist, k2, min(args.warmup, 10))
+        if rank == 0:
+            pk2, roof2, sw2 = kernel_report(r2, k2, "n=%d, band %d tiles" % (i2["n"], i2["band_tiles"]))
+            val2 = (n_gpus if ocfg == "C2" else 1) * k2 / r2["elapsed"]
+            other = {"workload": d2, "scaling": "weak" if ocfg == "C2" else "strong", "value": val2,
+                     "unit": "iters/s", "steps": k2, "ms_per_step": 1e3 * r2["elapsed"] / k2,
+                     "accepted_frac": r2["accepted"] / k2, "keyframes": f2.num_frames,
+                     "landmarks": f2.num_points, "observations": f2.num_obs, "per_rank": {
+                         "landmarks": p2.num_points, "observations": p2.num_obs}, "solver": i2,
+                     "kernel_ms_per_iter": pk2, "roofline": roof2, "roofline_sweep": sw2,
+                     "solve_from_start": st2, "shard_balance": b2}
 
     if rank != 0:
         if dist is not None:
@@ -229,34 +390,14 @@ def main():
             dist.destroy_process_group()
         return
 
-    per_iter_ms = {k: v[0] * v[1] / max(args.steps, 1) for k, v in ktimes.items()}
-    dominant = max(per_iter_ms, key=per_iter_ms.get)
-    # dominant kernel roofline (fp64 arithmetic)
-    dom_ms = ktimes[dominant][0]
-    dom_bytes, dom_flops = work[dominant]
-    if dom_flops > 0 and dominant in ("cholesky",):
-        ach = dom_flops / (dom_ms * 1e-3) / 1e12
-        roof = {"bound": "mfma", "achieved": ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": ach / FP64_PEAK_TFLOPS, "traffic": pmc_traffic("k_cholesky_window"), "kernel": dominant,
-                "note": "single-workgroup dense banded Cholesky of the reduced camera system (n=%d)"
-                        % (6 * (args.frames - 2))}
-    else:
-        ach = dom_bytes / (dom_ms * 1e-3) / 1e9
-        roof = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic("k_" + dominant), "kernel": dominant}
-    # Jacobian/Hessian sweep (north-star kernel): bytes per linearization / mean active launch time.
-    lin_total_ms = ktimes["linearize"][0] * ktimes["linearize"][1]
-    sweep = None
-    if n_lin > 0:
-        ach = work["linearize"][0] * n_lin / (lin_total_ms * 1e-3) / 1e9
-        sweep = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                 "frac": ach / HBM_PEAK_GBS, "bytes_per_launch": work["linearize"][0],
-                 "traffic": pmc_traffic("k_linearize"),
-                 "active_launches": n_lin, "launches": ktimes["linearize"][1]}
+    per_iter_ms, roof, sweep = kernel_report(res, args.steps, "n=%d, band %d tiles" % (info["n"], info["band_tiles"]))
 
-    # scaled sweep: the same kernel on a problem large enough to amortise launch latency
+    # scaled sweep: the linearization kernel on a problem large enough to amortise launch latency
     sweep_scaled = None
-    if args.sweep_obs > 0:
+    if args.sweep_obs > 0 and n_gpus == 1:
+        from slamgpu import ba
+        from slamgpu.capi import default_solver_options
+        from slamgpu.scene import make_scene
         npts = max(args.sweep_obs // 10, 1000)
         big = make_scene(num_frames=200, num_points=npts, seed=5, run_max=18)
         bp = ba.problem_from_map_frames(big, 198, 200, 2.0)
@@ -277,56 +418,47 @@ def main():
                         "traffic": pmc_traffic("k_linearize", largest_grid=True)}
         bs.close()
 
-    # CPU baseline: the oracle (C++ restatement of the same LM) on the host cores, bounded sample
     cpu = None
-    if args.cpu_seconds > 0 and n_gpus == 1:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle
-        threads = min(16, os.cpu_count() or 1)
-        po = full.copy()
-        o = default_solver_options(max_num_iterations=5, disable_termination=1)
-        done_iters, t_cpu = 0, 0.0
-        while t_cpu < args.cpu_seconds:
-            tt = time.perf_counter()
-            s = oracle.solve(po, o, nthreads=threads)
-            t_cpu += time.perf_counter() - tt
-            done_iters += s["num_lm_iterations"]
-        cpu = {"value": done_iters / t_cpu, "unit": "iters/s", "cores": threads, "kind": "port",
-               "sample": "%d LM iterations of config 2 (oracle/oracle_ba.cpp, dual-number Jacobians, "
-                         "OpenMP) in %.1f s, chunks of 5 iterations each re-linearising at start"
-                         % (done_iters, t_cpu)}
+    if args.cpu_runs > 0 and n_gpus == 1:
+        cpu = cpu_legs(full, args.cpu_runs, "48, 50, 2.0" if args.config == "C2" else "198, 200, 2.0")
 
     frontend = None
     if args.frontend and n_gpus == 1:
-        cs = min(args.cpu_seconds, 4.0)
+        cs = args.cpu_seconds
         frontend = {"tracker": bench_tracker(local, cs), "hamming": bench_hamming(local, cs)}
 
-    value = n_gpus * args.steps / elapsed
+    value = (1 if strong else n_gpus) * args.steps / res["elapsed"]
     line = {
-        "metric": "local-BA iters/sec (50 KF, 20k pts)",  # BASELINE metric; KLT tracks/sec under "frontend"
+        "metric": "local-BA iters/sec (%s)" % ("200 KF, 200k pts" if strong else "50 KF, 20k pts"),
         "value": value,
         "unit": "iters/s",
         "n_gpus": n_gpus,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": 1e3 * elapsed / args.steps,
+        "ms_per_step": 1e3 * res["elapsed"] / args.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (seeded scene generator, slamgpu/scene.py)",
-        "config": {"workload": "config 2: SolveFrames(48 of 50 KF) local BA, LM iteration",
-                   "keyframes": args.frames, "landmarks_per_gpu": prob.num_points,
+        "config": {"workload": desc, "keyframes": full.num_frames, "landmarks": full.num_points,
+                   "observations": full.num_obs, "landmarks_per_gpu": prob.num_points,
                    "observations_per_gpu": prob.num_obs, "free_frames": int(full.frame_rot_free.sum()),
                    "parallelism": "landmark-shard x%d (RCCL all-reduce of the camera system)" % n_gpus
                    if n_gpus > 1 else "single GPU"},
+        "accepted_frac": res["accepted"] / args.steps,
+        "solve_from_start": start,
+        "solver": info,
         "roofline": roof,
         "roofline_sweep": sweep,
         "roofline_sweep_scaled": sweep_scaled,
-        "kernel_ms_per_iter": {k: round(v, 5) for k, v in per_iter_ms.items()},
+        "kernel_ms_per_iter": per_iter_ms,
         "cpu_baseline": cpu,
         "speedup_vs_cpu": (value / cpu["value"]) if cpu else None,
-        "lm_state": {"final_cost": summary_after["final_cost"], "radius": summary_after["trust_region_radius"]},
+        "speedup_vs_cpu_from_start": (start["iters_per_s_wall"] / cpu["value"]) if cpu and start["iters_per_s_wall"] else None,
+        "lm_state": {"final_cost": res["summary"]["final_cost"], "radius": res["summary"]["trust_region_radius"]},
+        "shard_balance": bal,
+        "other_workload": other,
         "frontend": frontend,
         "traffic_source": "HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes "
                           "(tools/pmc_traffic.sh, profiles/*_pmc_traffic.json; FETCH_SIZE doubled on gfx950)",

@@ -150,7 +150,8 @@ typedef struct sg_solver_summary {
 
 typedef struct sg_device_options {
   int32_t device;                /* HIP device ordinal */
-  int32_t precision;             /* 0: fp64 everywhere; 1: fp32 Jacobian sweep, fp64 normal equations */
+  int32_t precision;             /* 0: fp64 everywhere, the reference's arithmetic (the only mode: any other
+                                    value is rejected with SG_EINVAL) */
   int32_t rank;                  /* landmark shard index (0 for single GPU) */
   int32_t nranks;                /* 1 for single GPU */
 } sg_device_options;
@@ -206,6 +207,18 @@ int sg_ba_set_timing(sg_ba* h, int32_t enable);
 int sg_ba_kernel_times(sg_ba* h, char* names, int32_t names_len, double* ms, int32_t* counts, int32_t max);
 /* Algorithmic byte / flop counts for the roofline (per launch of each timed kernel). */
 int sg_ba_kernel_work(sg_ba* h, double* bytes, double* flops, int32_t max);
+
+/* What the last sg_ba_load set up (diagnostics, benchmark records, shard balance). */
+typedef struct sg_ba_info {
+  int32_t num_frames, num_points, num_obs;   /* the loaded problem (this rank's landmark shard) */
+  int32_t num_blocks;                        /* free camera blocks (frames with a free rotation or translation) */
+  int32_t n;                                 /* reduced camera system dimension (6 blocks + free intrinsics) */
+  int32_t band_tiles;                        /* widest row of the Cholesky envelope, in 16-wide tiles */
+  int32_t cholesky_path;                     /* 0: tiled band (k_chol_tiles), 1: LDS window, 2: global memory */
+  int32_t num_pairs;                         /* Schur observation pairs (s <= t) of this rank's free points */
+  int32_t rank, nranks;
+} sg_ba_info;
+int sg_ba_info_get(const sg_ba* h, sg_ba_info* out);
 
 /* Jacobian/Hessian sweep only (benchmark of the HBM-bound kernel): n linearizations at the current
  * state (k_linearize + camera-block reduce), timed when sg_ba_set_timing is on. */

@@ -95,12 +95,30 @@ def problem_from_map_all(m, range_=2.0, solve_cameras=False):
     return pa
 
 
-def solve(pa: ProblemArrays, options: SgSolverOptions = None, nthreads: int = 1) -> dict:
-    """Solve in place (pa.q/t/X updated); returns the summary dict."""
+_FM = None
+
+
+def _fastmath_lib():
+    """oracle_ba.cpp built with the reference's -ffast-math (Makefile:4): CPU-baseline leg only."""
+    global _FM
+    if _FM is None:
+        path = os.path.join(HERE, "liboracle_fastmath.so")
+        if not os.path.exists(path):
+            build()
+        L = C.CDLL(path)
+        L.or_solve.argtypes = [C.POINTER(SgProblem), C.POINTER(SgSolverOptions), C.c_int,
+                               C.POINTER(SgSolverSummary)]
+        _FM = L
+    return _FM
+
+
+def solve(pa: ProblemArrays, options: SgSolverOptions = None, nthreads: int = 1, fastmath: bool = False) -> dict:
+    """Solve in place (pa.q/t/X updated); returns the summary dict.  fastmath: the -ffast-math build (CPU
+    baseline only; parity tests use the IEEE build)."""
     o = options or default_solver_options()
     s = SgSolverSummary()
     ps = pa.struct()
-    lib().or_solve(C.byref(ps), C.byref(o), nthreads, C.byref(s))
+    (_fastmath_lib() if fastmath else lib()).or_solve(C.byref(ps), C.byref(o), nthreads, C.byref(s))
     return s.as_dict()
 
 

@@ -39,6 +39,8 @@ class BaSolver {
   void CommInit(const void* id128, int nranks, int rank);
   static void UniqueId(void* id128);
 
+  void Info(sg_ba_info* out) const;
+
   // ReprojectMap (slam.cpp:523-548) over a whole map; used by the Slam facade.
   double ReprojectMap(sg_map* m);
 
@@ -70,6 +72,8 @@ class BaSolver {
   std::vector<int32_t> point_perm_;   // device order -> problem point
   std::vector<int32_t> obs_perm_;     // device order -> problem observation
   size_t schur_lds_ = 0;
+  int band_tiles_ = 0;     // widest Cholesky envelope row (16-wide tiles)
+  size_t npairs_ = 0;      // Schur observation pairs
   // Incremental problem update (replacing the per-call rebuild of slam.cpp:257-414):
   // the structure of the last Load.  A Load with the same structure (frames, cameras, freedom flags,
   // observation -> frame / point incidence, FrameDistance pairs) keeps the point order, the CSR, the sweep

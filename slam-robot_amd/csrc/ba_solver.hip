@@ -2751,6 +2751,8 @@ BaSolver::BaSolver(const sg_device_options& dev) : dev_(dev) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) throw Error(SG_ENODEV, "no HIP device available");
   SG_REQUIRE(dev.device >= 0 && dev.device < ndev, SG_ENODEV, "device ordinal out of range");
+  SG_REQUIRE(dev.precision == 0, SG_EINVAL,
+             "sg_device_options.precision: only 0 (fp64, the reference's arithmetic) is implemented");
   SG_HIP_CHECK(hipSetDevice(dev.device));
   SG_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   st_.Resize(1);
@@ -3068,6 +3070,7 @@ void BaSolver::Load(const sg_problem& p) {
     }
   }
   nseg_ = (int)segs.size();
+  npairs_ = pairs_flat.size() / 2;
   SG_REQUIRE(NB_ < 65536, SG_EINVAL, "too many camera blocks");
   if (pairs_flat.empty()) pairs_flat.assign(2, 0);
   lap("segments");
@@ -3185,6 +3188,9 @@ void BaSolver::Load(const sg_problem& p) {
   chol_window_ = npanel <= kJendSh;   // band ends cached in LDS
   for (int pk = 0; pk < npanel; ++pk)
     if (panel_jmax[pk] - pk * kCholNb > kCholWS) chol_window_ = false;
+  band_tiles_ = 0;
+  for (int pk = 0; pk < npanel; ++pk)
+    band_tiles_ = std::max(band_tiles_, (panel_jmax[pk] + kCholNb - 1) / kCholNb - pk);
   // tiled band Cholesky: every tile row's band within kTB tiles, x and z' of the whole system in LDS
   chol_tiles_ = n_ > 0 && nk_ == 0 && npanel <= kTileMaxNT && !getenv("SG_CHOL_WINDOW");
   for (int pk = 0; pk < npanel; ++pk)
@@ -3807,6 +3813,20 @@ int BaSolver::KernelWork(double* bytes, double* flops, int max) {
     flops[k] = fl[k];
   }
   return k;
+}
+
+void BaSolver::Info(sg_ba_info* o) const {
+  std::memset(o, 0, sizeof(*o));
+  o->num_frames = F_;
+  o->num_points = P_;
+  o->num_obs = M_;
+  o->num_blocks = NB_;
+  o->n = n_;
+  o->band_tiles = band_tiles_;
+  o->cholesky_path = chol_tiles_ ? 0 : (chol_window_ ? 1 : 2);
+  o->num_pairs = (int32_t)std::min<size_t>(npairs_, INT32_MAX);
+  o->rank = comm_ ? comm_->rank() : 0;
+  o->nranks = comm_ ? comm_->nranks() : 1;
 }
 
 double BaSolver::ReprojectMap(sg_map* m) {

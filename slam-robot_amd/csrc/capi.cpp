@@ -63,6 +63,13 @@ int sg_ba_load(sg_ba* h, const sg_problem* p) {
   SG_CAPI_END
 }
 
+int sg_ba_info_get(const sg_ba* h, sg_ba_info* out) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(h && out, SG_EINVAL, "null argument");
+  h->solver->Info(out);
+  SG_CAPI_END
+}
+
 int sg_ba_load_counts(const sg_ba* h, int32_t* full_loads, int32_t* value_loads) {
   SG_CAPI_BEGIN
   SG_REQUIRE(h && full_loads && value_loads, SG_EINVAL, "null argument");

@@ -10,8 +10,8 @@ import ctypes as C
 
 import numpy as np
 
-from .capi import (ProblemArrays, SgDeviceOptions, SgProblem, SgSolverOptions, SgSolverSummary, check,
-                   default_solver_options, load_library)
+from .capi import (ProblemArrays, SgBaInfo, SgDeviceOptions, SgProblem, SgSolverOptions, SgSolverSummary,
+                   check, default_solver_options, load_library)
 from .scene import MapArrays
 
 
@@ -101,6 +101,12 @@ class BundleAdjuster:
         full, vals = C.c_int32(0), C.c_int32(0)
         check(self.lib.sg_ba_load_counts(self.h, C.byref(full), C.byref(vals)), "sg_ba_load_counts")
         return full.value, vals.value
+
+    def info(self) -> dict:
+        """What the last load set up: sizes, Cholesky band and path, Schur pair count, shard."""
+        i = SgBaInfo()
+        check(self.lib.sg_ba_info_get(self.h, C.byref(i)), "sg_ba_info_get")
+        return i.as_dict()
 
     def solve(self, options: SgSolverOptions = None) -> dict:
         o = options or default_solver_options()

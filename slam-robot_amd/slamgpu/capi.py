@@ -76,6 +76,18 @@ class SgSolverSummary(C.Structure):
         return d
 
 
+class SgBaInfo(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in ("num_frames", "num_points", "num_obs", "num_blocks", "n", "band_tiles",
+                                         "cholesky_path", "num_pairs", "rank", "nranks")]
+    CHOLESKY_PATHS = {0: "tiled band (k_chol_tiles)", 1: "LDS window (k_cholesky_window)",
+                      2: "global memory (k_cholesky_global)"}
+
+    def as_dict(self):
+        d = {n: getattr(self, n) for n, _ in self._fields_}
+        d["cholesky"] = self.CHOLESKY_PATHS.get(self.cholesky_path, "?")
+        return d
+
+
 class SgDeviceOptions(C.Structure):
     _fields_ = [("device", C.c_int32), ("precision", C.c_int32), ("rank", C.c_int32),
                 ("nranks", C.c_int32)]
@@ -240,6 +252,7 @@ SYMBOLS = {
     "sg_ba_comm_init": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32]),
     "sg_ba_load": (C.c_int, [C.c_void_p, C.POINTER(SgProblem)]),
     "sg_ba_load_counts": (C.c_int, [C.c_void_p, _ip, _ip]),
+    "sg_ba_info_get": (C.c_int, [C.c_void_p, C.POINTER(SgBaInfo)]),
     "sg_ba_solve": (C.c_int, [C.c_void_p, C.POINTER(SgSolverOptions), C.POINTER(SgProblem),
                               C.POINTER(SgSolverSummary)]),
     "sg_ba_begin": (C.c_int, [C.c_void_p, C.POINTER(SgSolverOptions)]),

@@ -10,12 +10,13 @@ seeded synthetic scenes shaped like the robot's own data (main.cpp:474-552):
   * points uniform in the birth frame's frustum, depth U[1000, 6000] mm, stored as unit-norm
     homogeneous locations (localmap.cpp:35), uncertainty 1.0, flags clear (slam-usable);
   * each point observed in a contiguous run of frames starting at its birth frame, run length
-    U{2..run_max}, cut where it leaves the image; N(0, 0.5 px) pixel noise, 1 % outliers U(+-20 px);
+    U{run_min..run_max}, cut where it leaves the image; N(0, 0.5 px) pixel noise, 1 % outliers U(+-20 px);
   * initial perturbation of the free frames (0.5 deg rotation, 10 mm translation) and of the points
     (5 % depth along the birth ray).  The two oldest frames keep their true pose (gauge).
 
-Configs (BASELINE.json): C1 = 10 KF / 500 pts (seed 1), C2 = 50 KF / 20k pts (seed 2),
-C5 = 200 KF / 200k pts (seed 5).
+Configs (BASELINE.json): C1 = 10 KF / 500 pts (seed 1), C2 = 50 KF / 20k pts / ~150k obs (seed 2),
+C5 = 200 KF / 200k pts / ~2M obs (seed 5).  run_min sets the observation count per landmark without widening
+the co-visibility band (run_max bounds it).
 """
 from __future__ import annotations
 
@@ -31,8 +32,8 @@ K_ROBOT = np.array([0.0, 0.0, 0.0, 416.0, -416.0, 320.0, 240.0])
 
 CONFIGS = {
     "C1": dict(num_frames=10, num_points=500, seed=1, run_max=14),
-    "C2": dict(num_frames=50, num_points=20000, seed=2, run_max=14),
-    "C5": dict(num_frames=200, num_points=200000, seed=5, run_max=18),
+    "C2": dict(num_frames=50, num_points=20000, seed=2, run_max=14, run_min=4),
+    "C5": dict(num_frames=200, num_points=200000, seed=5, run_max=18, run_min=6),
 }
 
 
@@ -146,7 +147,7 @@ class MapArrays:
         return m
 
 
-def make_scene(num_frames: int, num_points: int, seed: int, run_max: int = 14, noise: float = 0.5,
+def make_scene(num_frames: int, num_points: int, seed: int, run_max: int = 14, run_min: int = 2, noise: float = 0.5,
                outlier_frac: float = 0.01, outlier_px: float = 20.0, rot_noise_deg: float = 0.5,
                trans_noise: float = 10.0, depth_noise: float = 0.05, num_const: int = 2,
                perturb: bool = True) -> MapArrays:
@@ -176,7 +177,7 @@ def make_scene(num_frames: int, num_points: int, seed: int, run_max: int = 14, n
     yp = (v - K_ROBOT[6]) / K_ROBOT[4]
     pc = np.stack([xp * depth, yp * depth, depth], 1)
     Xw = np.einsum("nji,nj->ni", R_true[birth], pc) + t_true[birth]
-    run = rng.integers(2, run_max + 1, size=P)
+    run = rng.integers(run_min, run_max + 1, size=P)
     obs_list = []   # (frame, point, u, v)
     nobs = np.zeros(P, dtype=np.int64)
     alive = np.ones(P, dtype=bool)

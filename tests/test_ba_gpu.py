@@ -103,6 +103,35 @@ def test_c2_solve_matches_oracle_iteration_for_iteration(gpu_lib, oracle_lib):
     assert abs(sg["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"]
 
 
+def test_c5_first_iterations_match_oracle(gpu_lib, oracle_lib):
+    """BASELINE config 5 on one GPU: 200 keyframes / ~194k landmarks / ~1.95M observations,
+    SolveFrames(map, 198, 200, 2.0) (slam.cpp:417-443).  The reduced camera system is n = 1188 (198 free
+    frames) with a co-visibility band of <= 8 16-wide tiles, factored by the tiled band Cholesky.  Three LM
+    iterations against the oracle's dense solve, iteration for iteration: the same accepted steps, cost to
+    1e-9 relative, rotations to 1e-9, translations to 1e-6 mm, points to 1e-9."""
+    import os
+    m = make_config("C5")
+    assert m.num_frames == 200 and m.num_points > 190000 and m.num_obs > 1.9e6
+    pa = ba.problem_from_map_frames(m, 198, 200, 2.0)
+    o = default_solver_options(max_num_iterations=3)
+    pg, po = pa.copy(), pa.copy()
+    g = ba.BundleAdjuster()
+    g.load(pg)
+    info = g.info()
+    assert info["n"] == 6 * 198 and info["band_tiles"] <= 8
+    assert info["cholesky"].startswith("tiled band")
+    sg = g.solve(o)
+    so = oracle_lib.solve(po, o, nthreads=min(16, os.cpu_count() or 1))
+    assert sg["ok"] == so["ok"] == 1
+    assert sg["num_iterations"] == so["num_iterations"] == 4
+    assert sg["num_successful_steps"] == so["num_successful_steps"]
+    assert abs(sg["initial_cost"] - so["initial_cost"]) <= 1e-10 * so["initial_cost"]
+    assert abs(sg["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"]
+    np.testing.assert_allclose(pg.q, po.q, rtol=0, atol=1e-9)
+    np.testing.assert_allclose(pg.t, po.t, rtol=0, atol=1e-6)
+    np.testing.assert_allclose(pg.X, po.X, rtol=0, atol=1e-9)
+
+
 def test_wide_points_and_edge_structure(gpu_lib, oracle_lib):
     """Points seen over > 24 free frames (global-atomic 'wide' path), constant points, a skipped previous
     frame whose translation is freed by FrameDistance, disabled observations and unusable points."""
