@@ -186,6 +186,15 @@ void sg_ba_destroy(sg_ba* h);
 /* RCCL communicator for landmark sharding: id is ncclUniqueId (128 bytes), from sg_comm_unique_id. */
 int sg_comm_unique_id(void* id128);
 int sg_ba_comm_init(sg_ba* h, const void* id128, int32_t nranks, int32_t rank);
+/* In-process communicator group: nranks (<= 8) solver handles on ONE device, each driven by its own host
+ * thread, exchange through the group instead of RCCL (each all-reduce synchronises the rank's stream, meets
+ * the others at a host barrier and sums in rank order).  Runs the landmark-sharded device chain (envelope
+ * union, rank-0 assembly, packed S exchange, the replicated decision) on a one-GPU machine; for tests.
+ * Destroy the group after every handle that uses it. */
+typedef struct sg_comm_group sg_comm_group;
+int sg_comm_group_create(sg_comm_group** out, int32_t nranks);
+void sg_comm_group_destroy(sg_comm_group* g);
+int sg_ba_comm_init_local(sg_ba* h, sg_comm_group* g, int32_t rank);
 /* Upload a problem (the problem's q/t/X are read now and written back by sg_ba_download). */
 int sg_ba_load(sg_ba* h, const sg_problem* p);
 /* Incremental problem update (replaces the per-call rebuild of slam.cpp:257-414): a

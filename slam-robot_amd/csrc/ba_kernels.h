@@ -64,6 +64,8 @@ struct SchurSeg {
   int32_t s_off;        // offset of the window partial in S_slab
   int32_t wide;         // global atomics instead of an LDS window
   int32_t pair_lo, pair_hi;
+  int32_t heavy;        // one point with more than kSegObsCap observations: P rows recomputed per pair,
+                        // not staged in LDS (a long-tracked point of a whole-map solve)
 };
 
 // k_linearize work decomposition: a chunk (one single-wave workgroup) is a run of consecutive points whose

@@ -37,6 +37,7 @@ class BaSolver {
   int KernelTimes(char* names, int names_len, double* ms, int32_t* counts, int max);
   int KernelWork(double* bytes, double* flops, int max);
   void CommInit(const void* id128, int nranks, int rank);
+  void CommInitLocal(std::shared_ptr<struct LocalGroup> g, int rank);   // in-process test group (comm.h)
   static void UniqueId(void* id128);
 
   void Info(sg_ba_info* out) const;

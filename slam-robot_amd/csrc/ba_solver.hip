@@ -781,16 +781,18 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d) {
     double Jp[8];
     load_Jp_scaled(d, o, s4, Jp);
     const double* Vi = vinv + 10 * lp;
-    double* Pr = Psh + 8 * (o - obs_lo);
+    if (!sg.heavy) {
+      double* Pr = Psh + 8 * (o - obs_lo);
 #pragma unroll
-    for (int rr = 0; rr < 2; ++rr)
+      for (int rr = 0; rr < 2; ++rr)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        double acc = 0.0;
+        for (int c = 0; c < 4; ++c) {
+          double acc = 0.0;
 #pragma unroll
-        for (int m = 0; m < 4; ++m) acc += Jp[4 * rr + m] * sym4(Vi, m, c);
-        Pr[4 * rr + c] = acc;
-      }
+          for (int m = 0; m < 4; ++m) acc += Jp[4 * rr + m] * sym4(Vi, m, c);
+          Pr[4 * rr + c] = acc;
+        }
+    }
     if (b < 0) continue;
     double Jc[12];
     load_Jc_scaled(d, o, b, Jc);
@@ -817,8 +819,24 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d) {
     load_Jc_scaled(d, ot, bt, Jct);
     load_Jp_scaled(d, ot, s4, Jpt);
     double Ps[8];
+    if (!sg.heavy) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) Ps[i] = Psh[8 * (os - obs_lo) + i];
+      for (int i = 0; i < 8; ++i) Ps[i] = Psh[8 * (os - obs_lo) + i];
+    } else {
+      // P_s = J~p,s V~^-1 recomputed (same arithmetic as the staged rows)
+      double Jps[8];
+      load_Jp_scaled(d, os, s4, Jps);
+      const double* Vi = vinv + 10 * (p - q0);
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          double acc = 0.0;
+#pragma unroll
+          for (int m = 0; m < 4; ++m) acc += Jps[4 * rr + m] * sym4(Vi, m, c);
+          Ps[4 * rr + c] = acc;
+        }
+    }
     const int I = bs < bt ? bs : bt, Jb = bs < bt ? bt : bs;
     if (sg.wide)
       schur_pair_add(d.S_wide + (size_t)(6 * I) * d.n + 6 * Jb, d.n, Jcs, Ps, Jpt, Jct, os == ot, bs == bt, bs < bt);
@@ -2766,13 +2784,21 @@ BaSolver::~BaSolver() {
   if (stream_) (void)hipStreamDestroy(stream_);
 }
 
-void BaSolver::UniqueId(void* id128) { Comm::UniqueId(id128); }
+void BaSolver::UniqueId(void* id128) { RcclComm::UniqueId(id128); }
 
 void BaSolver::CommInit(const void* id128, int nranks, int rank) {
   SG_REQUIRE(!loaded_, SG_EINVAL, "sg_ba_comm_init must precede sg_ba_load (exchange buffers are sized by it)");
   SG_HIP_CHECK(hipSetDevice(dev_.device));
-  comm_.reset(new Comm(id128, nranks, rank));
+  comm_.reset(new RcclComm(id128, nranks, rank));
   dev_.nranks = nranks;
+  dev_.rank = rank;
+}
+
+void BaSolver::CommInitLocal(std::shared_ptr<LocalGroup> g, int rank) {
+  SG_REQUIRE(!loaded_, SG_EINVAL, "sg_ba_comm_init_local must precede sg_ba_load");
+  SG_HIP_CHECK(hipSetDevice(dev_.device));
+  comm_.reset(new LocalComm(std::move(g), rank));
+  dev_.nranks = comm_->nranks();
   dev_.rank = rank;
 }
 
@@ -2794,13 +2820,30 @@ void BaSolver::Load(const sg_problem& p) {
     lap_log += buf;
     lt0 = t;
   };
-  ValidateProblem(&p);
-  SG_REQUIRE(!p.cameras_free || (p.num_cameras <= kMaxIntrCams && nranks() == 1), SG_EINVAL,
-             "free intrinsics: at most 4 cameras, on one rank (landmark shards keep the intrinsics constant)");
   SG_HIP_CHECK(hipSetDevice(dev_.device));
   {
+    // Everything that can reject this rank's problem runs before the first collective, and the verdict rides
+    // in that collective (2: some rank's problem is invalid), so that all ranks fail together instead of
+    // leaving the others blocked in an all-reduce.
+    int vcode = SG_OK;
+    std::string verr;
+    try {
+      ValidateProblem(&p);
+      SG_REQUIRE(!p.cameras_free || (p.num_cameras <= kMaxIntrCams && nranks() == 1), SG_EINVAL,
+                 "free intrinsics: at most 4 cameras, on one rank (landmark shards keep the intrinsics constant)");
+      SG_REQUIRE(p.num_cameras <= 0xff, SG_EINVAL, "too many cameras for the device solver");
+      int nfree = 0;
+      for (int f = 0; f < p.num_frames; ++f) nfree += (p.frame_rot_free[f] || p.frame_trans_free[f]) ? 1 : 0;
+      SG_REQUIRE(nfree < 0xffff, SG_EINVAL, "too many free frames for the device solver");
+      std::vector<int32_t> cnt(p.num_points, 0);
+      for (int o = 0; o < p.num_obs; ++o)
+        SG_REQUIRE(++cnt[p.obs_point[o]] < 65536, SG_EINVAL, "a point has 65536 or more observations");
+    } catch (const Error& e) {
+      vcode = e.code;
+      verr = e.what();
+    }
     // incremental update: every rank must take the same path (the full path has a load-time all-reduce)
-    double changed = (loaded_ && !getenv("SG_NO_REUSE") && SameStructure(p)) ? 0.0 : 1.0;
+    double changed = vcode != SG_OK ? 2.0 : (loaded_ && !getenv("SG_NO_REUSE") && SameStructure(p)) ? 0.0 : 1.0;
     if (comm_ && comm_->nranks() > 1) {
       DBuf<double> flag;
       flag.Upload(std::vector<double>{changed}, stream_);
@@ -2808,6 +2851,8 @@ void BaSolver::Load(const sg_problem& p) {
       SG_HIP_CHECK(hipMemcpyAsync(&changed, flag.ptr, sizeof(double), hipMemcpyDeviceToHost, stream_));
       SG_HIP_CHECK(hipStreamSynchronize(stream_));
     }
+    if (vcode != SG_OK) throw Error(vcode, verr);
+    if (changed == 2.0) throw Error(SG_EINVAL, "another landmark shard's problem failed validation");
     if (changed == 0.0) {
       LoadValues(p);
       lap("values");
@@ -2815,6 +2860,12 @@ void BaSolver::Load(const sg_problem& p) {
       return;
     }
   }
+  // Full path: the structure and every device list are rebuilt below.  Until that completes, this solver
+  // holds no usable problem: a failure part way (a device allocation, a hipFuncSetAttribute) must not leave
+  // the previous problem's structure key matching a later load's value-only path.
+  loaded_ = false;
+  began_ = false;
+  skey_ = StructKey{};
   F_ = p.num_frames;
   P_ = p.num_points;
   M_ = p.num_obs;
@@ -2874,7 +2925,6 @@ void BaSolver::Load(const sg_problem& p) {
     pfree[i] = p.point_free[pt];
     for (int a = 0; a < 4; ++a) X[4 * i + a] = p.X[4 * pt + a];
   }
-  SG_REQUIRE(NB_ < 0xffff && ncam_ <= 0xff, SG_EINVAL, "too many free frames or cameras for the device solver");
   std::vector<int32_t> obs_meta(M_);
   {
     // per frame: the frame part of the packed observation word
@@ -3006,6 +3056,7 @@ void BaSolver::Load(const sg_problem& p) {
   }
   int s_off = 0;
   max_seg_nb_ = 0;
+  max_seg_obs_ = 0;
   {
     auto span = [&](int i) { return pfirst[point_perm_[i]] >= NB_ ? 0 : plast[point_perm_[i]] - pfirst[point_perm_[i]] + 1; };
     // Window width: the widest single point (so no point needs the global-atomic "wide" path), capped at
@@ -3043,12 +3094,12 @@ void BaSolver::Load(const sg_problem& p) {
         sg.b_lo = lo;
         sg.nb = hi - lo + 1;
       }
-      SG_REQUIRE(nobs < 65536, SG_EINVAL, "a point has too many observations");
       sg.p1 = j;
       sg.s_off = s_off;
+      sg.heavy = nobs > kSegObsCap ? 1 : 0;   // only a single point exceeds the cap
       s_off += sg.wide ? 0 : sg.nb * (sg.nb + 1) / 2 * 36 + sg.nb * 6;
       max_seg_nb_ = std::max(max_seg_nb_, sg.nb);
-      max_seg_obs_ = std::max(max_seg_obs_, nobs);
+      if (!sg.heavy) max_seg_obs_ = std::max(max_seg_obs_, nobs);
       const int obs_lo = poff[i];
       sg.pair_lo = (int)pairs_flat.size() / 2;
       for (int pt = i; pt < j; ++pt) {
@@ -3071,7 +3122,6 @@ void BaSolver::Load(const sg_problem& p) {
   }
   nseg_ = (int)segs.size();
   npairs_ = pairs_flat.size() / 2;
-  SG_REQUIRE(NB_ < 65536, SG_EINVAL, "too many camera blocks");
   if (pairs_flat.empty()) pairs_flat.assign(2, 0);
   lap("segments");
   // deterministic reduction lists: for every camera block / block pair, the slab offsets of the chunk
@@ -3298,6 +3348,9 @@ void BaSolver::Load(const sg_problem& p) {
   ResetState(s);
   schur_lds_ = sizeof(double) * ((size_t)max_seg_nb_ * (max_seg_nb_ + 1) / 2 * kWinLd + max_seg_nb_ * 6 +
                                   (size_t)kSegPts * 14 + (size_t)std::max(max_seg_obs_, 1) * 8);
+  // bounded by construction: window <= kSegNbMax blocks, staged observations <= kSegObsCap (heavy points are
+  // not staged)
+  SG_REQUIRE(schur_lds_ <= 160 * 1024, SG_EINVAL, "Schur segment LDS budget exceeded");
   SG_HIP_CHECK(hipFuncSetAttribute((const void*)k_schur, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)schur_lds_));
   if (chol_tiles_)

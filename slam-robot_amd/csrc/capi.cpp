@@ -9,11 +9,16 @@
 #include <memory>
 
 #include "ba_solver.h"
+#include "comm.h"
 #include "common.h"
 #include "map_ops.h"
 
 struct sg_ba {
   std::unique_ptr<sg::BaSolver> solver;
+};
+
+struct sg_comm_group {
+  std::shared_ptr<sg::LocalGroup> g;
 };
 
 struct sg_slam {
@@ -53,6 +58,24 @@ int sg_ba_comm_init(sg_ba* h, const void* id128, int32_t nranks, int32_t rank) {
   SG_CAPI_BEGIN
   SG_REQUIRE(h && id128, SG_EINVAL, "null argument");
   h->solver->CommInit(id128, nranks, rank);
+  SG_CAPI_END
+}
+
+int sg_comm_group_create(sg_comm_group** out, int32_t nranks) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(out && nranks >= 1 && nranks <= sg::LocalGroup::kMaxRanks, SG_EINVAL, "bad group size");
+  auto g = std::make_unique<sg_comm_group>();
+  g->g = std::make_shared<sg::LocalGroup>(nranks);
+  *out = g.release();
+  SG_CAPI_END
+}
+
+void sg_comm_group_destroy(sg_comm_group* g) { delete g; }
+
+int sg_ba_comm_init_local(sg_ba* h, sg_comm_group* g, int32_t rank) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(h && g, SG_EINVAL, "null argument");
+  h->solver->CommInitLocal(g->g, rank);
   SG_CAPI_END
 }
 

@@ -59,6 +59,26 @@ def shard_problem(pa: ProblemArrays, rank: int, nranks: int) -> ProblemArrays:
     return sh
 
 
+class LocalCommGroup:
+    """sg_comm_group: nranks solver handles on one device exchanging in-process instead of over RCCL."""
+
+    def __init__(self, nranks: int):
+        self.lib = load_library()
+        self.h = C.c_void_p()
+        check(self.lib.sg_comm_group_create(C.byref(self.h), nranks), "sg_comm_group_create")
+
+    def close(self):
+        if self.h:
+            self.lib.sg_comm_group_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class BundleAdjuster:
     """The device solver (sg_ba): load a problem, solve or run fixed LM iterations."""
 
@@ -83,6 +103,10 @@ class BundleAdjuster:
     def comm_init(self, uid: bytes, nranks: int, rank: int):
         buf = C.create_string_buffer(uid, 128)
         check(self.lib.sg_ba_comm_init(self.h, buf, nranks, rank), "sg_ba_comm_init")
+
+    def comm_init_local(self, group: "LocalCommGroup", rank: int):
+        """Join an in-process communicator group (one device, one host thread per rank; tests)."""
+        check(self.lib.sg_ba_comm_init_local(self.h, group.h, rank), "sg_ba_comm_init_local")
 
     @staticmethod
     def unique_id() -> bytes:

@@ -250,6 +250,9 @@ SYMBOLS = {
     "sg_ba_destroy": (None, [C.c_void_p]),
     "sg_comm_unique_id": (C.c_int, [C.c_void_p]),
     "sg_ba_comm_init": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32]),
+    "sg_comm_group_create": (C.c_int, [C.POINTER(C.c_void_p), C.c_int32]),
+    "sg_comm_group_destroy": (None, [C.c_void_p]),
+    "sg_ba_comm_init_local": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32]),
     "sg_ba_load": (C.c_int, [C.c_void_p, C.POINTER(SgProblem)]),
     "sg_ba_load_counts": (C.c_int, [C.c_void_p, _ip, _ip]),
     "sg_ba_info_get": (C.c_int, [C.c_void_p, C.POINTER(SgBaInfo)]),
