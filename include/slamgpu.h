@@ -345,6 +345,10 @@ int sg_map_clean(sg_slam* s, sg_map* map, double error_threshold, int32_t* resul
 /* LocalMap::ApplyEpipolarConstraint() (localmap.cpp:232-276): writes point_flags and obs_disabled;
  * *num_violations = points whose |h2^T E h1| exceeded 0.15. */
 int sg_map_apply_epipolar(sg_slam* s, sg_map* map, int32_t* num_violations);
+/* LocalMap::Normalize (localmap.cpp:114-155): translate frame 0 to the origin, then rotate frame 0 to the
+ * identity (frames' rotations and translations, points' homogeneous locations; a map with < 2 frames is left
+ * alone).  main.cpp:602-605 checks that ReprojectMap is unchanged by it (CHECK_NEAR 0.1). */
+int sg_map_normalize(sg_slam* s, sg_map* map);
 
 /* ------------------------------------------------------------------------------------------------
  * Matcher::Track (matcher.h:20-26, matcher.cpp:301-405): the per-frame front end with its bookkeeping —

@@ -64,6 +64,7 @@ def lib():
         L.orm_clean.argtypes = [C.POINTER(SgMap), C.c_double]
         L.orm_apply_epipolar.restype = C.c_int
         L.orm_apply_epipolar.argtypes = [C.POINTER(SgMap)]
+        L.orm_normalize.argtypes = [C.POINTER(SgMap)]
         _LIB = L
     return _LIB
 
@@ -186,6 +187,12 @@ def apply_epipolar(m) -> int:
     """LocalMap::ApplyEpipolarConstraint (localmap.cpp:232-276) restated in oracle_map.cpp; mutates m."""
     s = m.struct()
     return int(lib().orm_apply_epipolar(C.byref(s)))
+
+
+def normalize(m):
+    """LocalMap::Normalize (localmap.cpp:114-155) in place on a MapArrays."""
+    st = m.struct()
+    lib().orm_normalize(C.byref(st))
 
 
 def slam_solve_frames(m, num_to_solve, num_to_present, range_=2.0, options=None, nthreads=1):

@@ -234,4 +234,72 @@ int orm_apply_epipolar(sg_map* m) {
   return hits;
 }
 
+// LocalMap::Normalize (localmap.cpp:114-155).  xlate = -t0, scale = 1 (line 125 overrides the 150 mm
+// baseline scale); every frame's translation and every point are moved by xlate (TrackedPoint::move
+// adds xlate * w, rescale(1 / scale) normalises the 4-vector); then rotate = q0.matrix(), each frame's rotation
+// becomes quaternion(R_f * rotate^-1) (Quaternion * Matrix3 is a matrix product, assigned back through
+// quaternionbase_assign_impl), each translation and point direction is multiplied by rotate.
+void orm_normalize(sg_map* m) {
+  if (m->num_frames < 2) return;
+  const double xl[3] = {-m->t[0], -m->t[1], -m->t[2]};
+  for (int f = 0; f < m->num_frames; ++f)
+    for (int c = 0; c < 3; ++c) m->t[3 * f + c] += xl[c];
+  for (int p = 0; p < m->num_points; ++p) {
+    double* x = m->X + 4 * p;
+    for (int c = 0; c < 3; ++c) x[c] += xl[c] * x[3];
+    const double nrm = std::sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3]);
+    for (int c = 0; c < 4; ++c) x[c] /= nrm;
+  }
+  double R[3][3], inv[3][3];
+  QuatMatrix(m->q, R);
+  {
+    // compute_inverse_size3_helper: cofactors, determinant along column 0
+    auto cof = [&](int i, int j) {
+      const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+      return R[i1][j1] * R[i2][j2] - R[i1][j2] * R[i2][j1];
+    };
+    const double c0 = cof(0, 0), c1 = cof(1, 0), c2 = cof(2, 0);
+    const double invdet = 1.0 / (c0 * R[0][0] + c1 * R[1][0] + c2 * R[2][0]);
+    inv[0][0] = c0 * invdet; inv[0][1] = c1 * invdet; inv[0][2] = c2 * invdet;
+    inv[1][0] = cof(0, 1) * invdet; inv[1][1] = cof(1, 1) * invdet; inv[1][2] = cof(2, 1) * invdet;
+    inv[2][0] = cof(0, 2) * invdet; inv[2][1] = cof(1, 2) * invdet; inv[2][2] = cof(2, 2) * invdet;
+  }
+  for (int f = 0; f < m->num_frames; ++f) {
+    double Rf[3][3], M[3][3];
+    QuatMatrix(m->q + 4 * f, Rf);
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) M[i][j] = Rf[i][0] * inv[0][j] + Rf[i][1] * inv[1][j] + Rf[i][2] * inv[2][j];
+    double* q = m->q + 4 * f;
+    // quaternionbase_assign_impl<Matrix3>: trace branch, else the largest diagonal
+    double t = M[0][0] + M[1][1] + M[2][2];
+    if (t > 0.0) {
+      t = std::sqrt(t + 1.0);
+      q[3] = 0.5 * t;
+      t = 0.5 / t;
+      q[0] = (M[2][1] - M[1][2]) * t;
+      q[1] = (M[0][2] - M[2][0]) * t;
+      q[2] = (M[1][0] - M[0][1]) * t;
+    } else {
+      int i = 0;
+      if (M[1][1] > M[0][0]) i = 1;
+      if (M[2][2] > M[i][i]) i = 2;
+      const int j = (i + 1) % 3, k = (j + 1) % 3;
+      t = std::sqrt(M[i][i] - M[j][j] - M[k][k] + 1.0);
+      q[i] = 0.5 * t;
+      t = 0.5 / t;
+      q[3] = (M[k][j] - M[j][k]) * t;
+      q[j] = (M[j][i] + M[i][j]) * t;
+      q[k] = (M[k][i] + M[i][k]) * t;
+    }
+    double* tf = m->t + 3 * f;
+    const double v[3] = {tf[0], tf[1], tf[2]};
+    for (int i = 0; i < 3; ++i) tf[i] = R[i][0] * v[0] + R[i][1] * v[1] + R[i][2] * v[2];
+  }
+  for (int p = 0; p < m->num_points; ++p) {
+    double* x = m->X + 4 * p;
+    const double v[3] = {x[0], x[1], x[2]};
+    for (int i = 0; i < 3; ++i) x[i] = R[i][0] * v[0] + R[i][1] * v[1] + R[i][2] * v[2];
+  }
+}
+
 }  // extern "C"

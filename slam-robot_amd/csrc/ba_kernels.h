@@ -66,6 +66,10 @@ struct SchurSeg {
   int32_t pair_lo, pair_hi;
   int32_t heavy;        // one point with more than kSegObsCap observations: P rows recomputed per pair,
                         // not staged in LDS (a long-tracked point of a whole-map solve)
+  int32_t det;          // deterministic mode (SG_DETERMINISTIC=1 at load): the pair list is split into 4
+  int32_t pw[3];        // per-wave lists [pair_lo, pw0), [pw0, pw1), [pw1, pw2), [pw2, pair_hi) so that each
+                        // window block (and each rhs block, through its observations' (o, o) pairs) is summed
+                        // by one wave in list order: bitwise reproducible runs, at ~1.3x the Schur time
 };
 
 // k_linearize work decomposition: a chunk (one single-wave workgroup) is a run of consecutive points whose

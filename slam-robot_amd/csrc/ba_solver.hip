@@ -793,7 +793,7 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d) {
           Pr[4 * rr + c] = acc;
         }
     }
-    if (b < 0) continue;
+    if (b < 0 || sg.det) continue;   // deterministic segments: the rhs rides on the (o, o) pair in phase 3
     double Jc[12];
     load_Jc_scaled(d, o, b, Jc);
     const double* tp = tpv + 4 * lp;
@@ -807,8 +807,16 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d) {
     }
   }
   __syncthreads();
-  // phase 3: one thread per observation pair
-  for (int k = sg.pair_lo + tid; k < sg.pair_hi; k += kSchurThreads) {
+  // phase 3: one thread per observation pair (a wide segment's pairs go to global atomics); in deterministic
+  // mode each wave walks its own list (every block summed by one wave, in list order)
+  int k0 = sg.pair_lo + tid, k1 = sg.pair_hi, kstep = kSchurThreads;
+  if (sg.det) {
+    const int w = tid >> 6;
+    k0 = (w == 0 ? sg.pair_lo : sg.pw[w - 1]) + (tid & 63);
+    k1 = w == 3 ? sg.pair_hi : sg.pw[w];
+    kstep = 64;
+  }
+  for (int k = k0; k < k1; k += kstep) {
     const int2 pr = d.pairs[k];
     const int os = obs_lo + (pr.x >> 16), ot = obs_lo + (pr.x & 0xffff);
     const int bs = pr.y >> 16, bt = pr.y & 0xffff;
@@ -836,6 +844,14 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d) {
           for (int m = 0; m < 4; ++m) acc += Jps[4 * rr + m] * sym4(Vi, m, c);
           Ps[4 * rr + c] = acc;
         }
+    }
+    if (sg.det && os == ot) {
+      // this observation's rhs term -A_c,o^T (A_p,o t_p), from the wave that owns its diagonal block
+      const double* tp = tpv + 4 * (p - q0);
+      const double e0 = Jpt[0] * tp[0] + Jpt[1] * tp[1] + Jpt[2] * tp[2] + Jpt[3] * tp[3];
+      const double e1 = Jpt[4] * tp[0] + Jpt[5] * tp[1] + Jpt[6] * tp[2] + Jpt[7] * tp[3];
+#pragma unroll
+      for (int a = 0; a < 6; ++a) atomicAdd(rhsw + (bs - sg.b_lo) * 6 + a, -(Jcs[a] * e0 + Jcs[6 + a] * e1));
     }
     const int I = bs < bt ? bs : bt, Jb = bs < bt ? bt : bs;
     if (sg.wide)
@@ -3055,6 +3071,8 @@ void BaSolver::Load(const sg_problem& p) {
     pairs_flat.reserve(2 * npairs + 2);
   }
   int s_off = 0;
+  // SG_DETERMINISTIC=1: window blocks summed by one wave each (bitwise reproducible; see SchurSeg::det)
+  const bool deterministic = getenv("SG_DETERMINISTIC") && getenv("SG_DETERMINISTIC")[0] == '1';
   max_seg_nb_ = 0;
   max_seg_obs_ = 0;
   {
@@ -3116,6 +3134,41 @@ void BaSolver::Load(const sg_problem& p) {
         }
       }
       sg.pair_hi = (int)pairs_flat.size() / 2;
+      sg.pw[0] = sg.pw[1] = sg.pw[2] = sg.pair_hi;
+      sg.det = deterministic && !sg.wide;
+      if (sg.det && sg.pair_hi > sg.pair_lo) {
+        // per-wave lists: window block rows I = min(b_s, b_t) (by pair count, largest first) to the least
+        // loaded of the 4 waves, pairs stably partitioned by their row's wave.  Every block, and every rhs
+        // block through its observations' (o, o) pairs, then belongs to one wave, while each list keeps the
+        // point-major order in which neighbouring lanes share an observation's rows (loads) and spread over
+        // different blocks (LDS atomics).
+        auto row = [&](int k) {
+          const int v = pairs_flat[2 * k + 1];
+          return std::min(v >> 16, v & 0xffff) - sg.b_lo;
+        };
+        std::vector<int> cnt(sg.nb, 0), order(sg.nb), wave_of(sg.nb, 0);
+        for (int k = sg.pair_lo; k < sg.pair_hi; ++k) cnt[row(k)]++;
+        std::iota(order.begin(), order.end(), 0);
+        std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cnt[a] > cnt[b]; });
+        long load[kSchurThreads / 64] = {0, 0, 0, 0};
+        for (int r : order) {
+          if (!cnt[r]) break;
+          const int w = int(std::min_element(load, load + kSchurThreads / 64) - load);
+          wave_of[r] = w;
+          load[w] += cnt[r];
+        }
+        std::vector<int32_t> tmp(pairs_flat.begin() + 2 * (size_t)sg.pair_lo, pairs_flat.end());
+        size_t at = 2 * (size_t)sg.pair_lo;
+        for (int w = 0; w < kSchurThreads / 64; ++w) {
+          if (w > 0) sg.pw[w - 1] = (int)(at / 2);
+          for (size_t e = 0; e < tmp.size(); e += 2) {
+            const int v = tmp[e + 1];
+            if (wave_of[std::min(v >> 16, v & 0xffff) - sg.b_lo] != w) continue;
+            pairs_flat[at++] = tmp[e];
+            pairs_flat[at++] = tmp[e + 1];
+          }
+        }
+      }
       segs.push_back(sg);
       i = j;
     }

@@ -305,6 +305,13 @@ int sg_map_apply_epipolar(sg_slam* s, sg_map* map, int32_t* num_violations) {
   SG_CAPI_END
 }
 
+int sg_map_normalize(sg_slam* s, sg_map* map) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(s && map, SG_EINVAL, "null argument");
+  MapOpsOf(s).Normalize(map);
+  SG_CAPI_END
+}
+
 int32_t sg_slam_iterations(const sg_slam* s) { return s ? s->iterations : 0; }
 double sg_slam_error(const sg_slam* s) { return s ? s->error : 0.0; }
 

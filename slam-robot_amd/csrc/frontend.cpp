@@ -103,10 +103,19 @@ class Frontend {
     *st = sg_frontend_stats{};
     batches_ = 0;
 
-    // The new view's pyramid (matcher.cpp:319-322).
+    // The new view's pyramid (matcher.cpp:319-322).  The slot goes back to the free list on every exit
+    // unless the view is kept (a callback failing or an expired view must not leak it).
     SG_REQUIRE(!free_slots_.empty(), SG_EINVAL, "no free pyramid slot");
     View view{frame, free_slots_.back(), next_view_seq_++, w, h};
     free_slots_.pop_back();
+    struct SlotGuard {
+      std::vector<int>& free;
+      int slot;
+      bool kept = false;
+      ~SlotGuard() {
+        if (!kept) free.push_back(slot);
+      }
+    } guard{free_slots_, view.slot};
     trk_->SetImage(view.slot, bgr, w, h, stride);
 
     // Remove bad matches (matcher.cpp:325-328).
@@ -129,8 +138,7 @@ class Frontend {
     st->track_batches = batches_;
 
     if ((int)matches.size() >= kMinMatches) {
-      free_slots_.push_back(view.slot);    // the view is not kept (matcher.cpp:350-351)
-      Finish(st);
+      Finish(st);                          // the view is not kept (matcher.cpp:350-351): the guard frees its slot
       return 1;
     }
 
@@ -145,6 +153,7 @@ class Frontend {
       mxy.push_back(m.second.second);
     }
     views_.push_back(view);
+    guard.kept = true;   // the slot now belongs to the kept view
 
     // AddNewFeatures (matcher.cpp:123-169) and the new points (matcher.cpp:368-392).
     std::vector<float> corners(2 * kMaxCorners), added(2 * kMaxCorners);

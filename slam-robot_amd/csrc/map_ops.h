@@ -1,4 +1,4 @@
-// map_ops.h — LocalMap maintenance on the device (Clean, ApplyEpipolarConstraint); see map_ops.hip.
+// map_ops.h — LocalMap maintenance on the device (Clean, ApplyEpipolarConstraint, Normalize); see map_ops.hip.
 #ifndef SG_MAP_OPS_H_
 #define SG_MAP_OPS_H_
 
@@ -17,6 +17,9 @@ class MapOps {
   int Clean(sg_map* m, double error_threshold);
   // LocalMap::ApplyEpipolarConstraint (localmap.cpp:232-276): returns the number of points over the cut.
   int ApplyEpipolarConstraint(sg_map* m);
+  // LocalMap::Normalize (localmap.cpp:114-155): frame 0 to the origin and the identity rotation; mutates
+  // the map's frame poses and point locations.
+  void Normalize(sg_map* m);
 
  private:
   void Upload(const sg_map* m);

@@ -2,6 +2,8 @@
 // (main.cpp:584-605):
 //   LocalMap::Clean(error_threshold)      localmap.cpp:283-398 (+ TrackedPoint::CheckFlags 44-83)
 //   LocalMap::ApplyEpipolarConstraint()   localmap.cpp:232-276 (+ EssentialMatrix 211-230)
+//   LocalMap::Normalize()                 localmap.cpp:114-155 (gauge: frame 0 to the origin and to the
+//                                         identity rotation; main.cpp:602-605 runs it between two ReprojectMap)
 //
 // Both are independent per point once a point's observations are listed in TrackedPoint::observations()
 // order (ascending frame index: Frame::Commit adds them frame by frame, localmap.cpp:85-89).  The only
@@ -269,6 +271,85 @@ __global__ __launch_bounds__(kThreads) void k_epipolar(MapDev d) {
   }
 }
 
+// ---- LocalMap::Normalize (localmap.cpp:114-155) with Eigen 3.2's arithmetic written out.
+
+// quaternionbase_assign_impl<Matrix3>: the trace branch, else the largest-diagonal branch.
+__device__ __forceinline__ void quat_from_matrix(const double m[3][3], double* q) {
+  double t = m[0][0] + m[1][1] + m[2][2];
+  if (t > 0.0) {
+    t = sqrt(t + 1.0);
+    q[3] = 0.5 * t;
+    t = 0.5 / t;
+    q[0] = (m[2][1] - m[1][2]) * t;
+    q[1] = (m[0][2] - m[2][0]) * t;
+    q[2] = (m[1][0] - m[0][1]) * t;
+  } else {
+    int i = 0;
+    if (m[1][1] > m[0][0]) i = 1;
+    if (m[2][2] > m[i][i]) i = 2;
+    const int j = (i + 1) % 3, k = (j + 1) % 3;
+    t = sqrt(m[i][i] - m[j][j] - m[k][k] + 1.0);
+    q[i] = 0.5 * t;
+    t = 0.5 / t;
+    q[3] = (m[k][j] - m[j][k]) * t;
+    q[j] = (m[j][i] + m[i][j]) * t;
+    q[k] = (m[k][i] + m[i][k]) * t;
+  }
+}
+
+// compute_inverse_size3_helper: cofactors, determinant along column 0.
+__device__ __forceinline__ void inverse3(const double m[3][3], double r[3][3]) {
+  auto cof = [&](int i, int j) {
+    const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+    return m[i1][j1] * m[i2][j2] - m[i1][j2] * m[i2][j1];
+  };
+  const double c0 = cof(0, 0), c1 = cof(1, 0), c2 = cof(2, 0);
+  const double invdet = 1.0 / (c0 * m[0][0] + c1 * m[1][0] + c2 * m[2][0]);
+  r[0][0] = c0 * invdet;
+  r[0][1] = c1 * invdet;
+  r[0][2] = c2 * invdet;
+  r[1][0] = cof(0, 1) * invdet;
+  r[1][1] = cof(1, 1) * invdet;
+  r[1][2] = cof(2, 1) * invdet;
+  r[2][0] = cof(0, 2) * invdet;
+  r[2][1] = cof(1, 2) * invdet;
+  r[2][2] = cof(2, 2) * invdet;
+}
+
+struct NormArgs {
+  double q0[4], t0[3];   // frame 0's pose before the call (every thread reads it, frame 0's thread rewrites it)
+};
+
+// Threads [0, F): frames; threads [F, F + P): points.  scale = 1 in the reference (localmap.cpp:125), so its
+// multiplications by scale are identities and are not performed.
+__global__ __launch_bounds__(kThreads) void k_normalize(NormArgs a, double* q, double* t, double* X, int F, int P) {
+  const int id = blockIdx.x * kThreads + threadIdx.x;
+  if (id >= F + P) return;
+  const double xl[3] = {-a.t0[0], -a.t0[1], -a.t0[2]};
+  double R[3][3];
+  quat_matrix(a.q0, R);   // rotate = pose1->rotation().matrix()
+  if (id < F) {
+    double* tf = t + 3 * id;
+    double v[3] = {tf[0] + xl[0], tf[1] + xl[1], tf[2] + xl[2]};
+    double inv[3][3], Rf[3][3], M[3][3];
+    inverse3(R, inv);
+    quat_matrix(q + 4 * id, Rf);
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) M[i][j] = Rf[i][0] * inv[0][j] + Rf[i][1] * inv[1][j] + Rf[i][2] * inv[2][j];
+    double qn[4];
+    quat_from_matrix(M, qn);
+    for (int c = 0; c < 4; ++c) q[4 * id + c] = qn[c];
+    for (int i = 0; i < 3; ++i) tf[i] = R[i][0] * v[0] + R[i][1] * v[1] + R[i][2] * v[2];
+  } else {
+    double* x = X + 4 * (size_t)(id - F);
+    double v[4] = {x[0] + xl[0] * x[3], x[1] + xl[1] * x[3], x[2] + xl[2] * x[3], x[3]};   // move(xlate)
+    const double nrm = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3]);    // normalize()
+    for (int c = 0; c < 4; ++c) v[c] /= nrm;
+    for (int i = 0; i < 3; ++i) x[i] = R[i][0] * v[0] + R[i][1] * v[1] + R[i][2] * v[2];
+    x[3] = v[3];
+  }
+}
+
 }  // namespace
 
 MapOps::MapOps(const sg_device_options& dev) : dev_(dev) {
@@ -382,6 +463,27 @@ int MapOps::Clean(sg_map* m, double error_threshold) {
   }
   Download(m, true, true);
   return counters_h_[0];
+}
+
+void MapOps::Normalize(sg_map* m) {
+  SG_REQUIRE(m && m->num_frames >= 0 && m->num_points >= 0, SG_EINVAL, "bad map");
+  if (m->num_frames < 2) return;   // localmap.cpp:115-116
+  const int F = m->num_frames, P = m->num_points;
+  hipStream_t s = stream_;
+  SG_HIP_CHECK(hipSetDevice(dev_.device));
+  q_.Upload(std::vector<double>(m->q, m->q + 4 * (size_t)F), s);
+  t_.Upload(std::vector<double>(m->t, m->t + 3 * (size_t)F), s);
+  X_.Upload(std::vector<double>(m->X, m->X + 4 * (size_t)P), s);
+  NormArgs a{};
+  for (int c = 0; c < 4; ++c) a.q0[c] = m->q[c];
+  for (int c = 0; c < 3; ++c) a.t0[c] = m->t[c];
+  hipLaunchKernelGGL(k_normalize, dim3((F + P + kThreads - 1) / kThreads), dim3(kThreads), 0, s, a, q_.ptr, t_.ptr,
+                     X_.ptr, F, P);
+  SG_HIP_CHECK(hipGetLastError());
+  SG_HIP_CHECK(hipMemcpyAsync(m->q, q_.ptr, 32 * (size_t)F, hipMemcpyDeviceToHost, s));
+  SG_HIP_CHECK(hipMemcpyAsync(m->t, t_.ptr, 24 * (size_t)F, hipMemcpyDeviceToHost, s));
+  if (P) SG_HIP_CHECK(hipMemcpyAsync(m->X, X_.ptr, 32 * (size_t)P, hipMemcpyDeviceToHost, s));
+  SG_HIP_CHECK(hipStreamSynchronize(s));
 }
 
 int MapOps::ApplyEpipolarConstraint(sg_map* m) {

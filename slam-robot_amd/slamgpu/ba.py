@@ -250,6 +250,11 @@ class Slam:
         check(self.lib.sg_map_apply_epipolar(self.h, C.byref(ms), C.byref(n)), "LocalMap::ApplyEpipolarConstraint")
         return n.value
 
+    def Normalize(self, m: MapArrays):
+        """LocalMap::Normalize (localmap.cpp:114-155) on the device; mutates m's poses and points in place."""
+        ms = m.struct()
+        check(self.lib.sg_map_normalize(self.h, C.byref(ms)), "LocalMap::Normalize")
+
     def iterations(self) -> int:
         return int(self.lib.sg_slam_iterations(self.h))
 

@@ -298,6 +298,7 @@ SYMBOLS = {
     "sg_slam_reproject_map": (C.c_int, [C.c_void_p, C.POINTER(SgMap), _dp]),
     "sg_map_clean": (C.c_int, [C.c_void_p, C.POINTER(SgMap), C.c_double, C.POINTER(C.c_int32)]),
     "sg_map_apply_epipolar": (C.c_int, [C.c_void_p, C.POINTER(SgMap), C.POINTER(C.c_int32)]),
+    "sg_map_normalize": (C.c_int, [C.c_void_p, C.POINTER(SgMap)]),
     "sg_slam_iterations": (C.c_int32, [C.c_void_p]),
     "sg_slam_load_counts": (C.c_int, [C.c_void_p, _ip, _ip]),
     "sg_slam_error": (C.c_double, [C.c_void_p]),

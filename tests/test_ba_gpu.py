@@ -328,3 +328,23 @@ def test_slam_solve_all_frames_with_cameras(gpu_lib, oracle_lib):
     assert abs(slam.error() - so["final_cost"]) <= 1e-6 * so["final_cost"]
     np.testing.assert_allclose(mg.k, mo.k, rtol=1e-5, atol=1e-6)
     assert not np.allclose(mg.k, m.k)
+
+
+def test_deterministic_mode_is_bitwise_reproducible(gpu_lib, monkeypatch):
+    """SG_DETERMINISTIC=1: every Schur window block is summed by one wave in a fixed order (the default sums
+    with LDS atomics from four waves, reproducible to rounding only), so two solves agree bit for bit."""
+    monkeypatch.setenv("SG_DETERMINISTIC", "1")
+    m = make_config("C2")
+    pa = ba.problem_from_map_frames(m, 48, 50, 2.0)
+    out = []
+    for _ in range(2):
+        p = pa.copy()
+        g = ba.BundleAdjuster()
+        g.load(p)
+        out.append((g.solve(), p))
+        g.close()
+    (s0, p0), (s1, p1) = out
+    assert s0 == s1
+    np.testing.assert_array_equal(p0.q, p1.q)
+    np.testing.assert_array_equal(p0.t, p1.t)
+    np.testing.assert_array_equal(p0.X, p1.X)

@@ -191,3 +191,35 @@ def test_matcher_track_matches_oracle(gpu_lib, oracle_run, sequence):
     pts, ids = mt.features()
     assert list(ids) == sorted(omt.features) and list(pts) == [omt.features[f]["point"] for f in sorted(omt.features)]
     mt.close()
+
+
+@pytest.mark.gpu
+def test_failing_callback_does_not_leak_pyramid_slots(gpu_lib, sequence, monkeypatch):
+    """A Track call whose callback fails (here point_state) returns the error and gives its pyramid slot back:
+    with the minimum of max_images = 5 slots, many failed calls are followed by normal tracking."""
+    import slamgpu.frontend as fe
+    from slamgpu.scene import MapArrays
+    frames, _ = sequence
+    z = lambda dt: np.zeros(0, dt)  # noqa: E731
+    m = MapArrays(k=K.copy(), q=z(np.float64), t=z(np.float64), frame_camera=z(np.int32), frame_prev=z(np.int32),
+                  X=z(np.float64), point_flags=z(np.int32), point_uncertainty=z(np.float64), obs_pt=z(np.float64),
+                  obs_frame=z(np.int32), obs_point=z(np.int32), obs_disabled=z(np.int32), obs_error=z(np.float64),
+                  frame_keyframe=z(np.int32))
+    mt = fe.Matcher(window=13, depth=6, max_images=5)
+    q, t = _pose(0)
+    fe.add_frame(m, 0, q, t)
+    assert mt.Track(frames[0], 0, 0, m)       # seeds features: the first keyframe view keeps a slot
+    assert m.num_points > 0
+
+    def broken(flags):
+        raise RuntimeError("point_state failed")
+    monkeypatch.setattr(fe, "feature_usable", broken)
+    for _ in range(8):
+        with pytest.raises(RuntimeError, match="point_state failed"):
+            mt.Track(frames[1], 0, 0, m)
+    monkeypatch.undo()
+    for i in (1, 2):
+        q, t = _pose(i)
+        fe.add_frame(m, 0, q, t)
+        assert mt.Track(frames[i], i, 0, m)
+    mt.close()

@@ -300,3 +300,25 @@ def test_clean_gpu_after_device_reproject(gpu_lib, oracle_lib):
     assert s.Clean(g, 2.0) == oracle_lib.clean(o, 2.0)
     assert s.ApplyEpipolarConstraint(g) == oracle_lib.apply_epipolar(o)
     _assert_maps_equal(g, o, unc_rtol=1e-13)
+
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["C1", "C2"])
+def test_device_normalize_matches_oracle_and_keeps_reprojection(gpu_lib, oracle_lib, name):
+    """LocalMap::Normalize on the device (sg_map_normalize) vs oracle_map.cpp, and main.cpp:602-605's
+    CHECK_NEAR(err1, err2, 0.1) around it with the device ReprojectMap."""
+    from slamgpu import ba
+    from slamgpu.scene import make_config
+    m = make_config(name)
+    slam = ba.Slam()
+    e1 = slam.ReprojectMap(m)
+    mg, mo = m.copy(), m.copy()
+    slam.Normalize(mg)
+    oracle_lib.normalize(mo)
+    np.testing.assert_allclose(mg.q, mo.q, rtol=0, atol=1e-12)
+    np.testing.assert_allclose(mg.t, mo.t, rtol=0, atol=1e-9)
+    np.testing.assert_allclose(mg.X, mo.X, rtol=0, atol=1e-12)
+    e2 = slam.ReprojectMap(mg)
+    assert abs(e1 - e2) < 0.1                 # CHECK_NEAR(err1, err2, 0.1)
+    assert abs(e1 - e2) <= 1e-9 * e1

@@ -206,3 +206,74 @@ def test_reproject_mean_invariant_under_gauge_normalisation(oracle_lib):
     e2 = oracle_lib.reproject_map(m)
     assert abs(e1 - e2) < 0.1
     assert abs(e1 - e2) < 1e-6 * e1
+
+
+def _numpy_normalize(m):
+    """The same gauge change as test_reproject_mean_invariant_under_gauge_normalisation, in numpy."""
+    from slamgpu.scene import quat_from_matrix, quat_to_matrix
+    q = m.q.reshape(-1, 4)
+    t = m.t.reshape(-1, 3)
+    X = m.X.reshape(-1, 4)
+    xl = -t[0].copy()
+    t += xl
+    X[:, :3] += xl * X[:, 3:4]
+    X /= np.linalg.norm(X, axis=1, keepdims=True)
+    R0 = quat_to_matrix(q[0])
+    inv = np.linalg.inv(R0)
+    for f in range(len(q)):
+        q[f] = quat_from_matrix(quat_to_matrix(q[f]) @ inv)
+        t[f] = R0 @ t[f]
+    X[:, :3] = X[:, :3] @ R0.T
+
+
+@pytest.mark.parametrize("yaw_deg", [0.0, 30.0, 179.0])
+def test_oracle_normalize_restatement(oracle_lib, yaw_deg):
+    """oracle_map.cpp's LocalMap::Normalize (localmap.cpp:114-155) against the numpy restatement: frame 0 ends at
+    the origin with the identity rotation, the map's reprojection is unchanged (main.cpp:602-605), and a frame
+    rotated ~180 deg from frame 0 takes Eigen's largest-diagonal branch of the quaternion-from-matrix."""
+    from slamgpu.scene import axis_angle, make_config, quat_from_matrix, quat_to_matrix
+    m = make_config("C1")
+    # rotate the whole scene (frames and points consistently) so that frame 0 is not the identity
+    R = axis_angle(np.deg2rad([10.0, yaw_deg, -5.0]))
+    q = m.q.reshape(-1, 4)
+    t = m.t.reshape(-1, 3)
+    for f in range(len(q)):
+        q[f] = quat_from_matrix(quat_to_matrix(q[f]) @ R.T)
+        t[f] = R @ t[f] + np.array([100.0, -40.0, 7.0])
+    X = m.X.reshape(-1, 4)
+    X[:, :3] = X[:, :3] @ R.T + np.array([100.0, -40.0, 7.0]) * X[:, 3:4]
+    X /= np.linalg.norm(X, axis=1, keepdims=True)
+    if yaw_deg > 90:
+        # frame 3 turned ~170 deg from frame 0: R_3 R_0^-1 has a negative trace
+        q[3] = quat_from_matrix(axis_angle(np.deg2rad([0.0, 170.0, 0.0])) @ quat_to_matrix(q[0]))
+        assert np.trace(quat_to_matrix(q[3]) @ quat_to_matrix(q[0]).T) < 0
+    e1 = oracle_lib.reproject_map(m)
+    mo, mn = m.copy(), m.copy()
+    oracle_lib.normalize(mo)
+    _numpy_normalize(mn)
+    np.testing.assert_allclose(mo.t, mn.t, rtol=0, atol=1e-9)
+    np.testing.assert_allclose(mo.X, mn.X, rtol=0, atol=1e-12)
+    # quaternions: the same rotation (q and -q are one rotation; numpy's restatement keeps w >= 0)
+    for f in range(mo.num_frames):
+        np.testing.assert_allclose(quat_to_matrix(mo.q[4 * f:4 * f + 4]), quat_to_matrix(mn.q[4 * f:4 * f + 4]),
+                                   rtol=0, atol=1e-12)
+    np.testing.assert_allclose(mo.t[:3], 0.0, atol=1e-12)
+    np.testing.assert_allclose(quat_to_matrix(mo.q[:4]), np.eye(3), atol=1e-12)
+    e2 = oracle_lib.reproject_map(mo)
+    assert abs(e1 - e2) < 0.1 and abs(e1 - e2) <= 1e-9 * e1
+
+
+def test_oracle_normalize_single_frame_is_untouched(oracle_lib):
+    from slamgpu.scene import make_config
+    m = make_config("C1")
+    one = m.copy()
+    one.q, one.t = one.q[:4].copy(), one.t[:3].copy()
+    one.frame_camera, one.frame_prev = one.frame_camera[:1].copy(), one.frame_prev[:1].copy()
+    keep = one.obs_frame == 0
+    one.obs_pt = one.obs_pt.reshape(-1, 2)[keep].reshape(-1).copy()
+    one.obs_frame, one.obs_point = one.obs_frame[keep].copy(), one.obs_point[keep].copy()
+    one.obs_disabled, one.obs_error = one.obs_disabled[keep].copy(), one.obs_error.reshape(-1, 2)[keep].reshape(-1).copy()
+    before = one.copy()
+    oracle_lib.normalize(one)
+    np.testing.assert_array_equal(one.X, before.X)
+    np.testing.assert_array_equal(one.t, before.t)

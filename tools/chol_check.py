@@ -1,4 +1,4 @@
-"""Diagnostic: the tiled band Cholesky vs the window kernel and vs itself (determinism) on one LM solve."""
+"""Diagnostic: two solves per setting (default, deterministic Schur sums, window Cholesky): bitwise reproducibility."""
 import os, subprocess, sys, json
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 code = r'''
@@ -15,7 +15,7 @@ for rep in range(2):
 print(json.dumps(out))
 ''' % ROOT
 for cfg in sys.argv[1:] or ["C2"]:
-    for env in ({}, {"SG_CHOL_WINDOW": "1"}):
+    for env in ({}, {"SG_DETERMINISTIC": "1"}, {"SG_CHOL_WINDOW": "1", "SG_DETERMINISTIC": "1"}):
         e = dict(os.environ, **env)
         r = subprocess.run([sys.executable, "-c", code, cfg], env=e, capture_output=True, text=True)
         print(cfg, env, r.stdout.strip() or r.stderr[-500:])
