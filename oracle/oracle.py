@@ -229,7 +229,7 @@ def _trk():
         L.ort_get_patch.argtypes = [_fp, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float, _fp, _fp, _fp]
         L.ort_mask.argtypes = [C.c_int, _fp]
         L.ort_track_fb.argtypes = [_fp, _fp, _i32p, C.c_int, C.c_int, C.c_int, _fp, _fp, _i32p, _i32p, _i32p,
-                                   C.c_int]
+                                   C.c_int, C.c_int]
         L.ort_seed_features.restype = C.c_int
         L.ort_seed_features.argtypes = [_u8p, C.c_int, C.c_int, C.c_int, _fp, C.c_int, C.c_int, C.c_double,
                                         C.c_double, _fp, _i32p, _fp]
@@ -357,8 +357,17 @@ def patch_mask(win: int):
     return out
 
 
-def track_fb(pyr_from, pyr_to, dims, win, from_xy, to_xy, levels=None, nthreads=1):
-    """matcher.cpp:173-206 + 247-251: forward/backward tracking.  Returns (to_xy, accepted, iterations)."""
+def set_sum_order(order: int):
+    """Patch-sum order of the HessianTracker restatement: 0 lane tree (the device's), 1 the reference's
+    sequential loop.  Process-global; reset to 0 after use."""
+    L = _trk()
+    L.ort_set_sum_order.argtypes = [C.c_int]
+    L.ort_set_sum_order(order)
+
+
+def track_fb(pyr_from, pyr_to, dims, win, from_xy, to_xy, levels=None, nthreads=1, retry_levels=6):
+    """matcher.cpp:173-206 + 247-251: forward/backward tracking, a failed attempt retried with retry_levels
+    (6, the matcher's; 0: no retry, sg_tracker_options.retry_levels).  Returns (to_xy, accepted, iterations)."""
     from_xy = np.ascontiguousarray(from_xy, dtype=np.float32).reshape(-1, 2)
     out = np.ascontiguousarray(to_xy, dtype=np.float32).reshape(-1, 2).copy()
     n = from_xy.shape[0]
@@ -370,7 +379,7 @@ def track_fb(pyr_from, pyr_to, dims, win, from_xy, to_xy, levels=None, nthreads=
     pt = np.ascontiguousarray(pyr_to, dtype=np.float32)
     _trk().ort_track_fb(pf.ctypes.data_as(_fp), pt.ctypes.data_as(_fp), d.ctypes.data_as(_i32p), len(d) // 2, win, n,
                         from_xy.ctypes.data_as(_fp), out.ctypes.data_as(_fp), lv.ctypes.data_as(_i32p),
-                        acc.ctypes.data_as(_i32p), it.ctypes.data_as(_i32p), nthreads)
+                        acc.ctypes.data_as(_i32p), it.ctypes.data_as(_i32p), nthreads, retry_levels)
     return out, acc, it
 
 

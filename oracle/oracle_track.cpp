@@ -158,7 +158,17 @@ struct Patch {
 // in a compiler-chosen vectorised order): 64 lane partials, partial[l] = sum over i = l (mod 64) in
 // increasing i, then a pairwise tree over consecutive partials.  This is the order of the device
 // tracker (one wave per track, DPP reduction), so the two agree bit for bit.
+// 0: the lane-tree order below (the device's); 1: the reference's textbook loop order, left to right
+// (hessian.h:86-88, 133-139 as written; its -ffast-math build may reassociate further).  Switchable so a
+// test can measure how far the two orders move a track (1e-3 px).
+static int g_sum_order = 0;
+
 inline float LaneTreeSum(const float* v, int n) {
+  if (g_sum_order == 1) {
+    float s = 0.f;
+    for (int i = 0; i < n; ++i) s += v[i];
+    return s;
+  }
   float part[64];
   for (int l = 0; l < 64; ++l) part[l] = 0.f;
   for (int i = 0; i < n; ++i) part[i & 63] += v[i];
@@ -317,7 +327,7 @@ int TrackFeature(const Tracker& T, const std::vector<Level>& src, const std::vec
 
 // matcher.cpp:173-206 (forward/backward TrackFeature) and the 3 -> 6 level retry of matcher.cpp:247-251.
 bool TrackFB(const Tracker& T, const std::vector<Level>& from, const std::vector<Level>& to, float fx, float fy,
-             int levels, float* tx, float* ty, int* iters) {
+             int levels, float* tx, float* ty, int* iters, int retry_levels = 6) {
   // The backward pass is skipped when the forward pass failed: the reference runs it but rejects the feature
   // either way (matcher.cpp:193), and it never modifies to_pt.  (Only the iteration count differs.)
   auto attempt = [&](int lv) {
@@ -330,8 +340,8 @@ bool TrackFB(const Tracker& T, const std::vector<Level>& from, const std::vector
     return !(std::sqrt((double)ex * ex + (double)ey * ey) > 0.3);
   };
   if (attempt(levels)) return true;
-  if (levels == 6) return false;
-  return attempt(6);
+  if (retry_levels <= 0 || levels == retry_levels) return false;   // sg_tracker_options.retry_levels
+  return attempt(retry_levels);
 }
 
 }  // namespace oracle_trk
@@ -339,6 +349,8 @@ bool TrackFB(const Tracker& T, const std::vector<Level>& from, const std::vector
 using namespace oracle_trk;
 
 extern "C" {
+
+void ort_set_sum_order(int order) { g_sum_order = order; }
 
 // MakePyramid (hessian.h:95-126): BGR u8 -> grey -> /255 -> GaussianBlur(5, 1.1); then per level
 // pyrDown + GaussianBlur(5, 0.8).  out holds the levels back to back; dims[2l], dims[2l+1] = w, h.
@@ -394,7 +406,7 @@ int ort_mask(int win, float* out) {
 // total Newton iterations per track.
 int ort_track_fb(const float* pyr_from, const float* pyr_to, const int32_t* dims, int depth, int win, int n,
                  const float* from_xy, float* to_xy, const int32_t* levels, int32_t* accepted, int32_t* iters,
-                 int nthreads) {
+                 int nthreads, int retry_levels) {
   std::vector<Level> from(depth), to(depth);
   size_t off = 0;
   for (int l = 0; l < depth; ++l) {
@@ -407,7 +419,7 @@ int ort_track_fb(const float* pyr_from, const float* pyr_to, const int32_t* dims
   for (int i = 0; i < n; ++i) {
     int it = 0;
     accepted[i] = TrackFB(T, from, to, from_xy[2 * i], from_xy[2 * i + 1], levels ? levels[i] : 3, &to_xy[2 * i],
-                          &to_xy[2 * i + 1], &it) ? 1 : 0;
+                          &to_xy[2 * i + 1], &it, retry_levels) ? 1 : 0;
     if (iters) iters[i] = it;
   }
   return 0;

@@ -109,3 +109,27 @@ def test_device_resident_runs_repeat_identically(gpu_lib, frames):
     np.testing.assert_array_equal(a1, a2)
     tm, pm = t.kernel_ms()
     assert tm > 0 and pm > 0
+
+
+def test_c3_config_fb_tracking_bit_exact(gpu_lib, frames):
+    """BASELINE config 3 exactly as bench.py runs it: 640x480, 2000 seeds, 3-level pyramid, 7x7 window,
+    forward + backward (matcher.cpp:173-206) from the seed positions, 3 levels without the matcher's 6-level
+    retry (the pyramid has 3).  The device-resident run (sg_tracker_load_features / run / results) against the
+    oracle, bit for bit."""
+    pts = seed_points(2000)
+    t = HessianTracker(window=7, depth=3, retry_levels=0)
+    t.MakePyramid(frames[0], 0)
+    t.MakePyramid(frames[1], 1)
+    t.load_features(pts, pts)
+    t.run(0, 1, repeats=1)
+    out, acc, its = t.results()
+    pf, dims = oracle.make_pyramid(frames[0], 3)
+    pt, _ = oracle.make_pyramid(frames[1], 3)
+    ro, racc, rits = oracle.track_fb(pf, pt, dims, 7, pts, pts, np.full(len(pts), 3, np.int32),
+                                     nthreads=min(16, os.cpu_count() or 1), retry_levels=0)
+    np.testing.assert_array_equal(acc.astype(np.int32), racc)
+    np.testing.assert_array_equal(its, rits)
+    np.testing.assert_array_equal(out, ro)
+    gt = ground_truth(pts, 1)
+    assert acc.mean() > 0.98
+    assert np.median(np.linalg.norm(out - gt, axis=1)[acc]) < 0.1

@@ -104,13 +104,16 @@ def test_mode_pyramids_gpu_bit_exact(gpu_lib, oracle_lib, frames, mode):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode,n,depth", [(HESSIAN, 300, 6), (KLT, 300, 3), (KLT, 64, 5), (BRUTE, 3, 3)])
+@pytest.mark.parametrize("mode,n,depth", [(HESSIAN, 300, 6), (KLT, 300, 3), (KLT, 64, 5), (BRUTE, 3, 3),
+                                          (BRUTE, 64, 3)])
 def test_track_feature_modes_gpu_bit_exact(gpu_lib, oracle_lib, frames, mode, n, depth):
     from slamgpu.tracker import HessianTracker
     rng = np.random.default_rng(n + mode)
     pts = seed_points(n)
-    if mode == BRUTE:   # interior points (the 13 px margin) and one inside the margin
+    if mode == BRUTE and n < 64:   # interior points (the 13 px margin) and one inside the margin
         pts = np.array([[200.5, 150.25], [420.0, 300.0], [333.3, 222.2], [6.0, 200.0]], np.float32)
+    elif mode == BRUTE:            # the grid of seeds plus two inside the 13 px margin
+        pts = np.concatenate([seed_points(62), [[6.0, 200.0], [630.5, 40.0]]]).astype(np.float32)
     start = (pts + rng.normal(0, 0.4, pts.shape)).astype(np.float32)
     levels = np.where(rng.random(len(pts)) < 0.3, 6, 3).astype(np.int32) if mode == HESSIAN else None
     t = HessianTracker(window=13, depth=depth, mode=mode)
@@ -121,5 +124,6 @@ def test_track_feature_modes_gpu_bit_exact(gpu_lib, oracle_lib, frames, mode, n,
     np.testing.assert_array_equal(gs, rs)
     np.testing.assert_array_equal(gi, ri)
     np.testing.assert_array_equal(go, ro)
-    assert (gs == 0).mean() > 0.6
+    # the seed grid reaches the frame border, where the brute search window does not fit (status 2)
+    assert (gs == 0).mean() > (0.5 if mode == BRUTE else 0.6)
     t.close()
