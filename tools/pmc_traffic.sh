@@ -8,7 +8,7 @@ TAG=${1:-r1}
 OUT="$R/gpurun_out/pmc_$TAG"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-KRE="k_cholesky_window|k_linearize|k_schur|k_track_fb|k_hamming_slices"
+KRE="k_chol_tiles|k_cholesky_window|k_linearize|k_schur|k_S_reduce|k_point_update|k_track_fb|k_hamming_slices"
 i=0
 for c in FETCH_SIZE WRITE_SIZE; do
   i=$((i+1))
