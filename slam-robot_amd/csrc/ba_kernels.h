@@ -9,7 +9,8 @@
 //                                  (r~ 2 | Jc 2x6 [rot_local 3, t 3] | Jp 2x4 | pad 2)
 //   V[P][10], g[P][4]              point normal-equation blocks (upper 4x4) and gradient
 //   Vinv[P][10], tp[P][4]          damped, scaled inverse and V^-1 g~ (per LM iteration)
-//   cam_slab / S_slab              per-chunk partial camera blocks / Schur window (deterministic reduce)
+//   cam_slab / S_slab              per-chunk partial camera blocks / per-segment Schur tiles (deterministic
+//                                  reduce)
 //   S[n][n], xc[n]                 dense reduced camera system (upper blocks), n = 6 * free frames, and
 //                                  its rhs, contiguous (one all-reduce over landmark shards)
 #ifndef SG_BA_KERNELS_H_
@@ -21,7 +22,6 @@
 
 namespace sg {
 
-constexpr int kSchurThreads = 256;
 constexpr int kCamV = 27;           // per camera block: upper(Jc^T Jc) 21 + Jc^T r 6
 constexpr int kJStride = 24;
 constexpr int kNScal = 16;          // per-chunk scalar slots
@@ -47,29 +47,42 @@ enum UpdX { kUModel = 0, kUCandCost, kUCandFail, kUStep2, kUCandX2, kULinFail, k
 enum CholX { kCStep2 = 0, kCCandX2, kCModel, kCCandCost, kCFail, kCNum };
 
 
-// Schur work unit: up to kSegPts consecutive points (device order) sharing a window of <= kSegNbMax
-// camera blocks (or one "wide" point), with its slice of the observation-pair list.
+// k_schur work decomposition (see ba_solver.hip): a segment is a run of consecutive points (device order)
+// whose camera columns fit a window of <= kSchurTW 16-column tiles of S, one 8-wave workgroup (4 waves holding
+// the window's upper tiles and rhs rows in MFMA accumulators, 4 building the operand tiles); it streams through
+// LDS in batches of <= kSchurBatchPts points whose operand tiles (64 doubles each) fit kSchurXCap.  The cells
+// of a point (one per block of its span) carry its observations.  A point spanning more than kSegNbMax blocks
+// is a WideSeg of its own (observation pairs, global atomics).
 #ifndef SG_SEG_NB
-#define SG_SEG_NB 24   // cap of the per-load window width (the widest point, see BaSolver::Load)
+#define SG_SEG_NB 24   // widest point of a segment, in blocks (6 * 24 + 14 <= 16 * kSchurTW columns)
 #endif
-#ifndef SG_SEG_PTS
-#define SG_SEG_PTS 32
-#endif
-constexpr int kSegPts = SG_SEG_PTS;
-constexpr int kSegObsCap = 8 * SG_SEG_PTS;
 constexpr int kSegNbMax = SG_SEG_NB;
+constexpr int kSchurThreads = 512;
+constexpr int kSchurWaves = kSchurThreads / 64;
+constexpr int kSchurTW = 10;
+constexpr int kSchurTiles = kSchurTW * (kSchurTW + 1) / 2;
+constexpr int kSchurCWaves = kSchurWaves / 2;   // MFMA (consumer) waves; the other half builds the cells
+constexpr int kSchurAug = kSchurTiles + kSchurTW;   // window tiles + one rhs tile per tile row
+constexpr int kSchurTPW = (kSchurAug + kSchurCWaves - 1) / kSchurCWaves;   // accumulator tiles per wave
+constexpr int kSchurXCap = 112 * 64;   // operand tiles (64 doubles each) per batch buffer
+constexpr int kSchurBatchPts = 32;   // <= 64: a batch's point table is one point per lane
+static_assert(6 * kSegNbMax + 14 <= 16 * kSchurTW, "a widest point must fit the tile window");
 struct SchurSeg {
   int32_t p0, p1;       // point range
-  int32_t b_lo, nb;     // window [b_lo, b_lo + nb)
-  int32_t s_off;        // offset of the window partial in S_slab
-  int32_t wide;         // global atomics instead of an LDS window
+  int32_t b_lo, nb;     // blocks the points observe: rhs partial [b_lo, b_lo + nb)
+  int32_t s_off;        // S_slab offset: ntw (ntw + 1) / 2 row-major 16x16 tiles, then 6 nb rhs entries
+  int32_t t0, ntw;      // window: tile columns [t0, t0 + ntw) of S
+  int32_t bt0, bt1;     // batches
+  int32_t pad;
+};
+struct SchurBatch {
+  int32_t p0, p1;       // points
+  int32_t c0, c1;       // cells
+};
+struct WideSeg {
+  int32_t p;            // the point
   int32_t pair_lo, pair_hi;
-  int32_t heavy;        // one point with more than kSegObsCap observations: P rows recomputed per pair,
-                        // not staged in LDS (a long-tracked point of a whole-map solve)
-  int32_t det;          // deterministic mode (SG_DETERMINISTIC=1 at load): the pair list is split into 4
-  int32_t pw[3];        // per-wave lists [pair_lo, pw0), [pw0, pw1), [pw1, pw2), [pw2, pair_hi) so that each
-                        // window block (and each rhs block, through its observations' (o, o) pairs) is summed
-                        // by one wave in list order: bitwise reproducible runs, at ~1.3x the Schur time
+  int32_t pad;
 };
 
 // k_linearize work decomposition: a chunk (one single-wave workgroup) is a run of consecutive points whose
@@ -157,8 +170,10 @@ struct Dev {
   // chunks and partials
   const int32_t* cam_loff;       // [NB+1] CSR: per camera block, offsets of its partials in cam_slab
   const int32_t* cam_lidx;
-  const int32_t* s_loff;         // [NB*NB+1] CSR: per block pair (I<=J), offsets of its partials in S_slab
+  const int32_t* s_loff;         // [nstile+1] CSR: per band tile of S, offsets of its partial tiles in S_slab
   const int32_t* s_lidx;
+  const int32_t* stile;          // [nstile] band tiles (R << 16) | C, R <= C, of the frame columns
+  int32_t nstile;
   const int32_t* r_loff;         // [NB+1] CSR: per block, offsets of its rhs partials in S_slab
   const int32_t* r_lidx;
   double* cam_slab;
@@ -189,8 +204,16 @@ struct Dev {
   int32_t npu;
   const struct SchurSeg* segs;   // [nseg] Schur work units
   int32_t nseg;
-  double* seg_fail;              // [nseg] point blocks whose damped inverse failed
-  const int2* pairs;             // {(s << 16) | t local observation indices, (b_s << 16) | b_t}
+  const struct SchurBatch* sbatch;
+  const int2* pinfo;             // [P] first cell, (first block << 8) | span (0: no Schur terms)
+  const int4* cells;             // [ncell] first observation (-1: none), point, (block << 16) | number of
+                                 // further observations, their offset in cell_obs
+  const int2* pmx;               // [P] operand offset in the point's batch buffer, last window tile (-1: none)
+  const int32_t* cell_obs;       // second and later observations of a cell
+  const struct WideSeg* wsegs;   // [nwide] points wider than a segment window
+  int32_t nwide;
+  double* seg_fail;              // [nseg + nwide] point blocks whose damped inverse failed
+  const int2* pairs;             // wide points: {(s << 16) | t local observation indices, (b_s << 16) | b_t}
   unsigned long long* stamps;    // diagnostic builds only: per-phase cycle counters (nullptr otherwise)
   // free intrinsics (SolveAllFrames(..., solve_cameras = true), slam.cpp:447-480): 7 columns per camera after
   // the 6 NB frame columns of S (nk = 0 when the intrinsics are constant)

@@ -72,7 +72,6 @@ class BaSolver {
   int F_ = 0, P_ = 0, M_ = 0, NB_ = 0, n_ = 0, D_ = 0, ncam_ = 0;
   std::vector<int32_t> point_perm_;   // device order -> problem point
   std::vector<int32_t> obs_perm_;     // device order -> problem observation
-  size_t schur_lds_ = 0;
   int band_tiles_ = 0;     // widest Cholesky envelope row (16-wide tiles)
   size_t npairs_ = 0;      // Schur observation pairs
   // Incremental problem update (replacing the per-call rebuild of slam.cpp:257-414):
@@ -124,7 +123,11 @@ class BaSolver {
   int nlin_ = 0;
   int npu_ = 0;
   DBuf<double> seg_fail_;
-  int nseg_ = 0, max_seg_nb_ = 0, max_seg_obs_ = 0;  // FrameDistance cross-block lookup
+  int nseg_ = 0, nwide_ = 0, nstile_ = 0;
+  double schur_mfma_ = 0.0;   // MFMA tile updates per k_schur launch (KernelWork)
+  DBuf<SchurBatch> sbatch_;
+  DBuf<WideSeg> wsegs_;
+  DBuf<int32_t> pinfo_, pmx_, cells_, cell_obs_, stile_;
   DBuf<double> rdg_;       // 1/U_jj of the factor
   DBuf<double> mk_, mq_, mt_, mX_, mobs_pt_, mobs_err_, mred_;
   double range_b_ = 4.0, fd_target_ = 150.0, fd_b2_ = 225.0;

@@ -33,6 +33,7 @@
 #include "ba_solver.h"
 #include "comm.h"
 #include "project_math.h"
+#include "schur_tiles.h"
 
 namespace sg {
 
@@ -42,6 +43,7 @@ namespace sg {
 
 // ------------------------------------------------------------------------------------------------
 // small device helpers
+
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -163,8 +165,11 @@ __device__ __forceinline__ void load_scaled_J(const Dev& d, int o, int b, const 
   for (int i = 0; i < 8; ++i) Jp[i] = buf[14 + i] * sp[i % 4];
 }
 
-// 4x4 SPD inverse via LL^T; A and Ainv packed upper (10).  Returns false on a non-positive pivot.
-__device__ __forceinline__ bool inv4_spd(const double* A, double* Ai) {
+// packed index of a lower-triangular 4x4 (c <= i)
+__device__ __forceinline__ int l4(int i, int c) { return i * (i + 1) / 2 + c; }
+// 4x4 SPD inverse via LL^T; A and Ainv packed upper (10), L^-1 packed lower (Lo, optional).  Returns false on
+// a non-positive pivot.
+__device__ __forceinline__ bool inv4_spd(const double* A, double* Ai, double* Lo = nullptr) {
   double L[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -208,6 +213,11 @@ __device__ __forceinline__ bool inv4_spd(const double* A, double* Ai) {
       Li[i][c] = s / L[i][i];
     }
   }
+  if (Lo)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int c = 0; c <= i; ++c) Lo[l4(i, c)] = Li[i][c];
   // A^-1 = Linv^T Linv
 #pragma unroll
   for (int a = 0; a < 4; ++a)
@@ -635,14 +645,25 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_schur: one chunk per workgroup, in point segments whose observations fit the LDS stage.  Three
-// fully parallel phases per segment (no per-point serialisation):
-//   1. thread per point: damped, scaled point block V~ = S V S + D^2, its inverse (LL^T) and t = V~^-1 g~
-//      (also written to global memory for k_point_update);
-//   2. thread per observation: P_o = J~p,o V~^-1 staged in LDS, and the rhs term -A_c,o^T (A_p,o t_p);
-//   3. thread per observation pair (s <= t) of a point, from a pair list built at load time: the 6x6 block
-//      -A_c,s^T (P_s A_p,t^T) A_c,t accumulated into the chunk's window of the reduced system (LDS atomics;
-//      windows wider than kSegNbMax blocks go to global atomics).
+// k_schur: the point elimination S -= W V~^-1 W^T and rhs -= W V~^-1 g~, as batched rank-4 updates on the
+// matrix cores.
+//
+// For a free point p with damped, scaled block V~ = L L^T, whiten its camera Jacobians per block b of its
+// span:  E_{p,b} = L^-1 sum_{o of p in b} J~p,o^T J~c,o  (4 x 6; zero for a block it does not observe).
+// Then its Schur term over every block pair of its span is E_p^T E_p with E_p = [E_{p,b}]_b (4 x 6 span), and
+// its rhs term is E_p^T w_p with w_p = L^-1 g~ — one v_mfma_f64_16x16x4f64 per 16x16 tile of S the point
+// touches (K = 4: one point per MFMA).  Two observations of p in one block simply sum into one E_{p,b}.
+//
+// One workgroup (4 waves) per segment: consecutive points (device order: by first block) whose columns fit
+// a window of kSchurTW tiles of S.  The window's upper tiles stay in MFMA accumulators for the whole
+// segment — wave w owns tiles u = w + 4 s (column-major upper order) — so every tile of a segment is
+// written once, summed in point order (bitwise reproducible).  The segment streams through LDS in batches:
+//   1. thread per point: V~, L^-1, V~^-1 and t = V~^-1 g~ (for k_point_update), w = L^-1 g~;
+//   2. thread per cell (point, block of its span): E_{p,b} and its rhs term E_{p,b}^T w_p;
+//   3. every wave walks the batch's points: operands X_j[lane i + 16 k] = E_p[k][16 j + i] read straight
+//      from the cells, one MFMA per owned tile inside the point's span; the rhs threads (6 per block of the
+//      segment) add the cells' rhs terms.
+// Points spanning more than kSegNbMax blocks take k_schur_wide (observation pairs, global atomics).
 
 __device__ __forceinline__ void load_Jc_scaled(const Dev& d, int o, int b, double* Jc) {
   const double2* J2 = reinterpret_cast<const double2*>(d.J + (size_t)o * kJStride) + 1;   // skip r
@@ -665,6 +686,249 @@ __device__ __forceinline__ void load_Jp_scaled(const Dev& d, int o, const double
   }
 }
 
+// Damped, scaled point block of point p: V~ = S V S + D^2 / radius (D^2 = clamped diag(S V S), refreshed
+// unless the step reuses it), its inverse and L^-1 (V~ = L L^T), t = V~^-1 g~, w = L^-1 g~; Vinv, tp and
+// diag_p go to global memory for k_point_update.  Returns false when V~ is not positive definite (Vi, Li NaN).
+__device__ __forceinline__ bool point_block(const Dev& d, const LmState* st, int p, double* Vi, double* Li,
+                                            double* w) {
+  const double* Vp = d.V + 10 * (size_t)p;
+  double V[10];
+#pragma unroll
+  for (int i = 0; i < 10; ++i) V[i] = Vp[i];
+  const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
+  const double sp[4] = {s4.x, s4.y, s4.z, s4.w};
+  const double4 g4 = reinterpret_cast<const double4*>(d.g)[p];
+  const double gs[4] = {g4.x * sp[0], g4.y * sp[1], g4.z * sp[2], g4.w * sp[3]};
+  double dp[4];
+  if (!st->reuse_diag) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a) dp[a] = fmin(fmax(sp[a] * sp[a] * V[u4(a, a)], st->min_diag), st->max_diag);
+    reinterpret_cast<double4*>(d.diag_p)[p] = make_double4(dp[0], dp[1], dp[2], dp[3]);
+  } else {
+    const double4 d4 = reinterpret_cast<const double4*>(d.diag_p)[p];
+    dp[0] = d4.x; dp[1] = d4.y; dp[2] = d4.z; dp[3] = d4.w;
+  }
+  const double radius = st->radius;
+  double Vt[10];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (c >= a) Vt[u4(a, c)] = sp[a] * V[u4(a, c)] * sp[c] + (a == c ? dp[a] / radius : 0.0);
+  const bool ok = inv4_spd(Vt, Vi, Li);
+  if (!ok) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) Vi[i] = Li[i] = NAN;
+  }
+  double tp[4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    double s = 0.0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) s += sym4(Vi, a, c) * gs[c];
+    tp[a] = s;
+  }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    double s = 0.0;
+#pragma unroll
+    for (int c = 0; c <= a; ++c) s += Li[l4(a, c)] * gs[c];
+    w[a] = s;
+  }
+  double* Vo = d.Vinv + 10 * (size_t)p;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) Vo[i] = Vi[i];
+  reinterpret_cast<double4*>(d.tp)[p] = make_double4(tp[0], tp[1], tp[2], tp[3]);
+  return ok;
+}
+
+// The segment's batches run as a software pipeline over two wave groups, one LDS barrier per step:
+//   producers (waves 0-3), step s: the operand tiles of batch s (buffer s % 2), then the point blocks of batch
+//            s + 1 (point slot (s + 1) % 3);
+//   consumers (waves 4-7), step s: the MFMAs of batch s - 1 (buffer (s - 1) % 2, point slot (s - 1) % 3).
+// The two groups run separate loops with the same barrier count, so the accumulators are not live in the
+// producer code.
+struct SchurLds {
+  double X[2][kSchurXCap + 64 * kSchurTW];   // operand tiles of the batch's points; padding for over-reads
+  double L[3][kSchurBatchPts * 10];          // L^-1 of the batch's points
+  double w[3][kSchurBatchPts * 4];           // w = L^-1 g~
+  int4 pinf[3][kSchurBatchPts];              // first block, span, operand offset, last window tile (jhi)
+  double red[kSchurThreads / 64];
+};
+
+// 1. thread per point of batch B (tid < npts)
+__device__ __forceinline__ double schur_points(const Dev& d, const LmState* st, const SchurBatch& B, int tid,
+                                               double* Lsh, double* wsh, int4* pinf) {
+  if (tid >= B.p1 - B.p0) return 0.0;
+  const int p = B.p0 + tid;
+  const int2 pi = d.pinfo[p];
+  const int2 pm = d.pmx[p];
+  int span = pi.y & 0xff, jhi = pm.y;
+  double fail = 0.0;
+  if (d.pfree[p]) {
+    double Vi[10], Li[10], w[4];
+    if (!point_block(d, st, p, Vi, Li, w)) fail = 1.0;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) Lsh[10 * tid + i] = Li[i];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) wsh[4 * tid + a] = w[a];
+  } else {
+    span = 0;
+    jhi = -1;
+  }
+  pinf[tid] = make_int4(pi.y >> 8, span, pm.x, jhi);
+  return fail;
+}
+
+// 2. thread per cell (point p, block b) of batch B: E_{p,b} = sum_o G_o J~c,o with G_o = L^-1 J~p,o^T (4 x 2),
+// written straight into the point's operand tiles: column c = 6 b + a - c0w of the window goes to tile c >> 4,
+// lane (c & 15) + 16 k.  The first and last cell of a point also zero the columns of its tiles 0 .. jhi outside
+// its span.
+__device__ __forceinline__ void schur_cells(const Dev& d, const SchurBatch& B, int tid, int c0w, const double* Lsh,
+                                            const double* wsh, const int4* pinf, double* Xb) {
+  (void)wsh;
+  for (int c = B.c0 + tid; c < B.c1; c += kSchurThreads / 2) {
+    const int4 ci = d.cells[c];   // first observation (-1: none), point, (block << 16) | further, their offset
+    const int lp = ci.y - B.p0;
+    const int4 pi = pinf[lp];
+    const int b = (int)((unsigned)ci.z >> 16), k1 = ci.w, k2 = ci.w + (ci.z & 0xffff);
+    const double* L = Lsh + 10 * lp;
+    double* xp = Xb + pi.z;
+    const int col0 = 6 * b - c0w;
+    auto at = [&](int col, int k) -> double& { return xp[64 * (col >> 4) + 16 * k + (col & 15)]; };
+    if (b == pi.x)   // left margin: the columns of tiles 0 .. jhi before the span (the consumer reads them all)
+      for (int col = 0; col < col0; ++col)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) at(col, k) = 0.0;
+    if (b == pi.x + pi.y - 1)   // right margin: after the span, to the end of tile jhi
+      for (int col = col0 + 6; col < 16 * (pi.w + 1); ++col)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) at(col, k) = 0.0;
+    if (ci.x < 0) {
+#pragma unroll
+      for (int a = 0; a < 6; ++a)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) at(col0 + a, k) = 0.0;
+      continue;
+    }
+    const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[ci.y];
+    const int k0 = k1 - 1;
+#pragma unroll 1
+    for (int k = k0; k < k2; ++k) {
+      const int o = k < k1 ? ci.x : d.cell_obs[k];
+      double G[4][2];
+      {
+        double Jp[8];
+        load_Jp_scaled(d, o, s4, Jp);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          double g0 = 0.0, g1 = 0.0;
+#pragma unroll
+          for (int m = 0; m <= kk; ++m) {
+            g0 += L[l4(kk, m)] * Jp[m];
+            g1 += L[l4(kk, m)] * Jp[4 + m];
+          }
+          G[kk][0] = g0;
+          G[kk][1] = g1;
+        }
+      }
+      double Jc[12];
+      load_Jc_scaled(d, o, b, Jc);
+      if (k == k0) {
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+          for (int a = 0; a < 6; ++a) at(col0 + a, kk) = G[kk][0] * Jc[a] + G[kk][1] * Jc[6 + a];
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+          for (int a = 0; a < 6; ++a) at(col0 + a, kk) += G[kk][0] * Jc[a] + G[kk][1] * Jc[6 + a];
+      }
+    }
+  }
+}
+
+// Diagnostic stamps (SG_STAMP=1): workgroup 0, lane 0 of waves 0 (producer, slots 32-39) and 4 (consumer,
+// slots 40-47) accumulate s_memtime deltas per phase.
+#define SG_SSTAMP(slot)                                                                  \
+  if (d.stamps && blockIdx.x == 0 && lane == 0 && (wave & 3) == 0) {                     \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime();                       \
+    d.stamps[(slot)] += now_ - last_;                                                    \
+    last_ = now_;                                                                        \
+  }
+__global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d) {
+  const LmState* st = d.st;
+  if (st->done || (int)blockIdx.x >= d.nseg) return;
+  __shared__ SchurLds sh;
+  unsigned long long last_ = __builtin_amdgcn_s_memtime();
+  const SchurSeg sg = d.segs[blockIdx.x];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nbt = sg.bt1 - sg.bt0;
+  const int c0w = 16 * sg.t0;
+  double* slab = d.S_slab + sg.s_off;
+  double linfail = 0.0;
+  if (wave < kSchurWaves / 2) {
+    // producers
+    if (nbt > 0) linfail += schur_points(d, st, d.sbatch[sg.bt0], tid, sh.L[0], sh.w[0], sh.pinf[0]);
+    SG_SSTAMP(32)
+    __syncthreads();
+    SG_SSTAMP(33)
+    for (int s = 0; s <= nbt; ++s) {
+      if (s < nbt)
+        schur_cells(d, d.sbatch[sg.bt0 + s], tid, c0w, sh.L[s % 3], sh.w[s % 3], sh.pinf[s % 3], sh.X[s & 1]);
+      SG_SSTAMP(34)
+      if (s + 1 < nbt) {
+        const int q = (s + 1) % 3;
+        linfail += schur_points(d, st, d.sbatch[sg.bt0 + s + 1], tid, sh.L[q], sh.w[q], sh.pinf[q]);
+      }
+      SG_SSTAMP(35)
+      __syncthreads();
+      SG_SSTAMP(36)
+    }
+  } else {
+    // consumers: wave cw owns the augmented window slots u = cw + 4 s
+    const int cw = wave - kSchurWaves / 2;
+    f64x4 acc[kSchurTPW];
+#pragma unroll
+    for (int s = 0; s < kSchurTPW; ++s) acc[s] = f64x4{0.0, 0.0, 0.0, 0.0};
+    SG_SSTAMP(40)
+    __syncthreads();
+    SG_SSTAMP(41)
+    for (int s = 0; s <= nbt; ++s) {
+      if (s >= 1) {
+        const SchurBatch B = d.sbatch[sg.bt0 + s - 1];
+        const int npts = B.p1 - B.p0;
+        const double* Xb = sh.X[(s - 1) & 1];
+        const double* wsh = sh.w[(s - 1) % 3];
+        const int4* pinf = sh.pinf[(s - 1) % 3];
+        switch (cw) {
+#define SG_SCHUR_CASE(W) \
+          case W: schur_wave_batch<W>(acc, Xb, wsh, pinf, npts, lane); break;
+          SG_SCHUR_CASE(0) SG_SCHUR_CASE(1) SG_SCHUR_CASE(2) SG_SCHUR_CASE(3)
+#undef SG_SCHUR_CASE
+        }
+        SG_SSTAMP(42)
+      }
+      __syncthreads();
+      SG_SSTAMP(44)
+    }
+    mfma_drain();
+    switch (cw) {
+#define SG_SCHUR_CASE(W) \
+      case W: schur_store<W>(acc, slab, sg.ntw, lane); break;
+      SG_SCHUR_CASE(0) SG_SCHUR_CASE(1) SG_SCHUR_CASE(2) SG_SCHUR_CASE(3)
+#undef SG_SCHUR_CASE
+    }
+    SG_SSTAMP(45)
+  }
+  linfail = block_sum<kSchurThreads>(linfail, sh.red);
+  if (tid == 0) d.seg_fail[blockIdx.x] = linfail;
+}
+
+// A point spanning more blocks than a segment window (a whole-map solve's long track): one workgroup, the
+// observation pairs (s <= t) of the point, each 6x6 block -A_c,s^T (P_s A_p,t^T) A_c,t into S_wide and the
+// rhs terms into rhs with global atomics (k_S_reduce adds both).
 __device__ __forceinline__ void schur_pair_add(double* dst, int ld, const double* Jcs, const double* Ps,
                                                const double* Jpt, const double* Jct, bool same_obs,
                                                bool same_blk, bool s_first) {
@@ -695,180 +959,55 @@ __device__ __forceinline__ void schur_pair_add(double* dst, int ld, const double
     }
 }
 
-// Window blocks are padded to 37 doubles in LDS: with 36 the same element of neighbouring blocks falls on
-// 8 banks (8-way conflicts for the atomics of a wave whose lanes hold different block pairs).
-constexpr int kWinLd = 37;
-
-__global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d) {
+__global__ __launch_bounds__(kSchurThreads) void k_schur_wide(Dev d) {
   const LmState* st = d.st;
-  if (st->done || (int)blockIdx.x >= d.nseg) return;
-  extern __shared__ double lds[];
-  __shared__ double red[kSchurThreads / 64];
-  const SchurSeg sg = d.segs[blockIdx.x];
-  const int npair = sg.nb * (sg.nb + 1) / 2;
-  const int nwin = sg.wide ? 0 : npair * kWinLd + sg.nb * 6;   // LDS: blocks padded to kWinLd doubles
-  double* win = lds;
-  double* rhsw = win + npair * kWinLd;
-  double* vinv = lds + nwin;                  // [kSegPts][10]
-  double* tpv = vinv + kSegPts * 10;          // [kSegPts][4]
-  double* Psh = tpv + kSegPts * 4;            // [segment observations][8]
-  const int tid = threadIdx.x;
-  for (int i = tid; i < nwin; i += kSchurThreads) win[i] = 0.0;
-  const double radius = st->radius;
-  const bool reuse = st->reuse_diag != 0;
-  double linfail = 0.0;
-  const int q0 = sg.p0, q1 = sg.p1;
-  const int obs_lo = d.poff[q0], obs_hi = d.poff[q1];
-  // phase 1: one thread per point
-  for (int t = tid; t < q1 - q0; t += kSchurThreads) {
-    const int p = q0 + t;
-    if (!d.pfree[p]) continue;
-    const double* Vp = d.V + 10 * (size_t)p;
-    double V[10];
+  if (st->done || (int)blockIdx.x >= d.nwide) return;
+  __shared__ double vinv[10], tpv[4];
+  const WideSeg ws = d.wsegs[blockIdx.x];
+  const int p = ws.p, tid = threadIdx.x;
+  if (!d.pfree[p]) return;
+  if (tid == 0) {
+    double Vi[10], Li[10], w[4];
+    d.seg_fail[d.nseg + blockIdx.x] = point_block(d, st, p, Vi, Li, w) ? 0.0 : 1.0;
 #pragma unroll
-    for (int i = 0; i < 10; ++i) V[i] = Vp[i];
-    const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
-    const double sp[4] = {s4.x, s4.y, s4.z, s4.w};
-    const double4 g4 = reinterpret_cast<const double4*>(d.g)[p];
-    const double gs[4] = {g4.x * sp[0], g4.y * sp[1], g4.z * sp[2], g4.w * sp[3]};
-    double dp[4];
-    if (!reuse) {
+    for (int i = 0; i < 10; ++i) vinv[i] = Vi[i];
 #pragma unroll
-      for (int a = 0; a < 4; ++a) dp[a] = fmin(fmax(sp[a] * sp[a] * V[u4(a, a)], st->min_diag), st->max_diag);
-      reinterpret_cast<double4*>(d.diag_p)[p] = make_double4(dp[0], dp[1], dp[2], dp[3]);
-    } else {
-      const double4 d4 = reinterpret_cast<const double4*>(d.diag_p)[p];
-      dp[0] = d4.x; dp[1] = d4.y; dp[2] = d4.z; dp[3] = d4.w;
-    }
-    double Vt[10];
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        if (c >= a) Vt[u4(a, c)] = sp[a] * V[u4(a, c)] * sp[c] + (a == c ? dp[a] / radius : 0.0);
-    double Vi[10];
-    if (!inv4_spd(Vt, Vi)) {
-      linfail += 1.0;
-#pragma unroll
-      for (int i = 0; i < 10; ++i) Vi[i] = NAN;
-    }
-    double tp[4];
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      double s = 0.0;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) s += sym4(Vi, a, c) * gs[c];
-      tp[a] = s;
-    }
-    double* Vo = d.Vinv + 10 * (size_t)p;
-#pragma unroll
-    for (int i = 0; i < 10; ++i) {
-      Vo[i] = Vi[i];
-      vinv[10 * t + i] = Vi[i];
-    }
-    reinterpret_cast<double4*>(d.tp)[p] = make_double4(tp[0], tp[1], tp[2], tp[3]);
-#pragma unroll
-    for (int a = 0; a < 4; ++a) tpv[4 * t + a] = tp[a];
+    for (int a = 0; a < 4; ++a) tpv[a] = d.tp[4 * (size_t)p + a];
   }
   __syncthreads();
-  // phase 2: one thread per observation
+  const int obs_lo = d.poff[p], obs_hi = d.poff[p + 1];
+  const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
   for (int o = obs_lo + tid; o < obs_hi; o += kSchurThreads) {
-    const int p = d.obs_pnt[o];
-    if (!d.pfree[p]) continue;
-    const int lp = p - q0;
     const int b = d.frame_block[d.obs_frame[o]];
-    const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
-    double Jp[8];
+    if (b < 0) continue;
+    double Jp[8], Jc[12];
     load_Jp_scaled(d, o, s4, Jp);
-    const double* Vi = vinv + 10 * lp;
-    if (!sg.heavy) {
-      double* Pr = Psh + 8 * (o - obs_lo);
-#pragma unroll
-      for (int rr = 0; rr < 2; ++rr)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          double acc = 0.0;
-#pragma unroll
-          for (int m = 0; m < 4; ++m) acc += Jp[4 * rr + m] * sym4(Vi, m, c);
-          Pr[4 * rr + c] = acc;
-        }
-    }
-    if (b < 0 || sg.det) continue;   // deterministic segments: the rhs rides on the (o, o) pair in phase 3
-    double Jc[12];
     load_Jc_scaled(d, o, b, Jc);
-    const double* tp = tpv + 4 * lp;
-    const double e0 = Jp[0] * tp[0] + Jp[1] * tp[1] + Jp[2] * tp[2] + Jp[3] * tp[3];
-    const double e1 = Jp[4] * tp[0] + Jp[5] * tp[1] + Jp[6] * tp[2] + Jp[7] * tp[3];
+    const double e0 = Jp[0] * tpv[0] + Jp[1] * tpv[1] + Jp[2] * tpv[2] + Jp[3] * tpv[3];
+    const double e1 = Jp[4] * tpv[0] + Jp[5] * tpv[1] + Jp[6] * tpv[2] + Jp[7] * tpv[3];
 #pragma unroll
-    for (int a = 0; a < 6; ++a) {
-      const double v = -(Jc[a] * e0 + Jc[6 + a] * e1);
-      if (sg.wide) atomicAdd(d.rhs + 6 * b + a, v);   // wide segments go straight to the global rhs partial
-      else atomicAdd(rhsw + (b - sg.b_lo) * 6 + a, v);
-    }
+    for (int a = 0; a < 6; ++a) atomicAdd(d.rhs + 6 * b + a, -(Jc[a] * e0 + Jc[6 + a] * e1));
   }
-  __syncthreads();
-  // phase 3: one thread per observation pair (a wide segment's pairs go to global atomics); in deterministic
-  // mode each wave walks its own list (every block summed by one wave, in list order)
-  int k0 = sg.pair_lo + tid, k1 = sg.pair_hi, kstep = kSchurThreads;
-  if (sg.det) {
-    const int w = tid >> 6;
-    k0 = (w == 0 ? sg.pair_lo : sg.pw[w - 1]) + (tid & 63);
-    k1 = w == 3 ? sg.pair_hi : sg.pw[w];
-    kstep = 64;
-  }
-  for (int k = k0; k < k1; k += kstep) {
+  for (int k = ws.pair_lo + tid; k < ws.pair_hi; k += kSchurThreads) {
     const int2 pr = d.pairs[k];
     const int os = obs_lo + (pr.x >> 16), ot = obs_lo + (pr.x & 0xffff);
     const int bs = pr.y >> 16, bt = pr.y & 0xffff;
-    const int p = d.obs_pnt[os];
-    const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
-    double Jcs[12], Jct[12], Jpt[8];
+    double Jcs[12], Jct[12], Jpt[8], Jps[8], Ps[8];
     load_Jc_scaled(d, os, bs, Jcs);
     load_Jc_scaled(d, ot, bt, Jct);
     load_Jp_scaled(d, ot, s4, Jpt);
-    double Ps[8];
-    if (!sg.heavy) {
+    load_Jp_scaled(d, os, s4, Jps);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) Ps[i] = Psh[8 * (os - obs_lo) + i];
-    } else {
-      // P_s = J~p,s V~^-1 recomputed (same arithmetic as the staged rows)
-      double Jps[8];
-      load_Jp_scaled(d, os, s4, Jps);
-      const double* Vi = vinv + 10 * (p - q0);
+    for (int rr = 0; rr < 2; ++rr)
 #pragma unroll
-      for (int rr = 0; rr < 2; ++rr)
+      for (int c = 0; c < 4; ++c) {
+        double a = 0.0;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          double acc = 0.0;
-#pragma unroll
-          for (int m = 0; m < 4; ++m) acc += Jps[4 * rr + m] * sym4(Vi, m, c);
-          Ps[4 * rr + c] = acc;
-        }
-    }
-    if (sg.det && os == ot) {
-      // this observation's rhs term -A_c,o^T (A_p,o t_p), from the wave that owns its diagonal block
-      const double* tp = tpv + 4 * (p - q0);
-      const double e0 = Jpt[0] * tp[0] + Jpt[1] * tp[1] + Jpt[2] * tp[2] + Jpt[3] * tp[3];
-      const double e1 = Jpt[4] * tp[0] + Jpt[5] * tp[1] + Jpt[6] * tp[2] + Jpt[7] * tp[3];
-#pragma unroll
-      for (int a = 0; a < 6; ++a) atomicAdd(rhsw + (bs - sg.b_lo) * 6 + a, -(Jcs[a] * e0 + Jcs[6 + a] * e1));
-    }
+        for (int m = 0; m < 4; ++m) a += Jps[4 * rr + m] * sym4(vinv, m, c);
+        Ps[4 * rr + c] = a;
+      }
     const int I = bs < bt ? bs : bt, Jb = bs < bt ? bt : bs;
-    if (sg.wide)
-      schur_pair_add(d.S_wide + (size_t)(6 * I) * d.n + 6 * Jb, d.n, Jcs, Ps, Jpt, Jct, os == ot, bs == bt, bs < bt);
-    else
-      schur_pair_add(win + wp(I - sg.b_lo, Jb - sg.b_lo, sg.nb) * kWinLd, 6, Jcs, Ps, Jpt, Jct, os == ot,
-                     bs == bt, bs < bt);
-  }
-  linfail = block_sum<kSchurThreads>(linfail, red);
-  if (tid == 0) d.seg_fail[blockIdx.x] = linfail;
-  __syncthreads();
-  if (!sg.wide) {
-    const int nslab = npair * 36 + sg.nb * 6;   // slab: compact 36-double blocks, then the rhs
-    for (int i = tid; i < nslab; i += kSchurThreads) {
-      const int blk = i / 36;
-      d.S_slab[sg.s_off + i] = blk < npair ? win[blk * kWinLd + (i - 36 * blk)] : rhsw[i - 36 * npair];
-    }
+    schur_pair_add(d.S_wide + (size_t)(6 * I) * d.n + 6 * Jb, d.n, Jcs, Ps, Jpt, Jct, os == ot, bs == bt, bs < bt);
   }
 }
 
@@ -876,79 +1015,108 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d) {
 // The camera-camera terms of the damped reduced system that do not come from the Schur complement:
 // blockdiag(U) (observation Jacobians) + FrameDistance diagonal and cross blocks + D^2 = diag/radius,
 // all Jacobi-scaled, for element (6I+a, 6J+c), J >= I.
-
-// k_S_reduce: the assembling rank also adds the camera-only terms and the S g_c part of the rhs, so S leaves
-// here damped.
-// One wave per block pair (I <= J) of S, then one wave per rhs block: the wave loads up to 64 slab offsets
-// of its partial list at once and walks them in list order (deterministic), lanes 0..35 (0..5 for the rhs)
-// summing their element, so every partial's load is independent and in flight together.
+//
+// k_S_reduce: one workgroup per 16x16 tile (R <= C) of the band of S (the frame columns), then one per rhs
+// block.  A tile's partials (one per segment whose window covers it, in segment order) are split over the four
+// waves (partial k to wave k mod 4, every lane summing 4 elements, 8 partials in flight), the four wave sums
+// combined in wave order (deterministic); then each thread finishes one element: the wide-point accumulator
+// and, on the assembling rank, the camera-only terms.  S leaves here damped; elements below the diagonal of a
+// diagonal tile are written as 0 (no factorisation reads them).  Tiles outside the band are never written
+// (zero since the load).
 __global__ __launch_bounds__(256) void k_S_reduce(Dev d) {
   const LmState* st = d.st;
   if (st->done) return;
-  const int lane = threadIdx.x & 63;
-  const int part = threadIdx.x >> 6;   // the four waves of a workgroup split one block's partial list
+  const int tid = threadIdx.x, lane = tid & 63, part = tid >> 6;
   const int wv = blockIdx.x;
-  const int npb = d.NB * (d.NB + 1) / 2;
-  if (wv >= npb + d.NB) return;
-  const bool is_rhs = wv >= npb;
-  int I = 0, Jb = 0, j0, j1;
-  const int32_t* lidx;
-  if (!is_rhs) {
-    int rem = wv;   // wave-uniform walk to (I, J)
-    while (rem >= d.NB - I) { rem -= d.NB - I; ++I; }
-    Jb = I + rem;
-    const int pr = I * d.NB + Jb;
-    j0 = d.s_loff[pr];
-    j1 = d.s_loff[pr + 1];
-    lidx = d.s_lidx;
-  } else {
-    I = wv - npb;
-    j0 = d.r_loff[I];
-    j1 = d.r_loff[I + 1];
-    lidx = d.r_lidx;
-  }
-  const int ne = is_rhs ? 6 : 36;
-  const int el = lane < ne ? lane : 0;
-  // Epilogue operands first (independent of the partials), so their round trips overlap the walk below:
-  // the wide-segment accumulator, and on the assembling rank blockdiag(U) + FrameDistance + damping (the
-  // assembly of slam.cpp's camera-only terms, Jacobi-scaled) or the S g_c part of the rhs.
-  const int a = el / 6, c = el % 6;
-  const int ei = is_rhs ? 6 * I + el : 6 * I + a, ej = 6 * Jb + c;
-  const size_t gi = (size_t)ei * d.n + ej;
+  if (wv >= d.nstile + d.NB) return;
   const double radius = st->radius;
-  const double e_acc = is_rhs ? d.rhs[ei] : d.S_wide[gi];
-  double e_si = 0.0, e_sj = 0.0, e_u = 0.0, e_fd = 0.0, e_dg = 0.0, e_g = 0.0, e_x0 = 0.0, e_x1 = 0.0;
-  int e_dd = -1, e_blk = -1;
-  if (d.assemble) {
-    e_si = d.scale_c[ei];
-    if (is_rhs) {
-      e_g = d.camg[ei];
-    } else {
-      e_sj = d.scale_c[ej];
+  const int nf = 6 * d.NB;   // frame columns
+  if (wv < d.nstile) {
+    const int rc = d.stile[wv];
+    const int R = rc >> 16, C = rc & 0xffff;
+    const int i = 16 * R + (tid >> 4), j = 16 * C + (tid & 15);
+    const bool live = i < nf && j < nf;
+    const bool up = live && i <= j;
+    const size_t gi = (size_t)(live ? i : 0) * d.n + (live ? j : 0);
+    // epilogue operands first, so their round trips overlap the partial walk
+    const double e_acc = (up && d.nwide) ? d.S_wide[gi] : 0.0;
+    const int I = i / 6, a = i - 6 * (i / 6), Jb = j / 6, c = j - 6 * (j / 6);
+    double e_si = 0.0, e_sj = 0.0, e_u = 0.0, e_fd = 0.0, e_dg = 0.0, e_x = 0.0;
+    if (d.assemble && up) {
+      e_si = d.scale_c[i];
+      e_sj = d.scale_c[j];
       if (I == Jb) {
-        e_u = d.xchg_cam[(size_t)I * kCamV + u6(min(a, c), max(a, c))];
+        e_u = d.xchg_cam[(size_t)I * kCamV + u6(a, c)];
         e_fd = (a >= 3 && c >= 3) ? d.fd_D[9 * I + 3 * (a - 3) + (c - 3)] : 0.0;
-        e_dg = d.diag_c[ei];
+        e_dg = a == c ? d.diag_c[i] : 0.0;
       } else if (a >= 3 && c >= 3) {
-        e_dd = d.fd_pair[I * d.NB + Jb];
-        if (e_dd >= 0) {
-          const double* Xd = d.fd_X + 9 * e_dd;   // J_a J_b^T, rows: frame a's translation
-          e_x0 = Xd[3 * (a - 3) + (c - 3)];
-          e_x1 = Xd[3 * (c - 3) + (a - 3)];
-          e_blk = d.frame_block[d.fd_a[e_dd]];
+        const int dd = d.fd_pair[I * d.NB + Jb];
+        if (dd >= 0) {
+          const double* Xd = d.fd_X + 9 * dd;   // J_a J_b^T, rows: frame a's translation
+          e_x = d.frame_block[d.fd_a[dd]] == I ? Xd[3 * (a - 3) + (c - 3)] : Xd[3 * (c - 3) + (a - 3)];
         }
       }
     }
+    const int j0 = d.s_loff[wv], j1 = d.s_loff[wv + 1];
+    __shared__ double wsum[4][256];
+    double s[4] = {0.0, 0.0, 0.0, 0.0};
+    constexpr int kSR = 8;
+    for (int base = j0 + part; base < j1; base += 4 * 64) {
+      const int cnt = min(64, (j1 - base + 3) / 4);
+      const int myoff = d.s_lidx[lane < cnt ? base + 4 * lane : j0];
+      for (int k = 0; k < cnt; k += kSR) {
+        double v[kSR][4];
+#pragma unroll
+        for (int u = 0; u < kSR; ++u) {
+          const double* src = d.S_slab + __builtin_amdgcn_readlane(myoff, min(k + u, 63)) + lane;
+#pragma unroll
+          for (int m = 0; m < 4; ++m) v[u][m] = src[64 * m];
+        }
+#pragma unroll
+        for (int u = 0; u < kSR; ++u)
+          if (k + u < cnt)
+#pragma unroll
+            for (int m = 0; m < 4; ++m) s[m] += v[u][m];
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) wsum[part][lane + 64 * m] = s[m];
+    __syncthreads();
+    if (!live) return;
+    if (!up) {
+      d.S[gi] = 0.0;
+      return;
+    }
+    double t = ((wsum[0][tid] + wsum[1][tid]) + wsum[2][tid]) + wsum[3][tid];
+    t += e_acc;
+    if (d.nwide) d.S_wide[gi] = 0.0;
+    if (d.assemble) {   // assembly_term, from the prefetched operands
+      double v;
+      if (I == Jb) {
+        v = (e_u + e_fd) * (e_si * e_sj);
+        if (a == c) v += e_dg / radius;
+      } else {
+        v = e_x * e_si * e_sj;
+      }
+      t += v;
+    }
+    d.S[gi] = t;
+    return;
   }
-  // Wave `part` sums every fourth 64-entry chunk of the list (in list order), kSR partial loads in flight;
-  // the four wave sums are combined in wave order (deterministic).
+  // rhs block I: one wave per 64-entry chunk of its partial list (in list order), lanes 0..5
+  const int I = wv - d.nstile;
+  const int j0 = d.r_loff[I], j1 = d.r_loff[I + 1];
+  const int el = lane < 6 ? lane : 0;
+  const int ei = 6 * I + el;
+  const double e_acc = d.rhs[ei];
+  const double e_si = d.assemble ? d.scale_c[ei] : 0.0, e_g = d.assemble ? d.camg[ei] : 0.0;
+  __shared__ double rsum[4][6];
   constexpr int kSR = 32;
-  __shared__ double wsum[4][36];
   double s = 0.0;
-  int myoff = lidx[(j0 + 64 * part + lane < j1) ? j0 + 64 * part + lane : 0];
+  int myoff = d.r_lidx[(j0 + 64 * part + lane < j1) ? j0 + 64 * part + lane : 0];
   for (int base = j0 + 64 * part; base < j1; base += 256) {
     const int cnt = min(64, j1 - base);
-    const int nxt = lidx[(base + 256 + lane < j1) ? base + 256 + lane : 0];
+    const int nxt = d.r_lidx[(base + 256 + lane < j1) ? base + 256 + lane : 0];
     for (int k = 0; k < cnt; k += kSR) {
       double v[kSR];
 #pragma unroll
@@ -959,31 +1127,14 @@ __global__ __launch_bounds__(256) void k_S_reduce(Dev d) {
     }
     myoff = nxt;
   }
-  if (lane < ne) wsum[part][lane] = s;
+  if (lane < 6) rsum[part][lane] = s;
   __syncthreads();
-  if (part != 0 || lane >= ne) return;
-  s = ((wsum[0][lane] + wsum[1][lane]) + wsum[2][lane]) + wsum[3][lane];
+  if (part != 0 || lane >= 6) return;
+  s = ((rsum[0][lane] + rsum[1][lane]) + rsum[2][lane]) + rsum[3][lane];
   s += e_acc;
-  if (!is_rhs) {
-    d.S_wide[gi] = 0.0;
-    if (d.assemble) {   // assembly_term, from the prefetched operands
-      double v = 0.0;
-      if (I == Jb) {
-        if (c >= a) {
-          v = (e_u + e_fd) * (e_si * e_sj);
-          if (a == c) v += e_dg / radius;
-        }
-      } else if (e_dd >= 0) {
-        v = (e_blk == I ? e_x0 : e_x1) * e_si * e_sj;
-      }
-      s += v;
-    }
-    d.S[gi] = s;
-  } else {
-    if (d.assemble) s += e_si * e_g;   // y = rhs_sub + S g_c
-    d.xc[ei] = s;       // local rhs partial (all-reduced with S); the wide accumulator is reset
-    d.rhs[ei] = 0.0;
-  }
+  if (d.assemble) s += e_si * e_g;   // y = rhs_sub + S g_c
+  d.xc[ei] = s;       // local rhs partial (all-reduced with S); the wide accumulator is reset
+  d.rhs[ei] = 0.0;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1298,7 +1449,6 @@ constexpr int kPanelWaves = 3;   // 16 + 3 x 48 >= kCholWS columns
 constexpr int kJendSh = 512;     // panel band ends cached in LDS (n <= 8192)
 constexpr int kCholLd = kCholWS + 1;
 constexpr size_t kCholLds = (size_t)kCholWS * kCholLd * sizeof(double);
-typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ double& Wn(double* win, int i, int j) {
   return win[(i & (kCholWS - 1)) * kCholLd + (j & (kCholWS - 1))];
@@ -2609,7 +2759,7 @@ __global__ __launch_bounds__(kRedThreads) void k_upd_reduce(Dev d, int fuse) {
         v[kUCandX2] += t[u][4];
       }
   }
-  for (int g = tid; g < d.nseg; g += kRedThreads) v[kULinFail] += d.seg_fail[g];
+  for (int g = tid; g < d.nseg + d.nwide; g += kRedThreads) v[kULinFail] += d.seg_fail[g];
   block_sum_multi<kRedThreads, kUNum>(v, red);
   if (tid == 0) {
 #pragma unroll
@@ -3048,157 +3198,159 @@ void BaSolver::Load(const sg_problem& p) {
   npu_ = (int)pu_units.size();
   if (pu_units.empty()) pu_units.push_back(0);
   lap("lin-lists");
-  // Schur segments: runs of at most kSegPts consecutive points (device order) whose observations fit the
-  // LDS stage and whose camera blocks fit a window of kSegNbMax blocks; one workgroup each, with its own
-  // window partial in S_slab.  A point spanning more blocks is a "wide" segment of its own (global
-  // atomics).  Per segment, the observation pairs (s <= t, both on free frames) of its free points.
-  std::vector<int32_t> obs_pnt(M_);
+  // Schur work lists (see SchurSeg): the cells of every free point (one per block of its span, with the
+  // point's observations in that block), segments of consecutive points whose columns fit kSchurTW tiles of
+  // S, their batches, and each wide point's observation pairs (s <= t, both on free frames).
+  std::vector<int32_t> obs_pnt(M_), obs_blk(M_);
   for (int i = 0; i < P_; ++i)
     for (int o = poff[i]; o < poff[i + 1]; ++o) obs_pnt[o] = i;
+  for (int o = 0; o < M_; ++o) obs_blk[o] = frame_block[obs_frame[o]];
+  // span in blocks of a free point's Schur terms (0: none)
+  auto sspan = [&](int i) {
+    const int pt = point_perm_[i];
+    return (pfree[i] && pfirst[pt] < NB_) ? plast[pt] - pfirst[pt] + 1 : 0;
+  };
+  std::vector<int32_t> pinfo(2 * (size_t)std::max(P_, 1), 0), pmx(2 * (size_t)std::max(P_, 1), 0), cells, cell_obs;
+  int ncell = 0;
   std::vector<SchurSeg> segs;
-  std::vector<int32_t> pairs_flat;   // int2 per pair
-  std::vector<int32_t> obs_blk(M_);
+  std::vector<SchurBatch> sbatch;
+  std::vector<WideSeg> wsegs;
+  std::vector<int32_t> pairs_flat;   // int2 per pair (wide points)
+  npairs_ = 0;
+  schur_mfma_ = 0.0;
   {
-    size_t npairs = 0;
+    std::vector<std::pair<int, int>> bo;
     for (int i = 0; i < P_; ++i) {
       size_t kb = 0;
-      for (int o = poff[i]; o < poff[i + 1]; ++o) {
-        obs_blk[o] = frame_block[obs_frame[o]];
-        kb += obs_blk[o] >= 0;
+      for (int o = poff[i]; o < poff[i + 1]; ++o) kb += obs_blk[o] >= 0;
+      if (pfree[i]) npairs_ += kb * (kb + 1) / 2;
+      const int sp = sspan(i);
+      if (sp == 0 || sp > kSegNbMax) continue;
+      const int pf = pfirst[point_perm_[i]];
+      pinfo[2 * i] = (int)(cells.size() / 4);
+      pinfo[2 * i + 1] = (pf << 8) | sp;
+      bo.clear();
+      for (int o = poff[i]; o < poff[i + 1]; ++o)
+        if (obs_blk[o] >= 0) bo.emplace_back(obs_blk[o], o);
+      std::sort(bo.begin(), bo.end());
+      size_t k = 0;
+      for (int b = pf; b < pf + sp; ++b) {
+        // {first observation or -1, point, (block << 16) | further observations, their offset in cell_obs}
+        int o0 = -1;
+        if (k < bo.size() && bo[k].first == b) o0 = bo[k++].second;
+        const int k1 = (int)cell_obs.size();
+        while (k < bo.size() && bo[k].first == b) cell_obs.push_back(bo[k++].second);
+        cells.insert(cells.end(), {o0, i, (int)(((unsigned)b << 16) | (unsigned)(cell_obs.size() - k1)), k1});
       }
-      if (pfree[i]) npairs += kb * (kb + 1) / 2;
     }
-    pairs_flat.reserve(2 * npairs + 2);
+    ncell = (int)cells.size() / 4;
+    if (cells.empty()) cells.assign(4, 0);
+    if (cell_obs.empty()) cell_obs.push_back(0);
   }
   int s_off = 0;
-  // SG_DETERMINISTIC=1: window blocks summed by one wave each (bitwise reproducible; see SchurSeg::det)
-  const bool deterministic = getenv("SG_DETERMINISTIC") && getenv("SG_DETERMINISTIC")[0] == '1';
-  max_seg_nb_ = 0;
-  max_seg_obs_ = 0;
   {
-    auto span = [&](int i) { return pfirst[point_perm_[i]] >= NB_ ? 0 : plast[point_perm_[i]] - pfirst[point_perm_[i]] + 1; };
-    // Window width: the widest single point (so no point needs the global-atomic "wide" path), capped at
-    // kSegNbMax.  A narrow window keeps the workgroup's LDS small enough for three resident workgroups per
-    // CU (measured at config 2: a 14-block window, 50 KB, runs the Schur kernel 13 % faster than 20 blocks).
-    int nbmax = 1;
-    for (int i = 0; i < P_; ++i) nbmax = std::max(nbmax, span(i));
-    nbmax = std::min(nbmax, kSegNbMax);
+    // points per segment: one segment per CU (the workgroup's LDS holds one per CU; fewer, longer segments
+    // write fewer partial tiles and keep the producer/consumer pipeline full; SG_SCHUR_SEGS: tuning)
+    int ncu = 256;
+    {
+      hipDeviceProp_t prop;
+      if (hipGetDeviceProperties(&prop, dev_.device) == hipSuccess && prop.multiProcessorCount > 0)
+        ncu = prop.multiProcessorCount;
+    }
+    const int target = getenv("SG_SCHUR_SEGS") ? std::max(1, atoi(getenv("SG_SCHUR_SEGS"))) : ncu;
+    const int maxpts = std::max(16, (P_ + target - 1) / target);
+    int cnext = 0;
     for (int i = 0; i < P_;) {
+      if (sspan(i) > kSegNbMax) {
+        WideSeg w{};
+        w.p = i;
+        w.pair_lo = (int)pairs_flat.size() / 2;
+        for (int os = poff[i]; os < poff[i + 1]; ++os) {
+          if (obs_blk[os] < 0) continue;
+          for (int ot = os; ot < poff[i + 1]; ++ot) {
+            if (obs_blk[ot] < 0) continue;
+            pairs_flat.push_back(((os - poff[i]) << 16) | (ot - poff[i]));
+            pairs_flat.push_back((obs_blk[os] << 16) | obs_blk[ot]);
+          }
+        }
+        w.pair_hi = (int)pairs_flat.size() / 2;
+        wsegs.push_back(w);
+        ++i;
+        continue;
+      }
       SchurSeg sg{};
       sg.p0 = i;
-      const int pt0 = point_perm_[i];
-      int j = i + 1, nobs = poff[i + 1] - poff[i];
-      if (span(i) > nbmax) {
-        sg.wide = 1;
-        sg.b_lo = pfirst[pt0];
-        sg.nb = 0;
-      } else {
-        const bool constonly = pfirst[pt0] >= NB_;
-        int lo = constonly ? 0 : pfirst[pt0], hi = constonly ? -1 : plast[pt0];
-        while (j < P_ && j - i < kSegPts) {
-          const int ptj = point_perm_[j];
-          const int kj = poff[j + 1] - poff[j];
-          if (nobs + kj > kSegObsCap) break;
-          if ((pfirst[ptj] >= NB_) != constonly) break;
-          if (!constonly) {
-            const int l2 = std::min(lo, pfirst[ptj]), h2 = std::max(hi, plast[ptj]);
-            if (h2 - l2 + 1 > nbmax) break;
-            lo = l2;
-            hi = h2;
-          }
-          nobs += kj;
-          ++j;
+      int clo = INT32_MAX, chi = -1, blo = INT32_MAX, bhi = -1;   // columns [clo, chi), blocks [blo, bhi]
+      int j = i;
+      while (j < P_ && j - i < maxpts) {
+        const int sp = sspan(j);
+        if (sp > kSegNbMax) break;
+        if (sp > 0) {
+          const int pf = pfirst[point_perm_[j]];
+          const int l2 = std::min(clo, 6 * pf), h2 = std::max(chi, 6 * (pf + sp));
+          if ((h2 + 15) / 16 - l2 / 16 > kSchurTW) break;
+          clo = l2;
+          chi = h2;
+          blo = std::min(blo, pf);
+          bhi = std::max(bhi, pf + sp - 1);
         }
-        sg.b_lo = lo;
-        sg.nb = hi - lo + 1;
+        ++j;
       }
       sg.p1 = j;
+      if (chi >= 0) {
+        sg.t0 = clo / 16;
+        sg.ntw = (chi + 15) / 16 - sg.t0;
+        sg.b_lo = blo;
+        sg.nb = bhi - blo + 1;
+      }
       sg.s_off = s_off;
-      sg.heavy = nobs > kSegObsCap ? 1 : 0;   // only a single point exceeds the cap
-      s_off += sg.wide ? 0 : sg.nb * (sg.nb + 1) / 2 * 36 + sg.nb * 6;
-      max_seg_nb_ = std::max(max_seg_nb_, sg.nb);
-      if (!sg.heavy) max_seg_obs_ = std::max(max_seg_obs_, nobs);
-      const int obs_lo = poff[i];
-      sg.pair_lo = (int)pairs_flat.size() / 2;
-      for (int pt = i; pt < j; ++pt) {
-        if (!pfree[pt]) continue;
-        for (int os = poff[pt]; os < poff[pt + 1]; ++os) {
-          const int bs = obs_blk[os];
-          if (bs < 0) continue;
-          for (int ot = os; ot < poff[pt + 1]; ++ot) {
-            const int bt = obs_blk[ot];
-            if (bt < 0) continue;
-            pairs_flat.push_back(((os - obs_lo) << 16) | (ot - obs_lo));
-            pairs_flat.push_back((bs << 16) | bt);
-          }
+      s_off += sg.ntw * (sg.ntw + 1) / 2 * 256 + 16 * sg.ntw;
+      // last window tile of each point's columns (-1: no Schur terms)
+      auto pjhi = [&](int k) {
+        const int sp = sspan(k);
+        return sp == 0 ? -1 : (6 * (pfirst[point_perm_[k]] + sp) - 1 - 16 * sg.t0) / 16;
+      };
+      sg.bt0 = (int)sbatch.size();
+      for (int k = i; k < j;) {
+        SchurBatch B{};
+        B.p0 = k;
+        B.c0 = cnext;
+        int nc = 0, nx = 0;
+        while (k < j && k - B.p0 < kSchurBatchPts && nx + 64 * (pjhi(k) + 1) <= kSchurXCap) {
+          pmx[2 * k] = nx;
+          pmx[2 * k + 1] = pjhi(k);
+          nx += 64 * (pjhi(k) + 1);
+          schur_mfma_ += schur_aug_base(pjhi(k) + 1);
+          nc += sspan(k++);
         }
+        B.p1 = k;
+        B.c1 = B.c0 + nc;
+        cnext += nc;
+        sbatch.push_back(B);
       }
-      sg.pair_hi = (int)pairs_flat.size() / 2;
-      sg.pw[0] = sg.pw[1] = sg.pw[2] = sg.pair_hi;
-      sg.det = deterministic && !sg.wide;
-      if (sg.det && sg.pair_hi > sg.pair_lo) {
-        // per-wave lists: window block rows I = min(b_s, b_t) (by pair count, largest first) to the least
-        // loaded of the 4 waves, pairs stably partitioned by their row's wave.  Every block, and every rhs
-        // block through its observations' (o, o) pairs, then belongs to one wave, while each list keeps the
-        // point-major order in which neighbouring lanes share an observation's rows (loads) and spread over
-        // different blocks (LDS atomics).
-        auto row = [&](int k) {
-          const int v = pairs_flat[2 * k + 1];
-          return std::min(v >> 16, v & 0xffff) - sg.b_lo;
-        };
-        std::vector<int> cnt(sg.nb, 0), order(sg.nb), wave_of(sg.nb, 0);
-        for (int k = sg.pair_lo; k < sg.pair_hi; ++k) cnt[row(k)]++;
-        std::iota(order.begin(), order.end(), 0);
-        std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return cnt[a] > cnt[b]; });
-        long load[kSchurThreads / 64] = {0, 0, 0, 0};
-        for (int r : order) {
-          if (!cnt[r]) break;
-          const int w = int(std::min_element(load, load + kSchurThreads / 64) - load);
-          wave_of[r] = w;
-          load[w] += cnt[r];
-        }
-        std::vector<int32_t> tmp(pairs_flat.begin() + 2 * (size_t)sg.pair_lo, pairs_flat.end());
-        size_t at = 2 * (size_t)sg.pair_lo;
-        for (int w = 0; w < kSchurThreads / 64; ++w) {
-          if (w > 0) sg.pw[w - 1] = (int)(at / 2);
-          for (size_t e = 0; e < tmp.size(); e += 2) {
-            const int v = tmp[e + 1];
-            if (wave_of[std::min(v >> 16, v & 0xffff) - sg.b_lo] != w) continue;
-            pairs_flat[at++] = tmp[e];
-            pairs_flat[at++] = tmp[e + 1];
-          }
-        }
-      }
+      sg.bt1 = (int)sbatch.size();
       segs.push_back(sg);
       i = j;
     }
+    SG_REQUIRE(cnext == ncell, SG_EINVAL, "Schur cells out of step with the batches");
   }
   nseg_ = (int)segs.size();
-  npairs_ = pairs_flat.size() / 2;
+  nwide_ = (int)wsegs.size();
   if (pairs_flat.empty()) pairs_flat.assign(2, 0);
   lap("segments");
-  // deterministic reduction lists: for every camera block / block pair, the slab offsets of the chunk
-  // partials that cover it (fixed chunk order)
+  // deterministic reduction lists: for every camera block, the slab offsets of the chunk partials that cover
+  // it (fixed chunk order), and of the segments' rhs partials
   std::vector<int32_t> cam_loff(NB_ + 1, 0), cam_lidx, r_loff(NB_ + 1, 0), r_lidx;
-  std::vector<int32_t> s_loff((size_t)NB_ * NB_ + 1, 0), s_lidx;
   {
     std::vector<std::vector<int32_t>> cl(NB_), rl(NB_);
-    std::vector<std::vector<int32_t>> sl((size_t)NB_ * NB_);
     for (const LinChunk& ch : lchunks) {
       if (ch.wide || ch.nb == 0) continue;
       for (int i = 0; i < ch.nb; ++i) cl[ch.b_lo + i].push_back(ch.cam_off + i * kCamV);
     }
-    for (const SchurSeg& sg : segs) {
-      if (sg.wide || sg.nb == 0) continue;
-      const int npair = sg.nb * (sg.nb + 1) / 2;
-      for (int i = 0; i < sg.nb; ++i) {
-        const int b = sg.b_lo + i;
-        rl[b].push_back(sg.s_off + npair * 36 + i * 6);
-        for (int j = i; j < sg.nb; ++j) {
-          const int wpij = i * sg.nb - i * (i - 1) / 2 + (j - i);
-          sl[(size_t)b * NB_ + sg.b_lo + j].push_back(sg.s_off + wpij * 36);
-        }
-      }
+    for (const SchurSeg& sg : segs) {   // rhs partial of block I: window columns 6 I - 16 t0 ..
+      const int ntile = sg.ntw * (sg.ntw + 1) / 2;
+      for (int i = 0; i < sg.nb; ++i)
+        rl[sg.b_lo + i].push_back(sg.s_off + 256 * ntile + 6 * (sg.b_lo + i) - 16 * sg.t0);
     }
     for (int b = 0; b < NB_; ++b) {
       cam_loff[b + 1] = cam_loff[b] + (int)cl[b].size();
@@ -3206,13 +3358,8 @@ void BaSolver::Load(const sg_problem& p) {
       r_loff[b + 1] = r_loff[b] + (int)rl[b].size();
       r_lidx.insert(r_lidx.end(), rl[b].begin(), rl[b].end());
     }
-    for (size_t pr = 0; pr < sl.size(); ++pr) {
-      s_loff[pr + 1] = s_loff[pr] + (int)sl[pr].size();
-      s_lidx.insert(s_lidx.end(), sl[pr].begin(), sl[pr].end());
-    }
     if (cam_lidx.empty()) cam_lidx.push_back(0);
     if (r_lidx.empty()) r_lidx.push_back(0);
-    if (s_lidx.empty()) s_lidx.push_back(0);
   }
   lap("reduce-lists");
   // FrameDistance
@@ -3304,6 +3451,31 @@ void BaSolver::Load(const sg_problem& p) {
     Wg_.Upload(wz, stream_);
     tile_lds_ = (size_t)npanel * 32 * sizeof(double) + (size_t)npanel * sizeof(int32_t);
   }
+  // k_S_reduce work: the band tiles (R <= C) of the frame columns, and per tile the segment tiles covering it
+  // (segment order).  A segment tile outside the band is zero (no point couples its rows and columns).
+  std::vector<int32_t> stile, s_loff(1, 0), s_lidx;
+  {
+    const int nft = (6 * NB_ + kCholNb - 1) / kCholNb;
+    std::vector<int32_t> row_off(nft + 1, 0), cend(nft, 0);
+    for (int R = 0; R < nft; ++R) {
+      cend[R] = std::min(nft, (panel_jmax[R] + kCholNb - 1) / kCholNb);
+      row_off[R + 1] = row_off[R] + std::max(0, cend[R] - R);
+      for (int C = R; C < cend[R]; ++C) stile.push_back((R << 16) | C);
+    }
+    std::vector<std::vector<int32_t>> tl(stile.size());
+    for (const SchurSeg& sg : segs)
+      for (int u = 0; u < sg.ntw * (sg.ntw + 1) / 2; ++u) {
+        const int R = sg.t0 + schur_tile_r(u), C = sg.t0 + schur_tile_c(u);
+        if (R < nft && C < cend[R]) tl[row_off[R] + C - R].push_back(sg.s_off + 256 * u);
+      }
+    for (const auto& l : tl) {
+      s_loff.push_back(s_loff.back() + (int)l.size());
+      s_lidx.insert(s_lidx.end(), l.begin(), l.end());
+    }
+    nstile_ = (int)stile.size();
+    if (stile.empty()) stile.push_back(0);
+    if (s_lidx.empty()) s_lidx.push_back(0);
+  }
   lap("envelope");
   // device uploads
   hipStream_t s = stream_;
@@ -3339,8 +3511,15 @@ void BaSolver::Load(const sg_problem& p) {
   llist_d_.Upload(llist, s);
   obs_pnt_.Upload(obs_pnt.empty() ? std::vector<int32_t>{0} : obs_pnt, s);
   segs_.Upload(segs.empty() ? std::vector<SchurSeg>(1) : segs, s);
+  sbatch_.Upload(sbatch.empty() ? std::vector<SchurBatch>(1) : sbatch, s);
+  wsegs_.Upload(wsegs.empty() ? std::vector<WideSeg>(1) : wsegs, s);
+  pinfo_.Upload(pinfo, s);
+  pmx_.Upload(pmx, s);
+  cells_.Upload(cells, s);
+  cell_obs_.Upload(cell_obs, s);
+  stile_.Upload(stile, s);
   pairs_.Upload(pairs_flat, s);
-  seg_fail_.Resize(std::max(nseg_, 1));
+  seg_fail_.Resize(std::max(nseg_ + nwide_, 1));
   cam_loff_.Upload(cam_loff, s);
   cam_lidx_.Upload(cam_lidx, s);
   s_loff_.Upload(s_loff, s);
@@ -3399,13 +3578,6 @@ void BaSolver::Load(const sg_problem& p) {
   stamp_on_ = getenv("SG_STAMP") && getenv("SG_STAMP")[0] == '1';
   if (stamp_on_) stamps_.Resize(64);
   ResetState(s);
-  schur_lds_ = sizeof(double) * ((size_t)max_seg_nb_ * (max_seg_nb_ + 1) / 2 * kWinLd + max_seg_nb_ * 6 +
-                                  (size_t)kSegPts * 14 + (size_t)std::max(max_seg_obs_, 1) * 8);
-  // bounded by construction: window <= kSegNbMax blocks, staged observations <= kSegObsCap (heavy points are
-  // not staged)
-  SG_REQUIRE(schur_lds_ <= 160 * 1024, SG_EINVAL, "Schur segment LDS budget exceeded");
-  SG_HIP_CHECK(hipFuncSetAttribute((const void*)k_schur, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)schur_lds_));
   if (chol_tiles_)
     for (const void* f : {(const void*)k_chol_tiles<false>, (const void*)k_chol_tiles<true>})
       SG_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tile_lds_));
@@ -3600,6 +3772,15 @@ Dev BaSolver::MakeDev() {
   d.lin_scal = lin_scal_.ptr;
   d.segs = segs_.ptr;
   d.nseg = nseg_;
+  d.sbatch = sbatch_.ptr;
+  d.pinfo = reinterpret_cast<const int2*>(pinfo_.ptr);
+  d.pmx = reinterpret_cast<const int2*>(pmx_.ptr);
+  d.cells = reinterpret_cast<const int4*>(cells_.ptr);
+  d.cell_obs = cell_obs_.ptr;
+  d.wsegs = wsegs_.ptr;
+  d.nwide = nwide_;
+  d.stile = stile_.ptr;
+  d.nstile = nstile_;
   d.seg_fail = seg_fail_.ptr;
   d.pairs = reinterpret_cast<const int2*>(pairs_.ptr);
   d.assemble = (!comm_ || comm_->rank() == 0) ? 1 : 0;
@@ -3689,10 +3870,11 @@ void BaSolver::Iterate(int n) {
     hipLaunchKernelGGL(k_cam_finalize, dim3(1), dim3(256), 0, stream_, d);
     TimedLaunchEnd(kKCamFinal);
     TimedLaunchBegin(kKSchur);
-    hipLaunchKernelGGL(k_schur, dim3(std::max(nseg_, 1)), dim3(kSchurThreads), schur_lds_, stream_, d);
+    hipLaunchKernelGGL(k_schur, dim3(std::max(nseg_, 1)), dim3(kSchurThreads), 0, stream_, d);
+    if (nwide_) hipLaunchKernelGGL(k_schur_wide, dim3(nwide_), dim3(kSchurThreads), 0, stream_, d);
     TimedLaunchEnd(kKSchur);
     TimedLaunchBegin(kKSReduce);
-    const int nwv = NB_ * (NB_ + 1) / 2 + NB_;
+    const int nwv = nstile_ + NB_;
     hipLaunchKernelGGL(k_S_reduce, dim3(std::max(nwv, 1)), dim3(256), 0, stream_, d);
     TimedLaunchEnd(kKSReduce);
     if (nk_) {
@@ -3910,6 +4092,7 @@ int BaSolver::KernelWork(double* bytes, double* flops, int max) {
   by[kKLin] = M * (16 + 4 + 1 + 192) + P * (32 + 4 + 80 + 32 + 1) + NB * kCamV * 8;
   fl[kKLin] = M * 420.0;
   by[kKSchur] = M * 192 + P * (80 + 32 + 32 + 32 + 80 + 32);
+  fl[kKSchur] = 2048.0 * schur_mfma_;   // v_mfma_f64_16x16x4f64 tile updates
   by[kKPointUpd] = M * (192 + 16 + 4) + P * (32 + 32 + 80 + 32 + 32);
   by[kKChol] = n * n * 8 * 2;
   fl[kKChol] = n * n * n / 3.0;

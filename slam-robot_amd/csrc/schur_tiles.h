@@ -1,0 +1,142 @@
+// schur_tiles.h — the matrix-core part of k_schur (ba_solver.hip): per segment window, the upper 16x16 tiles of
+// S and the rhs held in v_mfma_f64_16x16x4f64 accumulators, one MFMA per (point, tile) with K = 4 (the rows of
+// the point's whitened Jacobian E_p).  Device-only; shared with tools/schur_bench.hip.
+#ifndef SG_SCHUR_TILES_H_
+#define SG_SCHUR_TILES_H_
+
+#include <hip/hip_runtime.h>
+
+#include "ba_kernels.h"
+
+namespace sg {
+
+#ifndef SG_F64X4_DEFINED
+#define SG_F64X4_DEFINED
+typedef double f64x4 __attribute__((ext_vector_type(4)));   // v_mfma_f64_16x16x4f64 C/D operand
+#endif
+
+// Augmented slot order of a segment window: level c = 0 .. kSchurTW-1 holds the window tiles (0, c) .. (c, c),
+// then the rhs tile of tile row c (E_c^T w in its column 0).  A point whose columns end in window tile jhi
+// touches exactly the levels <= jhi: a prefix of schur_aug_base(jhi + 1) slots.  Wave W owns slots u = W + 4 s.
+__host__ __device__ constexpr int schur_aug_base(int c) { return c * (c + 3) / 2; }
+__host__ __device__ constexpr int schur_aug_c(int u) {
+  int c = 0;
+  while (schur_aug_base(c + 1) <= u) ++c;
+  return c;
+}
+__host__ __device__ constexpr int schur_aug_r(int u) { return u - schur_aug_base(schur_aug_c(u)); }   // c + 1: rhs
+// window tile (r, c), r <= c, in the segment slab's column-major upper order
+__host__ __device__ constexpr int schur_tile_index(int r, int c) { return c * (c + 1) / 2 + r; }
+__host__ __device__ constexpr int schur_tile_c(int t) {
+  int c = 0;
+  while ((c + 1) * (c + 2) / 2 <= t) ++c;
+  return c;
+}
+__host__ __device__ constexpr int schur_tile_r(int t) { return t - schur_tile_c(t) * (schur_tile_c(t) + 1) / 2; }
+// operand columns wave W reads
+__host__ __device__ constexpr unsigned schur_need(int W) {
+  unsigned m = 0;
+  for (int u = W; u < kSchurAug; u += kSchurCWaves) {
+    m |= 1u << schur_aug_c(u);
+    if (schur_aug_r(u) <= schur_aug_c(u)) m |= 1u << schur_aug_r(u);
+  }
+  return m;
+}
+
+// acc += A B with the accumulator tied in place.  A conditionally executed __builtin_amdgcn_mfma leaves the old
+// accumulator live beside the new one (a PHI), so the compiler picks the untied form and copies the
+// accumulators around every MFMA; the tied asm form keeps them in place.  The compiler does not see this as an
+// MFMA: the s_nop covers a VALU write -> MFMA read of an operand (2 wait states), and readers of the
+// accumulators must first call mfma_drain().  MFMA -> MFMA on the same accumulator is interlocked.
+__device__ __forceinline__ void mfma_acc(f64x4& acc, double a, double b) {
+  asm volatile("s_nop 1\n\tv_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+}
+// wait states after the last asm MFMA before VALU / memory instructions read its accumulator
+__device__ __forceinline__ void mfma_drain() { asm volatile("s_nop 15\n\ts_nop 15" ::: "memory"); }
+
+// One point: wave W runs the prefix of its slots below schur_aug_base(jhi + 1), as nested tests (a not-taken
+// branch per MFMA, one taken branch out).  The point's operand tiles are 0 .. jhi of the window (zero outside
+// its columns), so tiles with r below its first tile multiply zeros.
+template <int W, int S>
+__device__ __forceinline__ void schur_slots(f64x4 (&acc)[kSchurTPW], const double (&X)[kSchurTW], double wop, int ns) {
+  if constexpr (S < kSchurTPW && W + kSchurCWaves * S < kSchurAug) {
+    constexpr int u = W + kSchurCWaves * S;
+    constexpr int c = schur_aug_c(u), r = schur_aug_r(u);
+    if (__builtin_expect(S < ns, 1)) {
+      if constexpr (r <= c)
+        mfma_acc(acc[S], X[r], X[c]);
+      else
+        mfma_acc(acc[S], X[c], wop);
+      schur_slots<W, S + 1>(acc, X, wop, ns);
+    }
+  }
+}
+template <int W>
+__device__ __forceinline__ void schur_mfma(f64x4 (&acc)[kSchurTPW], const double (&X)[kSchurTW], double wop, int jhi) {
+  const int nu = schur_aug_base(jhi + 1);
+  schur_slots<W, 0>(acc, X, wop, (nu - W + kSchurCWaves - 1) / kSchurCWaves);
+}
+
+// Operands of point t of the batch (point table pv, one point per lane: {.., .., xoff, jhi}; t >= npts: none):
+// every operand column the wave may use, X_j[lane i + 16 k] = E_p[k][16 j + i] at xoff + 64 j (reads past the
+// point's tiles land in the next point or the buffer's padding and feed only skipped slots), and the w operand
+// (lanes 16 k hold w_k).
+template <unsigned kNeed>
+__device__ __forceinline__ void schur_fetch(const double* Xb, const double* wsh, const int4& pv, int t, int npts,
+                                            int lane, double (&X)[kSchurTW], double& wop, int& jhi) {
+  const int tt = min(t, npts - 1);
+  jhi = t < npts ? __builtin_amdgcn_readlane(pv.w, tt) : -1;
+  const double* xp = Xb + __builtin_amdgcn_readlane(pv.z, tt) + lane;
+#pragma unroll
+  for (int j = 0; j < kSchurTW; ++j)
+    if ((kNeed >> j) & 1u) X[j] = xp[64 * j];
+  const double wv = wsh[4 * tt + (lane >> 4)];
+  wop = (lane & 15) == 0 ? wv : 0.0;
+}
+// The wave's work on one batch (whole wave active: the point table is read by v_readlane): the operands of
+// point t + 1 are read before the MFMAs of point t.
+template <int W>
+__device__ __forceinline__ void schur_wave_batch(f64x4 (&acc)[kSchurTPW], const double* Xb, const double* wsh,
+                                                 const int4* pinf, int npts, int lane) {
+  constexpr unsigned kNeed = schur_need(W);
+  const int4 pv = pinf[min(lane, npts - 1)];   // npts <= 64
+  double XA[kSchurTW], XB[kSchurTW];
+#pragma unroll
+  for (int j = 0; j < kSchurTW; ++j) XA[j] = XB[j] = 0.0;
+  double wa, wb;
+  int ha, hb;
+  schur_fetch<kNeed>(Xb, wsh, pv, 0, npts, lane, XA, wa, ha);
+  for (int t = 0; t < npts; t += 2) {
+    schur_fetch<kNeed>(Xb, wsh, pv, t + 1, npts, lane, XB, wb, hb);
+    schur_mfma<W>(acc, XA, wa, ha);
+    schur_fetch<kNeed>(Xb, wsh, pv, t + 2, npts, lane, XA, wa, ha);
+    schur_mfma<W>(acc, XB, wb, hb);
+  }
+}
+
+// Slab of a segment: its ntw (ntw + 1) / 2 window tiles (row-major 16x16, column-major upper order), then the
+// rhs of its 16 ntw window columns.  The accumulators must be drained (mfma_drain) first.
+template <int W>
+__device__ __forceinline__ void schur_store(const f64x4 (&acc)[kSchurTPW], double* slab, int ntw, int lane) {
+  const int ntile = ntw * (ntw + 1) / 2;
+#pragma unroll
+  for (int S = 0; S < kSchurTPW; ++S) {
+    const int u = W + kSchurCWaves * S;
+    if (u >= kSchurAug) break;
+    const int c = schur_aug_c(u), r = schur_aug_r(u);
+    if (c >= ntw) continue;
+    if (r <= c) {
+      double* t = slab + 256 * schur_tile_index(r, c) + lane;   // element (lk + 4 q, li) at 16 lk + li + 64 q
+#pragma unroll
+      for (int q = 0; q < 4; ++q) t[64 * q] = -acc[S][q];
+    } else if ((lane & 15) == 0) {
+      // column 0 of E_c^T w: lanes 16 k hold window rows 16 c + k + 4 q
+#pragma unroll
+      for (int q = 0; q < 4; ++q) slab[256 * ntile + 16 * c + (lane >> 4) + 4 * q] = -acc[S][q];
+    }
+  }
+}
+
+}  // namespace sg
+
+#endif  // SG_SCHUR_TILES_H_
