@@ -48,8 +48,9 @@ enum CholX { kCStep2 = 0, kCCandX2, kCModel, kCCandCost, kCFail, kCNum };
 
 
 // k_schur work decomposition (see ba_solver.hip): a segment is a run of consecutive points (device order)
-// whose camera columns fit a window of <= kSchurTW 16-column tiles of S, one 8-wave workgroup (4 waves holding
-// the window's upper tiles and rhs rows in MFMA accumulators, 4 building the operand tiles); it streams through
+// whose camera columns fit a window of <= kSchurTW 16-column tiles of S, one workgroup (kSchurCWaves waves holding
+// the window's upper tiles and rhs rows in MFMA accumulators, a point wave, kSchurCellWaves building the
+// operand tiles); it streams through
 // LDS in batches of <= kSchurBatchPts points whose operand tiles (64 doubles each) fit kSchurXCap.  The cells
 // of a point (one per block of its span) carry its observations.  A point spanning more than kSegNbMax blocks
 // is a WideSeg of its own (observation pairs, global atomics).
@@ -57,15 +58,18 @@ enum CholX { kCStep2 = 0, kCCandX2, kCModel, kCCandCost, kCFail, kCNum };
 #define SG_SEG_NB 24   // widest point of a segment, in blocks (6 * 24 + 14 <= 16 * kSchurTW columns)
 #endif
 constexpr int kSegNbMax = SG_SEG_NB;
-constexpr int kSchurThreads = 512;
-constexpr int kSchurWaves = kSchurThreads / 64;
+static_assert(kSegNbMax <= 24, "cells of a batch: kSchurBatchCells");
+constexpr int kSchurCellWaves = 3;   // operand-tile waves (a batch has <= 64 kSchurCellWaves cells)
+constexpr int kSchurCWaves = 4;      // MFMA waves (one per SIMD); a point wave between the two groups
+constexpr int kSchurWaves = kSchurCellWaves + 1 + kSchurCWaves;
+constexpr int kSchurThreads = 64 * kSchurWaves;
 constexpr int kSchurTW = 10;
 constexpr int kSchurTiles = kSchurTW * (kSchurTW + 1) / 2;
-constexpr int kSchurCWaves = kSchurWaves / 2;   // MFMA (consumer) waves; the other half builds the cells
 constexpr int kSchurAug = kSchurTiles + kSchurTW;   // window tiles + one rhs tile per tile row
 constexpr int kSchurTPW = (kSchurAug + kSchurCWaves - 1) / kSchurCWaves;   // accumulator tiles per wave
 constexpr int kSchurXCap = 112 * 64;   // operand tiles (64 doubles each) per batch buffer
 constexpr int kSchurBatchPts = 32;   // <= 64: a batch's point table is one point per lane
+constexpr int kSchurBatchCells = kSchurBatchPts * 24;   // cells of a batch (spans <= kSegNbMax)
 static_assert(6 * kSegNbMax + 14 <= 16 * kSchurTW, "a widest point must fit the tile window");
 struct SchurSeg {
   int32_t p0, p1;       // point range
@@ -208,7 +212,8 @@ struct Dev {
   const int2* pinfo;             // [P] first cell, (first block << 8) | span (0: no Schur terms)
   const int4* cells;             // [ncell] first observation (-1: none), point, (block << 16) | number of
                                  // further observations, their offset in cell_obs
-  const int2* pmx;               // [P] operand offset in the point's batch buffer, last window tile (-1: none)
+  const int4* pmx;               // [P] operand offset in the batch buffer, last window tile (-1: none),
+                                 // observation of the first block (-1: use the cell records), first cell
   const int32_t* cell_obs;       // second and later observations of a cell
   const struct WideSeg* wsegs;   // [nwide] points wider than a segment window
   int32_t nwide;

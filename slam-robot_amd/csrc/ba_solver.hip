@@ -742,57 +742,61 @@ __device__ __forceinline__ bool point_block(const Dev& d, const LmState* st, int
   return ok;
 }
 
-// The segment's batches run as a software pipeline over two wave groups, one LDS barrier per step:
-//   producers (waves 0-3), step s: the operand tiles of batch s (buffer s % 2), then the point blocks of batch
-//            s + 1 (point slot (s + 1) % 3);
-//   consumers (waves 4-7), step s: the MFMAs of batch s - 1 (buffer (s - 1) % 2, point slot (s - 1) % 3).
-// The two groups run separate loops with the same barrier count, so the accumulators are not live in the
-// producer code.
+// The segment's batches run as a software pipeline over three wave groups, one LDS barrier per step:
+//   cell waves (kSchurCellWaves), step s: the operand tiles of batch s (buffer s % 2);
+//   the point wave, step s: the point blocks of batch s + 1 (point slot (s + 1) % 3);
+//   MFMA waves (kSchurCWaves), step s: batch s - 1 (buffer (s - 1) % 2, point slot (s - 1) % 3).
+// The groups run separate loops with the same barrier count, so the accumulators are not live elsewhere.
 struct SchurLds {
   double X[2][kSchurXCap + 64 * kSchurTW];   // operand tiles of the batch's points; padding for over-reads
   double L[3][kSchurBatchPts * 10];          // L^-1 of the batch's points
   double w[3][kSchurBatchPts * 4];           // w = L^-1 g~
   int4 pinf[3][kSchurBatchPts];              // first block, span, operand offset, last window tile (jhi)
+  int2 pob[3][kSchurBatchPts];               // observation of its first block (-1: cell records), first cell
+  uint8_t cmap[3][kSchurBatchCells];         // batch-local cell -> point
   double red[kSchurThreads / 64];
 };
 
-// 1. thread per point of batch B (tid < npts)
-__device__ __forceinline__ double schur_points(const Dev& d, const LmState* st, const SchurBatch& B, int tid,
-                                               double* Lsh, double* wsh, int4* pinf) {
-  if (tid >= B.p1 - B.p0) return 0.0;
-  const int p = B.p0 + tid;
+// Point wave, thread t < npts of batch B: its point block, table entries and cell map.
+__device__ __forceinline__ double schur_points(const Dev& d, const LmState* st, const SchurBatch& B, int t,
+                                               double* Lsh, double* wsh, int4* pinf, int2* pob, uint8_t* cmap) {
+  if (t >= B.p1 - B.p0) return 0.0;
+  const int p = B.p0 + t;
   const int2 pi = d.pinfo[p];
-  const int2 pm = d.pmx[p];
+  const int4 pm = d.pmx[p];   // operand offset, jhi, observation of the first block (-1), first cell
   int span = pi.y & 0xff, jhi = pm.y;
   double fail = 0.0;
   if (d.pfree[p]) {
     double Vi[10], Li[10], w[4];
     if (!point_block(d, st, p, Vi, Li, w)) fail = 1.0;
 #pragma unroll
-    for (int i = 0; i < 10; ++i) Lsh[10 * tid + i] = Li[i];
+    for (int i = 0; i < 10; ++i) Lsh[10 * t + i] = Li[i];
 #pragma unroll
-    for (int a = 0; a < 4; ++a) wsh[4 * tid + a] = w[a];
+    for (int a = 0; a < 4; ++a) wsh[4 * t + a] = w[a];
   } else {
     span = 0;
     jhi = -1;
   }
-  pinf[tid] = make_int4(pi.y >> 8, span, pm.x, jhi);
+  pinf[t] = make_int4(pi.y >> 8, span, pm.x, jhi);
+  pob[t] = make_int2(pm.z, pm.w);
+  for (int k = 0; k < span; ++k) cmap[pm.w + k] = (uint8_t)t;
   return fail;
 }
 
-// 2. thread per cell (point p, block b) of batch B: E_{p,b} = sum_o G_o J~c,o with G_o = L^-1 J~p,o^T (4 x 2),
-// written straight into the point's operand tiles: column c = 6 b + a - c0w of the window goes to tile c >> 4,
-// lane (c & 15) + 16 k.  The first and last cell of a point also zero the columns of its tiles 0 .. jhi outside
-// its span.
+// Cell waves: thread per cell (point p, block b) of batch B.  E_{p,b} = sum_o G_o J~c,o with
+// G_o = L^-1 J~p,o^T (4 x 2), written straight into the point's operand tiles: window column c = 6 b + a - c0w
+// goes to tile c >> 4, lane (c & 15) + 16 k.  A point observed once in every block of its span (obs sorted by
+// block at load) finds its observation at a fixed offset; others read the cell records.  The first and last
+// cell of a point also zero the columns of its tiles 0 .. jhi outside its span.
 __device__ __forceinline__ void schur_cells(const Dev& d, const SchurBatch& B, int tid, int c0w, const double* Lsh,
-                                            const double* wsh, const int4* pinf, double* Xb) {
-  (void)wsh;
-  for (int c = B.c0 + tid; c < B.c1; c += kSchurThreads / 2) {
-    const int4 ci = d.cells[c];   // first observation (-1: none), point, (block << 16) | further, their offset
-    const int lp = ci.y - B.p0;
-    const int4 pi = pinf[lp];
-    const int b = (int)((unsigned)ci.z >> 16), k1 = ci.w, k2 = ci.w + (ci.z & 0xffff);
-    const double* L = Lsh + 10 * lp;
+                                            const int4* pinf, const int2* pob, const uint8_t* cmap, double* Xb) {
+  const int ncell = B.c1 - B.c0;
+  for (int lc = tid; lc < ncell; lc += 64 * kSchurCellWaves) {
+    const int t = cmap[lc];
+    const int4 pi = pinf[t];
+    const int2 po = pob[t];
+    const int b = pi.x + (lc - po.y);
+    const double* L = Lsh + 10 * t;
     double* xp = Xb + pi.z;
     const int col0 = 6 * b - c0w;
     auto at = [&](int col, int k) -> double& { return xp[64 * (col >> 4) + 16 * k + (col & 15)]; };
@@ -804,18 +808,26 @@ __device__ __forceinline__ void schur_cells(const Dev& d, const SchurBatch& B, i
       for (int col = col0 + 6; col < 16 * (pi.w + 1); ++col)
 #pragma unroll
         for (int k = 0; k < 4; ++k) at(col, k) = 0.0;
-    if (ci.x < 0) {
+    int o0, k1 = 0, k2 = 0;
+    if (po.x >= 0) {
+      o0 = po.x + (b - pi.x);
+    } else {
+      const int4 ci = d.cells[B.c0 + lc];   // first observation (-1: none), point, (block << 16) | further, offset
+      o0 = ci.x;
+      k1 = ci.w;
+      k2 = ci.w + (ci.z & 0xffff);
+    }
+    if (o0 < 0) {
 #pragma unroll
       for (int a = 0; a < 6; ++a)
 #pragma unroll
         for (int k = 0; k < 4; ++k) at(col0 + a, k) = 0.0;
       continue;
     }
-    const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[ci.y];
-    const int k0 = k1 - 1;
+    const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[B.p0 + t];
 #pragma unroll 1
-    for (int k = k0; k < k2; ++k) {
-      const int o = k < k1 ? ci.x : d.cell_obs[k];
+    for (int k = k1 - 1; k < k2; ++k) {
+      const int o = k < k1 ? o0 : d.cell_obs[k];
       double G[4][2];
       {
         double Jp[8];
@@ -834,7 +846,7 @@ __device__ __forceinline__ void schur_cells(const Dev& d, const SchurBatch& B, i
       }
       double Jc[12];
       load_Jc_scaled(d, o, b, Jc);
-      if (k == k0) {
+      if (k < k1) {
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
@@ -849,10 +861,10 @@ __device__ __forceinline__ void schur_cells(const Dev& d, const SchurBatch& B, i
   }
 }
 
-// Diagnostic stamps (SG_STAMP=1): workgroup 0, lane 0 of waves 0 (producer, slots 32-39) and 4 (consumer,
-// slots 40-47) accumulate s_memtime deltas per phase.
+// Diagnostic stamps (SG_STAMP=1): workgroup 0, lane 0 of the first cell wave (slots 32-36), the point wave
+// (35, 37) and the first MFMA wave (40-45) accumulate s_memtime deltas per phase.
 #define SG_SSTAMP(slot)                                                                  \
-  if (d.stamps && blockIdx.x == 0 && lane == 0 && (wave & 3) == 0) {                     \
+  if (d.stamps && blockIdx.x == 0 && lane == 0 && (wave == 0 || wave == kSchurCellWaves || wave == kSchurCellWaves + 1)) { \
     const unsigned long long now_ = __builtin_amdgcn_s_memtime();                       \
     d.stamps[(slot)] += now_ - last_;                                                    \
     last_ = now_;                                                                        \
@@ -868,27 +880,35 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d) {
   const int c0w = 16 * sg.t0;
   double* slab = d.S_slab + sg.s_off;
   double linfail = 0.0;
-  if (wave < kSchurWaves / 2) {
-    // producers
-    if (nbt > 0) linfail += schur_points(d, st, d.sbatch[sg.bt0], tid, sh.L[0], sh.w[0], sh.pinf[0]);
+  if (wave < kSchurCellWaves) {
     SG_SSTAMP(32)
     __syncthreads();
     SG_SSTAMP(33)
     for (int s = 0; s <= nbt; ++s) {
       if (s < nbt)
-        schur_cells(d, d.sbatch[sg.bt0 + s], tid, c0w, sh.L[s % 3], sh.w[s % 3], sh.pinf[s % 3], sh.X[s & 1]);
+        schur_cells(d, d.sbatch[sg.bt0 + s], tid, c0w, sh.L[s % 3], sh.pinf[s % 3], sh.pob[s % 3], sh.cmap[s % 3],
+                    sh.X[s & 1]);
       SG_SSTAMP(34)
-      if (s + 1 < nbt) {
-        const int q = (s + 1) % 3;
-        linfail += schur_points(d, st, d.sbatch[sg.bt0 + s + 1], tid, sh.L[q], sh.w[q], sh.pinf[q]);
-      }
-      SG_SSTAMP(35)
       __syncthreads();
       SG_SSTAMP(36)
     }
+  } else if (wave == kSchurCellWaves) {
+    // the point wave
+    if (nbt > 0) linfail += schur_points(d, st, d.sbatch[sg.bt0], lane, sh.L[0], sh.w[0], sh.pinf[0], sh.pob[0], sh.cmap[0]);
+    __syncthreads();
+    for (int s = 0; s <= nbt; ++s) {
+      if (s + 1 < nbt) {
+        const int q = (s + 1) % 3;
+        linfail += schur_points(d, st, d.sbatch[sg.bt0 + s + 1], lane, sh.L[q], sh.w[q], sh.pinf[q], sh.pob[q],
+                                sh.cmap[q]);
+      }
+      SG_SSTAMP(35)
+      __syncthreads();
+      SG_SSTAMP(37)
+    }
   } else {
-    // consumers: wave cw owns the augmented window slots u = cw + 4 s
-    const int cw = wave - kSchurWaves / 2;
+    // MFMA waves: wave cw owns the augmented window slots u = cw + kSchurCWaves s
+    const int cw = wave - kSchurCellWaves - 1;
     f64x4 acc[kSchurTPW];
 #pragma unroll
     for (int s = 0; s < kSchurTPW; ++s) acc[s] = f64x4{0.0, 0.0, 0.0, 0.0};
@@ -3081,6 +3101,13 @@ void BaSolver::Load(const sg_problem& p) {
   {
     std::vector<int32_t> fill(poff.begin(), poff.end() - 1);
     for (int o = 0; o < M_; ++o) obs_perm_[fill[inv_perm[p.obs_point[o]]]++] = o;
+    // within a point: observations of constant frames first, then by camera block (stable), so that a point
+    // observed once in every block of its span finds the observation of block b at a fixed offset (k_schur)
+    if (!getenv("SG_NO_OBS_SORT"))
+    for (int i = 0; i < P_; ++i)
+      std::stable_sort(obs_perm_.begin() + poff[i], obs_perm_.begin() + poff[i + 1], [&](int a, int b) {
+        return frame_block[p.obs_frame[a]] < frame_block[p.obs_frame[b]];
+      });
   }
   std::vector<double> obs_pt(2 * (size_t)M_);
   std::vector<int32_t> obs_frame(M_);
@@ -3210,7 +3237,8 @@ void BaSolver::Load(const sg_problem& p) {
     const int pt = point_perm_[i];
     return (pfree[i] && pfirst[pt] < NB_) ? plast[pt] - pfirst[pt] + 1 : 0;
   };
-  std::vector<int32_t> pinfo(2 * (size_t)std::max(P_, 1), 0), pmx(2 * (size_t)std::max(P_, 1), 0), cells, cell_obs;
+  std::vector<int32_t> pinfo(2 * (size_t)std::max(P_, 1), 0), pmx(4 * (size_t)std::max(P_, 1), 0), cells, cell_obs;
+  std::vector<int32_t> simple_obs(std::max(P_, 1), -1);   // observation of the first block if one per block
   int ncell = 0;
   std::vector<SchurSeg> segs;
   std::vector<SchurBatch> sbatch;
@@ -3233,6 +3261,11 @@ void BaSolver::Load(const sg_problem& p) {
       for (int o = poff[i]; o < poff[i + 1]; ++o)
         if (obs_blk[o] >= 0) bo.emplace_back(obs_blk[o], o);
       std::sort(bo.begin(), bo.end());
+      {
+        bool one = (int)bo.size() == sp;   // observations sorted by block at load: consecutive
+        for (int q = 0; one && q < sp; ++q) one = bo[q].first == pf + q && bo[q].second == bo[0].second + q;
+        if (one) simple_obs[i] = bo[0].second;
+      }
       size_t k = 0;
       for (int b = pf; b < pf + sp; ++b) {
         // {first observation or -1, point, (block << 16) | further observations, their offset in cell_obs}
@@ -3316,9 +3349,12 @@ void BaSolver::Load(const sg_problem& p) {
         B.p0 = k;
         B.c0 = cnext;
         int nc = 0, nx = 0;
-        while (k < j && k - B.p0 < kSchurBatchPts && nx + 64 * (pjhi(k) + 1) <= kSchurXCap) {
-          pmx[2 * k] = nx;
-          pmx[2 * k + 1] = pjhi(k);
+        while (k < j && k - B.p0 < kSchurBatchPts && nx + 64 * (pjhi(k) + 1) <= kSchurXCap &&
+               nc + sspan(k) <= 64 * kSchurCellWaves) {
+          pmx[4 * k] = nx;
+          pmx[4 * k + 1] = pjhi(k);
+          pmx[4 * k + 2] = simple_obs[k];
+          pmx[4 * k + 3] = nc;
           nx += 64 * (pjhi(k) + 1);
           schur_mfma_ += schur_aug_base(pjhi(k) + 1);
           nc += sspan(k++);
@@ -3774,7 +3810,7 @@ Dev BaSolver::MakeDev() {
   d.nseg = nseg_;
   d.sbatch = sbatch_.ptr;
   d.pinfo = reinterpret_cast<const int2*>(pinfo_.ptr);
-  d.pmx = reinterpret_cast<const int2*>(pmx_.ptr);
+  d.pmx = reinterpret_cast<const int4*>(pmx_.ptr);
   d.cells = reinterpret_cast<const int4*>(cells_.ptr);
   d.cell_obs = cell_obs_.ptr;
   d.wsegs = wsegs_.ptr;

@@ -46,8 +46,9 @@ __host__ __device__ constexpr unsigned schur_need(int W) {
 // acc += A B with the accumulator tied in place.  A conditionally executed __builtin_amdgcn_mfma leaves the old
 // accumulator live beside the new one (a PHI), so the compiler picks the untied form and copies the
 // accumulators around every MFMA; the tied asm form keeps them in place.  The compiler does not see this as an
-// MFMA: the s_nop covers a VALU write -> MFMA read of an operand (2 wait states), and readers of the
-// accumulators must first call mfma_drain().  MFMA -> MFMA on the same accumulator is interlocked.
+// MFMA, so the hazards are ours: the s_nop covers a VALU write -> MFMA read of an operand (2 wait states; the
+// compiler may place a register copy of an operand right before the asm), and readers of the accumulators
+// must first call mfma_drain().  MFMA -> MFMA on the same accumulator is interlocked.
 __device__ __forceinline__ void mfma_acc(f64x4& acc, double a, double b) {
   asm volatile("s_nop 1\n\tv_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
 }
