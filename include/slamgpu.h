@@ -250,6 +250,10 @@ int sg_slam_reproject_map(sg_slam* s, sg_map* map, double* mean);               
 int32_t sg_slam_iterations(const sg_slam* s);                                    /* slam.h:49 */
 double sg_slam_error(const sg_slam* s);                                          /* slam.h:50 */
 int sg_slam_load_counts(const sg_slam* s, int32_t* full_loads, int32_t* value_loads);   /* see sg_ba_load_counts */
+/* Host wall time (ms) of the last SolveFrames / SolveAllFrames call by phase: [0] SetupProblem (problem build),
+ * [1] sg_ba_load (work lists + upload), [2] device LM loop incl. download, [3] write-back into the map.
+ * A development aid for sizing the host share of a real call (tools/e2e_timing.py). */
+int sg_slam_last_phase_ms(const sg_slam* s, double* ms4);
 int sg_slam_last_summary(const sg_slam* s, sg_solver_summary* out);
 
 /* ------------------------------------------------------------------------------------------------

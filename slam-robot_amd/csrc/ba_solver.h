@@ -61,6 +61,9 @@ class BaSolver {
   bool pack_force_ = getenv("SG_PACK_S") != nullptr;   // pack/unpack S on one rank too (tests the path)
   size_t npack_ = 0;                                      // band of S + rhs, doubles (all-reduce size)
   bool stamp_on_ = false;
+  int ncu_ = 256;                       // compute units (Schur segment count), queried once
+  size_t tile_lds_set_ = 0;             // dynamic LDS last granted to k_chol_tiles
+  std::unique_ptr<class Stager> stager_;   // batched structure uploads (stager.h)
   DBuf<unsigned long long> stamps_;
 
  public:

@@ -31,6 +31,7 @@
 #include <numeric>
 
 #include "ba_solver.h"
+#include "stager.h"
 #include "comm.h"
 #include "project_math.h"
 #include "schur_tiles.h"
@@ -2959,6 +2960,16 @@ BaSolver::BaSolver(const sg_device_options& dev) : dev_(dev) {
              "sg_device_options.precision: only 0 (fp64, the reference's arithmetic) is implemented");
   SG_HIP_CHECK(hipSetDevice(dev.device));
   SG_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev.device) == hipSuccess && prop.multiProcessorCount > 0)
+      ncu_ = prop.multiProcessorCount;
+  }
+  stager_.reset(new Stager());
+  SG_HIP_CHECK(hipFuncSetAttribute((const void*)k_cholesky_window<false>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCholLds));
+  SG_HIP_CHECK(hipFuncSetAttribute((const void*)k_cholesky_window<true>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCholLds));
   st_.Resize(1);
   timers_.resize(kKNum);
   for (int i = 0; i < kKNum; ++i) timers_[i].name = kKernelNames[i];
@@ -3052,6 +3063,7 @@ void BaSolver::Load(const sg_problem& p) {
   loaded_ = false;
   began_ = false;
   skey_ = StructKey{};
+  stager_->Clear();
   F_ = p.num_frames;
   P_ = p.num_points;
   M_ = p.num_obs;
@@ -3103,11 +3115,29 @@ void BaSolver::Load(const sg_problem& p) {
     for (int o = 0; o < M_; ++o) obs_perm_[fill[inv_perm[p.obs_point[o]]]++] = o;
     // within a point: observations of constant frames first, then by camera block (stable), so that a point
     // observed once in every block of its span finds the observation of block b at a fixed offset (k_schur)
+    // (a stable insertion sort: a point has a handful of observations, and std::stable_sort allocates a
+    // buffer per call)
     if (!getenv("SG_NO_OBS_SORT"))
-    for (int i = 0; i < P_; ++i)
-      std::stable_sort(obs_perm_.begin() + poff[i], obs_perm_.begin() + poff[i + 1], [&](int a, int b) {
-        return frame_block[p.obs_frame[a]] < frame_block[p.obs_frame[b]];
-      });
+      for (int i = 0; i < P_; ++i) {
+        int32_t* v = obs_perm_.data() + poff[i];
+        const int k = poff[i + 1] - poff[i];
+        if (k > 64) {
+          std::stable_sort(v, v + k, [&](int a, int b) {
+            return frame_block[p.obs_frame[a]] < frame_block[p.obs_frame[b]];
+          });
+          continue;
+        }
+        for (int x = 1; x < k; ++x) {
+          const int32_t o = v[x];
+          const int key = frame_block[p.obs_frame[o]];
+          int y = x - 1;
+          while (y >= 0 && frame_block[p.obs_frame[v[y]]] > key) {
+            v[y + 1] = v[y];
+            --y;
+          }
+          v[y + 1] = o;
+        }
+      }
   }
   std::vector<double> obs_pt(2 * (size_t)M_);
   std::vector<int32_t> obs_frame(M_);
@@ -3260,7 +3290,7 @@ void BaSolver::Load(const sg_problem& p) {
       bo.clear();
       for (int o = poff[i]; o < poff[i + 1]; ++o)
         if (obs_blk[o] >= 0) bo.emplace_back(obs_blk[o], o);
-      std::sort(bo.begin(), bo.end());
+      if (!std::is_sorted(bo.begin(), bo.end())) std::sort(bo.begin(), bo.end());   // sorted at load already
       {
         bool one = (int)bo.size() == sp;   // observations sorted by block at load: consecutive
         for (int q = 0; one && q < sp; ++q) one = bo[q].first == pf + q && bo[q].second == bo[0].second + q;
@@ -3284,12 +3314,7 @@ void BaSolver::Load(const sg_problem& p) {
   {
     // points per segment: one segment per CU (the workgroup's LDS holds one per CU; fewer, longer segments
     // write fewer partial tiles and keep the producer/consumer pipeline full; SG_SCHUR_SEGS: tuning)
-    int ncu = 256;
-    {
-      hipDeviceProp_t prop;
-      if (hipGetDeviceProperties(&prop, dev_.device) == hipSuccess && prop.multiProcessorCount > 0)
-        ncu = prop.multiProcessorCount;
-    }
+    const int ncu = ncu_;
     const int target = getenv("SG_SCHUR_SEGS") ? std::max(1, atoi(getenv("SG_SCHUR_SEGS"))) : ncu;
     const int maxpts = std::max(16, (P_ + target - 1) / target);
     int cnext = 0;
@@ -3468,7 +3493,7 @@ void BaSolver::Load(const sg_problem& p) {
     for (int pk = 0; pk < npanel; ++pk)
       off[pk + 1] = off[pk] + std::min(kCholNb, n_ - pk * kCholNb) * (panel_jmax[pk] - pk * kCholNb);
     npack_ = (size_t)off[npanel] + n_;
-    pack_off_.Upload(off, stream_);
+    stager_->Add(pack_off_, off);
     Spk_.Resize(std::max<size_t>(npack_, 1));
   }
   chol_window_ = npanel <= kJendSh;   // band ends cached in LDS
@@ -3484,7 +3509,7 @@ void BaSolver::Load(const sg_problem& p) {
   if (chol_tiles_) {
     std::vector<double> wz((size_t)npanel * kTB * 256 + 2, 0.0);   // W tiles, then the constants {0, 1}
     wz.back() = 1.0;
-    Wg_.Upload(wz, stream_);
+    stager_->Add(Wg_, wz);
     tile_lds_ = (size_t)npanel * 32 * sizeof(double) + (size_t)npanel * sizeof(int32_t);
   }
   // k_S_reduce work: the band tiles (R <= C) of the frame columns, and per tile the segment tiles covering it
@@ -3513,13 +3538,14 @@ void BaSolver::Load(const sg_problem& p) {
     if (s_lidx.empty()) s_lidx.push_back(0);
   }
   lap("envelope");
-  // device uploads
+  // device uploads: one pinned staging copy and one scatter launch (stager.h)
   hipStream_t s = stream_;
+  Stager& stg = *stager_;
   {
     std::vector<double> k2(14 * (size_t)ncam_);
     std::copy(p.k, p.k + 7 * ncam_, k2.begin());
     std::copy(p.k, p.k + 7 * ncam_, k2.begin() + 7 * ncam_);
-    k_.Upload(k2.empty() ? std::vector<double>{0.0} : k2, s);
+    stg.Add(k_, k2.empty() ? std::vector<double>{0.0} : k2);
   }
   std::vector<double> q2(8 * (size_t)F_), t2(6 * (size_t)F_), X2(8 * (size_t)P_);
   std::copy(p.q, p.q + 4 * F_, q2.begin());
@@ -3528,45 +3554,45 @@ void BaSolver::Load(const sg_problem& p) {
   std::copy(p.t, p.t + 3 * F_, t2.begin() + 3 * F_);
   std::copy(X.begin(), X.end(), X2.begin());
   std::copy(X.begin(), X.end(), X2.begin() + 4 * P_);
-  q_.Upload(q2, s);
-  t_.Upload(t2, s);
-  X_.Upload(X2, s);
-  frame_cam_.Upload(std::vector<int32_t>(p.frame_camera, p.frame_camera + F_), s);
-  frame_block_.Upload(frame_block, s);
-  rot_free_.Upload(std::vector<uint8_t>(p.frame_rot_free, p.frame_rot_free + F_), s);
-  trans_free_.Upload(std::vector<uint8_t>(p.frame_trans_free, p.frame_trans_free + F_), s);
-  pfree_.Upload(pfree, s);
-  poff_.Upload(poff, s);
-  obs_pt_.Upload(obs_pt, s);
-  obs_frame_.Upload(obs_frame, s);
-  obs_fixed_.Upload(obs_fixed, s);
-  obs_meta_.Upload(obs_meta.empty() ? std::vector<int32_t>{0} : obs_meta, s);
-  lchunks_d_.Upload(lchunks, s);
-  lrounds_d_.Upload(lrounds, s);
+  stg.Add(q_, q2);
+  stg.Add(t_, t2);
+  stg.Add(X_, X2);
+  stg.Add(frame_cam_, std::vector<int32_t>(p.frame_camera, p.frame_camera + F_));
+  stg.Add(frame_block_, frame_block);
+  stg.Add(rot_free_, std::vector<uint8_t>(p.frame_rot_free, p.frame_rot_free + F_));
+  stg.Add(trans_free_, std::vector<uint8_t>(p.frame_trans_free, p.frame_trans_free + F_));
+  stg.Add(pfree_, pfree);
+  stg.Add(poff_, poff);
+  stg.Add(obs_pt_, obs_pt);
+  stg.Add(obs_frame_, obs_frame);
+  stg.Add(obs_fixed_, obs_fixed);
+  stg.Add(obs_meta_, obs_meta.empty() ? std::vector<int32_t>{0} : obs_meta);
+  stg.Add(lchunks_d_, lchunks);
+  stg.Add(lrounds_d_, lrounds);
   if (llist.empty()) llist.push_back(0);
-  llist_d_.Upload(llist, s);
-  obs_pnt_.Upload(obs_pnt.empty() ? std::vector<int32_t>{0} : obs_pnt, s);
-  segs_.Upload(segs.empty() ? std::vector<SchurSeg>(1) : segs, s);
-  sbatch_.Upload(sbatch.empty() ? std::vector<SchurBatch>(1) : sbatch, s);
-  wsegs_.Upload(wsegs.empty() ? std::vector<WideSeg>(1) : wsegs, s);
-  pinfo_.Upload(pinfo, s);
-  pmx_.Upload(pmx, s);
-  cells_.Upload(cells, s);
-  cell_obs_.Upload(cell_obs, s);
-  stile_.Upload(stile, s);
-  pairs_.Upload(pairs_flat, s);
+  stg.Add(llist_d_, llist);
+  stg.Add(obs_pnt_, obs_pnt.empty() ? std::vector<int32_t>{0} : obs_pnt);
+  stg.Add(segs_, segs.empty() ? std::vector<SchurSeg>(1) : segs);
+  stg.Add(sbatch_, sbatch.empty() ? std::vector<SchurBatch>(1) : sbatch);
+  stg.Add(wsegs_, wsegs.empty() ? std::vector<WideSeg>(1) : wsegs);
+  stg.Add(pinfo_, pinfo);
+  stg.Add(pmx_, pmx);
+  stg.Add(cells_, cells);
+  stg.Add(cell_obs_, cell_obs);
+  stg.Add(stile_, stile);
+  stg.Add(pairs_, pairs_flat);
   seg_fail_.Resize(std::max(nseg_ + nwide_, 1));
-  cam_loff_.Upload(cam_loff, s);
-  cam_lidx_.Upload(cam_lidx, s);
-  s_loff_.Upload(s_loff, s);
-  s_lidx_.Upload(s_lidx, s);
-  r_loff_.Upload(r_loff, s);
-  r_lidx_.Upload(r_lidx, s);
-  fd_a_.Upload(fd_a, s);
-  fd_b_.Upload(fd_b, s);
-  fd_boff_.Upload(fd_boff, s);
-  fd_bidx_.Upload(fd_bidx.empty() ? std::vector<int32_t>{0} : fd_bidx, s);
-  work_i_.Upload(panel_jmax, s);
+  stg.Add(cam_loff_, cam_loff);
+  stg.Add(cam_lidx_, cam_lidx);
+  stg.Add(s_loff_, s_loff);
+  stg.Add(s_lidx_, s_lidx);
+  stg.Add(r_loff_, r_loff);
+  stg.Add(r_lidx_, r_lidx);
+  stg.Add(fd_a_, fd_a);
+  stg.Add(fd_b_, fd_b);
+  stg.Add(fd_boff_, fd_boff);
+  stg.Add(fd_bidx_, fd_bidx.empty() ? std::vector<int32_t>{0} : fd_bidx);
+  stg.Add(work_i_, panel_jmax);
   {
     // FrameDistance cross-block lookup for the on-the-fly assembly: fd_pair[I*NB+J] (I<J) = residual
     std::vector<int32_t> fd_pair((size_t)std::max(NB_, 1) * std::max(NB_, 1), -1);
@@ -3574,7 +3600,7 @@ void BaSolver::Load(const sg_problem& p) {
       const int ba = frame_block[fd_a[dd]], bb = frame_block[fd_b[dd]];
       if (ba >= 0 && bb >= 0 && ba != bb) fd_pair[(size_t)std::min(ba, bb) * NB_ + std::max(ba, bb)] = dd;
     }
-    fd_pair_.Upload(fd_pair, s);
+    stg.Add(fd_pair_, fd_pair);
     rdg_.Resize((size_t)std::max(n_, 1) + kCholNb);   // + padding rows of the last panel
   }
   J_.Resize((size_t)std::max(M_, 1) * kJStride);
@@ -3593,7 +3619,8 @@ void BaSolver::Load(const sg_problem& p) {
   lin_scal_.Resize((size_t)std::max(nlin_, 1) * kNScal);
   S_slab_.Resize(std::max(s_off, 1));
   chunk_scal_.Resize((size_t)std::max(npu_, 1) * kNScal);
-  pu_units_.Upload(pu_units, s);
+  stg.Add(pu_units_, pu_units);
+  stg.Flush(s);
   cam_wide_.Resize((size_t)std::max(NB_, 1) * kCamV);
   S_wide_.Resize(nn * nn);
   xchg_cam_.Resize((size_t)NB_ * kCamV + kXNum + nranks());
@@ -3614,13 +3641,11 @@ void BaSolver::Load(const sg_problem& p) {
   stamp_on_ = getenv("SG_STAMP") && getenv("SG_STAMP")[0] == '1';
   if (stamp_on_) stamps_.Resize(64);
   ResetState(s);
-  if (chol_tiles_)
+  if (chol_tiles_ && tile_lds_ > tile_lds_set_) {
     for (const void* f : {(const void*)k_chol_tiles<false>, (const void*)k_chol_tiles<true>})
       SG_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tile_lds_));
-  SG_HIP_CHECK(hipFuncSetAttribute((const void*)k_cholesky_window<false>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCholLds));
-  SG_HIP_CHECK(hipFuncSetAttribute((const void*)k_cholesky_window<true>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCholLds));
+    tile_lds_set_ = tile_lds_;
+  }
   SG_HIP_CHECK(hipStreamSynchronize(s));
   lap("uploads");
   SaveStructure(p);

@@ -29,6 +29,7 @@ struct sg_slam {
   int32_t iterations = 0;    // Slam::iterations_ (slam.cpp:517)
   double error = 0.0;        // Slam::error_ (slam.cpp:518)
   sg_solver_summary last{};
+  double phase_ms[4] = {0, 0, 0, 0};   // last SolveFrames / SolveAllFrames: setup, load, solve, write-back
 };
 
 extern "C" {
@@ -228,10 +229,13 @@ static void RunProblem(sg_slam* s, sg_problem* p, sg_map* map, const sg_solver_o
   s->solver->Solve(o, p, &sum);
   const auto t2 = now();
   if (sg_problem_write_back(p, map) != SG_OK) throw sg::Error(SG_EINVAL, sg_last_error());
-  if (timing) {
-    const auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-    fprintf(stderr, "[sg] load %.2f ms, solve %.2f ms, write-back %.2f ms\n", ms(t0, t1), ms(t1, t2), ms(t2, now()));
-  }
+  const auto t3 = now();
+  const auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+  s->phase_ms[1] = ms(t0, t1);
+  s->phase_ms[2] = ms(t1, t2);
+  s->phase_ms[3] = ms(t2, t3);
+  if (timing)
+    fprintf(stderr, "[sg] load %.2f ms, solve %.2f ms, write-back %.2f ms\n", ms(t0, t1), ms(t1, t2), ms(t2, t3));
   s->iterations += sum.num_iterations;   // iterations_ += summary.iterations.size()
   s->error = sum.final_cost;             // error_ = summary.final_cost
   s->last = sum;
@@ -245,8 +249,11 @@ int sg_slam_solve_frames(sg_slam* s, sg_map* map, int32_t num_to_solve, int32_t 
   *solved = 0;
   sg_problem p{};
   int32_t built = 0;
+  const auto ts = std::chrono::steady_clock::now();
   int rc = sg_problem_from_map_frames(map, num_to_solve, num_to_present, range, &p, &built);
   if (rc != SG_OK) return rc;
+  s->phase_ms[0] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts).count();
+  for (int i = 1; i < 4; ++i) s->phase_ms[i] = 0.0;
   if (!built) return SG_OK;   // "Slam aborted due to frame set too small": SolveFrames returns false
   try {
     RunProblem(s, &p, map, s->options, solved);   // Run(false)
@@ -264,8 +271,11 @@ int sg_slam_solve_all_frames(sg_slam* s, sg_map* map, double range, int32_t solv
   *solved = 0;
   sg_problem p{};
   int32_t built = 0;
+  const auto ts = std::chrono::steady_clock::now();
   int rc = sg_problem_from_map_all(map, range, solve_cameras, &p, &built);
   if (rc != SG_OK) return rc;
+  s->phase_ms[0] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts).count();
+  for (int i = 1; i < 4; ++i) s->phase_ms[i] = 0.0;
   if (!built) return SG_OK;
   sg_solver_options o = s->options;
   if (solve_cameras) o.function_tolerance = 1e-9;   // Run(fine = solve_cameras), slam.cpp:496-499
@@ -276,6 +286,13 @@ int sg_slam_solve_all_frames(sg_slam* s, sg_map* map, double range, int32_t solv
     throw;
   }
   sg_problem_free(&p);
+  SG_CAPI_END
+}
+
+int sg_slam_last_phase_ms(const sg_slam* s, double* ms4) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(s && ms4, SG_EINVAL, "null argument");
+  for (int i = 0; i < 4; ++i) ms4[i] = s->phase_ms[i];
   SG_CAPI_END
 }
 

@@ -19,11 +19,14 @@ struct DBuf {
   void Resize(size_t n) {
     size = n;
     if (n <= cap) return;
+    // grow geometrically: a map that grows by a frame per call (main.cpp's loop) would otherwise pay a
+    // hipFree (a device synchronisation) and a hipMalloc on almost every load
+    const size_t ncap = cap ? std::max(n, cap + cap / 2) : n;
     if (ptr) (void)hipFree(ptr);
     ptr = nullptr;
     cap = 0;
-    SG_HIP_CHECK(hipMalloc(&ptr, std::max<size_t>(n, 1) * sizeof(T)));
-    cap = n;
+    SG_HIP_CHECK(hipMalloc(&ptr, std::max<size_t>(ncap, 1) * sizeof(T)));
+    cap = ncap;
   }
   void Upload(const std::vector<T>& v, hipStream_t s) {
     Resize(v.size());

@@ -1,0 +1,111 @@
+// stager.h — batched host-to-device upload of a solver's structure arrays.
+//
+// A full sg_ba_load uploads some forty index lists and value arrays.  Issued one hipMemcpyAsync each from
+// pageable vectors, every copy is staged synchronously by the runtime, which dominated the load of the small
+// problems main.cpp solves every frame (SolveFrames(2, 5): tools/e2e_replay.py).  The Stager packs them into
+// one pinned host buffer (16-byte aligned pieces), copies it with one hipMemcpyAsync into a device staging
+// buffer and scatters the pieces to their buffers with one kernel launch.
+#ifndef SG_STAGER_H_
+#define SG_STAGER_H_
+
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <vector>
+
+#include "common.h"
+#include "dbuf.h"
+
+namespace sg {
+
+struct StagePiece {
+  unsigned long long dst;   // device address
+  unsigned long long off;   // byte offset in the staging buffer (16-aligned)
+  unsigned long long bytes;
+};
+
+// One workgroup column per piece (blockIdx.y); 16-byte copies for the aligned body, bytes for the tail.
+__global__ __launch_bounds__(256) void k_stage_scatter(const StagePiece* __restrict__ pieces,
+                                                       const unsigned char* __restrict__ stage) {
+  const StagePiece pc = pieces[blockIdx.y];
+  const unsigned char* src = stage + pc.off;
+  unsigned char* dst = reinterpret_cast<unsigned char*>(pc.dst);
+  const size_t n16 = pc.bytes / 16;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x)
+    reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+  if (blockIdx.x == 0 && threadIdx.x < pc.bytes - 16 * n16) dst[16 * n16 + threadIdx.x] = src[16 * n16 + threadIdx.x];
+}
+
+class Stager {
+ public:
+  ~Stager() {
+    if (host_) (void)hipHostFree(host_);
+  }
+
+  // Resize dst to v.size() and queue v for it (the copy happens in Flush).
+  template <typename T>
+  void Add(DBuf<T>& dst, const std::vector<T>& v) {
+    dst.Resize(v.size());
+    if (v.empty()) return;
+    const size_t bytes = v.size() * sizeof(T);
+    const size_t off = Reserve(bytes);
+    std::memcpy(host_ + off, v.data(), bytes);
+    pieces_.push_back(StagePiece{(unsigned long long)(uintptr_t)dst.ptr, off, bytes});
+    max_bytes_ = std::max(max_bytes_, bytes);
+  }
+
+  // Drop anything queued (a load that failed part way).
+  void Clear() {
+    pieces_.clear();
+    used_ = 0;
+    max_bytes_ = 0;
+  }
+
+  // One pinned copy and one scatter launch on stream s.  The pinned buffer is reused by the next batch, so
+  // the caller synchronises s before queueing again (sg_ba_load ends with a stream synchronisation).
+  void Flush(hipStream_t s) {
+    if (pieces_.empty()) return;
+    const size_t tbl = used_;
+    const size_t tbytes = pieces_.size() * sizeof(StagePiece);
+    Reserve(tbytes);
+    std::memcpy(host_ + tbl, pieces_.data(), tbytes);
+    dev_.Resize(used_);
+    SG_HIP_CHECK(hipMemcpyAsync(dev_.ptr, host_, used_, hipMemcpyHostToDevice, s));
+    const unsigned gx = (unsigned)std::min<size_t>(64, std::max<size_t>(1, (max_bytes_ / 16 + 255) / 256));
+    hipLaunchKernelGGL(k_stage_scatter, dim3(gx, (unsigned)pieces_.size()), dim3(256), 0, s,
+                       reinterpret_cast<const StagePiece*>(dev_.ptr + tbl), dev_.ptr);
+    SG_HIP_CHECK(hipGetLastError());
+    pieces_.clear();
+    used_ = 0;
+    max_bytes_ = 0;
+  }
+
+ private:
+  size_t Reserve(size_t bytes) {
+    const size_t off = (used_ + 15) & ~(size_t)15;
+    const size_t need = off + bytes;
+    if (need > cap_) {
+      // grow: keep what is queued (pieces_ hold offsets, not host pointers)
+      const size_t ncap = std::max(need, cap_ + cap_ / 2 + (1 << 16));
+      unsigned char* nh = nullptr;
+      SG_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&nh), ncap, hipHostMallocDefault));
+      if (host_) {
+        std::memcpy(nh, host_, used_);
+        (void)hipHostFree(host_);
+      }
+      host_ = nh;
+      cap_ = ncap;
+    }
+    used_ = need;
+    return off;
+  }
+
+  unsigned char* host_ = nullptr;
+  size_t cap_ = 0, used_ = 0, max_bytes_ = 0;
+  std::vector<StagePiece> pieces_;
+  DBuf<unsigned char> dev_;
+};
+
+}  // namespace sg
+
+#endif  // SG_STAGER_H_

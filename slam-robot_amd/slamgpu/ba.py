@@ -264,6 +264,12 @@ class Slam:
         check(self.lib.sg_slam_load_counts(self.h, C.byref(full), C.byref(vals)), "sg_slam_load_counts")
         return full.value, vals.value
 
+    def last_phase_ms(self) -> dict:
+        """Host wall time of the last SolveFrames / SolveAllFrames call by phase (ms)."""
+        v = (C.c_double * 4)()
+        check(self.lib.sg_slam_last_phase_ms(self.h, v), "sg_slam_last_phase_ms")
+        return {"setup": v[0], "load": v[1], "solve": v[2], "write_back": v[3]}
+
     def error(self) -> float:
         return float(self.lib.sg_slam_error(self.h))
 

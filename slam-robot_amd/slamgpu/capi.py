@@ -301,6 +301,7 @@ SYMBOLS = {
     "sg_map_normalize": (C.c_int, [C.c_void_p, C.POINTER(SgMap)]),
     "sg_slam_iterations": (C.c_int32, [C.c_void_p]),
     "sg_slam_load_counts": (C.c_int, [C.c_void_p, _ip, _ip]),
+    "sg_slam_last_phase_ms": (C.c_int, [C.c_void_p, C.POINTER(C.c_double)]),
     "sg_slam_error": (C.c_double, [C.c_void_p]),
     "sg_slam_last_summary": (C.c_int, [C.c_void_p, C.POINTER(SgSolverSummary)]),
     "sg_slam_set_options": (C.c_int, [C.c_void_p, C.POINTER(SgSolverOptions)]),

@@ -1,0 +1,107 @@
+"""Replay of main.cpp's bundle-adjustment call pattern (main.cpp:580-605) on a growing synthetic map, timing
+the host share of every real Slam::SolveFrames call.
+
+Per new frame f (the map holds frames 0..f-1 and their observations, as after Matcher::Track):
+  SolveFrames(2, 5) -> ReprojectMap -> Clean;  every 5th frame also SolveFrames(10, 20) -> ReprojectMap ->
+  Clean;  then ApplyEpipolarConstraint, ReprojectMap, Normalize, ReprojectMap.
+Every call changes the problem's structure (a new frame, observations disabled by Clean), so every load is
+a full one.  Prints per call type the mean host phases of sg_slam_last_phase_ms — SetupProblem, sg_ba_load
+(work lists + upload), device LM loop (incl. the poll and download) and write-back — and writes them as JSON
+(argv[1], default gpurun_out/e2e_replay.json)."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "slam-robot_amd"))
+from slamgpu import ba  # noqa: E402
+from slamgpu.scene import MapArrays, make_scene  # noqa: E402
+
+NF = int(os.environ.get("REPLAY_FRAMES", "60"))
+NP = int(os.environ.get("REPLAY_POINTS", "20000"))
+F0 = 12
+out_path = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "e2e_replay.json")
+
+full = make_scene(num_frames=NF, num_points=NP, seed=7, run_max=14)
+work = full.copy()
+
+
+def view(F):
+    """The map as it stands after frame F-1 was tracked: frames [0, F), their observations."""
+    sel = np.nonzero(work.obs_frame < F)[0]
+    kw = {}
+    for f in work.__dataclass_fields__:
+        v = getattr(work, f)
+        if v is None:
+            kw[f] = None
+        elif f in ("q", "q_true"):
+            kw[f] = v[:4 * F].copy()
+        elif f in ("t", "t_true"):
+            kw[f] = v[:3 * F].copy()
+        elif f in ("frame_camera", "frame_prev", "frame_keyframe"):
+            kw[f] = v[:F].copy()
+        elif f in ("obs_frame", "obs_point", "obs_disabled"):
+            kw[f] = v[sel].copy()
+        elif f in ("obs_pt", "obs_error"):
+            kw[f] = v.reshape(-1, 2)[sel].reshape(-1).copy()
+        else:
+            kw[f] = v.copy()
+    return MapArrays(**kw), sel
+
+
+def merge(mm, sel, F):
+    work.q[:4 * F] = mm.q
+    work.t[:3 * F] = mm.t
+    work.X[:] = mm.X
+    work.point_flags[:] = mm.point_flags
+    work.point_uncertainty[:] = mm.point_uncertainty
+    work.obs_disabled[sel] = mm.obs_disabled
+    e = work.obs_error.reshape(-1, 2)
+    e[sel] = mm.obs_error.reshape(-1, 2)
+
+
+slam = ba.Slam(device=0)
+stats = {"2/5": [], "10/20": []}
+t_all = time.perf_counter()
+for F in range(F0, NF + 1):
+    mm, sel = view(F)
+    calls = [("2/5", 2, 5)]
+    if F < 10 or F % 5 == 0:
+        calls.append(("10/20", 10, 20))
+    for name, ns, npres in calls:
+        it0 = slam.iterations()
+        t0 = time.perf_counter()
+        ok = slam.SolveFrames(mm, ns, npres, 2.0)
+        wall = 1e3 * (time.perf_counter() - t0)
+        ph = slam.last_phase_ms()
+        ph.update(wall=wall, iterations=slam.iterations() - it0, ok=bool(ok), frame=F)
+        stats[name].append(ph)
+        if ok:
+            slam.ReprojectMap(mm)
+            slam.Clean(mm, 2.0)
+    slam.ApplyEpipolarConstraint(mm)
+    slam.ReprojectMap(mm)
+    slam.Normalize(mm)
+    slam.ReprojectMap(mm)
+    merge(mm, sel, F)
+t_all = time.perf_counter() - t_all
+
+summary = {"frames": NF, "points": NP, "replayed_from": F0, "seconds": t_all, "load_counts": slam.load_counts()}
+for name, rows in stats.items():
+    rows = rows[2:]   # first calls pay code-object loading and allocations
+    if not rows:
+        continue
+    mean = {k: float(np.mean([r[k] for r in rows])) for k in ("setup", "load", "solve", "write_back", "wall",
+                                                               "iterations")}
+    mean["calls"] = len(rows)
+    summary[name] = mean
+    print("SolveFrames(%s): %d calls, %.1f LM iterations; setup %.2f ms, load %.2f ms, LM loop %.2f ms, "
+          "write-back %.2f ms, wall %.2f ms" % (name, len(rows), mean["iterations"], mean["setup"], mean["load"],
+                                                mean["solve"], mean["write_back"], mean["wall"]))
+print("load counts (full, values):", slam.load_counts())
+os.makedirs(os.path.dirname(out_path), exist_ok=True)
+with open(out_path, "w") as f:
+    json.dump({"summary": summary, "calls": stats}, f, indent=1)
