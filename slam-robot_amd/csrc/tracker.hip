@@ -201,6 +201,67 @@ __device__ __forceinline__ float sample(const float* img, int w, const Geo& g, i
   return zero ? 0.f : (edge ? re : rb);
 }
 
+// Staged sampling (Track's Newton probes): each wave copies a kStT x kStT tile of the destination level around
+// its estimate into LDS and samples from it with sample()'s index arithmetic (the same floats, so the results
+// are bit-identical) — an LDS round trip per probe batch instead of an L2 one.  The wave restages when the
+// estimate comes within a patch half-width + 3 pixels of the tile edge; near the image border (or on levels
+// smaller than the tile) it samples global memory as before.
+constexpr int kStT = 40;
+
+struct Stage {
+  int r0 = 0, c0 = 0;
+  bool on = false;
+};
+
+__device__ __forceinline__ float sample_lds(const float* tile, const Stage& st, const Geo& g, int i, int j) {
+  const bool zero = g.pw <= 0 || g.ph <= 0 || j < g.zx || i < g.zy;
+  const int ii = i - g.zy, jj = j - g.zx;
+  const bool same = (ii < g.ry || ii >= g.rh);
+  const int row = g.base_row + max(0, min(ii, g.rh) - g.ry);
+  const bool left = jj < g.rx, right = !left && jj >= g.rw;
+  const bool edge = left || right;
+  const int ce = g.col0 + (left ? g.rx : g.rw);
+  const int c0 = zero ? 0 : (edge ? ce : g.col0 + jj) - st.c0;
+  const int c1 = zero ? 0 : (edge ? ce : g.col0 + jj + 1) - st.c0;
+  const int r1 = zero ? 0 : (row - st.r0) * kStT;
+  const int r2 = (zero || same) ? r1 : r1 + kStT;
+  const float v11 = tile[r1 + c0], v12 = tile[r1 + c1], v21 = tile[r2 + c0], v22 = tile[r2 + c1];
+  const float re = v11 * g.b1 + v21 * g.b2;
+  const float rb = v11 * g.a11 + v12 * g.a12 + v21 * g.a21 + v22 * g.a22;
+  return zero ? 0.f : (edge ? re : rb);
+}
+
+// Every tap of the six probes around (x, y) lies in the staged tile (wave-uniform): the probes' windows span
+// columns floor(x -+ 0.02 - (W - 1) / 2) .. + W, rows likewise.
+__device__ __forceinline__ bool stage_covers(const Stage& st, float x, float y, int W) {
+  const float lo = 0.5f * W + 3.f, hi = kStT - 0.5f * W - 4.f;
+  return st.on && x >= st.c0 + lo && x <= st.c0 + hi && y >= st.r0 + lo && y <= st.r0 + hi;
+}
+
+// (Re)stage the tile around (x, y); levels smaller than the tile are never staged.
+__device__ __forceinline__ void stage_load(const LevelDev& L, float x, float y, int lane, float* tile, Stage& st) {
+  if (L.w < kStT || L.h < kStT) {
+    st.on = false;
+    return;
+  }
+  st.c0 = min(max((int)x - kStT / 2, 0), L.w - kStT);
+  st.r0 = min(max((int)y - kStT / 2, 0), L.h - kStT);
+  const __attribute__((address_space(1))) float* gi = (const __attribute__((address_space(1))) float*)L.img;
+  float v[(kStT * kStT + 63) / 64];
+#pragma unroll
+  for (int u = 0; u < (kStT * kStT + 63) / 64; ++u) {
+    const int idx = min(lane + 64 * u, kStT * kStT - 1);
+    v[u] = gi[(size_t)(st.r0 + idx / kStT) * L.w + st.c0 + idx % kStT];
+  }
+#pragma unroll
+  for (int u = 0; u < (kStT * kStT + 63) / 64; ++u) {
+    const int idx = lane + 64 * u;
+    if (idx < kStT * kStT) tile[idx] = v[u];
+  }
+  __builtin_amdgcn_wave_barrier();
+  st.on = true;
+}
+
 template <int kCtrl>
 __device__ __forceinline__ float dpp_f(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), kCtrl, 0xF, 0xF, false));
@@ -269,9 +330,11 @@ __device__ __forceinline__ void get_patch_ctx(const TrackCtx& c, const LevelDev&
 }
 
 // BruteHessian (hessian.h:147-172): the six probes sampled together, their sums reduced in batches.
+// kLds: the probes read the wave's staged tile (the caller checked stage_covers).
+template <bool kLds>
 __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev& L, const Tmpl& tp, float x, float y,
                                               float* mdx, float* mdy, float* mdxx, float* mdxy, float* mdyx,
-                                              float* mdyy) {
+                                              float* mdyy, const float* tile, const Stage& st) {
   const double hh = 0.02;
   float px[6], py[6];
   px[0] = x;              py[0] = y;                // sad0
@@ -288,7 +351,8 @@ __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev&
     float s = 0.f, q = 0.f;
 #pragma unroll
     for (int k = 0; k < kNP; ++k) {
-      const float v = k < c.nk ? sample(L.img, L.w, g, c.pi[k], c.pj[k]) : 0.f;   // 0 past the patch
+      const float sv = kLds ? sample_lds(tile, st, g, c.pi[k], c.pj[k]) : sample(L.img, L.w, g, c.pi[k], c.pj[k]);
+      const float v = k < c.nk ? sv : 0.f;   // 0 past the patch
       pv[r][k] = v;
       s += v;
       q += v * v;
@@ -336,7 +400,7 @@ __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev&
 // iterations of Track (185-241) on `dst` coarse to fine.  0 OK (*px, *py updated), 2 OUT_OF_BOUNDS.
 __device__ __forceinline__ int track_pass(const TrackCtx& c, const LevelDev* __restrict__ src,
                                           const LevelDev* __restrict__ dst, int lvls, float sx, float sy, float* px,
-                                          float* py, int* iters) {
+                                          float* py, int* iters, float* tile) {
   const double s = 1. / (1 << (lvls - 1));
   float x = (float)(*px * s), y = (float)(*py * s);
   for (int i = lvls - 1; i >= 0; --i) {
@@ -351,13 +415,18 @@ __device__ __forceinline__ int track_pass(const TrackCtx& c, const LevelDev* __r
     const float margin = 0.01f;
     int it = 0;
     bool oob = false;
+    Stage st;
     for (; it < c.max_it; ++it) {
       if (x < margin || y < margin || (x + margin) > Ld.w || (y + margin) > Ld.h) {
         oob = true;
         break;
       }
       float mdx, mdy, mdxx, mdxy, mdyx, mdyy;
-      brute_hessian(c, Ld, tp, x, y, &mdx, &mdy, &mdxx, &mdxy, &mdyx, &mdyy);
+      if (!stage_covers(st, x, y, c.W)) stage_load(Ld, x, y, c.lane, tile, st);
+      if (stage_covers(st, x, y, c.W))
+        brute_hessian<true>(c, Ld, tp, x, y, &mdx, &mdy, &mdxx, &mdxy, &mdyx, &mdyy, tile, st);
+      else
+        brute_hessian<false>(c, Ld, tp, x, y, &mdx, &mdy, &mdxx, &mdxy, &mdyx, &mdyy, tile, st);
       const double H00 = mdxx, H01 = mdxy, H10 = mdyx, H11 = mdyy;
       const double det = H00 * H11 - H10 * H01;
       const double invdet = 1.0 / det;
@@ -397,9 +466,11 @@ __global__ __launch_bounds__(64 * kTrackWaves) void k_track_fb(const LevelDev* _
                                                                TrackParams prm, int n, const float* from_xy,
                                                                const float* to_init, const int32_t* levels,
                                                                float* to_xy, int32_t* accepted, int32_t* iterations) {
+  __shared__ float stage_tiles[kTrackWaves][kStT * kStT];
   const int lane = threadIdx.x & 63;
   const int f = blockIdx.x * kTrackWaves + (threadIdx.x >> 6);
   if (f >= n) return;   // whole wave
+  float* tile = stage_tiles[threadIdx.x >> 6];
   TrackCtx c;
   c.W = prm.window;
   c.len = prm.window * prm.window;
@@ -434,7 +505,7 @@ __global__ __launch_bounds__(64 * kTrackWaves) void k_track_fb(const LevelDev* _
       const LevelDev* dst = pass ? from_lv : to_lv;
       const float sx = pass ? tx : fx, sy = pass ? ty : fy;
       float qx = pass ? bx : tx, qy = pass ? by : ty;
-      st = track_pass(c, src, dst, lvls, sx, sy, &qx, &qy, &iters);
+      st = track_pass(c, src, dst, lvls, sx, sy, &qx, &qy, &iters, tile);
       if (st != 0) break;
       if (pass == 0) {
         tx = qx;
@@ -502,15 +573,17 @@ __global__ __launch_bounds__(64 * kTrackWaves) void k_track_one(const LevelDev* 
                                                                 TrackParams prm, int n, const float* from_xy,
                                                                 float* to_xy, const int32_t* levels,
                                                                 int32_t* status, int32_t* iterations) {
+  __shared__ float stage_tiles[kTrackWaves][kStT * kStT];
   const int lane = threadIdx.x & 63;
   const int f = blockIdx.x * kTrackWaves + (threadIdx.x >> 6);
   if (f >= n) return;
+  float* tile = stage_tiles[threadIdx.x >> 6];
   TrackCtx c;
   init_ctx(c, prm, lane);
   const int lvls = min(depth, levels ? levels[f] : depth);
   float qx = to_xy[2 * f], qy = to_xy[2 * f + 1];
   int iters = 0;
-  const int st = track_pass(c, from_lv, to_lv, lvls, from_xy[2 * f], from_xy[2 * f + 1], &qx, &qy, &iters);
+  const int st = track_pass(c, from_lv, to_lv, lvls, from_xy[2 * f], from_xy[2 * f + 1], &qx, &qy, &iters, tile);
   if (lane == 0) {
     status[f] = st;
     if (st == 0) {
