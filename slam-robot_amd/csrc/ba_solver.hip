@@ -431,7 +431,7 @@ __global__ __launch_bounds__(kRedThreads) void k_cam_reduce(Dev d) {
     if (sl < kCamSlices) {
       const int j0 = d.cam_loff[b], j1 = d.cam_loff[b + 1];
       double acc = 0.0;
-      constexpr int kU = 8;   // offsets, then partials, kU at a time in flight
+      constexpr int kU = 16;   // offsets, then partials, kU at a time in flight (one round of each at C2)
       for (int jb = j0 + sl; jb < j1; jb += kU * kCamSlices) {
         int ix[kU];
         double v[kU];
@@ -497,24 +497,49 @@ __global__ __launch_bounds__(kRedThreads) void k_cam_reduce(Dev d) {
 // ------------------------------------------------------------------------------------------------
 // k_cam_finalize: one workgroup.  FrameDistance blocks (slam.cpp:86-105), total cost, gradient
 // max-norm, Jacobi scale (iteration 0), pending iteration push, max-iteration test, LM diagonal.
+// A single workgroup's latency chain: the FrameDistance Jacobians and the camera gradient / diagonal stay in
+// LDS for the passes that re-read them (global copies are still written for k_S_reduce), and the block
+// pass's exchange-buffer operands are loaded before the FrameDistance pass.
+constexpr int kFinFdSh = 256;    // FrameDistance residuals held in LDS (more: re-read from global)
+constexpr int kFinNSh = 1536;    // frame columns held in LDS (more: re-read from global)
 __global__ __launch_bounds__(256) void k_cam_finalize(Dev d) {
   LmState* st = d.st;
   if (st->done) return;
   __shared__ double red[4];
   __shared__ double fdcost[256];
+  __shared__ double fdJs[6 * kFinFdSh], fdrs[kFinFdSh];
+  __shared__ double gsh[kFinNSh], dgsh[kFinNSh], scsh[kFinNSh];
   __shared__ int done_sh;
   const int tid = threadIdx.x;
   const int cur = st->cur;
   const int nv = d.NB * kCamV;
-  if (st->need_lin) {
+  const int nf = 6 * d.NB;
+  const bool fd_lds = d.D <= kFinFdSh, n_lds = nf <= kFinNSh;
+  // read once, before thread 0 updates them below (no other thread re-reads LmState flags afterwards)
+  const bool lin = st->need_lin, first = st->first, jacobi = st->jacobi;
+  if (lin) {
+    // block pass operands of block tid (the common case NB <= 256), in flight during the FrameDistance pass
+    double Ug[6], Ud[6];
+    int e0 = 0, e1 = 0;
+    const int b0 = tid < d.NB ? tid : 0;
+    {
+      const double* U = d.xchg_cam + (size_t)b0 * kCamV;
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+        Ug[a] = U[21 + a];
+        Ud[a] = U[u6(a, a)];
+      }
+      e0 = d.fd_boff[b0];
+      e1 = d.fd_boff[b0 + 1];
+    }
     // FrameDistance residuals at x[cur]
     double myfd = 0.0;
     for (int dd = tid; dd < d.D; dd += blockDim.x) {
       const int fa = d.fd_a[dd], fb = d.fd_b[dd];
       const double* ta = d.t[cur] + 3 * fa;
       const double* tb = d.t[cur] + 3 * fb;
-      const double e0 = ta[0] - tb[0], e1 = ta[1] - tb[1], e2 = ta[2] - tb[2];
-      const double dist = sqrt(e0 * e0 + e1 * e1 + e2 * e2);
+      const double e0_ = ta[0] - tb[0], e1_ = ta[1] - tb[1], e2_ = ta[2] - tb[2];
+      const double dist = sqrt(e0_ * e0_ + e1_ * e1_ + e2_ * e2_);
       const double r = 0.1 * (dist - d.fd_target);
       double rho0, rho1;
       Cauchy(r * r, d.fd_b2, d.fd_inv_b2, &rho0, &rho1);
@@ -522,13 +547,18 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d) {
       const double sr = sqrt(rho1);
       d.fd_r[dd] = sr * r;
       const double gsc = sr * 0.1 / dist;
-      const double ga[3] = {gsc * e0, gsc * e1, gsc * e2};
+      const double ga[3] = {gsc * e0_, gsc * e1_, gsc * e2_};
       const bool af = d.trans_free[fa] && d.frame_block[fa] >= 0;
       const bool bf = d.trans_free[fb] && d.frame_block[fb] >= 0;
-      double* Jd = d.fd_J + 6 * dd;
+      double Jd[6];
       for (int j = 0; j < 3; ++j) {
         Jd[j] = af ? ga[j] : 0.0;
         Jd[3 + j] = bf ? -ga[j] : 0.0;
+      }
+      for (int j = 0; j < 6; ++j) d.fd_J[6 * dd + j] = Jd[j];
+      if (fd_lds) {
+        fdrs[dd] = sr * r;
+        for (int j = 0; j < 6; ++j) fdJs[6 * dd + j] = Jd[j];
       }
       double* Xd = d.fd_X + 9 * dd;
       for (int i = 0; i < 3; ++i)
@@ -540,23 +570,36 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d) {
     // per camera block: gradient, diag, FD diagonal block
     double gm = 0.0, xn2c = 0.0;
     for (int b = tid; b < d.NB; b += blockDim.x) {
+      if (b != tid) {   // NB > 256: operands not prefetched
+        const double* U = d.xchg_cam + (size_t)b * kCamV;
+        for (int a = 0; a < 6; ++a) {
+          Ug[a] = U[21 + a];
+          Ud[a] = U[u6(a, a)];
+        }
+        e0 = d.fd_boff[b];
+        e1 = d.fd_boff[b + 1];
+      }
       double fdD[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
       double gfd[3] = {0, 0, 0};
-      for (int e = d.fd_boff[b]; e < d.fd_boff[b + 1]; ++e) {
+      for (int e = e0; e < e1; ++e) {
         const int dd = d.fd_bidx[e] >> 1, side = d.fd_bidx[e] & 1;
-        const double* Jd = d.fd_J + 6 * dd + 3 * side;
+        const double* Jd = fd_lds ? fdJs + 6 * dd + 3 * side : d.fd_J + 6 * dd + 3 * side;
+        const double rr = fd_lds ? fdrs[dd] : d.fd_r[dd];
         for (int i = 0; i < 3; ++i) {
-          gfd[i] += Jd[i] * d.fd_r[dd];
+          gfd[i] += Jd[i] * rr;
           for (int j = 0; j < 3; ++j) fdD[3 * i + j] += Jd[i] * Jd[j];
         }
       }
       for (int i = 0; i < 9; ++i) d.fd_D[9 * b + i] = fdD[i];
-      const double* U = d.xchg_cam + (size_t)b * kCamV;
       for (int a = 0; a < 6; ++a) {
-        const double gg = U[21 + a] + (a >= 3 ? gfd[a - 3] : 0.0);
-        const double dg = U[u6(a, a)] + (a >= 3 ? fdD[4 * (a - 3)] : 0.0);
+        const double gg = Ug[a] + (a >= 3 ? gfd[a - 3] : 0.0);
+        const double dg = Ud[a] + (a >= 3 ? fdD[4 * (a - 3)] : 0.0);
         d.camg[6 * b + a] = gg;
         d.camdiag[6 * b + a] = dg;
+        if (n_lds) {
+          gsh[6 * b + a] = gg;
+          dgsh[6 * b + a] = dg;
+        }
       }
     }
     __syncthreads();
@@ -564,11 +607,12 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d) {
     for (int f = tid; f < d.F; f += blockDim.x) {
       const int b = d.frame_block[f];
       if (b < 0) continue;
+      const double* cg = n_lds ? gsh : d.camg;
       if (d.rot_free[f])
-        for (int a = 0; a < 3; ++a) gm = fmax(gm, fabs(d.camg[6 * b + a]));
+        for (int a = 0; a < 3; ++a) gm = fmax(gm, fabs(cg[6 * b + a]));
       if (d.trans_free[f])
-        for (int a = 3; a < 6; ++a) gm = fmax(gm, fabs(d.camg[6 * b + a]));
-      if (st->first) {
+        for (int a = 3; a < 6; ++a) gm = fmax(gm, fabs(cg[6 * b + a]));
+      if (first) {
         if (d.rot_free[f])
           for (int a = 0; a < 4; ++a) xn2c += d.q[cur][4 * f + a] * d.q[cur][4 * f + a];
         if (d.trans_free[f])
@@ -577,10 +621,14 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d) {
     }
     gm = block_max<256>(gm, red);
     xn2c = block_sum<256>(xn2c, red);
-    if (st->first && st->jacobi)
-      for (int i = tid; i < d.n; i += blockDim.x) d.scale_c[i] = 1.0 / (1.0 + sqrt(d.camdiag[i]));
-    else if (st->first)
-      for (int i = tid; i < d.n; i += blockDim.x) d.scale_c[i] = 1.0;
+    if (first) {
+      for (int i = tid; i < d.n; i += blockDim.x) {
+        const double cd = (n_lds && i < nf) ? dgsh[i] : d.camdiag[i];
+        const double sc = jacobi ? 1.0 / (1.0 + sqrt(cd)) : 1.0;
+        d.scale_c[i] = sc;
+        if (n_lds && i < nf) scsh[i] = sc;
+      }
+    }
     if (tid == 0) {
       double fd = 0.0;
       for (int i = 0; i < (int)blockDim.x; ++i) fd += fdcost[i];
@@ -588,7 +636,7 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d) {
       const double cost = xs[kXCost] + fd;
       double gmax = gm;
       for (int r = 0; r < d.nranks; ++r) gmax = fmax(gmax, xs[kXNum + r]);
-      if (st->first) {
+      if (first) {
         st->fixed_cost = xs[kXFixed];
         if (xs[kXFixedFail] > 0.0) {
           st->done = 1; st->ok = 0; st->termination = SG_DID_NOT_RUN;
@@ -640,8 +688,10 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d) {
   if (done_sh) return;
   if (!st->reuse_diag)
     for (int i = tid; i < d.n; i += blockDim.x) {
-      const double s = d.scale_c[i];
-      d.diag_c[i] = fmin(fmax(s * s * d.camdiag[i], st->min_diag), st->max_diag);
+      const bool sh = lin && n_lds && i < nf;   // written above in this launch
+      const double s = (sh && first) ? scsh[i] : d.scale_c[i];
+      const double cd = sh ? dgsh[i] : d.camdiag[i];
+      d.diag_c[i] = fmin(fmax(s * s * cd, st->min_diag), st->max_diag);
     }
 }
 
@@ -2188,7 +2238,6 @@ struct TileShared {
   double Dw[16 * kTLd];        // the owner's diagonal tile (one owner per phase)
   double Yw[16];
   double prw[2 * kCholNb];     // the owner's next two pivot rows
-  double bsp[2][kTB][16];      // back-substitution partials
   int fail;
 };
 
@@ -2501,38 +2550,72 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
   if (bad && lane == 0) sh.fail = 1;
   __syncthreads();   // W tiles (global) and z' visible to every wave
   SG_TSTAMP(4)
-  {
-    // back substitution, rows K = NT-1 .. 0: wave w < 7 forms the partial W_{K,K+1+w} x_{K+1+w}, every wave
-    // sums the seven partials in wave order (the same bits everywhere) into x_K, wave 0 stores it.  The W tile
-    // is loaded one row ahead.
-    const bool hasd = wave < kTB - 1;
-    const double* wbase = Wg + (size_t)(wave + 1) * 256 + lane;
-    double wc[4], wn[4];
+  if (wave == 0) {
+    // Back substitution in one wave, rows K = NT-1 .. 0:  x_K = z'_K - sum_{d=1..7} W_{K,K+d} x_{K+d}, with no
+    // LDS round trip on the row-to-row chain.  Lane (li, lk) holds rows lk + 4q, column li of each W tile
+    // (acc layout) and x_{K+d}[li] in registers (xw[d-1]; zero past the last row, and W tiles outside the
+    // band are zero), so the d >= 2 terms are formed before x_{K+1} is known.  The 16-lane row sums run as a
+    // DPP butterfly (quad xor 1, quad xor 2, half-row mirror, row mirror: bitwise the same sum in every lane),
+    // and one shuffle moves x_K[li] (row li & 3, register li >> 2) to every lane.  W rows are prefetched two
+    // rows ahead (two register buffers, the loop unrolled by two); z' is read one row ahead.
+    double xw[kTB - 1];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) wc[q] = wbase[(size_t)(NT - 1) * kTB * 256 + q * 64];
-    for (int K = NT - 1; K >= 0; --K) {
-      const double* src = wbase + (size_t)(K > 0 ? K - 1 : 0) * kTB * 256;
+    for (int dd = 0; dd < kTB - 1; ++dd) xw[dd] = 0.0;
+    auto wload = [&](double (&w)[kTB - 1][4], int K) {
+      const double* src = Wg + (size_t)(K >= 0 ? K : 0) * kTB * 256 + lane;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) wn[q] = src[q * 64];
-      const int Jt = K + 1 + wave;
-      const bool in = hasd && Jt < tend[K];
-      const double xr = xs[16 * (in ? Jt : K) + li];   // unconditional (a valid row either way)
-      const double xv = in ? xr : 0.0;
-      double t[4];
+      for (int dd = 1; dd < kTB; ++dd)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) t[q] = row_sum16((in ? wc[q] : 0.0) * xv);
-      const double tv = li == 0 ? t[0] : (li == 1 ? t[1] : (li == 2 ? t[2] : t[3]));
-      if (li < 4) sh.bsp[K & 1][wave][lk + 4 * li] = tv;
-      lds_barrier();
-      const double* bp = &sh.bsp[K & 1][0][li];
-      double sum = 0.0;
+        for (int q = 0; q < 4; ++q) w[dd - 1][q] = src[dd * 256 + q * 64];
+    };
+    const int srcl = 16 * (li & 3) + li;   // the lane holding x_K[li] after the row sums
+    unsigned qbits = 1u << (li >> 2);
+    asm volatile("" : "+v"(qbits));
+    auto bs_row = [&](int K, double (&w)[kTB - 1][4], const double (&zk)[4]) {
+      double p[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int w = 0; w < kTB - 1; ++w) sum += bp[16 * w];
-      const double xk = zp[16 * K + li] - sum;
-      if (wave == 0 && lk == 0) xs[16 * K + li] = xk;
+      for (int dd = kTB - 1; dd >= 1; --dd)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) wc[q] = wn[q];
+        for (int q = 0; q < 4; ++q) p[q] = fma(w[dd - 1][q], xw[dd - 1], p[q]);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        double v = p[q];
+        v += dpp_d<0xB1>(v);
+        v += dpp_d<0x4E>(v);
+        v += dpp_d<0x141>(v);
+        v += dpp_d<0x140>(v);
+        p[q] = zk[q] - v;   // x_K[lk + 4q], the same bits in every lane of the row
+      }
+      // register p[li >> 2] by opaque bit masks (a lane-dependent ?: chain compiles to divergent branches)
+      unsigned long long mb = 0ull;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        int m;
+        asm volatile("v_bfe_i32 %0, %1, %2, 1" : "=v"(m) : "v"(qbits), "n"(q));
+        mb |= (unsigned long long)__double_as_longlong(p[q]) & (unsigned long long)(long long)m;
+      }
+      const double xk = __shfl(__longlong_as_double((long long)mb), srcl);
+      xs[16 * K + li] = xk;   // the same bits from every row of lanes
+#pragma unroll
+      for (int dd = kTB - 2; dd >= 1; --dd) xw[dd] = xw[dd - 1];
+      xw[0] = xk;
+      wload(w, K - 2);   // this buffer's next row
+    };
+    double wA[kTB - 1][4], wB[kTB - 1][4], zA[4], zB[4];
+    wload(wA, NT - 1);
+    wload(wB, NT - 2);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) zA[q] = zp[16 * (NT - 1) + lk + 4 * q];
+    int K = NT - 1;
+    for (; K >= 1; K -= 2) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) zB[q] = zp[16 * (K - 1) + lk + 4 * q];
+      bs_row(K, wA, zA);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) zA[q] = zp[16 * (K >= 2 ? K - 2 : 0) + lk + 4 * q];
+      bs_row(K - 1, wB, zB);
     }
+    if (K == 0) bs_row(0, wA, zA);
   }
   SG_TSTAMP(5)
   __syncthreads();
