@@ -226,6 +226,8 @@ typedef struct sg_ba_info {
   int32_t cholesky_path;                     /* 0: tiled band (k_chol_tiles), 1: LDS window, 2: global memory */
   int32_t num_pairs;                         /* Schur observation pairs (s <= t) of this rank's free points */
   int32_t rank, nranks;
+  int32_t cholesky_split;                    /* tiled path: tile rows factored bottom-up by a second workgroup
+                                                (dissected band; 0: one workgroup) */
 } sg_ba_info;
 int sg_ba_info_get(const sg_ba* h, sg_ba_info* out);
 

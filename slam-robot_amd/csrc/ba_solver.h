@@ -57,7 +57,10 @@ class BaSolver {
   bool chol_window_ = true;
   bool chol_tiles_ = false;    // tiled register-resident band Cholesky (k_chol_tiles)
   size_t tile_lds_ = 0;        // its dynamic LDS
-  DBuf<double> Wg_;            // its back-substitution tiles W_KJ = U_KK^-1 U_KJ
+  DBuf<double> Wg_;            // its back-substitution tiles W_KJ = U_KK^-1 U_KJ (+ the bottom half's)
+  int chol_nd_ = 0;            // dissected band: tile rows the second workgroup factors bottom-up (0: one WG)
+  DBuf<int32_t> tflag_;        // dissected band hand-off counters {bottom done, top done}
+  int chol_simdmap_ = !(getenv("SG_CHOL_SIMDMAP") && atoi(getenv("SG_CHOL_SIMDMAP")) == 0);
   bool pack_force_ = getenv("SG_PACK_S") != nullptr;   // pack/unpack S on one rank too (tests the path)
   size_t npack_ = 0;                                      // band of S + rhs, doubles (all-reduce size)
   bool stamp_on_ = false;

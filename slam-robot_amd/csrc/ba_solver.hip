@@ -2239,6 +2239,7 @@ struct TileShared {
   double Yw[16];
   double prw[2 * kCholNb];     // the owner's next two pivot rows
   int fail;
+  int simd[kTB];               // SIMD of each wave
 };
 
 __device__ __forceinline__ f64x4 mfma_f64_k16(const double (&a)[4], const f64x4& b, f64x4 c) {
@@ -2272,25 +2273,32 @@ __device__ __forceinline__ double row_sum16(double v) {
 // factorisation masks them); the identity beyond n (padding rows of the last tile) and zeros for I < 0 come
 // from the constants {0, 1} stored after S and its rhs (S[n n + n], S[n n + n + 1]).  The index is selected,
 // not the value, so the loads stay in flight until the tile is first used.
-__device__ __forceinline__ f64x4 tile_load(const double* __restrict__ S, int n, int I, int J, int li, int lk) {
+// Where a workgroup's tiles come from.  The top half (and the one-workgroup factorisation) reads S as it is;
+// the bottom half of the dissected band (k_chol_tiles, blockIdx 1) factors the index-reversed matrix
+// P S P (index i -> 16 NT - 1 - i, still banded), whose upper tile (I, J) is the transposed lower tile of S,
+// and starts its separator tiles (rows and columns >= sep) and their rhs at zero: the top half holds S there.
+struct TileSrc {
+  int rev;   // 0: S as stored; 1: reversed
+  int np;    // 16 NT (padded order)
+  int sep;   // first separator tile row (reversed side only; the top half passes NT)
+};
+
+__device__ __forceinline__ f64x4 tile_load(const double* __restrict__ S, int n, int I, int J, int li, int lk,
+                                           const TileSrc& ts) {
   f64x4 t;
   const int cz = n * n + n;
+  const bool zsep = I >= ts.sep && J >= ts.sep;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int gi = 16 * I + lk + 4 * q, gj = 16 * J + li;
-    const bool in = (unsigned)gi < (unsigned)n && gj < n;
-    t[q] = S[in ? gi * n + gj : cz + (gi == gj ? 1 : 0)];
+    // source row / column in S's own order (upper triangle: si <= sj for I <= J)
+    const int si = ts.rev ? ts.np - 1 - gj : gi, sj = ts.rev ? ts.np - 1 - gi : gj;
+    const bool in = I >= 0 && si < n && sj < n && !zsep;
+    t[q] = S[in ? si * n + sj : cz + ((gi == gj && !zsep) ? 1 : 0)];
   }
   return t;
 }
 
-__device__ __forceinline__ void tile_col_load(f64x4 (&acc)[kTB], double& ypart, const Dev& d, int J, int li,
-                                              int lk) {
-#pragma unroll
-  for (int u = 0; u < kTB; ++u) acc[u] = tile_load(d.S, d.n, J - ((J - u) & 7), J, li, lk);
-  const int gj = 16 * J + li, n = d.n;
-  ypart = d.S[(lk == 0 && gj < n) ? n * n + gj : n * n + n];
-}
 
 // Factor one 16x16 diagonal tile D (upper triangle, pitch kTLd) with the identity (lanes 16-31) and the rhs
 // (lane 32) as augmented columns; lanes 0-15 hold the columns of D.  Right-looking, two pivots per LDS
@@ -2428,23 +2436,46 @@ __device__ __forceinline__ void tile_w_store(const f64x4& Wt, double* __restrict
   for (int q = 0; q < 4; ++q) wg[q * 64] = Wt[q];
 }
 
-// One phase (tile row K) of a wave; kU = K & 7.  `late`: this wave owned the diagonal of the previous phase
-// and still owes that phase's W tile and its column reload (it has no other work in this phase).
-template <int kU, bool kStamp>
+// The accumulator slots rotate with the phase: in phase K, slot s of a wave's column J holds tile row
+// I = J - ((J - (s + K - 1)) & 7) — row K-1 in slot 0, row K in slot 1, the next diagonal in slot 2, row
+// K-1+d in slot d — and every wave rotates its slots by one between phases (register moves, off the
+// critical path).  So one phase body serves every tile row and the kernel's code stays inside the
+// instruction cache (a phase body instantiated per K & 7 made the kernel 150 KB, streamed through a 64 KB
+// cache every eight phases).
+__device__ __forceinline__ void tile_rotate(f64x4 (&acc)[kTB]) {
+  const f64x4 t = acc[0];
+#pragma unroll
+  for (int u = 0; u < kTB - 1; ++u) acc[u] = acc[u + 1];
+  acc[kTB - 1] = t;
+}
+
+// Column J of S into the slots of phase K (slot s: row J - ((J - (s + K - 1)) & 7)).
+__device__ __forceinline__ void tile_col_load(f64x4 (&acc)[kTB], double& ypart, const Dev& d, int J, int K,
+                                              int li, int lk, const TileSrc& ts) {
+#pragma unroll
+  for (int u = 0; u < kTB; ++u) acc[u] = tile_load(d.S, d.n, J - ((J - (u + K - 1)) & 7), J, li, lk, ts);
+  const int gj = 16 * J + li, n = d.n;
+  const int sj = ts.rev ? ts.np - 1 - gj : gj;
+  ypart = d.S[(lk == 0 && sj < n && J < ts.sep) ? n * n + sj : n * n + n];
+}
+
+// One phase (tile row K) of a wave.  `late`: this wave owned the diagonal of the previous phase and still
+// owes that phase's W tile and its column reload (it has no other work in this phase).
+template <bool kStamp>
 __device__ __forceinline__ void tile_phase(f64x4 (&acc)[kTB], double& ypart, int& J, bool& late, bool& bad,
                                            TileShared& sh, const Dev& d, double* __restrict__ Wg, double* zp,
                                            const int* tend, int K, int NT, int lane, int li, int lk,
-                                           unsigned long long (&tacc)[16], unsigned long long& tlast) {
-  constexpr int um = (kU + kTB - 1) & (kTB - 1), v = (kU + 1) & (kTB - 1);
+                                           const TileSrc& ts, unsigned long long (&tacc)[16],
+                                           unsigned long long& tlast) {
   if (late) {
-    // the previous phase's owner (column J = K): its row K-1 tile (slot um) -> W, then column J + 8, which
+    // the previous phase's owner (column J = K): its row K-1 tile (slot 0) -> W, then column J + 8, which
     // row K + 1 touches first
     const bool hasw = J < tend[K - 1];
     f64x4 Wt = {0.0, 0.0, 0.0, 0.0};
-    if (hasw) Wt = tile_w(acc[um], sh.Zs[um & 3], li, lk);
+    if (hasw) Wt = tile_w(acc[0], sh.Zs[(K - 1) & 3], li, lk);
     const int Jw = J;
     J += kTB;
-    tile_col_load(acc, ypart, d, J, li, lk);
+    tile_col_load(acc, ypart, d, J, K, li, lk, ts);
     if (hasw) tile_w_store(Wt, Wg, K - 1, Jw, lane);
     late = false;
     SG_TSTAMP(13)
@@ -2452,14 +2483,14 @@ __device__ __forceinline__ void tile_phase(f64x4 (&acc)[kTB], double& ypart, int
   }
   // (0) trailing update by row K-1
   if (K >= 1 && J < tend[K - 1]) {
-    const double* Ub = sh.Ur[um & 1][0];
+    const double* Ub = sh.Ur[(K - 1) & 1][0];
 #pragma unroll
     for (int dd = 1; dd < kTB; ++dd) {
       if (K - 1 + dd <= J) {
         double a[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) a[s] = -Ub[(dd - 1) * 256 + s * 64 + lane];
-        acc[(um + dd) & (kTB - 1)] = mfma_f64_k16(a, acc[um], acc[(um + dd) & (kTB - 1)]);
+        acc[dd] = mfma_f64_k16(a, acc[0], acc[dd]);
       }
     }
   }
@@ -2467,18 +2498,18 @@ __device__ __forceinline__ void tile_phase(f64x4 (&acc)[kTB], double& ypart, int
   // (1) TRSM of row K's tile
   const int te = tend[K];
   const bool act = J < te;
-  const double* Zs = sh.Zs[kU & 3];
+  const double* Zs = sh.Zs[K & 3];
   if (act) {
     const f64x4 zero = {0.0, 0.0, 0.0, 0.0};
     double za[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) za[s] = Zs[li * kTLd + 4 * s + lk];
-    const f64x4 U = mfma_f64_k16(za, acc[kU], zero);
-    acc[kU] = U;
-    double* ur = sh.Ur[kU & 1][J - K - 1];
+    const f64x4 U = mfma_f64_k16(za, acc[1], zero);
+    acc[1] = U;
+    double* ur = sh.Ur[K & 1][J - K - 1];
 #pragma unroll
     for (int q = 0; q < 4; ++q) ur[q * 64 + lane] = U[q];
-    const double* zk = sh.zK[kU & 3];
+    const double* zk = sh.zK[K & 3];
 #pragma unroll
     for (int q = 0; q < 4; ++q) ypart = fma(-U[q], zk[lk + 4 * q], ypart);
   }
@@ -2488,23 +2519,178 @@ __device__ __forceinline__ void tile_phase(f64x4 (&acc)[kTB], double& ypart, int
     if (act) {
       double a[4];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) a[s] = -acc[kU][s];
-      acc[v] = mfma_f64_k16(a, acc[kU], acc[v]);
+      for (int s = 0; s < 4; ++s) a[s] = -acc[1][s];
+      acc[2] = mfma_f64_k16(a, acc[1], acc[2]);
     }
     SG_TSTAMP(10)
-    if (K + 1 < NT) bad |= tile_diag(acc[v], ypart, sh, zp, K + 1, lane, li, lk);
+    if (K + 1 < NT) bad |= tile_diag(acc[2], ypart, sh, zp, K + 1, lane, li, lk);
     late = true;
     SG_TSTAMP(11)
   } else if (act) {
     // (3) back-substitution tile
-    tile_w_store(tile_w(acc[kU], Zs, li, lk), Wg, K, J, lane);
+    tile_w_store(tile_w(acc[1], Zs, li, lk), Wg, K, J, lane);
     SG_TSTAMP(12)
   }
 }
 
+// The bottom half's step after its last factored row ND-1 (slots of phase ND): the previous owner's W tile,
+// and every other wave's update of its separator column by row ND-1 ((0) of a phase, nothing else).
+__device__ __forceinline__ void tile_final(f64x4 (&acc)[kTB], int J, bool& late, TileShared& sh,
+                                           double* __restrict__ Wg, const int* tend, int K, int lane, int li,
+                                           int lk) {
+  if (late) {
+    if (J < tend[K - 1]) tile_w_store(tile_w(acc[0], sh.Zs[(K - 1) & 3], li, lk), Wg, K - 1, J, lane);
+    late = false;
+    return;
+  }
+  if (J < tend[K - 1]) {
+    const double* Ub = sh.Ur[(K - 1) & 1][0];
+#pragma unroll
+    for (int dd = 1; dd < kTB; ++dd) {
+      if (K - 1 + dd <= J) {
+        double a[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) a[s] = -Ub[(dd - 1) * 256 + s * 64 + lane];
+        acc[dd] = mfma_f64_k16(a, acc[0], acc[dd]);
+      }
+    }
+  }
+}
+
+// Separator hand-off.  The bottom half writes its contribution to the separator tiles (its columns
+// ND..ND+6, rows >= ND) mapped back to S's order — reversed tile (I', J') element (a, b) is tile
+// (NT-1-J', NT-1-I') element (15-b, 15-a) — in the top half's accumulator layout, and its rhs partials
+// summed over the lane rows.
+__device__ __forceinline__ void sep_write(const f64x4 (&acc)[kTB], double ypart, int J, int ND, int NT, int m,
+                                          double* __restrict__ sepb, double* __restrict__ sepy, int li, int lk) {
+  if (J < ND || J >= ND + 7) return;
+  const double ys = sum_rows4(ypart);
+  const int Io = NT - 1 - J;
+#pragma unroll
+  for (int u = 0; u < kTB; ++u) {
+    const int I = J - ((J - (u + ND - 1)) & 7);   // slots of phase ND
+    if (I >= ND) {
+      double* dst = sepb + ((Io - m) * 7 + (NT - 1 - I - m)) * 256;
+      const int C0 = 15 - li;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int Rd = C0, Cd = 15 - (lk + 4 * q);   // source (a, b) = (lk + 4q, li) -> (15 - b, 15 - a)
+        dst[(Rd >> 2) * 64 + Cd + 16 * (Rd & 3)] = acc[u][q];
+      }
+    }
+  }
+  if (lk == 0) sepy[(Io - m) * 16 + 15 - li] = ys;
+}
+
+// The top half adds the bottom half's separator contribution to the separator columns it holds (before
+// the first separator diagonal is factored).
+__device__ __forceinline__ void sep_merge(f64x4 (&acc)[kTB], double& ypart, int J, int m,
+                                          const double* __restrict__ sepb, const double* __restrict__ sepy,
+                                          int lane, int li, int lk) {
+  if (J < m || J >= m + 7) return;
+#pragma unroll
+  for (int u = 0; u < kTB; ++u) {
+    const int I = J - ((J - (u + m - 2)) & 7);   // slots of phase m - 1
+    if (I >= m) {
+      const double* src = sepb + ((I - m) * 7 + (J - m)) * 256 + lane;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[u][q] += src[q * 64];
+    }
+  }
+  if (lk == 0) ypart += sepy[(J - m) * 16 + li];
+}
+
+// Back substitution of tile rows Khi .. Klo in one wave:  x_K = z'_K - sum_{d=1..7} W_{K,K+d} x_{K+d}, with no
+// LDS round trip on the row-to-row chain.  Lane (li, lk) holds rows lk + 4q, column li of each W tile (acc
+// layout) and x_{K+d}[li] in registers (xw[d-1]; zero past the last row, and W tiles outside the band are
+// zero), so the d >= 2 terms are formed before x_{K+1} is known.  The 16-lane row sums run as a DPP butterfly
+// (quad xor 1, quad xor 2, half-row mirror, row mirror: bitwise the same sum in every lane), and one shuffle
+// moves x_K[li] (row li & 3, register li >> 2) to every lane.  W rows are prefetched two rows ahead (two
+// register buffers, the loop unrolled by two); z' is read one row ahead.  kRev: the rows are the bottom
+// half's reversed order, x_K[li] is stored at S-order index 16 (NT-1-K) + 15 - li.
+template <bool kRev>
+__device__ __forceinline__ void bs_chain(const double* __restrict__ Wb, const double* zsrc, double* xs, int Khi,
+                                         int Klo, double (&xw)[kTB - 1], int NT, int lane, int li, int lk) {
+  auto wload = [&](double (&w)[kTB - 1][4], int K) {
+    const double* src = Wb + (size_t)(K >= 0 ? K : 0) * kTB * 256 + lane;
+#pragma unroll
+    for (int dd = 1; dd < kTB; ++dd)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) w[dd - 1][q] = src[dd * 256 + q * 64];
+  };
+  const int srcl = 16 * (li & 3) + li;   // the lane holding x_K[li] after the row sums
+  unsigned qbits = 1u << (li >> 2);
+  asm volatile("" : "+v"(qbits));
+  auto bs_row = [&](int K, double (&w)[kTB - 1][4], const double (&zk)[4]) {
+    double p[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int dd = kTB - 1; dd >= 1; --dd)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) p[q] = fma(w[dd - 1][q], xw[dd - 1], p[q]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      double v = p[q];
+      v += dpp_d<0xB1>(v);
+      v += dpp_d<0x4E>(v);
+      v += dpp_d<0x141>(v);
+      v += dpp_d<0x140>(v);
+      p[q] = zk[q] - v;   // x_K[lk + 4q], the same bits in every lane of the row
+    }
+    // register p[li >> 2] by opaque bit masks (a lane-dependent ?: chain compiles to divergent branches)
+    unsigned long long mb = 0ull;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      int msk;
+      asm volatile("v_bfe_i32 %0, %1, %2, 1" : "=v"(msk) : "v"(qbits), "n"(q));
+      mb |= (unsigned long long)__double_as_longlong(p[q]) & (unsigned long long)(long long)msk;
+    }
+    const double xk = __shfl(__longlong_as_double((long long)mb), srcl);
+    if (kRev)
+      xs[16 * (NT - 1 - K) + 15 - li] = xk;
+    else
+      xs[16 * K + li] = xk;   // the same bits from every row of lanes
+#pragma unroll
+    for (int dd = kTB - 2; dd >= 1; --dd) xw[dd] = xw[dd - 1];
+    xw[0] = xk;
+    wload(w, K - 2);   // this buffer's next row
+  };
+  double wA[kTB - 1][4], wB[kTB - 1][4], zA[4], zB[4];
+  wload(wA, Khi);
+  wload(wB, Khi - 1);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) zA[q] = zsrc[16 * Khi + lk + 4 * q];
+  int K = Khi;
+  for (; K >= Klo + 1; K -= 2) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) zB[q] = zsrc[16 * (K - 1) + lk + 4 * q];
+    bs_row(K, wA, zA);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) zA[q] = zsrc[16 * (K >= 2 ? K - 2 : 0) + lk + 4 * q];
+    bs_row(K - 1, wB, zB);
+  }
+  if (K == Klo) bs_row(K, wA, zA);
+}
+
+// Dissected band (nd > 0: two workgroups).  With m = NT - nd - 7, the tile rows split into the top part
+// A = [0, m), the separator [m, m+7) and the bottom part B = [m+7, NT).  The band is at most 8 tiles wide,
+// so A and B never couple: eliminating A, then B, then the separator is an exact Cholesky of S in that
+// order (nested dissection), and A and B are factored at the same time.
+//   * blockIdx 0 (top) runs the phases of rows 0 .. m+6 of S (band ends clamped to the separator); at
+//     phase m-1 each wave waits for the bottom half and adds its separator contribution, then factors the
+//     separator rows as usual.
+//   * blockIdx 1 (bottom) runs the phases of B in reversed order (P S P: rows NT-1 .. m+7 of S, then the
+//     separator as its trailing columns, started at zero), writes the separator contribution, its z' and
+//     W tiles, and signals with a release counter.
+//   * Back substitution (top workgroup): the separator rows, then A (wave 0) and B (wave 1, reversed W
+//     tiles) side by side.
+// The chain drops from NT tile rows to m + 7 (C2: 18 -> 13, C5: 75 -> 42).  The wait is bounded: on a
+// time-out the step fails (rejected by the LM decision) instead of hanging.
+constexpr int kSepSpinMax = 1 << 22;
+constexpr int kSplitMinNT = 13;
 template <bool kStamp>
 __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_t* panel_jend,
-                                                             double* __restrict__ Wg) {
+                                                             double* __restrict__ Wg, int32_t* tflag, int nd,
+                                                             int simdmap) {
   const LmState* st = d.st;
   if (st->done) return;
   unsigned long long tlast = kStamp ? __builtin_amdgcn_s_memtime() : 0ull, tacc[16] = {};
@@ -2514,109 +2700,135 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, lk = lane >> 4;
   const int NT = (n + 15) >> 4;
+  const bool bottom = nd > 0 && blockIdx.x == 1;
+  const int m = nd > 0 ? NT - nd - 7 : NT;   // first separator tile row (S order)
+  const int NTf = nd > 0 ? (bottom ? nd : m + 7) : NT;   // tile rows this workgroup factors
+  double* Wb = bottom ? Wg + (size_t)NT * kTB * 256 : Wg;
+  double* zpg = Wg + (size_t)2 * NT * kTB * 256;   // [16 nd] the bottom half's z'
+  double* sepb = zpg + 16 * NT;                     // [49][256] separator contribution
+  double* sepy = sepb + 49 * 256;                   // [7][16]   its rhs
+  const TileSrc ts{bottom ? 1 : 0, 16 * NT, bottom ? nd : (1 << 28)};
   double* xs = tdyn;              // [16 NT] back-substitution solution
   double* zp = tdyn + 16 * NT;    // [16 NT] Z_K^T z_K
   int* tend = reinterpret_cast<int*>(tdyn + 32 * NT);   // [NT] band end (tiles, exclusive) per tile row
-  for (int k = tid; k < NT; k += kTileThreads) tend[k] = (panel_jend[k] + 15) >> 4;
+  for (int k = tid; k < NT; k += kTileThreads) {
+    if (!bottom) {
+      tend[k] = min((panel_jend[k] + 15) >> 4, NTf);
+    } else {
+      // reversed row k = column c = NT-1-k of S: its band reaches back to lo(c), the first row whose band
+      // covers c (band ends are non-decreasing), so the reversed row ends at NT - lo(c)
+      const int c = NT - 1 - k;
+      int lo = c;
+      for (int i = max(0, c - kTB); i < c; ++i)
+        if (((panel_jend[i] + 15) >> 4) > c) { lo = i; break; }
+      tend[k] = min(NT - lo, nd + 7);
+    }
+  }
+  // hand-off counter: the bottom half has finished this launch once tflag[0] exceeds the top half's count
+  const int epoch = (nd > 0 && !bottom) ? tflag[1] : 0;
   if (tid == 0) sh.fail = 0;
   bool bad = false;
+  // Columns J and J+1 (mod 8) on one SIMD: the owner of phase K (column K+1) then shares its SIMD with the
+  // late wave of column K (one W tile, a reload) or with column K+2 (its first few tiles), not with a
+  // column four ahead and its full band of trailing MFMAs.  SIMD ids from HW_ID; any other placement than
+  // two waves per SIMD keeps column = wave.
+  if (lane == 0) sh.simd[wave] = __builtin_amdgcn_s_getreg((1 << 11) | (4 << 6) | 4);   // HW_ID.SIMD_ID
+  __syncthreads();
+  int col = wave;
+  if (simdmap) {
+    const int my = sh.simd[wave];
+    int cnt[4] = {0, 0, 0, 0}, rank = 0;
+#pragma unroll
+    for (int w = 0; w < kTB; ++w) {
+      const int sw = sh.simd[w] & 3;
+      cnt[sw] += 1;
+      if (w < wave && sw == my) rank += 1;
+    }
+    if (cnt[0] == 2 && cnt[1] == 2 && cnt[2] == 2 && cnt[3] == 2) col = 2 * my + rank;
+  }
   {
     f64x4 acc[kTB];
     double ypart = 0.0;
-    int J = wave;
+    int J = col;
     bool late = false;
-    tile_col_load(acc, ypart, d, J, li, lk);
-    if (J == 0) {   // D_0 has no updates: factor it and take column 8
-      bad |= tile_diag(acc[0], ypart, sh, zp, 0, lane, li, lk);
+    if (J == 0) {
+      // D_0 has no updates: load it and column 8 together, then factor D_0 while column 8 arrives
+      const f64x4 D0 = tile_load(d.S, d.n, 0, 0, li, lk, ts);
+      const int sj0 = ts.rev ? ts.np - 1 - li : li;
+      const double y0 = d.S[(lk == 0 && sj0 < n && 0 < ts.sep) ? n * n + sj0 : n * n + n];
       J = kTB;
-      tile_col_load(acc, ypart, d, J, li, lk);
+      tile_col_load(acc, ypart, d, J, 0, li, lk, ts);   // slots of phase 0
+      bad |= tile_diag(D0, y0, sh, zp, 0, lane, li, lk);
+    } else {
+      tile_col_load(acc, ypart, d, J, 0, li, lk, ts);
     }
     SG_TSTAMP(0)
     __syncthreads();
     SG_TSTAMP(1)
-    for (int K0 = 0; K0 < NT; K0 += kTB) {
-#define SG_TILE_PHASE(U)                                                                  \
-      if (K0 + (U) < NT) {                                                                \
-        tile_phase<U, kStamp>(acc, ypart, J, late, bad, sh, d, Wg, zp, tend, K0 + (U), NT, lane, li, lk, tacc, tlast); \
-        SG_TSTAMP(2)                                                                      \
-        lds_barrier();                                                                    \
-        SG_TSTAMP(3)                                                                      \
+#pragma nounroll
+    for (int K = 0; K < NTf; ++K) {
+      if (nd > 0 && !bottom && K == m - 1) {
+        // relaxed polls, one acquire (an acquiring poll would invalidate the cache on every round)
+        int spin = 0;
+        while (__hip_atomic_load(tflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= epoch &&
+               ++spin < kSepSpinMax)
+          __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        bad |= spin >= kSepSpinMax;
+        sep_merge(acc, ypart, J, m, sepb, sepy, lane, li, lk);
       }
-      SG_TILE_PHASE(0) SG_TILE_PHASE(1) SG_TILE_PHASE(2) SG_TILE_PHASE(3)
-      SG_TILE_PHASE(4) SG_TILE_PHASE(5) SG_TILE_PHASE(6) SG_TILE_PHASE(7)
-#undef SG_TILE_PHASE
+      tile_phase<kStamp>(acc, ypart, J, late, bad, sh, d, Wb, zp, tend, K, NTf, lane, li, lk, ts, tacc, tlast);
+      SG_TSTAMP(2)
+      // the owner of the next diagonal (now late) is on the critical path until the barrier: it rotates after
+      if (!late) tile_rotate(acc);
+      lds_barrier();
+      if (late) tile_rotate(acc);
+      SG_TSTAMP(3)
+    }
+    if (bottom) {
+      // row nd-1's updates of the separator columns (slots of phase nd), then the hand-off
+      tile_final(acc, J, late, sh, Wb, tend, nd, lane, li, lk);
+      sep_write(acc, ypart, J, nd, NT, m, sepb, sepy, li, lk);
     }
   }
+  if (bottom) {
+    if (bad && lane == 0) sh.fail = 1;
+    __syncthreads();   // every owner's z' in LDS
+    for (int i = tid; i < 16 * nd; i += kTileThreads) zpg[i] = zp[i];
+    if (tid == 0) zpg[16 * nd] = sh.fail ? 1.0 : 0.0;   // failure marker (slot past z': read by the top half)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // every wave's hand-off stores, then one signal
+    __syncthreads();
+    if (tid == 0) {
+      const int c = tflag[0];
+      __hip_atomic_store(tflag, c + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+  if (nd > 0 && zpg[16 * nd] != 0.0) bad = true;
   if (bad && lane == 0) sh.fail = 1;
   __syncthreads();   // W tiles (global) and z' visible to every wave
   SG_TSTAMP(4)
-  if (wave == 0) {
-    // Back substitution in one wave, rows K = NT-1 .. 0:  x_K = z'_K - sum_{d=1..7} W_{K,K+d} x_{K+d}, with no
-    // LDS round trip on the row-to-row chain.  Lane (li, lk) holds rows lk + 4q, column li of each W tile
-    // (acc layout) and x_{K+d}[li] in registers (xw[d-1]; zero past the last row, and W tiles outside the
-    // band are zero), so the d >= 2 terms are formed before x_{K+1} is known.  The 16-lane row sums run as a
-    // DPP butterfly (quad xor 1, quad xor 2, half-row mirror, row mirror: bitwise the same sum in every lane),
-    // and one shuffle moves x_K[li] (row li & 3, register li >> 2) to every lane.  W rows are prefetched two
-    // rows ahead (two register buffers, the loop unrolled by two); z' is read one row ahead.
+  {
     double xw[kTB - 1];
 #pragma unroll
     for (int dd = 0; dd < kTB - 1; ++dd) xw[dd] = 0.0;
-    auto wload = [&](double (&w)[kTB - 1][4], int K) {
-      const double* src = Wg + (size_t)(K >= 0 ? K : 0) * kTB * 256 + lane;
+    if (nd == 0) {
+      if (wave == 0) bs_chain<false>(Wg, zp, xs, NT - 1, 0, xw, NT, lane, li, lk);
+    } else {
+      // separator rows, then A (wave 0, continuing its registers) beside B (wave 1, reversed)
+      if (wave == 0) bs_chain<false>(Wg, zp, xs, m + 6, m, xw, NT, lane, li, lk);
+      __syncthreads();
+      if (wave == 0) {
+        bs_chain<false>(Wg, zp, xs, m - 1, 0, xw, NT, lane, li, lk);
+      } else if (wave == 1) {
+        // x of reversed rows nd .. nd+6 (the separator, S tile rows m+6 .. m)
 #pragma unroll
-      for (int dd = 1; dd < kTB; ++dd)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) w[dd - 1][q] = src[dd * 256 + q * 64];
-    };
-    const int srcl = 16 * (li & 3) + li;   // the lane holding x_K[li] after the row sums
-    unsigned qbits = 1u << (li >> 2);
-    asm volatile("" : "+v"(qbits));
-    auto bs_row = [&](int K, double (&w)[kTB - 1][4], const double (&zk)[4]) {
-      double p[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int dd = kTB - 1; dd >= 1; --dd)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) p[q] = fma(w[dd - 1][q], xw[dd - 1], p[q]);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        double v = p[q];
-        v += dpp_d<0xB1>(v);
-        v += dpp_d<0x4E>(v);
-        v += dpp_d<0x141>(v);
-        v += dpp_d<0x140>(v);
-        p[q] = zk[q] - v;   // x_K[lk + 4q], the same bits in every lane of the row
+        for (int dd = 1; dd < kTB; ++dd) xw[dd - 1] = xs[16 * (NT - nd - dd) + 15 - li];
+        bs_chain<true>(Wg + (size_t)NT * kTB * 256, zpg, xs, nd - 1, 0, xw, NT, lane, li, lk);
       }
-      // register p[li >> 2] by opaque bit masks (a lane-dependent ?: chain compiles to divergent branches)
-      unsigned long long mb = 0ull;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        int m;
-        asm volatile("v_bfe_i32 %0, %1, %2, 1" : "=v"(m) : "v"(qbits), "n"(q));
-        mb |= (unsigned long long)__double_as_longlong(p[q]) & (unsigned long long)(long long)m;
-      }
-      const double xk = __shfl(__longlong_as_double((long long)mb), srcl);
-      xs[16 * K + li] = xk;   // the same bits from every row of lanes
-#pragma unroll
-      for (int dd = kTB - 2; dd >= 1; --dd) xw[dd] = xw[dd - 1];
-      xw[0] = xk;
-      wload(w, K - 2);   // this buffer's next row
-    };
-    double wA[kTB - 1][4], wB[kTB - 1][4], zA[4], zB[4];
-    wload(wA, NT - 1);
-    wload(wB, NT - 2);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) zA[q] = zp[16 * (NT - 1) + lk + 4 * q];
-    int K = NT - 1;
-    for (; K >= 1; K -= 2) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) zB[q] = zp[16 * (K - 1) + lk + 4 * q];
-      bs_row(K, wA, zA);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) zA[q] = zp[16 * (K >= 2 ? K - 2 : 0) + lk + 4 * q];
-      bs_row(K - 1, wB, zB);
     }
-    if (K == 0) bs_row(0, wA, zA);
   }
+  if (tid == 0 && nd > 0) tflag[1] = epoch + 1;
   SG_TSTAMP(5)
   __syncthreads();
   double* y = d.work;
@@ -3589,10 +3801,19 @@ void BaSolver::Load(const sg_problem& p) {
   chol_tiles_ = n_ > 0 && nk_ == 0 && npanel <= kTileMaxNT && !getenv("SG_CHOL_WINDOW");
   for (int pk = 0; pk < npanel; ++pk)
     if ((panel_jmax[pk] + kCholNb - 1) / kCholNb - pk > kTB) chol_tiles_ = false;
+  // dissected band: a second workgroup factors the bottom nd tile rows (reversed) while the first factors
+  // the top, both meeting at a 7-tile separator (k_chol_tiles); worth it from about 12 tile rows
+  chol_nd_ = 0;
+  if (chol_tiles_ && npanel >= kSplitMinNT && !(getenv("SG_CHOL_SPLIT") && atoi(getenv("SG_CHOL_SPLIT")) == 0))
+    chol_nd_ = (npanel - 9) / 2;   // the bottom (nd rows + hand-off) done before the top reaches row m - 1
+  if (chol_nd_ > 0 && getenv("SG_CHOL_ND")) chol_nd_ = std::max(1, std::min(atoi(getenv("SG_CHOL_ND")), (npanel - 9) / 2 + 1));
   if (chol_tiles_) {
-    std::vector<double> wz((size_t)npanel * kTB * 256 + 2, 0.0);   // W tiles, then the constants {0, 1}
+    // W tiles of the top and bottom halves, the bottom's z' (+ failure slot), the separator contribution
+    // and its rhs, then the constants {0, 1}
+    std::vector<double> wz((size_t)2 * npanel * kTB * 256 + 16 * (size_t)npanel + 49 * 256 + 7 * 16 + 2, 0.0);
     wz.back() = 1.0;
     stager_->Add(Wg_, wz);
+    stager_->Add(tflag_, std::vector<int32_t>(2, 0));
     tile_lds_ = (size_t)npanel * 32 * sizeof(double) + (size_t)npanel * sizeof(int32_t);
   }
   // k_S_reduce work: the band tiles (R <= C) of the frame columns, and per tile the segment tiles covering it
@@ -4037,11 +4258,11 @@ void BaSolver::Iterate(int n) {
     }
     TimedLaunchBegin(kKChol);
     if (chol_tiles_ && d.stamps)
-      hipLaunchKernelGGL(k_chol_tiles<true>, dim3(1), dim3(kTileThreads), tile_lds_, stream_, d,
-                         (const int32_t*)work_i_.ptr, Wg_.ptr);
+      hipLaunchKernelGGL(k_chol_tiles<true>, dim3(chol_nd_ > 0 ? 2 : 1), dim3(kTileThreads), tile_lds_, stream_, d,
+                         (const int32_t*)work_i_.ptr, Wg_.ptr, tflag_.ptr, chol_nd_, chol_simdmap_);
     else if (chol_tiles_)
-      hipLaunchKernelGGL(k_chol_tiles<false>, dim3(1), dim3(kTileThreads), tile_lds_, stream_, d,
-                         (const int32_t*)work_i_.ptr, Wg_.ptr);
+      hipLaunchKernelGGL(k_chol_tiles<false>, dim3(chol_nd_ > 0 ? 2 : 1), dim3(kTileThreads), tile_lds_, stream_, d,
+                         (const int32_t*)work_i_.ptr, Wg_.ptr, tflag_.ptr, chol_nd_, chol_simdmap_);
     else if (chol_window_ && d.stamps)
       hipLaunchKernelGGL(k_cholesky_window<true>, dim3(1), dim3(kCholThreads), kCholLds, stream_, d,
                          (const int32_t*)work_i_.ptr, rdg_.ptr);
@@ -4257,6 +4478,7 @@ void BaSolver::Info(sg_ba_info* o) const {
   o->n = n_;
   o->band_tiles = band_tiles_;
   o->cholesky_path = chol_tiles_ ? 0 : (chol_window_ ? 1 : 2);
+  o->cholesky_split = chol_tiles_ ? chol_nd_ : 0;
   o->num_pairs = (int32_t)std::min<size_t>(npairs_, INT32_MAX);
   o->rank = comm_ ? comm_->rank() : 0;
   o->nranks = comm_ ? comm_->nranks() : 1;

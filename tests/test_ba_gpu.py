@@ -270,6 +270,41 @@ def test_packed_band_exchange_is_exact(gpu_lib, monkeypatch):
     np.testing.assert_allclose(p0.X, p1.X, rtol=1e-9, atol=1e-12)
 
 
+
+@pytest.mark.parametrize("frames,points", [(36, 8000), (40, 9000), (50, None)])
+def test_dissected_band_matches_one_workgroup(gpu_lib, monkeypatch, frames, points):
+    """The tiled Cholesky factors the band from both ends at once (k_chol_tiles: a second workgroup factors
+    the bottom tile rows of the index-reversed system and hands its separator contribution over; DESIGN.md
+    4).  Against the one-workgroup factorisation (SG_CHOL_SPLIT=0) the solve must be the same up to rounding
+    (the separator sums in another order): same steps, cost rel 1e-12, poses 1e-10.  Frame counts give
+    n = 204 (13 tile rows, padded: 2 bottom), 228 (15, padded: 3 bottom) and C2's 288 (18: 4 bottom)."""
+    if points is None:
+        m = make_config("C2")
+    else:
+        m = make_scene(num_frames=frames, num_points=points, seed=5, run_max=14)
+    pa = ba.problem_from_map_frames(m, m.num_frames - 2, m.num_frames, 2.0)
+    nt = (6 * (m.num_frames - 2) + 15) // 16
+    out = []
+    for split in (False, True):
+        monkeypatch.setenv("SG_CHOL_SPLIT", "1" if split else "0")
+        p = pa.copy()
+        g = ba.BundleAdjuster()
+        g.load(p)
+        info = g.info()
+        assert info["cholesky"].startswith("tiled band")
+        assert info["cholesky_split"] == ((nt - 9) // 2 if split else 0)
+        s = g.solve(default_solver_options(max_num_iterations=8))
+        out.append((s, p))
+        g.close()
+    (s0, p0), (s1, p1) = out
+    assert s0["ok"] == s1["ok"] == 1
+    assert s0["num_iterations"] == s1["num_iterations"]
+    assert s0["num_successful_steps"] == s1["num_successful_steps"]
+    assert abs(s0["final_cost"] - s1["final_cost"]) <= 1e-12 * s0["final_cost"]
+    np.testing.assert_allclose(p0.q, p1.q, rtol=0, atol=1e-10)
+    np.testing.assert_allclose(p0.t, p1.t, rtol=1e-10, atol=1e-10)
+    np.testing.assert_allclose(p0.X, p1.X, rtol=1e-9, atol=1e-10)
+
 def _intrinsics_scene(seed=1):
     """C1-sized scene whose intrinsics start off the generating camera (focal +0.4 %, principal point +1.5 px,
     a little radial distortion), so SolveAllFrames(..., solve_cameras=true) has intrinsics to recover."""
