@@ -61,6 +61,7 @@ class BaSolver {
   int chol_nd_ = 0;            // dissected band: tile rows the second workgroup factors bottom-up (0: one WG)
   DBuf<int32_t> tflag_;        // dissected band hand-off counters {bottom done, top done}
   int chol_simdmap_ = !(getenv("SG_CHOL_SIMDMAP") && atoi(getenv("SG_CHOL_SIMDMAP")) == 0);
+  bool chol_cand_lds_ = false;   // candidate-pass operands staged in the Cholesky's LDS (small problems)
   bool pack_force_ = getenv("SG_PACK_S") != nullptr;   // pack/unpack S on one rank too (tests the path)
   size_t npack_ = 0;                                      // band of S + rhs, doubles (all-reduce size)
   bool stamp_on_ = false;

@@ -1701,6 +1701,112 @@ __device__ __forceinline__ void chol_candidates(const Dev& d, const double* y, i
   }
 }
 
+// The tiled Cholesky's candidate pass with its operands staged in LDS: waves the back substitution does not
+// use load them (poses at x[cur], frame blocks and freedom flags, the column scales, the FrameDistance
+// pairs, Jacobians and residuals) while it runs, so the pass after it is LDS-only but for the candidate
+// stores.  Same arithmetic and summation order as chol_candidates.
+constexpr int kCandMax = 1024;   // frames / FrameDistance residuals staged (more: chol_candidates)
+struct CandLds {
+  double *q, *t, *sc, *J, *r, *tn;
+  int *fb, *fl, *fa, *fbb, *ba, *bb;
+  static size_t bytes(int F, int D, int n) {
+    return (size_t)(7 * F + n + 7 * D + 3 * F) * sizeof(double) + (size_t)(2 * F + 4 * D) * sizeof(int);
+  }
+  __device__ void carve(double* base, int F, int D, int n) {
+    q = base; t = q + 4 * F; sc = t + 3 * F; J = sc + n; r = J + 6 * D; tn = r + D;
+    fb = reinterpret_cast<int*>(tn + 3 * F); fl = fb + F; fa = fl + F; fbb = fa + D; ba = fbb + D; bb = ba + D;
+  }
+};
+
+__device__ __forceinline__ void cand_prefetch(const Dev& d, const CandLds& c, int cur, int i0, int ni) {
+  for (int f = i0; f < d.F; f += ni) {
+    const int b = d.frame_block[f];
+    c.fb[f] = b;
+    c.fl[f] = (d.rot_free[f] ? 1 : 0) | (d.trans_free[f] ? 2 : 0);
+    for (int a = 0; a < 4; ++a) c.q[4 * f + a] = d.q[cur][4 * f + a];
+    for (int a = 0; a < 3; ++a) c.t[3 * f + a] = d.t[cur][3 * f + a];
+  }
+  for (int i = i0; i < d.n; i += ni) c.sc[i] = d.scale_c[i];
+  for (int e = i0; e < d.D; e += ni) {
+    const int fa = d.fd_a[e], fb = d.fd_b[e];
+    c.fa[e] = fa;
+    c.fbb[e] = fb;
+    c.ba[e] = d.frame_block[fa];
+    c.bb[e] = d.frame_block[fb];
+    for (int j = 0; j < 6; ++j) c.J[6 * e + j] = d.fd_J[6 * e + j];
+    c.r[e] = d.fd_r[e];
+  }
+}
+
+template <int NT>
+__device__ __forceinline__ void chol_candidates_lds(const Dev& d, const double* y, int fail, const CandLds& c,
+                                                    int cur) {
+  __shared__ double red[4 * NT / 64];
+  const int tid = threadIdx.x;
+  const int nxt = cur ^ 1;
+  double step2 = 0.0, candx2 = 0.0, model = 0.0, candcost = 0.0;
+  for (int f = tid; f < d.F; f += NT) {
+    const double* q = c.q + 4 * f;
+    const double* t = c.t + 3 * f;
+    double* qn = d.q[nxt] + 4 * f;
+    double* tn = d.t[nxt] + 3 * f;
+    const int b = c.fb[f];
+    const int fl = c.fl[f];
+    double qq[4] = {q[0], q[1], q[2], q[3]}, tt[3] = {t[0], t[1], t[2]};
+    if (b >= 0) {
+      if (fl & 1) {
+        double dl[3];
+        for (int a = 0; a < 3; ++a) dl[a] = -y[6 * b + a] * c.sc[6 * b + a];
+        QuatPlus(q, dl, qq);
+        for (int a = 0; a < 4; ++a) {
+          step2 += (qq[a] - q[a]) * (qq[a] - q[a]);
+          candx2 += qq[a] * qq[a];
+        }
+      }
+      if (fl & 2) {
+        for (int a = 0; a < 3; ++a) {
+          tt[a] = t[a] - y[6 * b + 3 + a] * c.sc[6 * b + 3 + a];
+          step2 += (tt[a] - t[a]) * (tt[a] - t[a]);
+          candx2 += tt[a] * tt[a];
+        }
+      }
+    }
+    for (int a = 0; a < 4; ++a) qn[a] = qq[a];
+    for (int a = 0; a < 3; ++a) {
+      tn[a] = tt[a];
+      c.tn[3 * f + a] = tt[a];
+    }
+  }
+  __syncthreads();
+  for (int dd = tid; dd < d.D; dd += NT) {
+    const int fa = c.fa[dd], fb = c.fbb[dd];
+    const int ba = c.ba[dd], bb = c.bb[dd];
+    const double* Jd = c.J + 6 * dd;
+    double m = 0.0;
+    for (int j = 0; j < 3; ++j) {
+      if (ba >= 0) m += Jd[j] * c.sc[6 * ba + 3 + j] * (-y[6 * ba + 3 + j]);
+      if (bb >= 0) m += Jd[3 + j] * c.sc[6 * bb + 3 + j] * (-y[6 * bb + 3 + j]);
+    }
+    model -= m * (c.r[dd] + 0.5 * m);
+    const double* ta = c.tn + 3 * fa;
+    const double* tb = c.tn + 3 * fb;
+    const double e0 = ta[0] - tb[0], e1 = ta[1] - tb[1], e2 = ta[2] - tb[2];
+    const double r = 0.1 * (sqrt(e0 * e0 + e1 * e1 + e2 * e2) - d.fd_target);
+    double rho0, rho1;
+    Cauchy(r * r, d.fd_b2, d.fd_inv_b2, &rho0, &rho1);
+    candcost += 0.5 * rho0;
+  }
+  double sums[4] = {step2, candx2, model, candcost};
+  block_sum_multi<NT, 4>(sums, red);
+  if (tid == 0) {
+    d.xchg_chol[kCStep2] = sums[0];
+    d.xchg_chol[kCCandX2] = sums[1];
+    d.xchg_chol[kCModel] = sums[2];
+    d.xchg_chol[kCCandCost] = sums[3];
+    d.xchg_chol[kCFail] = fail ? 1.0 : 0.0;
+  }
+}
+
 // Diagnostic stamps (SG_STAMP=1 builds of the launch only): thread 0 accumulates s_memtime deltas per phase
 // in registers (a global read-modify-write here would wait on every outstanding load) and adds them to
 // d.stamps once at the end.
@@ -2240,6 +2346,7 @@ struct TileShared {
   double prw[2 * kCholNb];     // the owner's next two pivot rows
   int fail;
   int simd[kTB];               // SIMD of each wave
+  double Id[16 * kTLd];        // the identity (the factor's augmented columns)
 };
 
 __device__ __forceinline__ f64x4 mfma_f64_k16(const double (&a)[4], const f64x4& b, f64x4 c) {
@@ -2304,30 +2411,17 @@ __device__ __forceinline__ f64x4 tile_load(const double* __restrict__ S, int n, 
 // (lane 32) as augmented columns; lanes 0-15 hold the columns of D.  Right-looking, two pivots per LDS
 // broadcast (every lane derives pivot row j+1 after pivot j itself).  On return lanes 16-31 hold the columns
 // of Z = U^-T and lane 32 holds z = U^-T y.  Returns true on a non-positive pivot.
-__device__ __forceinline__ bool tile_factor(const double* D, const double* Yk, double* prw, double (&ca)[16]) {
+__device__ __forceinline__ bool tile_factor(const double* D, const double* Yk, const double* Id, double* prw,
+                                            double (&ca)[16]) {
   const int lane = opaque_lane();
   const int c = lane & 15;
   const bool isy = lane == 32;
-  const double* b0 = isy ? Yk : D + c;
+  // D arrives with its lower triangle zeroed and the identity is a constant LDS tile, so every lane just
+  // loads its column (no per-element masking on the critical path)
+  const double* b0 = isy ? Yk : ((lane >= 16 && lane < 32) ? Id + c : D + c);
   const int rs = isy ? 1 : kTLd;
 #pragma unroll
   for (int r = 0; r < kCholNb; ++r) ca[r] = b0[r * rs];
-  {
-    // rows kept (the upper part of D's columns, all of y) and the identity's ones, as opaque bit masks
-    unsigned keepbits = lane < 16 ? ((2u << c) - 1u) : (isy ? 0xFFFFu : 0u);
-    unsigned onebits = (lane >= 16 && lane < 32) ? (1u << c) : 0u;
-    asm volatile("" : "+v"(keepbits), "+v"(onebits));
-    const unsigned long long kOneBits = 0x3FF0000000000000ull;
-#pragma unroll
-    for (int r = 0; r < kCholNb; ++r) {
-      int km, om;
-      asm volatile("v_bfe_i32 %0, %1, %2, 1" : "=v"(km) : "v"(keepbits), "n"(r));
-      asm volatile("v_bfe_i32 %0, %1, %2, 1" : "=v"(om) : "v"(onebits), "n"(r));
-      const unsigned long long b = (unsigned long long)__double_as_longlong(ca[r]);
-      ca[r] = __longlong_as_double((long long)((b & (unsigned long long)(long long)km) |
-                                               (kOneBits & (unsigned long long)(long long)om)));
-    }
-  }
   bool bad = false;
   double u0[kCholNb], u1[kCholNb];
   double* prw2 = prw + kCholNb;
@@ -2387,11 +2481,11 @@ __device__ __forceinline__ bool tile_factor(const double* D, const double* Yk, d
 __device__ __forceinline__ bool tile_diag(const f64x4& D, double ypart, TileShared& sh, double* zp, int K,
                                           int lane, int li, int lk) {
 #pragma unroll
-  for (int q = 0; q < 4; ++q) sh.Dw[(lk + 4 * q) * kTLd + li] = D[q];
+  for (int q = 0; q < 4; ++q) sh.Dw[(lk + 4 * q) * kTLd + li] = (lk + 4 * q <= li) ? D[q] : 0.0;
   const double ys = sum_rows4(ypart);
   if (lk == 0) sh.Yw[li] = ys;
   double ca[kCholNb];
-  const bool bad = tile_factor(sh.Dw, sh.Yw, sh.prw, ca);
+  const bool bad = tile_factor(sh.Dw, sh.Yw, sh.Id, sh.prw, ca);
   double* Zs = sh.Zs[K & 3];
   double* zk = sh.zK[K & 3];
   if (lane >= 16 && lane < 32) {
@@ -2690,9 +2784,9 @@ constexpr int kSplitMinNT = 13;
 template <bool kStamp>
 __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_t* panel_jend,
                                                              double* __restrict__ Wg, int32_t* tflag, int nd,
-                                                             int simdmap) {
+                                                             int flags) {
+  const bool simdmap = (flags & 1) != 0;   // bit 0: columns J, J+1 on one SIMD; bit 1: LDS-staged candidates
   const LmState* st = d.st;
-  if (st->done) return;
   unsigned long long tlast = kStamp ? __builtin_amdgcn_s_memtime() : 0ull, tacc[16] = {};
   __shared__ TileShared sh;
   extern __shared__ double tdyn[];
@@ -2711,6 +2805,10 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
   double* xs = tdyn;              // [16 NT] back-substitution solution
   double* zp = tdyn + 16 * NT;    // [16 NT] Z_K^T z_K
   int* tend = reinterpret_cast<int*>(tdyn + 32 * NT);   // [NT] band end (tiles, exclusive) per tile row
+  // candidate-pass operands (staged during the back substitution) after the band ends
+  const bool cand_lds = (flags & 2) != 0;
+  CandLds cl;
+  cl.carve(tdyn + 32 * NT + (NT + 1) / 2, d.F, d.D, n);
   for (int k = tid; k < NT; k += kTileThreads) {
     if (!bottom) {
       tend[k] = min((panel_jend[k] + 15) >> 4, NTf);
@@ -2733,6 +2831,7 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
   // column four ahead and its full band of trailing MFMAs.  SIMD ids from HW_ID; any other placement than
   // two waves per SIMD keeps column = wave.
   if (lane == 0) sh.simd[wave] = __builtin_amdgcn_s_getreg((1 << 11) | (4 << 6) | 4);   // HW_ID.SIMD_ID
+  for (int i = tid; i < 16 * kTLd; i += kTileThreads) sh.Id[i] = (i / kTLd == i % kTLd) ? 1.0 : 0.0;
   __syncthreads();
   int col = wave;
   if (simdmap) {
@@ -2751,17 +2850,24 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
     double ypart = 0.0;
     int J = col;
     bool late = false;
+    // the first column's loads go out before the LmState read returns (a finished solve exits after them)
+    f64x4 D0;
+    double y0 = 0.0;
     if (J == 0) {
       // D_0 has no updates: load it and column 8 together, then factor D_0 while column 8 arrives
-      const f64x4 D0 = tile_load(d.S, d.n, 0, 0, li, lk, ts);
+      D0 = tile_load(d.S, d.n, 0, 0, li, lk, ts);
       const int sj0 = ts.rev ? ts.np - 1 - li : li;
-      const double y0 = d.S[(lk == 0 && sj0 < n && 0 < ts.sep) ? n * n + sj0 : n * n + n];
+      y0 = d.S[(lk == 0 && sj0 < n && 0 < ts.sep) ? n * n + sj0 : n * n + n];
       J = kTB;
-      tile_col_load(acc, ypart, d, J, 0, li, lk, ts);   // slots of phase 0
-      bad |= tile_diag(D0, y0, sh, zp, 0, lane, li, lk);
-    } else {
-      tile_col_load(acc, ypart, d, J, 0, li, lk, ts);
     }
+    const int done = st->done;
+    asm volatile("" ::: "memory");   // the LmState load goes out before column 8's (its wait then skips them)
+    tile_col_load(acc, ypart, d, J, 0, li, lk, ts);   // slots of phase 0
+    if (done) return;
+    if (col == 0)
+      bad |= tile_diag(D0, y0, sh, zp, 0, lane, li, lk);
+    else if (cand_lds)   // the seven waves that wait at the first barrier
+      cand_prefetch(d, cl, st->cur, (col - 1) * 64 + lane, kTileThreads - 64);
     SG_TSTAMP(0)
     __syncthreads();
     SG_TSTAMP(1)
@@ -2808,6 +2914,7 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
   if (bad && lane == 0) sh.fail = 1;
   __syncthreads();   // W tiles (global) and z' visible to every wave
   SG_TSTAMP(4)
+  const int cur = st->cur;
   {
     double xw[kTB - 1];
 #pragma unroll
@@ -2836,8 +2943,11 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
     d.xc[i] = xs[i];
     y[i] = xs[i];
   }
-  __syncthreads();
-  chol_candidates<kTileThreads>(d, xs, sh.fail);
+  if (!cand_lds) __syncthreads();
+  if (cand_lds)
+    chol_candidates_lds<kTileThreads>(d, xs, sh.fail, cl, cur);
+  else
+    chol_candidates<kTileThreads>(d, xs, sh.fail);
   SG_TSTAMP(6)
   if (kStamp && lane == 0 && wave < 2)
     for (int s_ = 0; s_ < 16; ++s_) d.stamps[16 * wave + s_] += tacc[s_];
@@ -3814,7 +3924,9 @@ void BaSolver::Load(const sg_problem& p) {
     wz.back() = 1.0;
     stager_->Add(Wg_, wz);
     stager_->Add(tflag_, std::vector<int32_t>(2, 0));
-    tile_lds_ = (size_t)npanel * 32 * sizeof(double) + (size_t)npanel * sizeof(int32_t);
+    tile_lds_ = (size_t)npanel * 32 * sizeof(double) + (size_t)(npanel + 1) / 2 * sizeof(double);
+    chol_cand_lds_ = F_ <= kCandMax && D_ <= kCandMax && tile_lds_ + CandLds::bytes(F_, D_, n_) <= 100 * 1024;
+    if (chol_cand_lds_) tile_lds_ += CandLds::bytes(F_, D_, n_);
   }
   // k_S_reduce work: the band tiles (R <= C) of the frame columns, and per tile the segment tiles covering it
   // (segment order).  A segment tile outside the band is zero (no point couples its rows and columns).
@@ -4259,10 +4371,12 @@ void BaSolver::Iterate(int n) {
     TimedLaunchBegin(kKChol);
     if (chol_tiles_ && d.stamps)
       hipLaunchKernelGGL(k_chol_tiles<true>, dim3(chol_nd_ > 0 ? 2 : 1), dim3(kTileThreads), tile_lds_, stream_, d,
-                         (const int32_t*)work_i_.ptr, Wg_.ptr, tflag_.ptr, chol_nd_, chol_simdmap_);
+                         (const int32_t*)work_i_.ptr, Wg_.ptr, tflag_.ptr, chol_nd_,
+                         chol_simdmap_ | (chol_cand_lds_ ? 2 : 0));
     else if (chol_tiles_)
       hipLaunchKernelGGL(k_chol_tiles<false>, dim3(chol_nd_ > 0 ? 2 : 1), dim3(kTileThreads), tile_lds_, stream_, d,
-                         (const int32_t*)work_i_.ptr, Wg_.ptr, tflag_.ptr, chol_nd_, chol_simdmap_);
+                         (const int32_t*)work_i_.ptr, Wg_.ptr, tflag_.ptr, chol_nd_,
+                         chol_simdmap_ | (chol_cand_lds_ ? 2 : 0));
     else if (chol_window_ && d.stamps)
       hipLaunchKernelGGL(k_cholesky_window<true>, dim3(1), dim3(kCholThreads), kCholLds, stream_, d,
                          (const int32_t*)work_i_.ptr, rdg_.ptr);
