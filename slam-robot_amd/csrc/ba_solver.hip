@@ -462,10 +462,11 @@ __global__ __launch_bounds__(kRedThreads) void k_cam_reduce(Dev d) {
   __shared__ double redm[kRedThreads / 64];
   double v[kXNum] = {0, 0, 0, 0, 0};
   double gm = 0.0;
-  for (int c0 = tid; c0 < d.nlin; c0 += 2 * kRedThreads) {
-    double t[2][kXNum + 1];
+  constexpr int kScalU = 2;   // chunks' loads in flight per thread (8 measured slower)
+  for (int c0 = tid; c0 < d.nlin; c0 += kScalU * kRedThreads) {
+    double t[kScalU][kXNum + 1];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < kScalU; ++u) {
       const int c = c0 + u * kRedThreads;
       const double* sc = d.lin_scal + (c < d.nlin ? c : 0);   // coalesced: slot j at [j * nlin + chunk]
       const size_t ns = d.nlin;
@@ -477,7 +478,7 @@ __global__ __launch_bounds__(kRedThreads) void k_cam_reduce(Dev d) {
       t[u][kXNum] = sc[kGmax * ns];
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < kScalU; ++u)
       if (c0 + u * kRedThreads < d.nlin) {
 #pragma unroll
         for (int j = 0; j < kXNum; ++j) v[j] += t[u][j];
@@ -2496,13 +2497,20 @@ __device__ __forceinline__ bool tile_diag(const f64x4& D, double ypart, TileShar
 #pragma unroll
     for (int r = 0; r < kCholNb; ++r) zk[r] = ca[r];
   }
-  if (lane >= 16 && lane < 32) {
+  return bad;
+}
+
+// z'_K = Z_K^T z_K for the back substitution, from the posted Z_K and z_K (LDS ring slot K & 3): formed by
+// the owner one phase later (its late phase), off the pivot chain.
+__device__ __forceinline__ void tile_zp(const TileShared& sh, double* zp, int K, int lane) {
+  if (lane < 16) {
+    const double* Zs = sh.Zs[K & 3];
+    const double* zk = sh.zK[K & 3];
     double s = 0.0;
 #pragma unroll
-    for (int r = 0; r < kCholNb; ++r) s = fma(ca[r], zk[r], s);
-    zp[16 * K + lane - 16] = s;
+    for (int r = 0; r < kCholNb; ++r) s = fma(Zs[r * kTLd + lane], zk[r], s);
+    zp[16 * K + lane] = s;
   }
-  return bad;
 }
 
 // Diagnostic stamps (SG_STAMP=1): lane 0 of every wave accumulates s_memtime deltas per phase; waves 0 and 1
@@ -2571,6 +2579,7 @@ __device__ __forceinline__ void tile_phase(f64x4 (&acc)[kTB], double& ypart, int
     J += kTB;
     tile_col_load(acc, ypart, d, J, K, li, lk, ts);
     if (hasw) tile_w_store(Wt, Wg, K - 1, Jw, lane);
+    tile_zp(sh, zp, K, lane);   // the diagonal this wave factored last phase
     late = false;
     SG_TSTAMP(13)
     return;
@@ -2864,8 +2873,10 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
     asm volatile("" ::: "memory");   // the LmState load goes out before column 8's (its wait then skips them)
     tile_col_load(acc, ypart, d, J, 0, li, lk, ts);   // slots of phase 0
     if (done) return;
-    if (col == 0)
+    if (col == 0) {
       bad |= tile_diag(D0, y0, sh, zp, 0, lane, li, lk);
+      tile_zp(sh, zp, 0, lane);   // (the wave's own LDS writes: visible to it in order)
+    }
     else if (cand_lds)   // the seven waves that wait at the first barrier
       cand_prefetch(d, cl, st->cur, (col - 1) * 64 + lane, kTileThreads - 64);
     SG_TSTAMP(0)
@@ -3162,10 +3173,11 @@ __global__ __launch_bounds__(kRedThreads) void k_upd_reduce(Dev d, int fuse) {
     for (int j = 0; j < kCNum; ++j) cc[j] = d.xchg_chol[j];
   }
   double v[kUNum] = {0, 0, 0, 0, 0, 0};
-  for (int c0 = tid; c0 < d.npu; c0 += 4 * kRedThreads) {
-    double t[4][5];
+  constexpr int kUpdU = 4;   // work units' loads in flight per thread (8 measured slower)
+  for (int c0 = tid; c0 < d.npu; c0 += kUpdU * kRedThreads) {
+    double t[kUpdU][5];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < kUpdU; ++u) {
       const int c = c0 + u * kRedThreads;
       const double* sc = d.chunk_scal + (c < d.npu ? c : 0);   // coalesced: slot j at [j * npu + unit]
       const size_t ns = d.npu;
@@ -3176,7 +3188,7 @@ __global__ __launch_bounds__(kRedThreads) void k_upd_reduce(Dev d, int fuse) {
       t[u][4] = sc[kCandX2 * ns];
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < kUpdU; ++u)
       if (c0 + u * kRedThreads < d.npu) {
         v[kUModel] += t[u][0];
         v[kUCandCost] += t[u][1];
