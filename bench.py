@@ -65,7 +65,11 @@ def pmc_traffic(kernel, largest_grid=False):
     (tools/pmc_traffic.sh -> profiles/<round>_pmc_traffic.json, newest file wins).  Among several launch
     shapes of one kernel the smallest grid is the config-2 / bench launch, the largest the scaled sweep."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    def order(f):   # r<round>_v<version>: numeric, so r2_v22 comes after r2_v5
+        import re
+        m = re.match(r"r(\d+)_v(\d+)_", os.path.basename(f))
+        return (int(m.group(1)), int(m.group(2))) if m else (0, 0)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), key=order)
     if not files:
         return None
     groups = [g for g in json.load(open(files[-1]))["kernels"].values() if g["kernel"] == kernel]
@@ -316,7 +320,7 @@ def kernel_report(res, steps, n_text):
         roof = {"bound": "mfma", "achieved": ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": ach / FP64_PEAK_TFLOPS, "traffic": pmc_traffic("k_chol_tiles"), "kernel": dominant,
                 "us_per_launch": 1e3 * dom_ms,
-                "note": "single-workgroup tiled band Cholesky of the reduced camera system (%s), n^3/3 flops "
+                "note": "dissected tiled band Cholesky of the reduced camera system (two workgroups; %s), n^3/3 flops "
                         "over its mean HIP-event launch time" % n_text}
     else:
         ach = dom_bytes / (dom_ms * 1e-3) / 1e9
