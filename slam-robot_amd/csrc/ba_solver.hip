@@ -2584,12 +2584,12 @@ __device__ __forceinline__ void tile_phase(f64x4 (&acc)[kTB], double& ypart, int
     SG_TSTAMP(13)
     return;
   }
-  // (0) trailing update by row K-1
+  // (0) trailing update by row K-1 (the owner's diagonal tile, dd = 2, already took it last phase)
   if (K >= 1 && J < tend[K - 1]) {
     const double* Ub = sh.Ur[(K - 1) & 1][0];
 #pragma unroll
     for (int dd = 1; dd < kTB; ++dd) {
-      if (K - 1 + dd <= J) {
+      if (K - 1 + dd <= J && !(dd == 2 && J == K + 1)) {
         double a[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) a[s] = -Ub[(dd - 1) * 256 + s * 64 + lane];
@@ -2615,6 +2615,14 @@ __device__ __forceinline__ void tile_phase(f64x4 (&acc)[kTB], double& ypart, int
     const double* zk = sh.zK[K & 3];
 #pragma unroll
     for (int q = 0; q < 4; ++q) ypart = fma(-U[q], zk[lk + 4 * q], ypart);
+    if (J == K + 2) {
+      // next phase's owner: its diagonal tile's update by row K uses only its own U_{K,J}; apply it now,
+      // off next phase's critical chain (slot 3 = row K + 2)
+      double a[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) a[s] = -U[s];
+      acc[3] = mfma_f64_k16(a, U, acc[3]);
+    }
   }
   SG_TSTAMP(9)
   if (J == K + 1) {
@@ -2650,7 +2658,7 @@ __device__ __forceinline__ void tile_final(f64x4 (&acc)[kTB], int J, bool& late,
     const double* Ub = sh.Ur[(K - 1) & 1][0];
 #pragma unroll
     for (int dd = 1; dd < kTB; ++dd) {
-      if (K - 1 + dd <= J) {
+      if (K - 1 + dd <= J && !(dd == 2 && J == K + 1)) {   // (the diagonal of column K+1: applied early)
         double a[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) a[s] = -Ub[(dd - 1) * 256 + s * 64 + lane];
