@@ -2826,19 +2826,6 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
   const bool cand_lds = (flags & 2) != 0;
   CandLds cl;
   cl.carve(tdyn + 32 * NT + (NT + 1) / 2, d.F, d.D, n);
-  for (int k = tid; k < NT; k += kTileThreads) {
-    if (!bottom) {
-      tend[k] = min((panel_jend[k] + 15) >> 4, NTf);
-    } else {
-      // reversed row k = column c = NT-1-k of S: its band reaches back to lo(c), the first row whose band
-      // covers c (band ends are non-decreasing), so the reversed row ends at NT - lo(c)
-      const int c = NT - 1 - k;
-      int lo = c;
-      for (int i = max(0, c - kTB); i < c; ++i)
-        if (((panel_jend[i] + 15) >> 4) > c) { lo = i; break; }
-      tend[k] = min(NT - lo, nd + 7);
-    }
-  }
   // hand-off counter: the bottom half has finished this launch once tflag[0] exceeds the top half's count
   const int epoch = (nd > 0 && !bottom) ? tflag[1] : 0;
   if (tid == 0) sh.fail = 0;
@@ -2880,6 +2867,20 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
     const int done = st->done;
     asm volatile("" ::: "memory");   // the LmState load goes out before column 8's (its wait then skips them)
     tile_col_load(acc, ypart, d, J, 0, li, lk, ts);   // slots of phase 0
+    // band ends (read first in phase 0, after the barrier below): their loads follow the column's
+    for (int k = tid; k < NT; k += kTileThreads) {
+      if (!bottom) {
+        tend[k] = min((panel_jend[k] + 15) >> 4, NTf);
+      } else {
+        // reversed row k = column c = NT-1-k of S: its band reaches back to lo(c), the first row whose band
+        // covers c (band ends are non-decreasing), so the reversed row ends at NT - lo(c)
+        const int c = NT - 1 - k;
+        int lo = c;
+        for (int i = max(0, c - kTB); i < c; ++i)
+          if (((panel_jend[i] + 15) >> 4) > c) { lo = i; break; }
+        tend[k] = min(NT - lo, nd + 7);
+      }
+    }
     if (done) return;
     if (col == 0) {
       bad |= tile_diag(D0, y0, sh, zp, 0, lane, li, lk);
