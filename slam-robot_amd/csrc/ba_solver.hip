@@ -2782,6 +2782,100 @@ __device__ __forceinline__ void bs_chain(const double* __restrict__ Wb, const do
   if (K == Klo) bs_row(K, wA, zA);
 }
 
+// The same chain on two waves: wave `par` takes rows Khi - par, Khi - par - 2, ..., so each wave has two
+// rows' time to bring in its next W rows (its register buffers hold rows 2 and 4 ahead of the chain); the
+// other wave's newest x arrives through LDS behind a per-row flag (`done[K]`: set after x_K is written; the
+// LDS accesses of one wave execute in order).  xw: x_{Khi+1 .. Khi+7} (zero past the system).  The flag wait
+// is bounded; a time-out sets `bad`.
+template <bool kRev>
+__device__ __forceinline__ void bs_chain2(const double* __restrict__ Wb, const double* zsrc, double* xs,
+                                          int* done, int Khi, int Klo, double (&xw)[kTB - 1], int NT, int par,
+                                          int lane, int li, int lk, bool& bad) {
+  auto xat = [&](int K) -> double& { return kRev ? xs[16 * (NT - 1 - K) + 15 - li] : xs[16 * K + li]; };
+  auto wload = [&](double (&w)[kTB - 1][4], int K) {
+    const double* src = Wb + (size_t)(K >= 0 ? K : 0) * kTB * 256 + lane;
+#pragma unroll
+    for (int dd = 1; dd < kTB; ++dd)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) w[dd - 1][q] = src[dd * 256 + q * 64];
+  };
+  const int srcl = 16 * (li & 3) + li;
+  unsigned qbits = 1u << (li >> 2);
+  asm volatile("" : "+v"(qbits));
+  double xown = 0.0;   // this wave's previous result (x_{K+2} at row K)
+  auto wait_row = [&](int K) {   // x_K of the other wave
+    int spin = 0;
+    while (__hip_atomic_load(done + K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0 && ++spin < (1 << 20))
+      __builtin_amdgcn_s_sleep(0);
+    bad |= spin >= (1 << 20);
+    asm volatile("" ::: "memory");
+  };
+  auto bs_row = [&](int K, double (&w)[kTB - 1][4], const double (&zk)[4], bool first) {
+    // window x_{K+1 .. K+7}
+    if (K + 1 <= Khi) {
+      wait_row(K + 1);
+      const double xo = xat(K + 1);
+      if (first) {   // par 1's first row: x_{Khi} ahead of the initial window
+#pragma unroll
+        for (int dd = kTB - 2; dd >= 1; --dd) xw[dd] = xw[dd - 1];
+        xw[0] = xo;
+      } else {       // two new rows: the other wave's x_{K+1}, this wave's x_{K+2}
+#pragma unroll
+        for (int dd = kTB - 2; dd >= 2; --dd) xw[dd] = xw[dd - 2];
+        xw[1] = xown;
+        xw[0] = xo;
+      }
+    }
+    double p[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int dd = kTB - 1; dd >= 1; --dd)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) p[q] = fma(w[dd - 1][q], xw[dd - 1], p[q]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      double v = p[q];
+      v += dpp_d<0xB1>(v);
+      v += dpp_d<0x4E>(v);
+      v += dpp_d<0x141>(v);
+      v += dpp_d<0x140>(v);
+      p[q] = zk[q] - v;
+    }
+    unsigned long long mb = 0ull;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      int msk;
+      asm volatile("v_bfe_i32 %0, %1, %2, 1" : "=v"(msk) : "v"(qbits), "n"(q));
+      mb |= (unsigned long long)__double_as_longlong(p[q]) & (unsigned long long)(long long)msk;
+    }
+    const double xk = __shfl(__longlong_as_double((long long)mb), srcl);
+    xat(K) = xk;
+    asm volatile("" ::: "memory");
+    if (lane == 0) __hip_atomic_store(done + K, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    xown = xk;
+    wload(w, K - 4);   // this buffer's next row (two of this wave's rows ahead)
+  };
+  const int K0 = Khi - par;
+  if (K0 < Klo) return;
+  double wA[kTB - 1][4], wB[kTB - 1][4], zA[4], zB[4];
+  wload(wA, K0);
+  wload(wB, K0 - 2);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) zA[q] = zsrc[16 * K0 + lk + 4 * q];
+  // (par 0's first row, K = Khi, keeps the initial window: bs_row skips the update when K + 1 > Khi)
+  int K = K0;
+  bool first = true;
+  for (; K >= Klo + 2; K -= 4) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) zB[q] = zsrc[16 * (K - 2) + lk + 4 * q];
+    bs_row(K, wA, zA, first);
+    first = false;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) zA[q] = zsrc[16 * (K >= 4 ? K - 4 : 0) + lk + 4 * q];
+    bs_row(K - 2, wB, zB, false);
+  }
+  if (K >= Klo) bs_row(K, wA, zA, first);
+}
+
 // Dissected band (nd > 0: two workgroups).  With m = NT - nd - 7, the tile rows split into the top part
 // A = [0, m), the separator [m, m+7) and the bottom part B = [m+7, NT).  The band is at most 8 tiles wide,
 // so A and B never couple: eliminating A, then B, then the separator is an exact Cholesky of S in that
@@ -2822,10 +2916,13 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
   double* xs = tdyn;              // [16 NT] back-substitution solution
   double* zp = tdyn + 16 * NT;    // [16 NT] Z_K^T z_K
   int* tend = reinterpret_cast<int*>(tdyn + 32 * NT);   // [NT] band end (tiles, exclusive) per tile row
+  int* rdone = tend + NT;                                 // [NT] back substitution: row K's x is in xs
+  int* rdone_b = rdone + NT;                              // [NT] the same for the bottom's reversed rows
+  for (int k = tid; k < 2 * NT; k += kTileThreads) rdone[k] = 0;
   // candidate-pass operands (staged during the back substitution) after the band ends
   const bool cand_lds = (flags & 2) != 0;
   CandLds cl;
-  cl.carve(tdyn + 32 * NT + (NT + 1) / 2, d.F, d.D, n);
+  cl.carve(tdyn + 32 * NT + (3 * NT + 1) / 2, d.F, d.D, n);
   // hand-off counter: the bottom half has finished this launch once tflag[0] exceeds the top half's count
   const int epoch = (nd > 0 && !bottom) ? tflag[1] : 0;
   if (tid == 0) sh.fail = 0;
@@ -2939,23 +3036,40 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
     double xw[kTB - 1];
 #pragma unroll
     for (int dd = 0; dd < kTB - 1; ++dd) xw[dd] = 0.0;
+    // A long chain alternates its rows between two waves (bs_chain2: C5 back substitution 73 k -> 63 k
+    // cycles); a short one stays on one wave (the hand-off costs more than it hides: C2 18.6 k -> 24.9 k).
+    constexpr int kBs2Rows = 12;
     if (nd == 0) {
-      if (wave == 0) bs_chain<false>(Wg, zp, xs, NT - 1, 0, xw, NT, lane, li, lk);
+      if (NT >= kBs2Rows) {
+        if (wave < 2) bs_chain2<false>(Wg, zp, xs, rdone, NT - 1, 0, xw, NT, wave, lane, li, lk, bad);
+      } else if (wave == 0) {
+        bs_chain<false>(Wg, zp, xs, NT - 1, 0, xw, NT, lane, li, lk);
+      }
     } else {
-      // separator rows, then A (wave 0, continuing its registers) beside B (wave 1, reversed)
+      // separator rows (one wave), then A (waves 0, 1) beside B (waves 2, 3, reversed)
       if (wave == 0) bs_chain<false>(Wg, zp, xs, m + 6, m, xw, NT, lane, li, lk);
       __syncthreads();
-      if (wave == 0) {
-        bs_chain<false>(Wg, zp, xs, m - 1, 0, xw, NT, lane, li, lk);
-      } else if (wave == 1) {
+      if (wave < 2) {
+#pragma unroll
+        for (int dd = 1; dd < kTB; ++dd) xw[dd - 1] = xs[16 * (m - 1 + dd) + li];
+        if (m >= kBs2Rows)
+          bs_chain2<false>(Wg, zp, xs, rdone, m - 1, 0, xw, NT, wave, lane, li, lk, bad);
+        else if (wave == 0)
+          bs_chain<false>(Wg, zp, xs, m - 1, 0, xw, NT, lane, li, lk);
+      } else if (wave < 4) {
         // x of reversed rows nd .. nd+6 (the separator, S tile rows m+6 .. m)
 #pragma unroll
         for (int dd = 1; dd < kTB; ++dd) xw[dd - 1] = xs[16 * (NT - nd - dd) + 15 - li];
-        bs_chain<true>(Wg + (size_t)NT * kTB * 256, zpg, xs, nd - 1, 0, xw, NT, lane, li, lk);
+        if (nd >= kBs2Rows)
+          bs_chain2<true>(Wg + (size_t)NT * kTB * 256, zpg, xs, rdone_b, nd - 1, 0, xw, NT, wave - 2, lane, li,
+                          lk, bad);
+        else if (wave == 2)
+          bs_chain<true>(Wg + (size_t)NT * kTB * 256, zpg, xs, nd - 1, 0, xw, NT, lane, li, lk);
       }
     }
   }
   if (tid == 0 && nd > 0) tflag[1] = epoch + 1;
+  if (bad && lane == 0) sh.fail = 1;   // (a back-substitution hand-off that timed out)
   SG_TSTAMP(5)
   __syncthreads();
   double* y = d.work;
@@ -3945,7 +4059,7 @@ void BaSolver::Load(const sg_problem& p) {
     wz.back() = 1.0;
     stager_->Add(Wg_, wz);
     stager_->Add(tflag_, std::vector<int32_t>(2, 0));
-    tile_lds_ = (size_t)npanel * 32 * sizeof(double) + (size_t)(npanel + 1) / 2 * sizeof(double);
+    tile_lds_ = (size_t)npanel * 32 * sizeof(double) + (size_t)(3 * npanel + 1) / 2 * sizeof(double);
     chol_cand_lds_ = F_ <= kCandMax && D_ <= kCandMax && tile_lds_ + CandLds::bytes(F_, D_, n_) <= 100 * 1024;
     if (chol_cand_lds_) tile_lds_ += CandLds::bytes(F_, D_, n_);
   }
