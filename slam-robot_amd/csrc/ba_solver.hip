@@ -565,9 +565,14 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d) {
       for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j) Xd[3 * i + j] = Jd[i] * Jd[3 + j];
     }
-    // per-thread FD cost into a fixed slot (deterministic order below)
-    fdcost[tid] = myfd;
+    // FrameDistance cost: DPP wave sums, then the four waves in order (the barrier also publishes the LDS
+    // FD terms for the block pass)
+    {
+      const double w = wave_sum_full(myfd);
+      if ((tid & 63) == 0) fdcost[tid >> 6] = w;
+    }
     __syncthreads();
+    const double fd_total = (fdcost[0] + fdcost[1]) + (fdcost[2] + fdcost[3]);
     // per camera block: gradient, diag, FD diagonal block
     double gm = 0.0, xn2c = 0.0;
     for (int b = tid; b < d.NB; b += blockDim.x) {
@@ -631,8 +636,7 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d) {
       }
     }
     if (tid == 0) {
-      double fd = 0.0;
-      for (int i = 0; i < (int)blockDim.x; ++i) fd += fdcost[i];
+      const double fd = fd_total;
       const double* xs = d.xchg_cam + nv;
       const double cost = xs[kXCost] + fd;
       double gmax = gm;
