@@ -1100,12 +1100,14 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur_wide(Dev d) {
 // diagonal tile are written as 0 (no factorisation reads them).  Tiles outside the band are never written
 // (zero since the load).
 __global__ __launch_bounds__(256) void k_S_reduce(Dev d) {
+  // LmState is read beside the first work-list loads, not ahead of them: the done test comes after the
+  // partial walk (a finished solve's trailing launches walk once more; every other launch saves a round trip)
   const LmState* st = d.st;
-  if (st->done) return;
+  const int done = st->done;
+  const double radius = st->radius;
   const int tid = threadIdx.x, lane = tid & 63, part = tid >> 6;
   const int wv = blockIdx.x;
   if (wv >= d.nstile + d.NB) return;
-  const double radius = st->radius;
   const int nf = 6 * d.NB;   // frame columns
   if (wv < d.nstile) {
     const int rc = d.stile[wv];
@@ -1158,7 +1160,7 @@ __global__ __launch_bounds__(256) void k_S_reduce(Dev d) {
 #pragma unroll
     for (int m = 0; m < 4; ++m) wsum[part][lane + 64 * m] = s[m];
     __syncthreads();
-    if (!live) return;
+    if (done || !live) return;
     if (!up) {
       d.S[gi] = 0.0;
       return;
@@ -1205,7 +1207,7 @@ __global__ __launch_bounds__(256) void k_S_reduce(Dev d) {
   }
   if (lane < 6) rsum[part][lane] = s;
   __syncthreads();
-  if (part != 0 || lane >= 6) return;
+  if (done || part != 0 || lane >= 6) return;
   s = ((rsum[0][lane] + rsum[1][lane]) + rsum[2][lane]) + rsum[3][lane];
   s += e_acc;
   if (d.assemble) s += e_si * e_g;   // y = rhs_sub + S g_c
@@ -3288,7 +3290,7 @@ __device__ void decide_step(LmState& s, const double* u, const double* c);
 // fuse: single rank, no all-reduce in between: thread 0 also runs k_decide's step (one launch less).
 __global__ __launch_bounds__(kRedThreads) void k_upd_reduce(Dev d, int fuse) {
   const LmState* st = d.st;
-  if (st->done) return;
+  const int done = st->done;   // tested after the scalar loads are out (see k_S_reduce)
   __shared__ double red[kRedThreads / 64 * kUNum];
   const int tid = threadIdx.x;
   // the decision's inputs are loaded up front (one round trip overlapping the reduction, not a chain of
@@ -3325,6 +3327,7 @@ __global__ __launch_bounds__(kRedThreads) void k_upd_reduce(Dev d, int fuse) {
       }
   }
   for (int g = tid; g < d.nseg + d.nwide; g += kRedThreads) v[kULinFail] += d.seg_fail[g];
+  if (done) return;
   block_sum_multi<kRedThreads, kUNum>(v, red);
   if (tid == 0) {
 #pragma unroll
