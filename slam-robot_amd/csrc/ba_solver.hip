@@ -505,38 +505,41 @@ constexpr int kFinFdSh = 256;    // FrameDistance residuals held in LDS (more: r
 constexpr int kFinNSh = 1536;    // frame columns held in LDS (more: re-read from global)
 __global__ __launch_bounds__(256) void k_cam_finalize(Dev d) {
   LmState* st = d.st;
-  if (st->done) return;
   __shared__ double red[4];
   __shared__ double fdcost[256];
   __shared__ double fdJs[6 * kFinFdSh], fdrs[kFinFdSh];
   __shared__ double gsh[kFinNSh], dgsh[kFinNSh], scsh[kFinNSh];
   __shared__ int done_sh;
   const int tid = threadIdx.x;
-  const int cur = st->cur;
   const int nv = d.NB * kCamV;
   const int nf = 6 * d.NB;
   const bool fd_lds = d.D <= kFinFdSh, n_lds = nf <= kFinNSh;
-  // read once, before thread 0 updates them below (no other thread re-reads LmState flags afterwards)
-  const bool lin = st->need_lin, first = st->first, jacobi = st->jacobi;
-  if (lin) {
-    // block pass operands of block tid (the common case NB <= 256), in flight during the FrameDistance pass
-    double Ug[6], Ud[6];
-    int e0 = 0, e1 = 0;
-    const int b0 = tid < d.NB ? tid : 0;
-    {
-      const double* U = d.xchg_cam + (size_t)b0 * kCamV;
+  // block pass operands of block tid (the common case NB <= 256) and the first FrameDistance pair: their
+  // loads go out beside LmState's (see k_S_reduce) and stay in flight during the FrameDistance pass
+  double Ug[6], Ud[6];
+  int e0 = 0, e1 = 0;
+  const int b0 = tid < d.NB ? tid : 0;
+  {
+    const double* U = d.xchg_cam + (size_t)b0 * kCamV;
 #pragma unroll
-      for (int a = 0; a < 6; ++a) {
-        Ug[a] = U[21 + a];
-        Ud[a] = U[u6(a, a)];
-      }
-      e0 = d.fd_boff[b0];
-      e1 = d.fd_boff[b0 + 1];
+    for (int a = 0; a < 6; ++a) {
+      Ug[a] = U[21 + a];
+      Ud[a] = U[u6(a, a)];
     }
+    e0 = d.fd_boff[b0];
+    e1 = d.fd_boff[b0 + 1];
+  }
+  const int dd0 = tid < d.D ? tid : 0;
+  const int fa0 = d.fd_a[dd0], fb0 = d.fd_b[dd0];
+  // read once, before thread 0 updates them below (no other thread re-reads LmState flags afterwards)
+  const int cur = st->cur;
+  const bool lin = st->need_lin, first = st->first, jacobi = st->jacobi;
+  if (st->done) return;
+  if (lin) {
     // FrameDistance residuals at x[cur]
     double myfd = 0.0;
     for (int dd = tid; dd < d.D; dd += blockDim.x) {
-      const int fa = d.fd_a[dd], fb = d.fd_b[dd];
+      const int fa = dd == tid ? fa0 : d.fd_a[dd], fb = dd == tid ? fb0 : d.fd_b[dd];
       const double* ta = d.t[cur] + 3 * fa;
       const double* tb = d.t[cur] + 3 * fb;
       const double e0_ = ta[0] - tb[0], e1_ = ta[1] - tb[1], e2_ = ta[2] - tb[2];
