@@ -930,10 +930,12 @@ __device__ __forceinline__ void schur_cells(const Dev& d, const SchurBatch& B, i
   }
 __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d) {
   const LmState* st = d.st;
-  if (st->done || (int)blockIdx.x >= d.nseg) return;
+  if ((int)blockIdx.x >= d.nseg) return;
   __shared__ SchurLds sh;
   unsigned long long last_ = __builtin_amdgcn_s_memtime();
+  // the segment's descriptor load goes out beside LmState's (see k_S_reduce)
   const SchurSeg sg = d.segs[blockIdx.x];
+  if (st->done) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nbt = sg.bt1 - sg.bt0;
   const int c0w = 16 * sg.t0;
