@@ -15,10 +15,17 @@ Workloads (synthetic scenes, slamgpu/scene.py; fp64 arithmetic, the reference's 
       ranks; value = K / time.
 The default run also measures the other workload (C5 next to a C2 headline: strong over the same N ranks).
 
-The timed region is K LM iterations with termination disabled, after W warm-up iterations: past
-convergence, so about half the steps are rejected (a rejected step skips the linearization, as in Ceres).
-`accepted_frac` reports that share, and `solve_from_start` times complete solves from the perturbed start
-(Slam::SolveFrames semantics, termination on, mostly accepted steps): iterations / wall time.
+The timed region is K LM iterations with termination disabled after W warm-up iterations, and every
+iteration is SURVEY.md 8d's full unit of work: linearize + Schur + Cholesky + back-substitution + candidate
+cost + decision.  Ceres skips the linearization after a rejected step; the benchmark re-linearizes there too
+(sg_solver_options.always_linearize: the same values, so the same trajectory), so value and ms_per_step do
+not depend on K, W or how many steps past convergence get rejected.  `lm_regime` times the same K with
+Ceres's own skipping (its share of accepted steps depends on K), and `solve_from_start` times complete solves
+from the perturbed start (Slam::SolveFrames semantics, termination on): iterations / wall time.
+
+Roofline `traffic` fields come from the per-workload rocprofv3 --pmc passes (tools/profile_round.sh ->
+profiles/<tag>_pmc_traffic_<workload>.json, newest tag wins), run with `--only <workload>` so each file holds
+that workload's own launches; `--only` also serves the per-workload kernel-trace profiles.
 
 Prints ONE JSON line on rank 0.
 """
@@ -53,30 +60,52 @@ def parse():
     ap.add_argument("--frontend", type=int, default=1,
                     help="also measure the front end at N=1: KLT tracks/sec (config 3) and the 256-bit "
                          "Hamming matcher (config 4)")
-    return ap.parse_args()
+    ap.add_argument("--only", choices=("all", "C2", "C5", "sweep", "frontend"), default="all",
+                    help="profiling runs: one workload alone (its kernels are then the only ones launched)")
+    args = ap.parse_args()
+    if args.only != "all":
+        args.cpu_runs = 0
+        args.cpu_seconds = 0
+        args.other = 0
+        args.frontend = 1 if args.only == "frontend" else 0
+        args.sweep_obs = args.sweep_obs if args.only == "sweep" else 0
+        if args.only in ("C2", "C5"):
+            args.config = args.only
+    return args
 
 
 FP32_PEAK_TFLOPS = 157.3     # MI355X FP32 vector peak
 I8_MFMA_PEAK_TOPS = 5033.0    # int8 MFMA (dense): 2048 ops/clk/SIMD (16x16x64 in 16 cycles) x 1024 SIMDs x 2.4 GHz
 
 
-def pmc_traffic(kernel, largest_grid=False):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE passes
-    (tools/pmc_traffic.sh -> profiles/<round>_pmc_traffic.json, newest file wins).  Among several launch
-    shapes of one kernel the smallest grid is the config-2 / bench launch, the largest the scaled sweep."""
+def pmc_traffic(kernel, workload):
+    """HBM bytes per launch of `kernel` in `workload` (C2, C5, sweep, frontend) from the committed
+    rocprofv3 FETCH_SIZE / WRITE_SIZE passes of `bench.py --only <workload>` (tools/profile_round.sh ->
+    profiles/r<round>_v<version>_pmc_traffic_<workload>.json, newest version wins).  Each file holds one
+    workload's launches only, so the figure is that workload's own kernel; returns (bytes, file) or
+    (None, None)."""
     import glob
-    def order(f):   # r<round>_v<version>: numeric, so r2_v22 comes after r2_v5
-        import re
+    import re
+
+    def order(f):   # r<round>_v<version>: numeric, so r3_v12 comes after r3_v5
         m = re.match(r"r(\d+)_v(\d+)_", os.path.basename(f))
         return (int(m.group(1)), int(m.group(2))) if m else (0, 0)
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), key=order)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic_%s.json" % workload)), key=order)
     if not files:
-        return None
+        return None, None
     groups = [g for g in json.load(open(files[-1]))["kernels"].values() if g["kernel"] == kernel]
     if not groups:
-        return None
-    g = (max if largest_grid else min)(groups, key=lambda g: g["grid_size"])
-    return g["traffic_bytes"]
+        return None, os.path.basename(files[-1])
+    g = max(groups, key=lambda g: g["active_dispatches"])
+    return g["traffic_bytes"], os.path.basename(files[-1])
+
+
+def traffic_fields(kernel, workload, algorithmic_bytes=None):
+    t, src = pmc_traffic(kernel, workload)
+    d = {"traffic": t, "traffic_file": src}
+    if t is not None and algorithmic_bytes:
+        d["traffic_over_algorithmic"] = t / algorithmic_bytes
+    return d
 
 
 def bench_tracker(local, cpu_seconds):
@@ -110,7 +139,7 @@ def bench_tracker(local, cpu_seconds):
            "newton_iterations_max_track": int(its.max()),
            "us_per_newton_iteration_on_longest_track": ms * 1e3 / max(int(its.max()), 1),
            "roofline": {"bound": "valu", "achieved": ach, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                        "frac": ach / FP32_PEAK_TFLOPS, "traffic": pmc_traffic("k_track_fb"), "kernel": "k_track_fb",
+                        "frac": ach / FP32_PEAK_TFLOPS, **traffic_fields("k_track_fb", "frontend"), "kernel": "k_track_fb",
                         "note": "108*W^2 flops per Newton iteration (6 probes of bilinear sampling, moments, "
                                 "score); one wave per feature"}}
     if cpu_seconds > 0:
@@ -146,12 +175,17 @@ def bench_hamming(local, cpu_seconds):
     pairs = float(len(A)) * len(B)
     ops = pairs * 512.0      # per pair: a 256-term int8 dot product (256 multiply-adds) on the matrix cores
     ach = ops / (ms * 1e-3) / 1e12
+    alg_ops = pairs * 12.0   # 4 XOR + 4 POPC + 3 ADD + 1 MIN per pair (the algorithm's count)
     res = {"metric": "256-bit Hamming all-pairs query-rows/sec (10k x 10k)", "value": len(B) / (ms * 1e-3),
            "unit": "rows/s", "pairs_per_s": pairs / (ms * 1e-3), "ms": ms,
            "recall_of_true_matches": float((bi[truth >= 0] == truth[truth >= 0]).mean()),
            "roofline": {"bound": "mfma", "achieved": ach, "peak": I8_MFMA_PEAK_TOPS, "unit": "TOPS (int8)",
-                        "frac": ach / I8_MFMA_PEAK_TOPS, "traffic": pmc_traffic("k_hamming_slices"),
+                        "frac": ach / I8_MFMA_PEAK_TOPS, **traffic_fields("k_hamming_slices", "frontend"),
                         "kernel": "k_hamming_slices",
+                        "algorithmic_int_ops_per_s": alg_ops / (ms * 1e-3),
+                        "algorithmic_note": "SURVEY.md 8d prices the algorithm at 12 integer ops per pair "
+                                            "(XOR/POPC/ADD/MIN on 4 x u64); the frac above prices the "
+                                            "implementation's 512 int8 MFMA ops per pair",
                         "note": "+-1 int8 dot products (v_mfma_i32_16x16x64_i8, 2 x 256 ops per pair) with the "
                                 "expansion and the arg-min fused; whole match (slices + merge) per HIP-event time"}}
     if cpu_seconds > 0:
@@ -255,13 +289,12 @@ class Runner:
         self.dist.all_reduce(e, op=self.dist.ReduceOp.MAX)
         return float(e.item())
 
-    def timed(self, steps, warmup):
-        """W warm-up then exactly K LM iterations (termination disabled), barrier + synchronize on both
-        sides, max over ranks; then the same K with per-kernel HIP-event timing."""
+    def _timed_block(self, steps, warmup, always_lin):
         import torch
         from slamgpu.capi import default_solver_options
         g = self.solver
-        g.begin(default_solver_options(max_num_iterations=warmup + 2 * steps + 16, disable_termination=1))
+        g.begin(default_solver_options(max_num_iterations=warmup + 2 * steps + 16, disable_termination=1,
+                                       always_linearize=always_lin))
         g.iterate(warmup)
         g.sync()
         s0 = g.summary()
@@ -274,15 +307,30 @@ class Runner:
         self.barrier()
         elapsed = self.max_over_ranks(time.perf_counter() - t0)
         s1 = g.summary()
+        assert s1["sync_timeouts"] == 0 and s1["num_lm_iterations"] == warmup + steps, s1
+        return elapsed, s0, s1
+
+    def timed(self, steps, warmup):
+        """W warm-up then exactly K LM iterations (termination disabled, every iteration linearizes: the
+        SURVEY.md 8d unit), barrier + synchronize on both sides, max over ranks; then the same K with
+        per-kernel HIP-event timing; then the same K in Ceres's regime (no linearization after a rejected
+        step), reported beside the headline."""
+        g = self.solver
+        elapsed, s0, s1 = self._timed_block(steps, warmup, 1)
         g.set_timing(True)
         g.iterate(steps)
         g.sync()
         kt = g.kernel_times()
         g.set_timing(False)
         s2 = g.summary()
+        lm_elapsed, l0, l1 = self._timed_block(steps, warmup, 0)
+        lm = {"ms_per_step": 1e3 * lm_elapsed / steps, "value": steps / lm_elapsed,
+              "accepted_frac": (l1["num_successful_steps"] - l0["num_successful_steps"]) / steps,
+              "note": "Ceres regime: a rejected step skips the linearization, so this figure depends on how many "
+                      "of the K steps after W warm-up steps are rejected"}
         return {"elapsed": elapsed, "accepted": s1["num_successful_steps"] - s0["num_successful_steps"],
-                "kt": kt, "work": g.kernel_work(), "lin_active": s2["num_successful_steps"] - s1["num_successful_steps"],
-                "summary": s1}
+                "kt": kt, "work": g.kernel_work(), "lin_active": s2["num_lm_iterations"] - s1["num_lm_iterations"],
+                "summary": s1, "lm_regime": lm}
 
     def solve_from_start(self):
         """Complete solves from the perturbed start (termination on): iterations over wall time (includes
@@ -308,7 +356,7 @@ class Runner:
                 "device_kernel_ms": dev_ms, "iters_per_s_device": its / (dev_ms * 1e-3) if dev_ms else None}
 
 
-def kernel_report(res, steps, n_text):
+def kernel_report(res, steps, n_text, workload):
     """Per-iteration kernel times, the dominant kernel's roofline and the sweep roofline."""
     kt, work = res["kt"], res["work"]
     per_iter_ms = {k: v[0] * v[1] / max(steps, 1) for k, v in kt.items()}
@@ -318,14 +366,14 @@ def kernel_report(res, steps, n_text):
     if dom_flops > 0 and dominant == "cholesky":
         ach = dom_flops / (dom_ms * 1e-3) / 1e12
         roof = {"bound": "mfma", "achieved": ach, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": ach / FP64_PEAK_TFLOPS, "traffic": pmc_traffic("k_chol_tiles"), "kernel": dominant,
+                "frac": ach / FP64_PEAK_TFLOPS, **traffic_fields("k_chol_tiles", workload), "kernel": dominant,
                 "us_per_launch": 1e3 * dom_ms,
                 "note": "dissected tiled band Cholesky of the reduced camera system (two workgroups; %s), n^3/3 flops "
                         "over its mean HIP-event launch time" % n_text}
     else:
         ach = dom_bytes / (dom_ms * 1e-3) / 1e9
         roof = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic("k_" + dominant), "kernel": dominant,
+                "frac": ach / HBM_PEAK_GBS, **traffic_fields("k_" + dominant, workload, dom_bytes), "kernel": dominant,
                 "us_per_launch": 1e3 * dom_ms}
     sweep = None
     n_lin = res["lin_active"]
@@ -334,7 +382,8 @@ def kernel_report(res, steps, n_text):
         ach = work["linearize"][0] * n_lin / (lin_total_ms * 1e-3) / 1e9
         sweep = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                  "frac": ach / HBM_PEAK_GBS, "bytes_per_launch": work["linearize"][0],
-                 "traffic": pmc_traffic("k_linearize"), "active_launches": n_lin, "launches": kt["linearize"][1]}
+                 **traffic_fields("k_linearize", workload, work["linearize"][0]), "active_launches": n_lin,
+                 "launches": kt["linearize"][1]}
     return {k: round(v, 5) for k, v in per_iter_ms.items()}, roof, sweep
 
 
@@ -359,10 +408,41 @@ def run_workload(cfg, args, n_gpus, rank, local, dist, steps, warmup):
     return full, prob, desc, res, info, start, bal
 
 
+def bench_sweep(local, sweep_obs):
+    """Scaled sweep: the linearization kernel on a problem large enough to amortise launch latency."""
+    from slamgpu import ba
+    from slamgpu.capi import default_solver_options
+    from slamgpu.scene import make_scene
+    npts = max(sweep_obs // 10, 1000)
+    big = make_scene(num_frames=200, num_points=npts, seed=5, run_max=18)
+    bp = ba.problem_from_map_frames(big, 198, 200, 2.0)
+    bs = ba.BundleAdjuster(device=local)
+    bs.load(bp)
+    bs.begin(default_solver_options())
+    bs.sweep(3)
+    bs.sync()
+    bs.set_timing(True)
+    bs.sweep(20)
+    bs.sync()
+    kt = bs.kernel_times()["linearize"]
+    wb = bs.kernel_work()["linearize"][0]
+    ach = wb / (kt[0] * 1e-3) / 1e9
+    bs.close()
+    return {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": ach / HBM_PEAK_GBS, "obs": bp.num_obs, "points": bp.num_points,
+            "ms_per_launch": kt[0], "bytes_per_launch": wb, **traffic_fields("k_linearize", "sweep", wb)}
+
+
 def main():
     args = parse()
     ws, rank, local = dist_env()
     import torch
+
+    if args.only in ("sweep", "frontend"):   # profiling runs of one non-headline workload (N = 1)
+        out = bench_sweep(local, args.sweep_obs) if args.only == "sweep" else \
+            {"tracker": bench_tracker(local, 0), "hamming": bench_hamming(local, 0)}
+        print(json.dumps({"only": args.only, "result": out}), flush=True)
+        return
 
     dist = None
     if ws > 1:
@@ -381,11 +461,11 @@ def main():
         k2 = min(args.steps, 50)
         f2, p2, d2, r2, i2, st2, b2 = run_workload(ocfg, args, n_gpus, rank, local, dist, k2, min(args.warmup, 10))
         if rank == 0:
-            pk2, roof2, sw2 = kernel_report(r2, k2, "n=%d, band %d tiles" % (i2["n"], i2["band_tiles"]))
+            pk2, roof2, sw2 = kernel_report(r2, k2, "n=%d, band %d tiles" % (i2["n"], i2["band_tiles"]), ocfg)
             val2 = (n_gpus if ocfg == "C2" else 1) * k2 / r2["elapsed"]
             other = {"workload": d2, "scaling": "weak" if ocfg == "C2" else "strong", "value": val2,
                      "unit": "iters/s", "steps": k2, "ms_per_step": 1e3 * r2["elapsed"] / k2,
-                     "accepted_frac": r2["accepted"] / k2, "keyframes": f2.num_frames,
+                     "accepted_frac": r2["accepted"] / k2, "lm_regime": r2["lm_regime"], "keyframes": f2.num_frames,
                      "landmarks": f2.num_points, "observations": f2.num_obs, "per_rank": {
                          "landmarks": p2.num_points, "observations": p2.num_obs}, "solver": i2,
                      "kernel_ms_per_iter": pk2, "roofline": roof2, "roofline_sweep": sw2,
@@ -397,33 +477,10 @@ def main():
             dist.destroy_process_group()
         return
 
-    per_iter_ms, roof, sweep = kernel_report(res, args.steps, "n=%d, band %d tiles" % (info["n"], info["band_tiles"]))
+    per_iter_ms, roof, sweep = kernel_report(res, args.steps, "n=%d, band %d tiles" % (info["n"], info["band_tiles"]),
+                                             args.config)
 
-    # scaled sweep: the linearization kernel on a problem large enough to amortise launch latency
-    sweep_scaled = None
-    if args.sweep_obs > 0 and n_gpus == 1:
-        from slamgpu import ba
-        from slamgpu.capi import default_solver_options
-        from slamgpu.scene import make_scene
-        npts = max(args.sweep_obs // 10, 1000)
-        big = make_scene(num_frames=200, num_points=npts, seed=5, run_max=18)
-        bp = ba.problem_from_map_frames(big, 198, 200, 2.0)
-        bs = ba.BundleAdjuster(device=local)
-        bs.load(bp)
-        bs.begin(default_solver_options())
-        bs.sweep(3)
-        bs.sync()
-        bs.set_timing(True)
-        bs.sweep(20)
-        bs.sync()
-        kt = bs.kernel_times()["linearize"]
-        wb = bs.kernel_work()["linearize"][0]
-        ach = wb / (kt[0] * 1e-3) / 1e9
-        sweep_scaled = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": ach / HBM_PEAK_GBS, "obs": bp.num_obs, "points": bp.num_points,
-                        "ms_per_launch": kt[0], "bytes_per_launch": wb,
-                        "traffic": pmc_traffic("k_linearize", largest_grid=True)}
-        bs.close()
+    sweep_scaled = bench_sweep(local, args.sweep_obs) if args.sweep_obs > 0 and n_gpus == 1 else None
 
     cpu = None
     if args.cpu_runs > 0 and n_gpus == 1:
@@ -454,6 +511,8 @@ def main():
                    "parallelism": "landmark-shard x%d (RCCL all-reduce of the camera system)" % n_gpus
                    if n_gpus > 1 else "single GPU"},
         "accepted_frac": res["accepted"] / args.steps,
+        "timed_regime": "every LM iteration linearizes (sg_solver_options.always_linearize; SURVEY.md 8d unit)",
+        "lm_regime": res["lm_regime"],
         "solve_from_start": start,
         "solver": info,
         "roofline": roof,
@@ -467,8 +526,9 @@ def main():
         "shard_balance": bal,
         "other_workload": other,
         "frontend": frontend,
-        "traffic_source": "HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes "
-                          "(tools/pmc_traffic.sh, profiles/*_pmc_traffic.json; FETCH_SIZE doubled on gfx950)",
+        "traffic_source": "HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes over "
+                          "bench.py --only <workload> --steps 20 --warmup 5 (tools/profile_round.sh, "
+                          "profiles/*_pmc_traffic_<workload>.json; FETCH_SIZE doubled on gfx950)",
     }
     print(json.dumps(line), flush=True)
     if dist is not None:

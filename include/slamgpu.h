@@ -46,7 +46,9 @@ enum sg_termination {
   SG_GRADIENT_TOLERANCE = 2,
   SG_PARAMETER_TOLERANCE = 3,
   SG_NUMERICAL_FAILURE = 4,
-  SG_DID_NOT_RUN = 5
+  SG_DID_NOT_RUN = 5,
+  SG_DEVICE_TIMEOUT = 6   /* not a Ceres type: a device hand-off of the Cholesky hit its spin limit (the GPU was
+                             shared or stalled); the step is not trusted and the solve fails (ok = 0) */
 };
 
 /*
@@ -130,6 +132,8 @@ typedef struct sg_solver_options {
   int32_t max_num_consecutive_invalid_steps; /* 5 */
   int32_t jacobi_scaling;                /* 1 */
   int32_t disable_termination;           /* benchmark mode: run exactly max_num_iterations LM iterations */
+  int32_t always_linearize;              /* benchmark mode: a rejected step re-linearizes too (same values),
+                                            so every iteration is SURVEY.md 8d's full unit of work; 0 = Ceres */
 } sg_solver_options;
 
 /* ceres::Solver::Summary fields the reference reads (slam.cpp:510-520). */
@@ -145,7 +149,8 @@ typedef struct sg_solver_summary {
   double fixed_cost;
   double trust_region_radius;
   int32_t num_lm_iterations;     /* LM loop iterations executed on the device (benchmark unit) */
-  int32_t reserved;
+  int32_t sync_timeouts;         /* Cholesky hand-off waits that hit their spin limit (0 in a healthy solve; a
+                                    non-zero count ends the solve with SG_DEVICE_TIMEOUT) */
 } sg_solver_summary;
 
 typedef struct sg_device_options {
@@ -197,6 +202,11 @@ void sg_comm_group_destroy(sg_comm_group* g);
 int sg_ba_comm_init_local(sg_ba* h, sg_comm_group* g, int32_t rank);
 /* Upload a problem (the problem's q/t/X are read now and written back by sg_ba_download). */
 int sg_ba_load(sg_ba* h, const sg_problem* p);
+/* Pre-size the handle's device and pinned staging buffers for problems of up to max_frames frames, max_points
+ * points and max_obs observations (a map's high-water mark), so loads that follow do not reallocate on their
+ * critical path.  Reallocation drops the loaded problem (load again).  The Slam facade does this itself from
+ * the map's size whenever the map outgrows its last reservation. */
+int sg_ba_reserve(sg_ba* h, int32_t max_frames, int32_t max_points, int32_t max_obs);
 /* Incremental problem update (replaces the per-call rebuild of slam.cpp:257-414): a
  * load whose structure equals the previous load's (frames, cameras, freedom flags, observation incidence,
  * FrameDistance pairs) re-uploads the values only.  Counts of full and value-only loads on this handle. */
@@ -254,7 +264,7 @@ double sg_slam_error(const sg_slam* s);                                         
 int sg_slam_load_counts(const sg_slam* s, int32_t* full_loads, int32_t* value_loads);   /* see sg_ba_load_counts */
 /* Host wall time (ms) of the last SolveFrames / SolveAllFrames call by phase: [0] SetupProblem (problem build),
  * [1] sg_ba_load (work lists + upload), [2] device LM loop incl. download, [3] write-back into the map.
- * A development aid for sizing the host share of a real call (tools/e2e_timing.py). */
+ * A development aid for sizing the host share of a real call (tools/e2e_replay.py). */
 int sg_slam_last_phase_ms(const sg_slam* s, double* ms4);
 int sg_slam_last_summary(const sg_slam* s, sg_solver_summary* out);
 

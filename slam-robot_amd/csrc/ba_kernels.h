@@ -43,8 +43,10 @@ __host__ __device__ __forceinline__ int meta_cam(int m) { return (m >> kMetaCamS
 
 // Exchange-buffer scalar slots appended after the camera blocks.
 enum CamX { kXCost = 0, kXFail, kXFixed, kXFixedFail, kXXnorm2, kXNum };
-enum UpdX { kUModel = 0, kUCandCost, kUCandFail, kUStep2, kUCandX2, kULinFail, kUNum };
-enum CholX { kCStep2 = 0, kCCandX2, kCModel, kCCandCost, kCFail, kCNum };
+enum UpdX { kUModel = 0, kUCandCost, kUCandFail, kUStep2, kUCandX2, kULinFail, kUTimeout, kUNum };
+// kCTimeout: cross-wave / cross-workgroup hand-offs of the tiled Cholesky that hit their spin limit (the
+// step is then not trusted: the solve ends with SG_DEVICE_TIMEOUT, see decide_step)
+enum CholX { kCStep2 = 0, kCCandX2, kCModel, kCCandCost, kCFail, kCTimeout, kCNum };
 
 
 // k_schur work decomposition (see ba_solver.hip): a segment is a run of consecutive points (device order)
@@ -116,12 +118,13 @@ struct LinChunk {
 struct LmState {
   // options (copied from sg_solver_options)
   int32_t max_iter, max_invalid, disable_term, jacobi;
+  int32_t always_lin, pad1;   // benchmark: linearize after a rejected step too (sg_solver_options.always_linearize)
   double ftol, gtol, ptol, min_rel_dec, max_radius, min_radius, min_diag, max_diag;
   // minimizer state
   int32_t cur, need_lin, first, done;
   int32_t termination, ok, pushed, lm_iters;
   int32_t n_succ, n_unsucc, n_invalid, consecutive_invalid;
-  int32_t reuse_diag, pad0;
+  int32_t reuse_diag, sync_timeouts;   // sync_timeouts: Cholesky hand-off time-outs seen (kCTimeout)
   double radius, decrease_factor;
   double cost, fixed_cost, initial_cost, x_norm, abs_gtol, min_pushed_cost;
   double last_model, last_new_cost, last_rel_decrease, last_step_norm;

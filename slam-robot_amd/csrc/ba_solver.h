@@ -25,6 +25,10 @@ class BaSolver {
   ~BaSolver();
 
   void Load(const sg_problem& p);
+  // Pre-size every buffer that scales with the problem for up to F frames, P points and M observations (a
+  // map's high-water mark), so that a later Load does not reallocate on its critical path.  Reallocating
+  // drops the loaded structure (the next Load is a full one).
+  void Reserve(int F, int P, int M);
   void Begin(const sg_solver_options& o);
   void Iterate(int n);
   void Sweep(int n);
@@ -62,6 +66,8 @@ class BaSolver {
   DBuf<int32_t> tflag_;        // dissected band hand-off counters {bottom done, top done}
   int chol_simdmap_ = !(getenv("SG_CHOL_SIMDMAP") && atoi(getenv("SG_CHOL_SIMDMAP")) == 0);
   bool chol_cand_lds_ = false;   // candidate-pass operands staged in the Cholesky's LDS (small problems)
+  // tests only: force the dissected Cholesky's separator wait to time out (k_chol_tiles flags bit 2)
+  bool chol_force_tmo_ = getenv("SG_CHOL_FORCE_TIMEOUT") && atoi(getenv("SG_CHOL_FORCE_TIMEOUT")) != 0;
   bool pack_force_ = getenv("SG_PACK_S") != nullptr;   // pack/unpack S on one rank too (tests the path)
   size_t npack_ = 0;                                      // band of S + rhs, doubles (all-reduce size)
   bool stamp_on_ = false;

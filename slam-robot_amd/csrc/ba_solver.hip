@@ -530,7 +530,7 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d) {
     e1 = d.fd_boff[b0 + 1];
   }
   const int dd0 = tid < d.D ? tid : 0;
-  const int fa0 = d.fd_a[dd0], fb0 = d.fd_b[dd0];
+  const int fa0 = d.D > 0 ? d.fd_a[dd0] : 0, fb0 = d.D > 0 ? d.fd_b[dd0] : 0;
   // read once, before thread 0 updates them below (no other thread re-reads LmState flags afterwards)
   const int cur = st->cur;
   const bool lin = st->need_lin, first = st->first, jacobi = st->jacobi;
@@ -1168,6 +1168,7 @@ __global__ __launch_bounds__(256) void k_S_reduce(Dev d) {
     if (done || !live) return;
     if (!up) {
       d.S[gi] = 0.0;
+      if (d.nwide) d.S_wide[gi] = 0.0;   // schur_pair_add also adds a diagonal block's lower half: keep it clean
       return;
     }
     double t = ((wsum[0][tid] + wsum[1][tid]) + wsum[2][tid]) + wsum[3][tid];
@@ -1645,7 +1646,7 @@ __device__ __noinline__ void chol_backsub(const double* A, const double* rdg, do
 
 // Candidate camera poses x+ = Plus(x, -S x_c) for every frame, FrameDistance model / candidate terms.
 template <int NT>
-__device__ __forceinline__ void chol_candidates(const Dev& d, const double* y, int fail) {
+__device__ __forceinline__ void chol_candidates(const Dev& d, const double* y, int fail, int tmo = 0) {
   const LmState* st = d.st;
   __shared__ double red[4 * NT / 64];
   const int tid = threadIdx.x;
@@ -1710,6 +1711,7 @@ __device__ __forceinline__ void chol_candidates(const Dev& d, const double* y, i
     d.xchg_chol[kCModel] = model;
     d.xchg_chol[kCCandCost] = candcost;
     d.xchg_chol[kCFail] = fail ? 1.0 : 0.0;
+    d.xchg_chol[kCTimeout] = tmo ? 1.0 : 0.0;
   }
 }
 
@@ -1752,7 +1754,7 @@ __device__ __forceinline__ void cand_prefetch(const Dev& d, const CandLds& c, in
 
 template <int NT>
 __device__ __forceinline__ void chol_candidates_lds(const Dev& d, const double* y, int fail, const CandLds& c,
-                                                    int cur) {
+                                                    int cur, int tmo) {
   __shared__ double red[4 * NT / 64];
   const int tid = threadIdx.x;
   const int nxt = cur ^ 1;
@@ -1816,6 +1818,7 @@ __device__ __forceinline__ void chol_candidates_lds(const Dev& d, const double* 
     d.xchg_chol[kCModel] = sums[2];
     d.xchg_chol[kCCandCost] = sums[3];
     d.xchg_chol[kCFail] = fail ? 1.0 : 0.0;
+    d.xchg_chol[kCTimeout] = tmo ? 1.0 : 0.0;
   }
 }
 
@@ -2357,6 +2360,7 @@ struct TileShared {
   double Yw[16];
   double prw[2 * kCholNb];     // the owner's next two pivot rows
   int fail;
+  int tmo;                     // a hand-off wait hit its spin limit (kCTimeout)
   int simd[kTB];               // SIMD of each wave
   double Id[16 * kTLd];        // the identity (the factor's augmented columns)
 };
@@ -2797,11 +2801,11 @@ __device__ __forceinline__ void bs_chain(const double* __restrict__ Wb, const do
 // rows' time to bring in its next W rows (its register buffers hold rows 2 and 4 ahead of the chain); the
 // other wave's newest x arrives through LDS behind a per-row flag (`done[K]`: set after x_K is written; the
 // LDS accesses of one wave execute in order).  xw: x_{Khi+1 .. Khi+7} (zero past the system).  The flag wait
-// is bounded; a time-out sets `bad`.
+// is bounded; a time-out sets `tmo` (counted in kCTimeout: the solve then ends with SG_DEVICE_TIMEOUT).
 template <bool kRev>
 __device__ __forceinline__ void bs_chain2(const double* __restrict__ Wb, const double* zsrc, double* xs,
                                           int* done, int Khi, int Klo, double (&xw)[kTB - 1], int NT, int par,
-                                          int lane, int li, int lk, bool& bad) {
+                                          int lane, int li, int lk, bool& tmo) {
   auto xat = [&](int K) -> double& { return kRev ? xs[16 * (NT - 1 - K) + 15 - li] : xs[16 * K + li]; };
   auto wload = [&](double (&w)[kTB - 1][4], int K) {
     const double* src = Wb + (size_t)(K >= 0 ? K : 0) * kTB * 256 + lane;
@@ -2818,7 +2822,7 @@ __device__ __forceinline__ void bs_chain2(const double* __restrict__ Wb, const d
     int spin = 0;
     while (__hip_atomic_load(done + K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0 && ++spin < (1 << 20))
       __builtin_amdgcn_s_sleep(0);
-    bad |= spin >= (1 << 20);
+    tmo |= spin >= (1 << 20);
     asm volatile("" ::: "memory");
   };
   auto bs_row = [&](int K, double (&w)[kTB - 1][4], const double (&zk)[4], bool first) {
@@ -2900,7 +2904,10 @@ __device__ __forceinline__ void bs_chain2(const double* __restrict__ Wb, const d
 //   * Back substitution (top workgroup): the separator rows, then A (wave 0) and B (wave 1, reversed W
 //     tiles) side by side.
 // The chain drops from NT tile rows to m + 7 (C2: 18 -> 13, C5: 75 -> 42).  The wait is bounded: on a
-// time-out the step fails (rejected by the LM decision) instead of hanging.
+// time-out the launch reports it (kCTimeout) and the LM decision ends the solve with SG_DEVICE_TIMEOUT
+// instead of hanging or silently rejecting the step.
+//   flags bit 2 (SG_CHOL_FORCE_TIMEOUT, tests only): the bottom workgroup sleeps ~2 ms before its work and
+//   the top one polls at most 256 times, so the time-out path runs deterministically.
 constexpr int kSepSpinMax = 1 << 22;
 constexpr int kSplitMinNT = 13;
 template <bool kStamp>
@@ -2936,8 +2943,14 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
   cl.carve(tdyn + 32 * NT + (3 * NT + 1) / 2, d.F, d.D, n);
   // hand-off counter: the bottom half has finished this launch once tflag[0] exceeds the top half's count
   const int epoch = (nd > 0 && !bottom) ? tflag[1] : 0;
-  if (tid == 0) sh.fail = 0;
-  bool bad = false;
+  if (tid == 0) {
+    sh.fail = 0;
+    sh.tmo = 0;
+  }
+  bool bad = false, tmo = false;
+  const int spin_max = (flags & 4) ? 256 : kSepSpinMax;
+  if (bottom && (flags & 4))
+    for (int i = 0; i < 640; ++i) __builtin_amdgcn_s_sleep(127);
   // Columns J and J+1 (mod 8) on one SIMD: the owner of phase K (column K+1) then shares its SIMD with the
   // late wave of column K (one W tile, a reload) or with column K+2 (its first few tiles), not with a
   // column four ahead and its full band of trailing MFMAs.  SIMD ids from HW_ID; any other placement than
@@ -3005,10 +3018,10 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
         // relaxed polls, one acquire (an acquiring poll would invalidate the cache on every round)
         int spin = 0;
         while (__hip_atomic_load(tflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= epoch &&
-               ++spin < kSepSpinMax)
+               ++spin < spin_max)
           __builtin_amdgcn_s_sleep(1);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        bad |= spin >= kSepSpinMax;
+        tmo |= spin >= spin_max;
         sep_merge(acc, ypart, J, m, sepb, sepy, lane, li, lk);
       }
       tile_phase<kStamp>(acc, ypart, J, late, bad, sh, d, Wb, zp, tend, K, NTf, lane, li, lk, ts, tacc, tlast);
@@ -3052,7 +3065,7 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
     constexpr int kBs2Rows = 12;
     if (nd == 0) {
       if (NT >= kBs2Rows) {
-        if (wave < 2) bs_chain2<false>(Wg, zp, xs, rdone, NT - 1, 0, xw, NT, wave, lane, li, lk, bad);
+        if (wave < 2) bs_chain2<false>(Wg, zp, xs, rdone, NT - 1, 0, xw, NT, wave, lane, li, lk, tmo);
       } else if (wave == 0) {
         bs_chain<false>(Wg, zp, xs, NT - 1, 0, xw, NT, lane, li, lk);
       }
@@ -3064,7 +3077,7 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
 #pragma unroll
         for (int dd = 1; dd < kTB; ++dd) xw[dd - 1] = xs[16 * (m - 1 + dd) + li];
         if (m >= kBs2Rows)
-          bs_chain2<false>(Wg, zp, xs, rdone, m - 1, 0, xw, NT, wave, lane, li, lk, bad);
+          bs_chain2<false>(Wg, zp, xs, rdone, m - 1, 0, xw, NT, wave, lane, li, lk, tmo);
         else if (wave == 0)
           bs_chain<false>(Wg, zp, xs, m - 1, 0, xw, NT, lane, li, lk);
       } else if (wave < 4) {
@@ -3073,14 +3086,15 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
         for (int dd = 1; dd < kTB; ++dd) xw[dd - 1] = xs[16 * (NT - nd - dd) + 15 - li];
         if (nd >= kBs2Rows)
           bs_chain2<true>(Wg + (size_t)NT * kTB * 256, zpg, xs, rdone_b, nd - 1, 0, xw, NT, wave - 2, lane, li,
-                          lk, bad);
+                          lk, tmo);
         else if (wave == 2)
           bs_chain<true>(Wg + (size_t)NT * kTB * 256, zpg, xs, nd - 1, 0, xw, NT, lane, li, lk);
       }
     }
   }
   if (tid == 0 && nd > 0) tflag[1] = epoch + 1;
-  if (bad && lane == 0) sh.fail = 1;   // (a back-substitution hand-off that timed out)
+  if (bad && lane == 0) sh.fail = 1;
+  if (tmo && lane == 0) sh.tmo = 1;   // a separator or back-substitution hand-off that timed out
   SG_TSTAMP(5)
   __syncthreads();
   double* y = d.work;
@@ -3090,9 +3104,9 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
   }
   if (!cand_lds) __syncthreads();
   if (cand_lds)
-    chol_candidates_lds<kTileThreads>(d, xs, sh.fail, cl, cur);
+    chol_candidates_lds<kTileThreads>(d, xs, sh.fail, cl, cur, sh.tmo);
   else
-    chol_candidates<kTileThreads>(d, xs, sh.fail);
+    chol_candidates<kTileThreads>(d, xs, sh.fail, sh.tmo);
   SG_TSTAMP(6)
   if (kStamp && lane == 0 && wave < 2)
     for (int s_ = 0; s_ < 16; ++s_) d.stamps[16 * wave + s_] += tacc[s_];
@@ -3306,7 +3320,9 @@ __global__ __launch_bounds__(kRedThreads) void k_upd_reduce(Dev d, int fuse) {
     s = *st;
     for (int j = 0; j < kCNum; ++j) cc[j] = d.xchg_chol[j];
   }
-  double v[kUNum] = {0, 0, 0, 0, 0, 0};
+  double v[kUNum] = {};
+  // the Cholesky's hand-off time-outs ride in the scalar exchange, so every shard ends the solve together
+  if (tid == 0) v[kUTimeout] = d.xchg_chol[kCTimeout];
   constexpr int kUpdU = 4;   // work units' loads in flight per thread (8 measured slower)
   for (int c0 = tid; c0 < d.npu; c0 += kUpdU * kRedThreads) {
     double t[kUpdU][5];
@@ -3359,6 +3375,13 @@ __global__ void k_decide(Dev d) {
 
 __device__ void decide_step(LmState& s, const double* u, const double* c) {
   if (s.done) return;
+  if (u[kUTimeout] > 0.0) {
+    // a Cholesky hand-off wait hit its spin limit: the step's solution is not trusted, and the solve reports
+    // it (summary.error in the reference, slam.cpp:520) instead of silently rejecting the step
+    s.sync_timeouts += (int)u[kUTimeout];
+    s.done = 1; s.ok = 0; s.termination = SG_DEVICE_TIMEOUT;
+    return;
+  }
   const double model = u[kUModel] + c[kCModel];
   const double step2 = u[kUStep2] + c[kCStep2];
   const bool solved = u[kULinFail] == 0.0 && c[kCFail] == 0.0 && isfinite(step2) && isfinite(model);
@@ -3412,6 +3435,12 @@ __device__ void decide_step(LmState& s, const double* u, const double* c) {
   s.reuse_diag = 1;
   if (!s.disable_term && s.radius < s.min_radius) {
     s.done = 1; s.ok = 1; s.termination = SG_PARAMETER_TOLERANCE;
+    return;
+  }
+  if (s.always_lin) {
+    // benchmark unit (every LM iteration linearizes): re-linearize at the same x — the same
+    // residuals, Jacobians and diagonal, so the same trajectory — and let k_cam_finalize push the iteration
+    s.need_lin = 1;
     return;
   }
   s.pushed += 1;
@@ -4151,8 +4180,9 @@ void BaSolver::Load(const sg_problem& p) {
   stg.Add(s_lidx_, s_lidx);
   stg.Add(r_loff_, r_loff);
   stg.Add(r_lidx_, r_lidx);
-  stg.Add(fd_a_, fd_a);
-  stg.Add(fd_b_, fd_b);
+  // padded to one entry: k_cam_finalize prefetches fd_a[0] / fd_b[0] beside LmState even when D = 0
+  stg.Add(fd_a_, fd_a.empty() ? std::vector<int32_t>{0} : fd_a);
+  stg.Add(fd_b_, fd_b.empty() ? std::vector<int32_t>{0} : fd_b);
   stg.Add(fd_boff_, fd_boff);
   stg.Add(fd_bidx_, fd_bidx.empty() ? std::vector<int32_t>{0} : fd_bidx);
   stg.Add(work_i_, panel_jmax);
@@ -4220,6 +4250,50 @@ void BaSolver::Load(const sg_problem& p) {
   }
   loaded_ = true;
   began_ = false;
+}
+
+void BaSolver::Reserve(int F, int P, int M) {
+  SG_REQUIRE(F >= 0 && P >= 0 && M >= 0, SG_EINVAL, "negative reservation");
+  SG_HIP_CHECK(hipSetDevice(dev_.device));
+  const size_t f = std::max(F, 1), pp = std::max(P, 1), m = std::max(M, 1);
+  bool moved = false;
+  // per observation (device order records, the Jacobian rows, the Schur cells)
+  moved |= J_.Reserve(m * kJStride);
+  moved |= obs_pt_.Reserve(2 * m);
+  moved |= obs_frame_.Reserve(m);
+  moved |= obs_fixed_.Reserve(m);
+  moved |= obs_meta_.Reserve(m);
+  moved |= obs_pnt_.Reserve(m);
+  moved |= cells_.Reserve(4 * m);
+  moved |= cell_obs_.Reserve(m);
+  moved |= llist_d_.Reserve(2 * m);
+  // per point
+  moved |= X_.Reserve(8 * pp);
+  moved |= V_.Reserve(10 * pp);
+  moved |= Vinv_.Reserve(10 * pp);
+  moved |= g_.Reserve(4 * pp);
+  moved |= tp_.Reserve(4 * pp);
+  moved |= scale_p_.Reserve(4 * pp);
+  moved |= diag_p_.Reserve(4 * pp);
+  moved |= pfree_.Reserve(pp);
+  moved |= poff_.Reserve(pp + 1);
+  moved |= pinfo_.Reserve(2 * pp);
+  moved |= pmx_.Reserve(4 * pp);
+  // per frame
+  moved |= q_.Reserve(8 * f);
+  moved |= t_.Reserve(6 * f);
+  moved |= frame_cam_.Reserve(f);
+  moved |= frame_block_.Reserve(f);
+  moved |= rot_free_.Reserve(f);
+  moved |= trans_free_.Reserve(f);
+  // the pinned staging buffer and its device copy: about 51 B per observation, 93 B per point, and per frame
+  // the pose slots, the FrameDistance pair table (NB^2) and the Cholesky's W tiles (2 * 8 tiles per 16 columns)
+  moved |= stager_->ReserveBytes(64 * m + 128 * pp + 16384 * f + 4 * f * f + (1u << 20));
+  if (moved) {   // the buffers of the loaded structure are gone: the next Load rebuilds everything
+    loaded_ = false;
+    began_ = false;
+    skey_ = StructKey{};
+  }
 }
 
 bool BaSolver::SameStructure(const sg_problem& p) const {
@@ -4434,6 +4508,7 @@ void BaSolver::Begin(const sg_solver_options& o) {
   s.max_iter = o.max_num_iterations;
   s.max_invalid = o.max_num_consecutive_invalid_steps;
   s.disable_term = o.disable_termination;
+  s.always_lin = o.always_linearize;
   s.jacobi = o.jacobi_scaling;
   s.ftol = o.function_tolerance;
   s.gtol = o.gradient_tolerance;
@@ -4519,11 +4594,11 @@ void BaSolver::Iterate(int n) {
     if (chol_tiles_ && d.stamps)
       hipLaunchKernelGGL(k_chol_tiles<true>, dim3(chol_nd_ > 0 ? 2 : 1), dim3(kTileThreads), tile_lds_, stream_, d,
                          (const int32_t*)work_i_.ptr, Wg_.ptr, tflag_.ptr, chol_nd_,
-                         chol_simdmap_ | (chol_cand_lds_ ? 2 : 0));
+                         chol_simdmap_ | (chol_cand_lds_ ? 2 : 0) | (chol_force_tmo_ ? 4 : 0));
     else if (chol_tiles_)
       hipLaunchKernelGGL(k_chol_tiles<false>, dim3(chol_nd_ > 0 ? 2 : 1), dim3(kTileThreads), tile_lds_, stream_, d,
                          (const int32_t*)work_i_.ptr, Wg_.ptr, tflag_.ptr, chol_nd_,
-                         chol_simdmap_ | (chol_cand_lds_ ? 2 : 0));
+                         chol_simdmap_ | (chol_cand_lds_ ? 2 : 0) | (chol_force_tmo_ ? 4 : 0));
     else if (chol_window_ && d.stamps)
       hipLaunchKernelGGL(k_cholesky_window<true>, dim3(1), dim3(kCholThreads), kCholLds, stream_, d,
                          (const int32_t*)work_i_.ptr, rdg_.ptr);
@@ -4598,6 +4673,7 @@ void BaSolver::Summary(sg_solver_summary* s) {
   s->fixed_cost = h.fixed_cost;
   s->trust_region_radius = h.radius;
   s->num_lm_iterations = h.lm_iters;
+  s->sync_timeouts = h.sync_timeouts;
 }
 
 void BaSolver::Download(sg_problem* p) {

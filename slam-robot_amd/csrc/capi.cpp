@@ -30,6 +30,7 @@ struct sg_slam {
   double error = 0.0;        // Slam::error_ (slam.cpp:518)
   sg_solver_summary last{};
   double phase_ms[4] = {0, 0, 0, 0};   // last SolveFrames / SolveAllFrames: setup, load, solve, write-back
+  int32_t res_f = 0, res_p = 0, res_m = 0;   // buffers reserved for a map of this size (high-water mark)
 };
 
 extern "C" {
@@ -84,6 +85,13 @@ int sg_ba_load(sg_ba* h, const sg_problem* p) {
   SG_CAPI_BEGIN
   SG_REQUIRE(h && p, SG_EINVAL, "null argument");
   h->solver->Load(*p);
+  SG_CAPI_END
+}
+
+int sg_ba_reserve(sg_ba* h, int32_t max_frames, int32_t max_points, int32_t max_obs) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(h, SG_EINVAL, "null handle");
+  h->solver->Reserve(max_frames, max_points, max_obs);
   SG_CAPI_END
 }
 
@@ -223,6 +231,16 @@ static void RunProblem(sg_slam* s, sg_problem* p, sg_map* map, const sg_solver_o
   static const bool timing = getenv("SG_HOST_TIMING") != nullptr;   // development aid: phase times to stderr
   auto now = [] { return std::chrono::steady_clock::now(); };
   const auto t0 = now();
+  // every window problem of this map is bounded by the whole map: reserve for it (with a quarter's headroom
+  // for the frames still to come) whenever the map outgrows the last reservation, so the device and pinned
+  // buffers do not grow inside the loads of the calls that follow (main.cpp's loop grows the map by a frame
+  // per call)
+  if (map->num_frames > s->res_f || map->num_points > s->res_p || map->num_obs > s->res_m) {
+    s->res_f = map->num_frames + map->num_frames / 4 + 4;
+    s->res_p = map->num_points + map->num_points / 4 + 64;
+    s->res_m = map->num_obs + map->num_obs / 4 + 512;
+    s->solver->Reserve(s->res_f, s->res_p, s->res_m);
+  }
   s->solver->Load(*p);
   const auto t1 = now();
   sg_solver_summary sum{};

@@ -21,12 +21,18 @@ struct DBuf {
     if (n <= cap) return;
     // grow geometrically: a map that grows by a frame per call (main.cpp's loop) would otherwise pay a
     // hipFree (a device synchronisation) and a hipMalloc on almost every load
-    const size_t ncap = cap ? std::max(n, cap + cap / 2) : n;
+    Reserve(cap ? std::max(n, 2 * cap) : n);
+  }
+  // Capacity for n elements without changing size (pre-sizing from a high-water mark: no reallocation, and
+  // so no hipFree / hipMalloc, on a later load's critical path).  Contents are not preserved.
+  bool Reserve(size_t ncap) {
+    if (ncap <= cap) return false;
     if (ptr) (void)hipFree(ptr);
     ptr = nullptr;
     cap = 0;
     SG_HIP_CHECK(hipMalloc(&ptr, std::max<size_t>(ncap, 1) * sizeof(T)));
     cap = ncap;
+    return true;
   }
   void Upload(const std::vector<T>& v, hipStream_t s) {
     Resize(v.size());

@@ -182,6 +182,7 @@ void sg_solver_options_default(sg_solver_options* o) {
   o->max_num_consecutive_invalid_steps = 5;
   o->jacobi_scaling = 1;
   o->disable_termination = 0;
+  o->always_linearize = 0;
 }
 
 void sg_device_options_default(sg_device_options* o) {

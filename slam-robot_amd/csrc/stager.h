@@ -39,8 +39,18 @@ __global__ __launch_bounds__(256) void k_stage_scatter(const StagePiece* __restr
 class Stager {
  public:
   ~Stager() {
+    WaitCopy();
+    if (copied_) (void)hipEventDestroy(copied_);
     if (host_) (void)hipHostFree(host_);
   }
+
+  // Pre-size the pinned buffer (a caller that knows its map's high-water mark): growing it later costs a
+  // pinned allocation (milliseconds for tens of MB) on the load's critical path.
+  bool ReserveBytes(size_t bytes) {
+    if (bytes > cap_) Grow(bytes);
+    return dev_.Reserve(bytes);
+  }
+  size_t staged_bytes() const { return last_bytes_; }
 
   // Resize dst to v.size() and queue v for it (the copy happens in Flush).
   template <typename T>
@@ -54,8 +64,10 @@ class Stager {
     max_bytes_ = std::max(max_bytes_, bytes);
   }
 
-  // Drop anything queued (a load that failed part way).
+  // Drop anything queued (a load that failed part way).  The previous batch's DMA may still read the pinned
+  // buffer if that load threw between Flush and its stream synchronisation: wait for it first.
   void Clear() {
+    WaitCopy();
     pieces_.clear();
     used_ = 0;
     max_bytes_ = 0;
@@ -71,6 +83,10 @@ class Stager {
     std::memcpy(host_ + tbl, pieces_.data(), tbytes);
     dev_.Resize(used_);
     SG_HIP_CHECK(hipMemcpyAsync(dev_.ptr, host_, used_, hipMemcpyHostToDevice, s));
+    if (!copied_) SG_HIP_CHECK(hipEventCreateWithFlags(&copied_, hipEventDisableTiming));
+    SG_HIP_CHECK(hipEventRecord(copied_, s));
+    pending_ = true;
+    last_bytes_ = used_;
     const unsigned gx = (unsigned)std::min<size_t>(64, std::max<size_t>(1, (max_bytes_ / 16 + 255) / 256));
     hipLaunchKernelGGL(k_stage_scatter, dim3(gx, (unsigned)pieces_.size()), dim3(256), 0, s,
                        reinterpret_cast<const StagePiece*>(dev_.ptr + tbl), dev_.ptr);
@@ -81,27 +97,40 @@ class Stager {
   }
 
  private:
+  void WaitCopy() {
+    if (pending_) {
+      (void)hipEventSynchronize(copied_);
+      pending_ = false;
+    }
+  }
+
   size_t Reserve(size_t bytes) {
+    if (used_ == 0) WaitCopy();   // first piece of a batch: the buffer is about to be rewritten
     const size_t off = (used_ + 15) & ~(size_t)15;
     const size_t need = off + bytes;
-    if (need > cap_) {
-      // grow: keep what is queued (pieces_ hold offsets, not host pointers)
-      const size_t ncap = std::max(need, cap_ + cap_ / 2 + (1 << 16));
-      unsigned char* nh = nullptr;
-      SG_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&nh), ncap, hipHostMallocDefault));
-      if (host_) {
-        std::memcpy(nh, host_, used_);
-        (void)hipHostFree(host_);
-      }
-      host_ = nh;
-      cap_ = ncap;
-    }
+    if (need > cap_) Grow(std::max(need, 2 * cap_));   // geometric: a growing map re-pins O(log) times
     used_ = need;
     return off;
   }
 
+  // Keeps what is queued (pieces_ hold offsets, not host pointers).  At least 8 MB, rounded to 1 MB.
+  void Grow(size_t want) {
+    WaitCopy();
+    const size_t ncap = (std::max<size_t>(want, 8u << 20) + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);
+    unsigned char* nh = nullptr;
+    SG_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&nh), ncap, hipHostMallocDefault));
+    if (host_) {
+      std::memcpy(nh, host_, used_);
+      (void)hipHostFree(host_);
+    }
+    host_ = nh;
+    cap_ = ncap;
+  }
+
   unsigned char* host_ = nullptr;
-  size_t cap_ = 0, used_ = 0, max_bytes_ = 0;
+  size_t cap_ = 0, used_ = 0, max_bytes_ = 0, last_bytes_ = 0;
+  hipEvent_t copied_ = nullptr;
+  bool pending_ = false;
   std::vector<StagePiece> pieces_;
   DBuf<unsigned char> dev_;
 };

@@ -120,6 +120,11 @@ class BundleAdjuster:
         ps = pa.struct()
         check(self.lib.sg_ba_load(self.h, C.byref(ps)), "sg_ba_load")
 
+    def reserve(self, max_frames: int, max_points: int, max_obs: int):
+        """Pre-size the device / pinned buffers for problems up to this size (drops the loaded problem if it
+        reallocates)."""
+        check(self.lib.sg_ba_reserve(self.h, max_frames, max_points, max_obs), "sg_ba_reserve")
+
     def load_counts(self) -> tuple:
         """(full loads, value-only loads): a load with the previous load's structure reuses its index lists."""
         full, vals = C.c_int32(0), C.c_int32(0)

@@ -16,7 +16,8 @@ LIB_PATH = os.path.join(CSRC_DIR, "libslamgpu.so")
 
 SG_OK = 0
 TERMINATION = {0: "NO_CONVERGENCE", 1: "FUNCTION_TOLERANCE", 2: "GRADIENT_TOLERANCE",
-               3: "PARAMETER_TOLERANCE", 4: "NUMERICAL_FAILURE", 5: "DID_NOT_RUN"}
+               3: "PARAMETER_TOLERANCE", 4: "NUMERICAL_FAILURE", 5: "DID_NOT_RUN",
+               6: "DEVICE_TIMEOUT"}
 
 # TrackedPoint::Flags bit positions (localmap.h:184-190)
 BAD_LOCATION, NO_BASELINE, NO_OBSERVATIONS, MISMATCHED, BAD_FEATURE = range(5)
@@ -57,7 +58,7 @@ class SgSolverOptions(C.Structure):
         ("max_trust_region_radius", C.c_double), ("min_trust_region_radius", C.c_double),
         ("min_lm_diagonal", C.c_double), ("max_lm_diagonal", C.c_double),
         ("max_num_consecutive_invalid_steps", C.c_int32), ("jacobi_scaling", C.c_int32),
-        ("disable_termination", C.c_int32),
+        ("disable_termination", C.c_int32), ("always_linearize", C.c_int32),
     ]
 
 
@@ -67,11 +68,11 @@ class SgSolverSummary(C.Structure):
         ("num_unsuccessful_steps", C.c_int32), ("num_invalid_steps", C.c_int32),
         ("termination_type", C.c_int32), ("ok", C.c_int32),
         ("initial_cost", C.c_double), ("final_cost", C.c_double), ("fixed_cost", C.c_double),
-        ("trust_region_radius", C.c_double), ("num_lm_iterations", C.c_int32), ("reserved", C.c_int32),
+        ("trust_region_radius", C.c_double), ("num_lm_iterations", C.c_int32), ("sync_timeouts", C.c_int32),
     ]
 
     def as_dict(self):
-        d = {name: getattr(self, name) for name, _ in self._fields_ if name != "reserved"}
+        d = {name: getattr(self, name) for name, _ in self._fields_}
         d["termination"] = TERMINATION.get(self.termination_type, "?")
         return d
 
@@ -100,7 +101,7 @@ def default_solver_options(**kw) -> SgSolverOptions:
         parameter_tolerance=1e-8, min_relative_decrease=1e-3, initial_trust_region_radius=1e4,
         max_trust_region_radius=1e16, min_trust_region_radius=1e-32, min_lm_diagonal=1e-6,
         max_lm_diagonal=1e32, max_num_consecutive_invalid_steps=5, jacobi_scaling=1,
-        disable_termination=0)
+        disable_termination=0, always_linearize=0)
     for key, val in kw.items():
         setattr(o, key, val)
     return o
@@ -254,6 +255,7 @@ SYMBOLS = {
     "sg_comm_group_destroy": (None, [C.c_void_p]),
     "sg_ba_comm_init_local": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32]),
     "sg_ba_load": (C.c_int, [C.c_void_p, C.POINTER(SgProblem)]),
+    "sg_ba_reserve": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32]),
     "sg_ba_load_counts": (C.c_int, [C.c_void_p, _ip, _ip]),
     "sg_ba_info_get": (C.c_int, [C.c_void_p, C.POINTER(SgBaInfo)]),
     "sg_ba_solve": (C.c_int, [C.c_void_p, C.POINTER(SgSolverOptions), C.POINTER(SgProblem),

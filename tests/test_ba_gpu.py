@@ -40,6 +40,7 @@ def _solve_both(oracle_lib, pa, options=None, nthreads=1):
 
 def _assert_same_minimum(oracle_lib, pg, sg, po, so):
     assert sg["ok"] == so["ok"] == 1
+    assert sg["sync_timeouts"] == 0
     assert sg["termination"] == so["termination"] or {sg["termination"], so["termination"]} <= {
         "FUNCTION_TOLERANCE", "PARAMETER_TOLERANCE", "GRADIENT_TOLERANCE"}
     assert abs(sg["initial_cost"] - so["initial_cost"]) <= 1e-10 * so["initial_cost"]
@@ -69,7 +70,28 @@ def test_residual_sweep_matches_oracle(gpu_lib, oracle_lib):
         assert abs(cost - co) <= 1e-12 * co
 
 
+def test_golden_c1_first_20_iterations(gpu_lib):
+    """The C1 golden's first 20 LM iterations, iteration for iteration: the same accepted steps, cost to 1e-9
+    relative, poses and points to 1e-9.  (From about iteration 25 the trust radius passes 1e15, where the
+    homogeneous 4x4 point blocks — rank 3: X and lambda X project alike — are singular to rounding and steps
+    turn invalid by rounding-level differences; see test_golden_c1_solve.)"""
+    pa, g = _golden()
+    b = ba.BundleAdjuster()
+    pg = pa.copy()
+    b.load(pg)
+    s = b.solve(default_solver_options(max_num_iterations=20))
+    assert s["num_successful_steps"] == int(g["oracle20_num_successful"]) == 20
+    assert abs(s["final_cost"] - float(g["oracle20_final_cost"])) <= 1e-9 * float(g["oracle20_final_cost"])
+    np.testing.assert_allclose(pg.q, g["oracle20_q"], rtol=0, atol=1e-9)
+    np.testing.assert_allclose(pg.t, g["oracle20_t"], rtol=0, atol=1e-6)
+    np.testing.assert_allclose(pg.X, g["oracle20_X"], rtol=0, atol=1e-9)
+
+
 def test_golden_c1_solve(gpu_lib, oracle_lib):
+    """The full C1 solve.  The oracle takes 158 iterations, 72 of them invalid steps at trust radii >= 1e15
+    where the homogeneous point blocks are singular to rounding (test_golden_c1_first_20_iterations): the two
+    solvers' invalid-step counts there differ with rounding, so the iteration count is compared within 20
+    and the minimum to 1e-6 relative cost, 1e-2 mm, 1e-6."""
     pa, g = _golden()
     b = ba.BundleAdjuster()
     pg = pa.copy()
@@ -81,8 +103,34 @@ def test_golden_c1_solve(gpu_lib, oracle_lib):
     assert abs(s["num_iterations"] - int(g["oracle_num_iterations"])) <= 20
     np.testing.assert_allclose(pg.t, g["oracle_t"], atol=1e-2)
     np.testing.assert_allclose(pg.q, g["oracle_q"], atol=1e-6)
-    # and against the independent scipy minimum
+    # scipy started at the oracle's minimum stays there (local-minimum check)
     np.testing.assert_allclose(pg.t, g["scipy_t"], atol=1e-2)
+
+
+def test_golden_c1_clean_matches_independent_minimum(gpu_lib):
+    """the outlier-free C1 scene solved on the device (tight tolerances) reaches the minimum
+    scipy found from the perturbed start with no oracle code (tests/golden/make_golden.py): objective to 1e-8
+    relative, translations 1e-2 mm, rotations 1e-6, points (unit homogeneous) 1e-5."""
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "c1_clean_ba.npz"))
+    pa = ProblemArrays(**{f: g[f"in_{f}"] for f in ProblemArrays.FIELDS if f not in
+                          ("frame_map_index", "point_map_index")},
+                       frame_map_index=g["in_frame_map_index"], point_map_index=g["in_point_map_index"],
+                       range_=float(g["in_range"]))
+    b = ba.BundleAdjuster()
+    pg = pa.copy()
+    b.load(pg)
+    s = b.solve(default_solver_options(function_tolerance=1e-13, parameter_tolerance=1e-13,
+                                       max_num_iterations=500))
+    assert s["ok"] == 1 and s["sync_timeouts"] == 0
+    var = s["final_cost"] - s["fixed_cost"]
+    assert abs(var - float(g["scipy_cost"])) <= 1e-8 * var
+    np.testing.assert_allclose(pg.t, g["scipy_t"], atol=1e-2)
+    np.testing.assert_allclose(pg.q, g["scipy_q"], atol=1e-6)
+    Xg = pg.X.reshape(-1, 4)
+    Xs = g["scipy_X"].reshape(-1, 4)
+    unit = lambda X: X / np.linalg.norm(X, axis=1, keepdims=True) * np.sign(X[:, 3:])  # noqa: E731
+    np.testing.assert_allclose(unit(Xg), unit(Xs), atol=1e-5)
 
 
 @pytest.mark.parametrize("seed", [1, 3, 4, 7])
@@ -122,7 +170,7 @@ def test_c5_first_iterations_match_oracle(gpu_lib, oracle_lib):
     assert info["cholesky"].startswith("tiled band")
     sg = g.solve(o)
     so = oracle_lib.solve(po, o, nthreads=min(16, os.cpu_count() or 1))
-    assert sg["ok"] == so["ok"] == 1
+    assert sg["ok"] == so["ok"] == 1 and sg["sync_timeouts"] == 0
     assert sg["num_iterations"] == so["num_iterations"] == 4
     assert sg["num_successful_steps"] == so["num_successful_steps"]
     assert abs(sg["initial_cost"] - so["initial_cost"]) <= 1e-10 * so["initial_cost"]
@@ -247,8 +295,9 @@ def test_slam_too_few_frames_returns_false(gpu_lib):
 def test_packed_band_exchange_is_exact(gpu_lib, monkeypatch):
     """The landmark-shard exchange packs the band of S (per panel: rows of the panel, columns up to its band
     end) and the rhs into one buffer for the all-reduce and unpacks it afterwards.  Forced on
-    one GPU (SG_PACK_S), the pack/unpack round trip must leave the solve unchanged.  k_schur accumulates the
-    window blocks with LDS atomics, so two runs agree to rounding only (cost rel 1e-12), not bit for bit."""
+    one GPU (SG_PACK_S), the pack/unpack round trip must leave the solve unchanged.  It is a copy, and the
+    device chain is deterministic at C2 (k_schur sums each window tile in MFMA accumulators in point order;
+    no point is wide enough for the global-atomic k_schur_wide path), so the two solves agree bit for bit."""
     m = make_config("C2")
     pa = ba.problem_from_map_frames(m, m.num_frames - 2, m.num_frames, 2.0)
     out = []
@@ -262,12 +311,10 @@ def test_packed_band_exchange_is_exact(gpu_lib, monkeypatch):
         out.append((s, p))
         g.close()
     (s0, p0), (s1, p1) = out
-    assert s0["num_iterations"] == s1["num_iterations"]
-    assert s0["num_successful_steps"] == s1["num_successful_steps"]
-    assert abs(s0["final_cost"] - s1["final_cost"]) <= 1e-12 * s0["final_cost"]
-    np.testing.assert_allclose(p0.q, p1.q, rtol=0, atol=1e-12)
-    np.testing.assert_allclose(p0.t, p1.t, rtol=1e-9, atol=1e-9)
-    np.testing.assert_allclose(p0.X, p1.X, rtol=1e-9, atol=1e-12)
+    assert s0 == s1
+    np.testing.assert_array_equal(p0.q, p1.q)
+    np.testing.assert_array_equal(p0.t, p1.t)
+    np.testing.assert_array_equal(p0.X, p1.X)
 
 
 
@@ -298,6 +345,7 @@ def test_dissected_band_matches_one_workgroup(gpu_lib, monkeypatch, frames, poin
         g.close()
     (s0, p0), (s1, p1) = out
     assert s0["ok"] == s1["ok"] == 1
+    assert s0["sync_timeouts"] == s1["sync_timeouts"] == 0
     assert s0["num_iterations"] == s1["num_iterations"]
     assert s0["num_successful_steps"] == s1["num_successful_steps"]
     assert abs(s0["final_cost"] - s1["final_cost"]) <= 1e-12 * s0["final_cost"]
@@ -365,10 +413,11 @@ def test_slam_solve_all_frames_with_cameras(gpu_lib, oracle_lib):
     assert not np.allclose(mg.k, m.k)
 
 
-def test_deterministic_mode_is_bitwise_reproducible(gpu_lib, monkeypatch):
-    """SG_DETERMINISTIC=1: every Schur window block is summed by one wave in a fixed order (the default sums
-    with LDS atomics from four waves, reproducible to rounding only), so two solves agree bit for bit."""
-    monkeypatch.setenv("SG_DETERMINISTIC", "1")
+def test_solve_is_bitwise_reproducible(gpu_lib):
+    """Two C2 solves on fresh handles agree bit for bit: k_schur sums every window tile in MFMA accumulators
+    in point order, the camera and Schur partials are reduced in host-fixed order, and the in-wave LDS
+    accumulation of k_linearize is serialised by its per-block lists (only k_schur_wide, for points wider
+    than a segment window, uses global atomics; C2 has none)."""
     m = make_config("C2")
     pa = ba.problem_from_map_frames(m, 48, 50, 2.0)
     out = []
@@ -383,3 +432,40 @@ def test_deterministic_mode_is_bitwise_reproducible(gpu_lib, monkeypatch):
     np.testing.assert_array_equal(p0.q, p1.q)
     np.testing.assert_array_equal(p0.t, p1.t)
     np.testing.assert_array_equal(p0.X, p1.X)
+
+
+def test_problem_without_frame_distance(gpu_lib, oracle_lib):
+    """num_dist = 0 (no frame has a presented previous frame): k_cam_finalize's FrameDistance prefetch must not
+    touch the (padded) empty pair arrays, and the solve matches the oracle."""
+    m = make_config("C1")
+    pa = ba.problem_from_map_frames(m, 8, 10, 2.0)
+    pa.dist_frame = np.zeros(0, np.int32)
+    pa.dist_prev = np.zeros(0, np.int32)
+    pg, sg, po, so = _solve_both(oracle_lib, pa, default_solver_options(max_num_iterations=4))
+    assert sg["ok"] == so["ok"] == 1
+    assert sg["num_successful_steps"] == so["num_successful_steps"]
+    assert abs(sg["final_cost"] - so["final_cost"]) <= 1e-9 * so["final_cost"]
+    np.testing.assert_allclose(pg.t, po.t, rtol=0, atol=1e-6)
+
+
+def test_cholesky_handoff_timeout_is_reported(gpu_lib, monkeypatch):
+    """The dissected Cholesky's separator wait is bounded.  Forced to time out (SG_CHOL_FORCE_TIMEOUT: the
+    bottom workgroup sleeps ~2 ms, the top polls 256 times), the solve must end with DEVICE_TIMEOUT, ok = 0 and
+    a non-zero sync_timeouts count (slam.cpp:520: the caller sees the failure) instead of silently rejecting
+    the step; without the knob the same solve reports zero time-outs."""
+    m = make_config("C2")
+    pa = ba.problem_from_map_frames(m, 48, 50, 2.0)
+    o = default_solver_options(max_num_iterations=3)
+    g = ba.BundleAdjuster()
+    g.load(pa.copy())
+    assert g.info()["cholesky_split"] > 0
+    s = g.solve(o)
+    assert s["ok"] == 1 and s["sync_timeouts"] == 0
+    g.close()
+    monkeypatch.setenv("SG_CHOL_FORCE_TIMEOUT", "1")
+    g = ba.BundleAdjuster()
+    g.load(pa.copy())
+    s = g.solve(o)
+    g.close()
+    assert s["termination"] == "DEVICE_TIMEOUT" and s["ok"] == 0
+    assert s["sync_timeouts"] >= 1

@@ -199,8 +199,8 @@ def test_failed_load_then_reload(gpu_lib):
     g.load(pa.copy())
     with pytest.raises(SlamGpuError, match="65536"):
         g.load(bad)
-    # k_schur sums each window block with LDS atomics from four waves (order not fixed), so two runs agree
-    # to rounding: compare three iterations, not a ~150-iteration solve whose stopping step can move
+    # the device chain is deterministic (k_schur: MFMA accumulators in point order; fixed-order partial
+    # reductions), so the reloaded handle and a fresh one agree bit for bit
     o = default_solver_options(max_num_iterations=3)
     p1 = pa.copy()
     g.load(p1)
@@ -210,6 +210,6 @@ def test_failed_load_then_reload(gpu_lib):
     f.load(p2)
     s2 = f.solve(o)
     assert s1["num_iterations"] == s2["num_iterations"] == 4
-    assert s1["num_successful_steps"] == s2["num_successful_steps"]
-    assert abs(s1["final_cost"] - s2["final_cost"]) <= 1e-12 * s2["final_cost"]
-    np.testing.assert_allclose(p1.X, p2.X, rtol=0, atol=1e-12)
+    assert s1 == s2
+    np.testing.assert_array_equal(p1.X, p2.X)
+    np.testing.assert_array_equal(p1.q, p2.q)

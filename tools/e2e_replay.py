@@ -101,6 +101,17 @@ for name, rows in stats.items():
     print("SolveFrames(%s): %d calls, %.1f LM iterations; setup %.2f ms, load %.2f ms, LM loop %.2f ms, "
           "write-back %.2f ms, wall %.2f ms" % (name, len(rows), mean["iterations"], mean["setup"], mean["load"],
                                                 mean["solve"], mean["write_back"], mean["wall"]))
+allc = [r for rows in stats.values() for r in rows]
+later = sorted(allc, key=lambda r: r["frame"])[1:]
+crit = {"sum_load_ms": float(sum(r["load"] for r in allc)), "sum_solve_ms": float(sum(r["solve"] for r in allc)),
+        "max_load_after_first_ms": float(max(r["load"] for r in later)) if later else None}
+crit["load_over_solve"] = crit["sum_load_ms"] / crit["sum_solve_ms"]
+for name, rows in stats.items():
+    if rows:
+        crit["median_load_ms_%s" % name] = float(np.median([r["load"] for r in rows]))
+        crit["median_solve_ms_%s" % name] = float(np.median([r["solve"] for r in rows]))
+summary["criteria"] = crit
+print("criteria:", json.dumps(crit))
 print("load counts (full, values):", slam.load_counts())
 os.makedirs(os.path.dirname(out_path), exist_ok=True)
 with open(out_path, "w") as f:

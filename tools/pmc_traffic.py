@@ -5,7 +5,7 @@ reports half the bytes of a wide coalesced read (128-B requests tallied at 64 B)
 WRITE_SIZE is taken as is.  Dispatches are grouped by (kernel, grid size) so the config-2 BA launches and
 the scaled-sweep launches of k_linearize stay apart; a kernel that early-exits on some launches
 (k_linearize after a rejected LM step) is summarised over its active launches (write traffic above half
-of the group's maximum).  Usage: pmc_traffic.py <pmc dir> <out.json>
+of the group's maximum).  Usage: pmc_traffic.py <pmc dir> <out.json> [command that was profiled]
 """
 import collections
 import csv
@@ -46,8 +46,9 @@ def main():
         groups["%s@grid%d" % (name, grid)] = {
             "kernel": name, "grid_size": grid, "dispatches": n, "active_dispatches": len(act),
             "fetch_bytes": fb, "write_bytes": wb, "traffic_bytes": fb + wb}
-    res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) over bench.py "
-                     "--steps 20 --warmup 4 --cpu-seconds 0; FETCH_SIZE doubled (gfx950), KiB -> bytes",
+    cmd = sys.argv[3] if len(sys.argv) > 3 else "bench.py --steps 20 --warmup 4 --cpu-seconds 0"
+    res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) over %s; FETCH_SIZE "
+                     "doubled (gfx950), KiB -> bytes" % cmd,
            "kernels": groups}
     json.dump(res, open(out, "w"), indent=1)
     for k, g in sorted(groups.items()):
