@@ -60,6 +60,8 @@ def parse():
     ap.add_argument("--frontend", type=int, default=1,
                     help="also measure the front end at N=1: KLT tracks/sec (config 3) and the 256-bit "
                          "Hamming matcher (config 4)")
+    ap.add_argument("--model-scaling", type=int, default=1,
+                    help="N = 1: model C5 strong scaling over 2/4/8 landmark shards from measured kernel times")
     ap.add_argument("--only", choices=("all", "C2", "C5", "sweep", "frontend"), default="all",
                     help="profiling runs: one workload alone (its kernels are then the only ones launched)")
     args = ap.parse_args()
@@ -433,6 +435,59 @@ def bench_sweep(local, sweep_obs):
             "ms_per_launch": kt[0], "bytes_per_launch": wb, **traffic_fields("k_linearize", "sweep", wb)}
 
 
+REPLICATED = ("cam_finalize", "cholesky", "decide")   # every landmark shard runs these on the whole system
+
+
+def model_scaling(local, full, full_kernel_ms, ns=(2, 4, 8), steps=20, warmup=3,
+                  allreduce_us=20.0, band_gbs=50.0):
+    """Modelled strong scaling of a BA workload over N landmark shards, from measured kernel times: every
+    shard of the N-way split (sg_problem_shard) is loaded alone on this GPU and timed (always-linearize
+    iterations, HIP events); a shard's iteration = its shardable kernels (linearize, camera reduce, Schur,
+    S reduce, point update, update reduce) + the replicated ones measured on the whole problem (camera
+    finalize, Cholesky, decision: every rank runs them on the full reduced system) + three all-reduces per
+    iteration (camera blocks, the packed band of S, the update scalars) priced at `allreduce_us` each plus the
+    band at `band_gbs` (assumptions, not measurements: RCCL over xGMI is not measurable on this 1-GPU box).
+    The slowest shard sets the pace."""
+    from slamgpu import ba
+    from slamgpu.capi import default_solver_options
+    rep_ms = sum(full_kernel_ms.get(k, 0.0) for k in REPLICATED)
+    one_ms = sum(full_kernel_ms.values())
+    out = {"n": [1], "ms_per_iter": [one_ms], "speedup": [1.0], "replicated_ms": rep_ms,
+           "shard_compute_ms": [one_ms - rep_ms], "allreduce_ms": [0.0]}
+    for n in ns:
+        worst = 0.0
+        band = None
+        for r in range(n):
+            sh = ba.shard_problem(full, r, n)
+            g = ba.BundleAdjuster(device=local)
+            g.load(sh)
+            if band is None:
+                info = g.info()
+                band = 8.0 * info["n"] * min(info["n"], 16 * (info["band_tiles"] + 1))
+            g.begin(default_solver_options(max_num_iterations=warmup + steps + 4, disable_termination=1,
+                                           always_linearize=1))
+            g.iterate(warmup)
+            g.sync()
+            g.set_timing(True)
+            g.iterate(steps)
+            g.sync()
+            kt = g.kernel_times()
+            g.close()
+            shard_ms = sum(v[0] * v[1] for k, v in kt.items() if k not in REPLICATED) / steps
+            worst = max(worst, shard_ms)
+        ar_ms = 3 * allreduce_us * 1e-3 + band / (band_gbs * 1e9) * 1e3
+        t = worst + rep_ms + ar_ms
+        out["n"].append(n)
+        out["shard_compute_ms"].append(worst)
+        out["allreduce_ms"].append(ar_ms)
+        out["ms_per_iter"].append(t)
+        out["speedup"].append(one_ms / t)
+    out["assumptions"] = ("all-reduce %.0f us each (3 per iteration) + the packed band at %.0f GB/s; the slowest "
+                          "shard's measured shardable kernels + the whole problem's replicated kernels (%s)"
+                          % (allreduce_us, band_gbs, ", ".join(REPLICATED)))
+    return out
+
+
 def main():
     args = parse()
     ws, rank, local = dist_env()
@@ -463,13 +518,16 @@ def main():
         if rank == 0:
             pk2, roof2, sw2 = kernel_report(r2, k2, "n=%d, band %d tiles" % (i2["n"], i2["band_tiles"]), ocfg)
             val2 = (n_gpus if ocfg == "C2" else 1) * k2 / r2["elapsed"]
+            scal = None
+            if ocfg == "C5" and n_gpus == 1 and args.model_scaling:
+                scal = model_scaling(local, f2, pk2)
             other = {"workload": d2, "scaling": "weak" if ocfg == "C2" else "strong", "value": val2,
                      "unit": "iters/s", "steps": k2, "ms_per_step": 1e3 * r2["elapsed"] / k2,
                      "accepted_frac": r2["accepted"] / k2, "lm_regime": r2["lm_regime"], "keyframes": f2.num_frames,
                      "landmarks": f2.num_points, "observations": f2.num_obs, "per_rank": {
                          "landmarks": p2.num_points, "observations": p2.num_obs}, "solver": i2,
                      "kernel_ms_per_iter": pk2, "roofline": roof2, "roofline_sweep": sw2,
-                     "solve_from_start": st2, "shard_balance": b2}
+                     "solve_from_start": st2, "shard_balance": b2, "strong_scaling_model": scal}
 
     if rank != 0:
         if dist is not None:

@@ -2361,6 +2361,9 @@ struct TileShared {
   double prw[2 * kCholNb];     // the owner's next two pivot rows
   int fail;
   int tmo;                     // a hand-off wait hit its spin limit (kCTimeout)
+  int uflag;                   // look-ahead: the last phase whose owner has posted U_{K,K+1} (Ur[K & 1][0])
+  int dflag;                   // Dinv mode: the last phase whose D_K^-1 and z'_K are posted (Dv, zp)
+  double Dv[16 * kTLd];        // Dinv mode: D_K^-1 = Z_K^T Z_K, row-major
   int simd[kTB];               // SIMD of each wave
   double Id[16 * kTLd];        // the identity (the factor's augmented columns)
 };
@@ -2493,7 +2496,50 @@ __device__ __forceinline__ bool tile_factor(const double* D, const double* Yk, c
   return bad;
 }
 
+// The same factorisation with the pivot rows broadcast by v_readlane (wave-uniform SGPR multipliers, no LDS
+// round trip on the pivot chain), two pivots per step: rows j and j+1 are read together and every lane
+// derives pivot j+1's row from them (uniform arithmetic), then applies both eliminations to its own column.
+// Same arithmetic as tile_factor up to rounding (the second pivot row is formed as in tile_factor's v1).
+__device__ __forceinline__ bool tile_factor_rl(const double* D, const double* Yk, const double* Id,
+                                               double (&ca)[16]) {
+  const int lane = opaque_lane();
+  const int c = lane & 15;
+  const bool isy = lane == 32;
+  const double* b0 = isy ? Yk : ((lane >= 16 && lane < 32) ? Id + c : D + c);
+  const int rs = isy ? 1 : kTLd;
+#pragma unroll
+  for (int r = 0; r < kCholNb; ++r) ca[r] = b0[r * rs];
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < kCholNb; j += 2) {
+    double a[kCholNb], b[kCholNb];   // raw rows j and j+1 at columns >= j / >= j+1 (uniform)
+#pragma unroll
+    for (int r = j; r < kCholNb; ++r) a[r] = readlane_d(ca[j], r);
+#pragma unroll
+    for (int r = j + 1; r < kCholNb; ++r) b[r] = readlane_d(ca[j + 1], r);
+    const double p0 = a[j];
+    bad |= !(p0 > 0.0);
+    const double i0 = rsq_nr1(p0);
+    const double r0 = i0 * i0;
+    const double w1 = a[j + 1] * r0;
+    const double p1 = fma(-w1, a[j + 1], b[j + 1]);
+    bad |= !(p1 > 0.0);
+    const double i1 = rsq_nr1(p1);
+    const double r1 = i1 * i1;
+    const double cj = ca[j];
+    const double t0 = cj * r0;
+    ca[j] = cj * i0;
+    const double cj1 = fma(-a[j + 1], t0, ca[j + 1]);
+    const double t1 = cj1 * r1;
+    ca[j + 1] = cj1 * i1;
+#pragma unroll
+    for (int r = j + 2; r < kCholNb; ++r) ca[r] = fma(-fma(-w1, a[r], b[r]), t1, fma(-a[r], t0, ca[r]));
+  }
+  return bad;
+}
+
 // The owner of the next diagonal: D (acc layout) and its rhs partials -> Z, z and Z^T z of tile row K.
+template <bool kRl = false>
 __device__ __forceinline__ bool tile_diag(const f64x4& D, double ypart, TileShared& sh, double* zp, int K,
                                           int lane, int li, int lk) {
 #pragma unroll
@@ -2501,7 +2547,7 @@ __device__ __forceinline__ bool tile_diag(const f64x4& D, double ypart, TileShar
   const double ys = sum_rows4(ypart);
   if (lk == 0) sh.Yw[li] = ys;
   double ca[kCholNb];
-  const bool bad = tile_factor(sh.Dw, sh.Yw, sh.Id, sh.prw, ca);
+  const bool bad = kRl ? tile_factor_rl(sh.Dw, sh.Yw, sh.Id, ca) : tile_factor(sh.Dw, sh.Yw, sh.Id, sh.prw, ca);
   double* Zs = sh.Zs[K & 3];
   double* zk = sh.zK[K & 3];
   if (lane >= 16 && lane < 32) {
@@ -2528,6 +2574,23 @@ __device__ __forceinline__ void tile_zp(const TileShared& sh, double* zp, int K,
   }
 }
 
+// Dinv mode (flags bit 5): D_K^-1 = Z_K^T Z_K (one MFMA chain from the posted Z_K) and z'_K, posted for the
+// phase's other waves by the wave that factored D_K (in its late step), released by dflag = K.
+__device__ __forceinline__ void tile_dinv_post(TileShared& sh, double* zp, int K, int lane, int li, int lk) {
+  const double* Zs = sh.Zs[K & 3];
+  double zt[4];
+  f64x4 zb;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) zb[s] = zt[s] = Zs[(4 * s + lk) * kTLd + li];
+  const f64x4 zero = {0.0, 0.0, 0.0, 0.0};
+  const f64x4 Dv = mfma_f64_k16(zt, zb, zero);   // (Z^T Z)[lk + 4q][li]
+#pragma unroll
+  for (int q = 0; q < 4; ++q) sh.Dv[(lk + 4 * q) * kTLd + li] = Dv[q];
+  tile_zp(sh, zp, K, lane);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (lane == 0) __hip_atomic_store(&sh.dflag, K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // Diagnostic stamps (SG_STAMP=1): lane 0 of every wave accumulates s_memtime deltas per phase; waves 0 and 1
 // report (tools/tile_stamps.py).
 #define SG_TSTAMP(slot)                                                                  \
@@ -2536,6 +2599,12 @@ __device__ __forceinline__ void tile_zp(const TileShared& sh, double* zp, int K,
     tacc[slot] += now_ - tlast;                                                          \
     tlast = now_;                                                                        \
   }
+// Per-phase absolute times (SG_STAMP=1 builds; tools/phase_trace.py): d.stamps[64 + (wg 128 + K) 16 + slot],
+// slots 0-7 the waves' barrier arrivals, 8-12 the owner's chain (start, after (0), TRSM, D update, factor).
+constexpr int kTraceK = 128;
+#define SG_PTRACE(K, slot)                                                                  \
+  if (kStamp && lane == 0 && (K) < kTraceK)                                                \
+    d.stamps[64 + ((size_t)blockIdx.x * kTraceK + (K)) * 16 + (slot)] = __builtin_amdgcn_s_memtime();
 
 // W_KJ = Z_K^T U_KJ (= U_KK^-1 U_KJ) of one row-K tile, and its store to global memory for the back
 // substitution (kept apart so that loads issued in between do not reuse the stores' data registers, which
@@ -2578,12 +2647,21 @@ __device__ __forceinline__ void tile_col_load(f64x4 (&acc)[kTB], double& ypart, 
 
 // One phase (tile row K) of a wave.  `late`: this wave owned the diagonal of the previous phase and still
 // owes that phase's W tile and its column reload (it has no other work in this phase).
+// Owner look-ahead (flags bit 3): the next phase's owner (column K+2) applies row K's update to its row-(K+1)
+// tile in phase K — U_{K,K+1} is posted by this phase's owner right after its TRSM (an LDS flag, no barrier)
+// — so that update (four MFMAs) leaves the next phase's critical chain (TRSM -> D update -> factor).  The
+// row-(K+1) tile exists iff K + 2 < tend[K] (the band is contiguous), the same condition both phases test.
+constexpr int kLaSpinMax = 1 << 20;
+__device__ __forceinline__ bool la_done(int la, const int* tend, int Kp) {   // look-ahead ran in phase Kp
+  return (la & 1) && Kp >= 0 && Kp + 2 < tend[Kp];
+}
+
 template <bool kStamp>
 __device__ __forceinline__ void tile_phase(f64x4 (&acc)[kTB], double& ypart, int& J, bool& late, bool& bad,
-                                           TileShared& sh, const Dev& d, double* __restrict__ Wg, double* zp,
-                                           const int* tend, int K, int NT, int lane, int li, int lk,
-                                           const TileSrc& ts, unsigned long long (&tacc)[16],
-                                           unsigned long long& tlast) {
+                                           bool& tmo, int la, TileShared& sh, const Dev& d,
+                                           double* __restrict__ Wg, double* zp, const int* tend, int K, int NT,
+                                           int lane, int li, int lk, const TileSrc& ts,
+                                           unsigned long long (&tacc)[16], unsigned long long& tlast) {
   if (late) {
     // the previous phase's owner (column J = K): its row K-1 tile (slot 0) -> W, then column J + 8, which
     // row K + 1 touches first
@@ -2591,20 +2669,24 @@ __device__ __forceinline__ void tile_phase(f64x4 (&acc)[kTB], double& ypart, int
     f64x4 Wt = {0.0, 0.0, 0.0, 0.0};
     if (hasw) Wt = tile_w(acc[0], sh.Zs[(K - 1) & 3], li, lk);
     const int Jw = J;
+    if (la & 4) tile_dinv_post(sh, zp, K, lane, li, lk);   // D_K^-1 and z'_K for the phase's other waves first
     J += kTB;
     tile_col_load(acc, ypart, d, J, K, li, lk, ts);
     if (hasw) tile_w_store(Wt, Wg, K - 1, Jw, lane);
-    tile_zp(sh, zp, K, lane);   // the diagonal this wave factored last phase
+    if (!(la & 4)) tile_zp(sh, zp, K, lane);   // the diagonal this wave factored last phase
     late = false;
     SG_TSTAMP(13)
     return;
   }
-  // (0) trailing update by row K-1 (the owner's diagonal tile, dd = 2, already took it last phase)
+  if (J == K + 1) SG_PTRACE(K, 8)
+  // (0) trailing update by row K-1 (the owner's diagonal tile, dd = 2, already took it last phase; with the
+  // look-ahead its row-K tile, dd = 1, too)
   if (K >= 1 && J < tend[K - 1]) {
     const double* Ub = sh.Ur[(K - 1) & 1][0];
+    const bool own_la = J == K + 1 && la_done(la, tend, K - 1);
 #pragma unroll
     for (int dd = 1; dd < kTB; ++dd) {
-      if (K - 1 + dd <= J && !(dd == 2 && J == K + 1)) {
+      if (K - 1 + dd <= J && !(dd == 2 && J == K + 1) && !(dd == 1 && own_la)) {
         double a[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) a[s] = -Ub[(dd - 1) * 256 + s * 64 + lane];
@@ -2613,10 +2695,64 @@ __device__ __forceinline__ void tile_phase(f64x4 (&acc)[kTB], double& ypart, int
     }
   }
   SG_TSTAMP(8)
+  if (J == K + 1) SG_PTRACE(K, 9)
   // (1) TRSM of row K's tile
   const int te = tend[K];
   const bool act = J < te;
   const double* Zs = sh.Zs[K & 3];
+  if ((la & 4) && act && J != K + 1) {
+    // Dinv mode, a column off the critical chain: no TRSM.  Its raw row-K tile A_KJ goes to the exchange
+    // ring (the trailing updates become A_IJ -= A_KI^T W_KJ), W_KJ = D_K^-1 A_KJ (= U_KK^-1 U_KJ) is both the
+    // back-substitution tile and this column's operand for the next phase's update, and the rhs term is
+    // A_KJ^T z'_K (= U_KJ^T z_K).
+    const f64x4 A = acc[1];
+    double* ur = sh.Ur[K & 1][J - K - 1];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ur[q * 64 + lane] = A[q];
+    int spin = 0;
+    while (__hip_atomic_load(&sh.dflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < K && ++spin < kLaSpinMax)
+      __builtin_amdgcn_s_sleep(0);
+    tmo |= spin >= kLaSpinMax;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    double da[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) da[s] = sh.Dv[li * kTLd + 4 * s + lk];
+    const f64x4 zero = {0.0, 0.0, 0.0, 0.0};
+    const f64x4 W = mfma_f64_k16(da, A, zero);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ypart = fma(-A[q], zp[16 * K + lk + 4 * q], ypart);
+    tile_w_store(W, Wg, K, J, lane);
+    acc[1] = W;
+    if (J == K + 2) {
+      double a[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) a[s] = -A[s];
+      acc[3] = mfma_f64_k16(a, W, acc[3]);   // D_{K+2} -= A_{K,K+2}^T W_{K,K+2}
+      if (la_done(la, tend, K)) {
+        int spin2 = 0;
+        while (__hip_atomic_load(&sh.uflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < K &&
+               ++spin2 < kLaSpinMax)
+          __builtin_amdgcn_s_sleep(0);
+        tmo |= spin2 >= kLaSpinMax;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const double* A1 = sh.Ur[K & 1][0];   // the owner's raw A_{K,K+1}
+        double b1[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) b1[s] = -A1[s * 64 + lane];
+        acc[2] = mfma_f64_k16(b1, W, acc[2]);   // A_{K+1,K+2} -= A_{K,K+1}^T W_{K,K+2}
+      }
+    }
+    SG_TSTAMP(9)
+    return;
+  }
+  if ((la & 4) && act && J == K + 1) {
+    // Dinv mode, the owner: its raw row-K tile to the ring first (the next owner's look-ahead operand)
+    double* ur = sh.Ur[K & 1][0];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) ur[q * 64 + lane] = acc[1][q];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) __hip_atomic_store(&sh.uflag, K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
   if (act) {
     const f64x4 zero = {0.0, 0.0, 0.0, 0.0};
     double za[4];
@@ -2625,22 +2761,44 @@ __device__ __forceinline__ void tile_phase(f64x4 (&acc)[kTB], double& ypart, int
     const f64x4 U = mfma_f64_k16(za, acc[1], zero);
     acc[1] = U;
     double* ur = sh.Ur[K & 1][J - K - 1];
+    if (!(la & 4)) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) ur[q * 64 + lane] = U[q];
+      for (int q = 0; q < 4; ++q) ur[q * 64 + lane] = U[q];
+    }
+    if ((la & 1) && !(la & 4) && J == K + 1) {
+      // the owner: U_{K,K+1} is the next owner's look-ahead operand (in-order LDS: data, then the flag)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) __hip_atomic_store(&sh.uflag, K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     const double* zk = sh.zK[K & 3];
 #pragma unroll
     for (int q = 0; q < 4; ++q) ypart = fma(-U[q], zk[lk + 4 * q], ypart);
-    if (J == K + 2) {
+    if (J == K + 2 && !(la & 4)) {
       // next phase's owner: its diagonal tile's update by row K uses only its own U_{K,J}; apply it now,
       // off next phase's critical chain (slot 3 = row K + 2)
       double a[4];
 #pragma unroll
       for (int s = 0; s < 4; ++s) a[s] = -U[s];
       acc[3] = mfma_f64_k16(a, U, acc[3]);
+      if (la_done(la, tend, K)) {
+        // look-ahead: the row-(K+1) tile (slot 2) takes row K's update now, U_{K,K+1} from the owner
+        int spin = 0;
+        while (__hip_atomic_load(&sh.uflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < K &&
+               ++spin < kLaSpinMax)
+          __builtin_amdgcn_s_sleep(0);
+        tmo |= spin >= kLaSpinMax;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const double* U1 = sh.Ur[K & 1][0];
+        double b1[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) b1[s] = -U1[s * 64 + lane];
+        acc[2] = mfma_f64_k16(b1, U, acc[2]);
+      }
     }
   }
   SG_TSTAMP(9)
   if (J == K + 1) {
+    SG_PTRACE(K, 10)
     // (2) the next diagonal: apply row K, factor, post; its W tile and the reload follow next phase
     if (act) {
       double a[4];
@@ -2649,7 +2807,11 @@ __device__ __forceinline__ void tile_phase(f64x4 (&acc)[kTB], double& ypart, int
       acc[2] = mfma_f64_k16(a, acc[1], acc[2]);
     }
     SG_TSTAMP(10)
-    if (K + 1 < NT) bad |= tile_diag(acc[2], ypart, sh, zp, K + 1, lane, li, lk);
+    SG_PTRACE(K, 11)
+    if (K + 1 < NT)
+      bad |= (la & 2) ? tile_diag<true>(acc[2], ypart, sh, zp, K + 1, lane, li, lk)
+                      : tile_diag<false>(acc[2], ypart, sh, zp, K + 1, lane, li, lk);
+    SG_PTRACE(K, 12)
     late = true;
     SG_TSTAMP(11)
   } else if (act) {
@@ -2661,7 +2823,7 @@ __device__ __forceinline__ void tile_phase(f64x4 (&acc)[kTB], double& ypart, int
 
 // The bottom half's step after its last factored row ND-1 (slots of phase ND): the previous owner's W tile,
 // and every other wave's update of its separator column by row ND-1 ((0) of a phase, nothing else).
-__device__ __forceinline__ void tile_final(f64x4 (&acc)[kTB], int J, bool& late, TileShared& sh,
+__device__ __forceinline__ void tile_final(f64x4 (&acc)[kTB], int J, bool& late, int la, TileShared& sh,
                                            double* __restrict__ Wg, const int* tend, int K, int lane, int li,
                                            int lk) {
   if (late) {
@@ -2671,9 +2833,11 @@ __device__ __forceinline__ void tile_final(f64x4 (&acc)[kTB], int J, bool& late,
   }
   if (J < tend[K - 1]) {
     const double* Ub = sh.Ur[(K - 1) & 1][0];
+    const bool own_la = J == K + 1 && la_done(la, tend, K - 1);
 #pragma unroll
     for (int dd = 1; dd < kTB; ++dd) {
-      if (K - 1 + dd <= J && !(dd == 2 && J == K + 1)) {   // (the diagonal of column K+1: applied early)
+      // (the diagonal of column K+1: applied early; its row-K tile too under the look-ahead)
+      if (K - 1 + dd <= J && !(dd == 2 && J == K + 1) && !(dd == 1 && own_la)) {
         double a[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) a[s] = -Ub[(dd - 1) * 256 + s * 64 + lane];
@@ -2946,7 +3110,12 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
   if (tid == 0) {
     sh.fail = 0;
     sh.tmo = 0;
+    sh.uflag = -1;
+    sh.dflag = -1;
   }
+  // la bit 0: owner look-ahead (flags bit 3); bit 1: readlane factorisation (flags bit 4); bit 2: Dinv mode
+  // (flags bit 5: off-chain columns skip the TRSM)
+  const int la = ((flags & 8) ? 1 : 0) | ((flags & 16) ? 2 : 0) | ((flags & 32) ? 4 : 0);
   bool bad = false, tmo = false;
   const int spin_max = (flags & 4) ? 256 : kSepSpinMax;
   if (bottom && (flags & 4))
@@ -3004,8 +3173,12 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
     }
     if (done) return;
     if (col == 0) {
-      bad |= tile_diag(D0, y0, sh, zp, 0, lane, li, lk);
-      tile_zp(sh, zp, 0, lane);   // (the wave's own LDS writes: visible to it in order)
+      bad |= (flags & 16) ? tile_diag<true>(D0, y0, sh, zp, 0, lane, li, lk)
+                          : tile_diag<false>(D0, y0, sh, zp, 0, lane, li, lk);
+      if (la & 4)
+        tile_dinv_post(sh, zp, 0, lane, li, lk);
+      else
+        tile_zp(sh, zp, 0, lane);   // (the wave's own LDS writes: visible to it in order)
     }
     else if (cand_lds)   // the seven waves that wait at the first barrier
       cand_prefetch(d, cl, st->cur, (col - 1) * 64 + lane, kTileThreads - 64);
@@ -3024,17 +3197,19 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
         tmo |= spin >= spin_max;
         sep_merge(acc, ypart, J, m, sepb, sepy, lane, li, lk);
       }
-      tile_phase<kStamp>(acc, ypart, J, late, bad, sh, d, Wb, zp, tend, K, NTf, lane, li, lk, ts, tacc, tlast);
+      tile_phase<kStamp>(acc, ypart, J, late, bad, tmo, la, sh, d, Wb, zp, tend, K, NTf, lane, li, lk, ts, tacc,
+                         tlast);
       SG_TSTAMP(2)
       // the owner of the next diagonal (now late) is on the critical path until the barrier: it rotates after
       if (!late) tile_rotate(acc);
+      SG_PTRACE(K, wave)
       lds_barrier();
       if (late) tile_rotate(acc);
       SG_TSTAMP(3)
     }
     if (bottom) {
       // row nd-1's updates of the separator columns (slots of phase nd), then the hand-off
-      tile_final(acc, J, late, sh, Wb, tend, nd, lane, li, lk);
+      tile_final(acc, J, late, la, sh, Wb, tend, nd, lane, li, lk);
       sep_write(acc, ypart, J, nd, NT, m, sepb, sepy, li, lk);
     }
   }
@@ -3586,6 +3761,13 @@ void BaSolver::AllReduceSum(double* buf, size_t n) {
   if (comm_ && comm_->nranks() > 1) comm_->AllReduceSum(buf, n, stream_);
 }
 
+__global__ __launch_bounds__(256) void k_fill_obs_pnt(const int32_t* __restrict__ poff, int32_t* __restrict__ obs_pnt,
+                                                      int P) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= P) return;
+  for (int o = poff[i]; o < poff[i + 1]; ++o) obs_pnt[o] = i;
+}
+
 void BaSolver::Load(const sg_problem& p) {
   static const bool host_timing = getenv("SG_HOST_TIMING") != nullptr;   // development aid: phase times
   auto lt0 = std::chrono::steady_clock::now();
@@ -3747,13 +3929,52 @@ void BaSolver::Load(const sg_problem& p) {
     }
   }
   lap("obs-csr");
+  // upload batch 1 — poses, intrinsics, points (current slot; the candidate slot is a device copy) and the
+  // observation arrays: its pinned copy and DMA overlap the host's work-list construction below (stager.h)
+  hipStream_t s = stream_;
+  Stager& stg = *stager_;
+  stg.ResetBytes();
+  stg.AddInto(k_, std::max<size_t>(14 * (size_t)ncam_, 1),
+              ncam_ > 0 ? std::vector<double>(p.k, p.k + 7 * ncam_) : std::vector<double>{0.0});
+  stg.AddInto(q_, 8 * (size_t)F_, std::vector<double>(p.q, p.q + 4 * F_));
+  stg.AddInto(t_, 6 * (size_t)F_, std::vector<double>(p.t, p.t + 3 * F_));
+  stg.AddInto(X_, 8 * (size_t)P_, X);
+  stg.Add(frame_cam_, std::vector<int32_t>(p.frame_camera, p.frame_camera + F_));
+  stg.Add(frame_block_, frame_block);
+  stg.Add(rot_free_, std::vector<uint8_t>(p.frame_rot_free, p.frame_rot_free + F_));
+  stg.Add(trans_free_, std::vector<uint8_t>(p.frame_trans_free, p.frame_trans_free + F_));
+  stg.Add(pfree_, pfree);
+  stg.Add(poff_, poff);
+  stg.Add(obs_pt_, obs_pt);
+  stg.Add(obs_frame_, obs_frame);
+  stg.Add(obs_fixed_, obs_fixed);
+  stg.Add(obs_meta_, obs_meta.empty() ? std::vector<int32_t>{0} : obs_meta);
+  stg.Flush(s);
+  {
+    auto dup = [&](double* base, size_t half) {   // candidate slot = current slot
+      if (half) SG_HIP_CHECK(hipMemcpyAsync(base + half, base, half * sizeof(double), hipMemcpyDeviceToDevice, s));
+    };
+    dup(k_.ptr, 7 * (size_t)ncam_);
+    dup(q_.ptr, 4 * (size_t)F_);
+    dup(t_.ptr, 3 * (size_t)F_);
+    dup(X_.ptr, 4 * (size_t)P_);
+    // the point of every observation (device order) from the CSR, on the device
+    obs_pnt_.Resize(std::max(M_, 1));
+    if (P_ > 0)
+      hipLaunchKernelGGL(k_fill_obs_pnt, dim3((P_ + 255) / 256), dim3(256), 0, s, (const int32_t*)poff_.ptr,
+                         obs_pnt_.ptr, P_);
+    SG_HIP_CHECK(hipGetLastError());
+  }
+  lap("upload-1");
   // k_linearize decomposition (see LinChunk): rounds of whole points (<= kLinObs observations), up to
   // maxr rounds per chunk sharing one camera window; fewer rounds per chunk on small problems so that the
   // grid still fills the chip.
   std::vector<LinRound> lrounds;
   std::vector<LinChunk> lchunks;
   std::vector<uint16_t> llist;
+  llist.reserve((size_t)M_ + (size_t)M_ / 4 + 64);
   int lcam_off = 0;
+  std::vector<int> cnt;   // per round: window-block counters (scratch, reused)
   {
     int maxr = std::max(1, std::min(kLinMaxRounds, M_ / (kLinObs * 1024)));
     if (getenv("SG_LIN_MAXR")) maxr = std::max(1, atoi(getenv("SG_LIN_MAXR")));   // tuning experiments
@@ -3808,7 +4029,7 @@ void BaSolver::Load(const sg_problem& p) {
         LinRound& R = lrounds[r];
         R.lst = (int)llist.size();
         if (c.nb == 0) continue;
-        std::vector<int> cnt(c.nb + 1, 0);
+        cnt.assign(c.nb + 1, 0);
         for (int o = R.o0; o < R.o1; ++o) {
           const int b = frame_block[obs_frame[o]];
           if (b >= 0) cnt[b - c.b_lo + 1]++;
@@ -3839,9 +4060,7 @@ void BaSolver::Load(const sg_problem& p) {
   // Schur work lists (see SchurSeg): the cells of every free point (one per block of its span, with the
   // point's observations in that block), segments of consecutive points whose columns fit kSchurTW tiles of
   // S, their batches, and each wide point's observation pairs (s <= t, both on free frames).
-  std::vector<int32_t> obs_pnt(M_), obs_blk(M_);
-  for (int i = 0; i < P_; ++i)
-    for (int o = poff[i]; o < poff[i + 1]; ++o) obs_pnt[o] = i;
+  std::vector<int32_t> obs_blk(M_);
   for (int o = 0; o < M_; ++o) obs_blk[o] = frame_block[obs_frame[o]];
   // span in blocks of a free point's Schur terms (0: none)
   auto sspan = [&](int i) {
@@ -3859,6 +4078,8 @@ void BaSolver::Load(const sg_problem& p) {
   schur_mfma_ = 0.0;
   {
     std::vector<std::pair<int, int>> bo;
+    cells.reserve(4 * (size_t)M_ + 4);
+    cell_obs.reserve((size_t)M_ / 4 + 1);
     for (int i = 0; i < P_; ++i) {
       size_t kb = 0;
       for (int o = poff[i]; o < poff[i + 1]; ++o) kb += obs_blk[o] >= 0;
@@ -4130,40 +4351,11 @@ void BaSolver::Load(const sg_problem& p) {
     if (s_lidx.empty()) s_lidx.push_back(0);
   }
   lap("envelope");
-  // device uploads: one pinned staging copy and one scatter launch (stager.h)
-  hipStream_t s = stream_;
-  Stager& stg = *stager_;
-  {
-    std::vector<double> k2(14 * (size_t)ncam_);
-    std::copy(p.k, p.k + 7 * ncam_, k2.begin());
-    std::copy(p.k, p.k + 7 * ncam_, k2.begin() + 7 * ncam_);
-    stg.Add(k_, k2.empty() ? std::vector<double>{0.0} : k2);
-  }
-  std::vector<double> q2(8 * (size_t)F_), t2(6 * (size_t)F_), X2(8 * (size_t)P_);
-  std::copy(p.q, p.q + 4 * F_, q2.begin());
-  std::copy(p.q, p.q + 4 * F_, q2.begin() + 4 * F_);
-  std::copy(p.t, p.t + 3 * F_, t2.begin());
-  std::copy(p.t, p.t + 3 * F_, t2.begin() + 3 * F_);
-  std::copy(X.begin(), X.end(), X2.begin());
-  std::copy(X.begin(), X.end(), X2.begin() + 4 * P_);
-  stg.Add(q_, q2);
-  stg.Add(t_, t2);
-  stg.Add(X_, X2);
-  stg.Add(frame_cam_, std::vector<int32_t>(p.frame_camera, p.frame_camera + F_));
-  stg.Add(frame_block_, frame_block);
-  stg.Add(rot_free_, std::vector<uint8_t>(p.frame_rot_free, p.frame_rot_free + F_));
-  stg.Add(trans_free_, std::vector<uint8_t>(p.frame_trans_free, p.frame_trans_free + F_));
-  stg.Add(pfree_, pfree);
-  stg.Add(poff_, poff);
-  stg.Add(obs_pt_, obs_pt);
-  stg.Add(obs_frame_, obs_frame);
-  stg.Add(obs_fixed_, obs_fixed);
-  stg.Add(obs_meta_, obs_meta.empty() ? std::vector<int32_t>{0} : obs_meta);
+  // upload batch 2 — the work lists: one pinned staging copy and one scatter launch (stager.h)
   stg.Add(lchunks_d_, lchunks);
   stg.Add(lrounds_d_, lrounds);
   if (llist.empty()) llist.push_back(0);
   stg.Add(llist_d_, llist);
-  stg.Add(obs_pnt_, obs_pnt.empty() ? std::vector<int32_t>{0} : obs_pnt);
   stg.Add(segs_, segs.empty() ? std::vector<SchurSeg>(1) : segs);
   stg.Add(sbatch_, sbatch.empty() ? std::vector<SchurBatch>(1) : sbatch);
   stg.Add(wsegs_, wsegs.empty() ? std::vector<WideSeg>(1) : wsegs);
@@ -4232,7 +4424,7 @@ void BaSolver::Load(const sg_problem& p) {
     kst_.Resize(56 * (size_t)ncam_);
   }
   stamp_on_ = getenv("SG_STAMP") && getenv("SG_STAMP")[0] == '1';
-  if (stamp_on_) stamps_.Resize(64);
+  if (stamp_on_) stamps_.Resize(64 + 2 * 128 * 16);
   ResetState(s);
   if (chol_tiles_ && tile_lds_ > tile_lds_set_) {
     for (const void* f : {(const void*)k_chol_tiles<false>, (const void*)k_chol_tiles<true>})
@@ -4241,6 +4433,11 @@ void BaSolver::Load(const sg_problem& p) {
   }
   SG_HIP_CHECK(hipStreamSynchronize(s));
   lap("uploads");
+  if (host_timing) {
+    char buf[64];
+    snprintf(buf, sizeof(buf), " (staged %.2f MB)", stg.staged_bytes() / 1e6);
+    lap_log += buf;
+  }
   SaveStructure(p);
   full_loads_++;
   if (host_timing) {
@@ -4594,11 +4791,13 @@ void BaSolver::Iterate(int n) {
     if (chol_tiles_ && d.stamps)
       hipLaunchKernelGGL(k_chol_tiles<true>, dim3(chol_nd_ > 0 ? 2 : 1), dim3(kTileThreads), tile_lds_, stream_, d,
                          (const int32_t*)work_i_.ptr, Wg_.ptr, tflag_.ptr, chol_nd_,
-                         chol_simdmap_ | (chol_cand_lds_ ? 2 : 0) | (chol_force_tmo_ ? 4 : 0));
+                         chol_simdmap_ | (chol_cand_lds_ ? 2 : 0) | (chol_force_tmo_ ? 4 : 0) |
+                         (chol_lookahead_ ? 8 : 0) | (chol_factor_rl_ ? 16 : 0) | (chol_dinv_ ? 32 : 0));
     else if (chol_tiles_)
       hipLaunchKernelGGL(k_chol_tiles<false>, dim3(chol_nd_ > 0 ? 2 : 1), dim3(kTileThreads), tile_lds_, stream_, d,
                          (const int32_t*)work_i_.ptr, Wg_.ptr, tflag_.ptr, chol_nd_,
-                         chol_simdmap_ | (chol_cand_lds_ ? 2 : 0) | (chol_force_tmo_ ? 4 : 0));
+                         chol_simdmap_ | (chol_cand_lds_ ? 2 : 0) | (chol_force_tmo_ ? 4 : 0) |
+                         (chol_lookahead_ ? 8 : 0) | (chol_factor_rl_ ? 16 : 0) | (chol_dinv_ ? 32 : 0));
     else if (chol_window_ && d.stamps)
       hipLaunchKernelGGL(k_cholesky_window<true>, dim3(1), dim3(kCholThreads), kCholLds, stream_, d,
                          (const int32_t*)work_i_.ptr, rdg_.ptr);
@@ -4648,9 +4847,9 @@ void BaSolver::Sweep(int n) {
 }
 
 std::vector<unsigned long long> BaSolver::Stamps() {
-  std::vector<unsigned long long> v(64, 0);
+  std::vector<unsigned long long> v(stamp_on_ ? stamps_.size : 64, 0);
   if (!stamp_on_) return v;
-  SG_HIP_CHECK(hipMemcpyAsync(v.data(), stamps_.ptr, 64 * 8, hipMemcpyDeviceToHost, stream_));
+  SG_HIP_CHECK(hipMemcpyAsync(v.data(), stamps_.ptr, v.size() * 8, hipMemcpyDeviceToHost, stream_));
   SG_HIP_CHECK(hipStreamSynchronize(stream_));
   return v;
 }

@@ -52,13 +52,20 @@ SG_HD bool Project(const T* q, const T* t, const T* k, const T* X, T* uv) {
 }
 
 // Value + analytic Jacobian of the projection.  Outputs (row-major, 2 rows):
-//   Jq[2][4]  d(uv)/d(q memory [x,y,z,w])     (global, before the local parameterization)
+//   Jq[2][4]  d(uv)/d(q memory [x,y,z,w])     (global, before the local parameterization; if Jq != nullptr)
 //   Jt[2][3]  d(uv)/d(t)
 //   Jk[2][7]  d(uv)/d(k)                        (only if Jk != nullptr)
 //   JX[2][4]  d(uv)/d(X)
+//   Jr[2][3]  d(uv)/d(delta): the rotation in ceres::QuaternionParameterization's tangent space at q, i.e.
+//             Jq * QuatLocalJacobian(q), formed directly (if Jr != nullptr).  Ceres's Plus reads Eigen's
+//             [x,y,z,w] memory as [w,x,y,z] (slam.cpp:312-313), so its tangent basis is permuted against
+//             Eigen's rotation; worked out symbolically, dp/d(delta) = (R(q) + (|q|^2 - 1) I) A(v) with
+//             A(v) = 2 [[v1, v2, 0], [-v0, 0, v2], [0, -v0, -v1]] (v = X.xyz - t X.w, R the matrix of Eigen's
+//             _transformVector, exact for any |q|), so d(uv)/d(delta) = (G R + (|q|^2 - 1) G) A(v): 24 flops
+//             instead of forming the 3x4 dp/dq (~50), G dp/dq (24 FMAs) and the 4x3 product (24 FMAs).
 template <typename T>
 SG_HD bool ProjectJacobian(const T* q, const T* t, const T* k, const T* X, T* uv, T* Jq, T* Jt, T* Jk,
-                           T* JX) {
+                           T* JX, T* Jr = nullptr) {
   T v[3], p[3];
   CameraPoint(q, t, X, v, p);
   if (p[2] < T(0.001) * X[3]) return false;
@@ -98,30 +105,42 @@ SG_HD bool ProjectJacobian(const T* q, const T* t, const T* k, const T* X, T* uv
   R[2][0] = T(2) * (ux * uz - w * uy);
   R[2][1] = T(2) * (uy * uz + w * ux);
   R[2][2] = T(1) - T(2) * (ux * ux + uy * uy);
-  // dp/du = -2w[v]x + 2 (u v^T + (u.v) I - 2 v u^T) ;  dp/dw = 2 (u x v)
-  const T udv = ux * v[0] + uy * v[1] + uz * v[2];
-  const T uu[3] = {ux, uy, uz};
-  T Pq[3][4];
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) Pq[i][j] = T(2) * (uu[i] * v[j] - T(2) * v[i] * uu[j] + (i == j ? udv : T(0)));
-  // -2w [v]x : [v]x = [[0,-v2,v1],[v2,0,-v0],[-v1,v0,0]]
-  Pq[0][1] += T(2) * w * v[2];
-  Pq[0][2] -= T(2) * w * v[1];
-  Pq[1][0] -= T(2) * w * v[2];
-  Pq[1][2] += T(2) * w * v[0];
-  Pq[2][0] += T(2) * w * v[1];
-  Pq[2][1] -= T(2) * w * v[0];
-  Pq[0][3] = T(2) * (uy * v[2] - uz * v[1]);
-  Pq[1][3] = T(2) * (uz * v[0] - ux * v[2]);
-  Pq[2][3] = T(2) * (ux * v[1] - uy * v[0]);
   // GR = G R
   T GR[2][3];
   for (int r = 0; r < 2; ++r)
     for (int c = 0; c < 3; ++c) GR[r][c] = G[r][0] * R[0][c] + G[r][1] * R[1][c] + G[r][2] * R[2][c];
   const T Rt0 = GR[0][0] * t[0] + GR[0][1] * t[1] + GR[0][2] * t[2];
   const T Rt1 = GR[1][0] * t[0] + GR[1][1] * t[1] + GR[1][2] * t[2];
+  if (Jq) {
+    // dp/du = -2w[v]x + 2 (u v^T + (u.v) I - 2 v u^T) ;  dp/dw = 2 (u x v)
+    const T udv = ux * v[0] + uy * v[1] + uz * v[2];
+    const T uu[3] = {ux, uy, uz};
+    T Pq[3][4];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) Pq[i][j] = T(2) * (uu[i] * v[j] - T(2) * v[i] * uu[j] + (i == j ? udv : T(0)));
+    // -2w [v]x : [v]x = [[0,-v2,v1],[v2,0,-v0],[-v1,v0,0]]
+    Pq[0][1] += T(2) * w * v[2];
+    Pq[0][2] -= T(2) * w * v[1];
+    Pq[1][0] -= T(2) * w * v[2];
+    Pq[1][2] += T(2) * w * v[0];
+    Pq[2][0] += T(2) * w * v[1];
+    Pq[2][1] -= T(2) * w * v[0];
+    Pq[0][3] = T(2) * (uy * v[2] - uz * v[1]);
+    Pq[1][3] = T(2) * (uz * v[0] - ux * v[2]);
+    Pq[2][3] = T(2) * (ux * v[1] - uy * v[0]);
+    for (int r = 0; r < 2; ++r)
+      for (int c = 0; c < 4; ++c) Jq[4 * r + c] = G[r][0] * Pq[0][c] + G[r][1] * Pq[1][c] + G[r][2] * Pq[2][c];
+  }
+  if (Jr) {
+    const T n1 = (ux * ux + uy * uy) + (uz * uz + w * w) - T(1);
+    for (int r = 0; r < 2; ++r) {
+      const T g0 = GR[r][0] + n1 * G[r][0], g1 = GR[r][1] + n1 * G[r][1], g2 = GR[r][2] + n1 * G[r][2];
+      Jr[3 * r + 0] = T(2) * (g0 * v[1] - g1 * v[0]);
+      Jr[3 * r + 1] = T(2) * (g0 * v[2] - g2 * v[0]);
+      Jr[3 * r + 2] = T(2) * (g1 * v[2] - g2 * v[1]);
+    }
+  }
   for (int r = 0; r < 2; ++r) {
-    for (int c = 0; c < 4; ++c) Jq[4 * r + c] = G[r][0] * Pq[0][c] + G[r][1] * Pq[1][c] + G[r][2] * Pq[2][c];
     for (int c = 0; c < 3; ++c) Jt[3 * r + c] = -X[3] * GR[r][c];
     for (int c = 0; c < 3; ++c) JX[4 * r + c] = GR[r][c];
   }
@@ -175,8 +194,8 @@ SG_HD void Cauchy(T s, T b, T inv_b, T* rho0, T* rho1) {
 template <typename T>
 SG_HD bool LinearizeObservation(const T* q, const T* t, const T* k, const T* X, const T* pt, T b, T inv_b,
                                 T* r, T* Jc, T* Jp, T* cost, T* Jk = nullptr) {
-  T uv[2], Jq[8], Jt[6], JX[8];
-  if (!ProjectJacobian(q, t, k, X, uv, Jq, Jt, Jk, JX)) return false;
+  T uv[2], Jr[6], Jt[6], JX[8];
+  if (!ProjectJacobian(q, t, k, X, uv, (T*)nullptr, Jt, Jk, JX, Jr)) return false;
   const T r0 = uv[0] - pt[0], r1 = uv[1] - pt[1];
   T rho0, rho1;
   Cauchy(r0 * r0 + r1 * r1, b, inv_b, &rho0, &rho1);
@@ -184,12 +203,8 @@ SG_HD bool LinearizeObservation(const T* q, const T* t, const T* k, const T* X, 
   const T sr = sqrt(rho1);
   r[0] = sr * r0;
   r[1] = sr * r1;
-  T L[12];
-  QuatLocalJacobian(q, L);
   for (int i = 0; i < 2; ++i) {
-    for (int c = 0; c < 3; ++c)
-      Jc[6 * i + c] = sr * (Jq[4 * i + 0] * L[c] + Jq[4 * i + 1] * L[3 + c] + Jq[4 * i + 2] * L[6 + c] +
-                            Jq[4 * i + 3] * L[9 + c]);
+    for (int c = 0; c < 3; ++c) Jc[6 * i + c] = sr * Jr[3 * i + c];
     for (int c = 0; c < 3; ++c) Jc[6 * i + 3 + c] = sr * Jt[3 * i + c];
     for (int c = 0; c < 4; ++c) Jp[4 * i + c] = sr * JX[4 * i + c];
   }

@@ -24,6 +24,10 @@ struct StagePiece {
   unsigned long long bytes;
 };
 
+// A load may flush in several batches (the observation arrays early, so their DMA overlaps the host's work-list
+// construction, then the lists): each batch occupies its own region of the pinned buffer and of the device
+// staging buffer, at the same offsets, and the pinned buffer is only rewritten after Clear() (next load) has
+// waited for the last batch's copy.
 // One workgroup column per piece (blockIdx.y); 16-byte copies for the aligned body, bytes for the tail.
 __global__ __launch_bounds__(256) void k_stage_scatter(const StagePiece* __restrict__ pieces,
                                                        const unsigned char* __restrict__ stage) {
@@ -55,7 +59,12 @@ class Stager {
   // Resize dst to v.size() and queue v for it (the copy happens in Flush).
   template <typename T>
   void Add(DBuf<T>& dst, const std::vector<T>& v) {
-    dst.Resize(v.size());
+    AddInto(dst, v.size(), v);
+  }
+  // Resize dst to n >= v.size() elements and queue v for its first v.size() elements.
+  template <typename T>
+  void AddInto(DBuf<T>& dst, size_t n, const std::vector<T>& v) {
+    dst.Resize(n);
     if (v.empty()) return;
     const size_t bytes = v.size() * sizeof(T);
     const size_t off = Reserve(bytes);
@@ -70,31 +79,35 @@ class Stager {
     WaitCopy();
     pieces_.clear();
     used_ = 0;
+    batch0_ = 0;
     max_bytes_ = 0;
   }
 
-  // One pinned copy and one scatter launch on stream s.  The pinned buffer is reused by the next batch, so
-  // the caller synchronises s before queueing again (sg_ba_load ends with a stream synchronisation).
+  // One pinned copy of this batch's region and one scatter launch on stream s.  The batch's pinned region
+  // is not rewritten before the next load's Clear() waits for the copy.
   void Flush(hipStream_t s) {
     if (pieces_.empty()) return;
     const size_t tbl = used_;
     const size_t tbytes = pieces_.size() * sizeof(StagePiece);
-    Reserve(tbytes);
-    std::memcpy(host_ + tbl, pieces_.data(), tbytes);
-    dev_.Resize(used_);
-    SG_HIP_CHECK(hipMemcpyAsync(dev_.ptr, host_, used_, hipMemcpyHostToDevice, s));
+    const size_t tbl_off = Reserve(tbytes);
+    std::memcpy(host_ + tbl_off, pieces_.data(), tbytes);
+    (void)tbl;
+    dev_.Resize(used_);   // (reserved: no reallocation; a reallocation would synchronise the device first)
+    SG_HIP_CHECK(hipMemcpyAsync(dev_.ptr + batch0_, host_ + batch0_, used_ - batch0_, hipMemcpyHostToDevice, s));
     if (!copied_) SG_HIP_CHECK(hipEventCreateWithFlags(&copied_, hipEventDisableTiming));
     SG_HIP_CHECK(hipEventRecord(copied_, s));
     pending_ = true;
-    last_bytes_ = used_;
+    last_bytes_ += used_ - batch0_;
     const unsigned gx = (unsigned)std::min<size_t>(64, std::max<size_t>(1, (max_bytes_ / 16 + 255) / 256));
     hipLaunchKernelGGL(k_stage_scatter, dim3(gx, (unsigned)pieces_.size()), dim3(256), 0, s,
-                       reinterpret_cast<const StagePiece*>(dev_.ptr + tbl), dev_.ptr);
+                       reinterpret_cast<const StagePiece*>(dev_.ptr + tbl_off), dev_.ptr);
     SG_HIP_CHECK(hipGetLastError());
     pieces_.clear();
-    used_ = 0;
+    batch0_ = (used_ + 15) & ~(size_t)15;
+    used_ = batch0_;
     max_bytes_ = 0;
   }
+  void ResetBytes() { last_bytes_ = 0; }
 
  private:
   void WaitCopy() {
@@ -105,7 +118,7 @@ class Stager {
   }
 
   size_t Reserve(size_t bytes) {
-    if (used_ == 0) WaitCopy();   // first piece of a batch: the buffer is about to be rewritten
+    if (used_ == 0) WaitCopy();   // first piece of a load: the buffer is about to be rewritten
     const size_t off = (used_ + 15) & ~(size_t)15;
     const size_t need = off + bytes;
     if (need > cap_) Grow(std::max(need, 2 * cap_));   // geometric: a growing map re-pins O(log) times
@@ -128,7 +141,7 @@ class Stager {
   }
 
   unsigned char* host_ = nullptr;
-  size_t cap_ = 0, used_ = 0, max_bytes_ = 0, last_bytes_ = 0;
+  size_t cap_ = 0, used_ = 0, batch0_ = 0, max_bytes_ = 0, last_bytes_ = 0;
   hipEvent_t copied_ = nullptr;
   bool pending_ = false;
   std::vector<StagePiece> pieces_;

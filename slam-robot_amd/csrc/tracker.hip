@@ -312,12 +312,18 @@ struct TrackCtx {
   int pi[kNP], pj[kNP];   // this lane's patch pixels (row, column); pi = -1 past the patch
 };
 
+// NK: patch pixels per lane the launch's window needs, ceil(W^2 / 64) (the kernels are instantiated per NK:
+// slots past the patch only ever add zeros, so skipping them changes no bit and saves their sampling — at
+// W = 7 three of the four slots).
+template <int NK>
 __device__ __forceinline__ void get_patch_ctx(const TrackCtx& c, const LevelDev& L, float px, float py, Tmpl& t) {
   Geo g;
   make_geo(px, py, c.W, L.w, L.h, g);
   float s = 0.f, q = 0.f;
 #pragma unroll
-  for (int k = 0; k < kNP; ++k) {
+  for (int k = 0; k < kNP; ++k) t.v[k] = 0.f;
+#pragma unroll
+  for (int k = 0; k < NK; ++k) {
     const float v = k < c.nk ? sample(L.img, L.w, g, c.pi[k], c.pj[k]) : 0.f;   // 0 past the patch
     t.v[k] = v;
     s += v;
@@ -331,7 +337,7 @@ __device__ __forceinline__ void get_patch_ctx(const TrackCtx& c, const LevelDev&
 
 // BruteHessian (hessian.h:147-172): the six probes sampled together, their sums reduced in batches.
 // kLds: the probes read the wave's staged tile (the caller checked stage_covers).
-template <bool kLds>
+template <int NK, bool kLds>
 __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev& L, const Tmpl& tp, float x, float y,
                                               float* mdx, float* mdy, float* mdxx, float* mdxy, float* mdyx,
                                               float* mdyy, const float* tile, const Stage& st) {
@@ -343,14 +349,14 @@ __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev&
   px[3] = (float)(x + hh); py[3] = y;               // sadp1x
   px[4] = x;              py[4] = (float)(y + hh);  // sadp1y
   px[5] = (float)(x + hh); py[5] = (float)(y + hh); // sadxy
-  float pv[6][kNP], ps[6], pq[6];
+  float pv[6][NK], ps[6], pq[6];
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
     Geo g;
     make_geo(px[r], py[r], c.W, L.w, L.h, g);
     float s = 0.f, q = 0.f;
 #pragma unroll
-    for (int k = 0; k < kNP; ++k) {
+    for (int k = 0; k < NK; ++k) {
       const float sv = kLds ? sample_lds(tile, st, g, c.pi[k], c.pj[k]) : sample(L.img, L.w, g, c.pi[k], c.pj[k]);
       const float v = k < c.nk ? sv : 0.f;   // 0 past the patch
       pv[r][k] = v;
@@ -373,7 +379,7 @@ __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev&
     const float beta = tp.mean - alpha * mean;
     float acc = 0.f;
 #pragma unroll
-    for (int k = 0; k < kNP; ++k) {
+    for (int k = 0; k < NK; ++k) {
       float term = 0.f;
       const float a = tp.v[k], b = pv[r][k];
       if (!(a == 0 || b == 0)) {
@@ -398,6 +404,7 @@ __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev&
 
 // One TrackFeature (hessian.h:243-264) pass: templates from `src` at (sx, sy) (GetPatches, 175-183), Newton
 // iterations of Track (185-241) on `dst` coarse to fine.  0 OK (*px, *py updated), 2 OUT_OF_BOUNDS.
+template <int NK>
 __device__ __forceinline__ int track_pass(const TrackCtx& c, const LevelDev* __restrict__ src,
                                           const LevelDev* __restrict__ dst, int lvls, float sx, float sy, float* px,
                                           float* py, int* iters, float* tile) {
@@ -411,7 +418,7 @@ __device__ __forceinline__ int track_pass(const TrackCtx& c, const LevelDev* __r
     }
     const LevelDev Ls = src[i], Ld = dst[i];
     Tmpl tp;
-    get_patch_ctx(c, Ls, tx, ty, tp);
+    get_patch_ctx<NK>(c, Ls, tx, ty, tp);
     const float margin = 0.01f;
     int it = 0;
     bool oob = false;
@@ -424,9 +431,9 @@ __device__ __forceinline__ int track_pass(const TrackCtx& c, const LevelDev* __r
       float mdx, mdy, mdxx, mdxy, mdyx, mdyy;
       if (!stage_covers(st, x, y, c.W)) stage_load(Ld, x, y, c.lane, tile, st);
       if (stage_covers(st, x, y, c.W))
-        brute_hessian<true>(c, Ld, tp, x, y, &mdx, &mdy, &mdxx, &mdxy, &mdyx, &mdyy, tile, st);
+        brute_hessian<NK, true>(c, Ld, tp, x, y, &mdx, &mdy, &mdxx, &mdxy, &mdyx, &mdyy, tile, st);
       else
-        brute_hessian<false>(c, Ld, tp, x, y, &mdx, &mdy, &mdxx, &mdxy, &mdyx, &mdyy, tile, st);
+        brute_hessian<NK, false>(c, Ld, tp, x, y, &mdx, &mdy, &mdxx, &mdxy, &mdyx, &mdyy, tile, st);
       const double H00 = mdxx, H01 = mdxy, H10 = mdyx, H11 = mdyy;
       const double det = H00 * H11 - H10 * H01;
       const double invdet = 1.0 / det;
@@ -461,6 +468,7 @@ __device__ __forceinline__ int track_pass(const TrackCtx& c, const LevelDev* __r
 // matcher.cpp TrackFeature (173-206) + FindMatches' retry with more levels (247-251), one wave per feature.
 // The attempt and pass loops share one inlined body.  The backward pass is skipped when the forward pass
 // failed: the matcher rejects the feature either way and the backward pass does not touch to_pt.
+template <int NK>
 __global__ __launch_bounds__(64 * kTrackWaves) void k_track_fb(const LevelDev* __restrict__ from_lv,
                                                                const LevelDev* __restrict__ to_lv, int depth,
                                                                TrackParams prm, int n, const float* from_xy,
@@ -505,7 +513,7 @@ __global__ __launch_bounds__(64 * kTrackWaves) void k_track_fb(const LevelDev* _
       const LevelDev* dst = pass ? from_lv : to_lv;
       const float sx = pass ? tx : fx, sy = pass ? ty : fy;
       float qx = pass ? bx : tx, qy = pass ? by : ty;
-      st = track_pass(c, src, dst, lvls, sx, sy, &qx, &qy, &iters, tile);
+      st = track_pass<NK>(c, src, dst, lvls, sx, sy, &qx, &qy, &iters, tile);
       if (st != 0) break;
       if (pass == 0) {
         tx = qx;
@@ -568,6 +576,7 @@ __device__ __forceinline__ void init_ctx(TrackCtx& c, const TrackParams& prm, in
 }
 
 // HessianTracker::TrackFeature (hessian.h:243-264) alone, one wave per feature.
+template <int NK>
 __global__ __launch_bounds__(64 * kTrackWaves) void k_track_one(const LevelDev* __restrict__ from_lv,
                                                                 const LevelDev* __restrict__ to_lv, int depth,
                                                                 TrackParams prm, int n, const float* from_xy,
@@ -583,7 +592,7 @@ __global__ __launch_bounds__(64 * kTrackWaves) void k_track_one(const LevelDev* 
   const int lvls = min(depth, levels ? levels[f] : depth);
   float qx = to_xy[2 * f], qy = to_xy[2 * f + 1];
   int iters = 0;
-  const int st = track_pass(c, from_lv, to_lv, lvls, from_xy[2 * f], from_xy[2 * f + 1], &qx, &qy, &iters, tile);
+  const int st = track_pass<NK>(c, from_lv, to_lv, lvls, from_xy[2 * f], from_xy[2 * f + 1], &qx, &qy, &iters, tile);
   if (lane == 0) {
     status[f] = st;
     if (st == 0) {
@@ -1074,6 +1083,15 @@ void Tracker::LoadFeatures(int n, const float* from_xy, const float* to_xy, cons
   its_.Resize(std::max(n, 1));
 }
 
+// Launch KERN<NK> for a W x W window (NK = ceil(W^2 / 64) patch pixels per lane, W <= 16).
+#define SG_TRK_NK(W, KERN, ...)                                              \
+  switch (((W) * (W) + 63) / 64) {                                           \
+    case 1: hipLaunchKernelGGL(KERN<1>, __VA_ARGS__); break;                 \
+    case 2: hipLaunchKernelGGL(KERN<2>, __VA_ARGS__); break;                 \
+    case 3: hipLaunchKernelGGL(KERN<3>, __VA_ARGS__); break;                 \
+    default: hipLaunchKernelGGL(KERN<4>, __VA_ARGS__); break;                \
+  }
+
 void Tracker::Run(int from, int to, int repeats) {
   SG_REQUIRE(from >= 0 && from < (int)slots_.size() && slots_[from].valid, SG_EINVAL, "empty 'from' slot");
   SG_REQUIRE(to >= 0 && to < (int)slots_.size() && slots_[to].valid, SG_EINVAL, "empty 'to' slot");
@@ -1086,9 +1104,9 @@ void Tracker::Run(int from, int to, int repeats) {
   SG_HIP_CHECK(hipEventRecord(ev_[0], stream_));
   if (n_ > 0)
     for (int r = 0; r < repeats; ++r)
-      hipLaunchKernelGGL(k_track_fb, dim3((n_ + kTrackWaves - 1) / kTrackWaves), dim3(64 * kTrackWaves), 0, stream_,
-                         (const LevelDev*)a.table.ptr, (const LevelDev*)b.table.ptr, opt_.depth, prm, n_, from_.ptr,
-                         init_.ptr, levels_.ptr, out_.ptr, acc_.ptr, its_.ptr);
+      SG_TRK_NK(opt_.window, k_track_fb, dim3((n_ + kTrackWaves - 1) / kTrackWaves), dim3(64 * kTrackWaves), 0,
+                stream_, (const LevelDev*)a.table.ptr, (const LevelDev*)b.table.ptr, opt_.depth, prm, n_, from_.ptr,
+                init_.ptr, levels_.ptr, out_.ptr, acc_.ptr, its_.ptr);
   SG_HIP_CHECK(hipEventRecord(ev_[1], stream_));
   SG_HIP_CHECK(hipGetLastError());
   ran_ = true;
@@ -1137,8 +1155,8 @@ void Tracker::TrackFeature(int from, int to, int n, const float* from_xy, float*
   const LevelDev* lb = (const LevelDev*)b.table.ptr;
   const dim3 grid((n + kTrackWaves - 1) / kTrackWaves), block(64 * kTrackWaves);
   if (opt_.mode == SG_TRACKER_HESSIAN) {
-    hipLaunchKernelGGL(k_track_one, grid, block, 0, st, la, lb, depth, prm, n, from_.ptr, out_.ptr,
-                       levels ? (const int32_t*)levels_.ptr : nullptr, acc_.ptr, its_.ptr);
+    SG_TRK_NK(W, k_track_one, grid, block, 0, st, la, lb, depth, prm, n, from_.ptr, out_.ptr,
+              levels ? (const int32_t*)levels_.ptr : nullptr, acc_.ptr, its_.ptr);
   } else if (opt_.mode == SG_TRACKER_KLT) {
     hipLaunchKernelGGL(k_track_klt, grid, block, 0, st, la, lb, depth, prm, n, from_.ptr, out_.ptr, acc_.ptr,
                        its_.ptr);

@@ -29,6 +29,20 @@ int main(int argc, char** argv) {
     if (ok != (bool)ok_o) { printf("ok mismatch trial %d\n", trial); return 1; }
     if (!ok) continue;
     ++n_ok;
+    // the tangent-space rotation Jacobian formed directly == Jq * QuatLocalJacobian(q)
+    {
+      double Jq2[8], Jt2[6], JX2[8], Jr[6], uv2[2], L[12];
+      sg::ProjectJacobian(q, t, k, X, uv2, (double*)nullptr, Jt2, (double*)nullptr, JX2, Jr);
+      sg::QuatLocalJacobian(q, L);
+      double sc = 0;
+      for (int i = 0; i < 8; ++i) sc = fmax(sc, fabs(Jq[i]));
+      for (int r = 0; r < 2; ++r)
+        for (int c = 0; c < 3; ++c) {
+          const double ref = Jq[4*r]*L[c] + Jq[4*r+1]*L[3+c] + Jq[4*r+2]*L[6+c] + Jq[4*r+3]*L[9+c];
+          worst_rel = fmax(worst_rel, fabs(Jr[3*r+c] - ref) / (sc + 1e-300));
+        }
+      (void)Jq2;
+    }
     double mine[36];
     for (int r = 0; r < 2; ++r) {
       for (int c = 0; c < 4; ++c) mine[18*r+c] = Jq[4*r+c];

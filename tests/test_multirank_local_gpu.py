@@ -146,6 +146,31 @@ def test_two_shards_c5_first_iterations_match_one_rank(gpu_lib):
     _check_against_one_rank(pa, res, o, 1e-12, 1e-10, 1e-6, 1e-10)
 
 
+@pytest.mark.parametrize("nranks", [4, 8])
+def test_many_shards_c5_first_iterations_match_one_rank(gpu_lib, nranks):
+    """BASELINE config 5 split into nranks landmark shards (8: the 8-GPU split config 5 names), each driven by
+    its own host thread and handle on one GPU through the in-process group: the sharded device chain (envelope
+    union, rank-0 assembly, packed band exchange, replicated factorisation and decision) against the one-rank
+    solve of the whole problem, two LM iterations."""
+    m = make_config("C5")
+    pa = ba.problem_from_map_frames(m, 198, 200, 2.0)
+    o = default_solver_options(max_num_iterations=2)
+    res = _sharded(pa, nranks, o, timeout=600)
+    s0, _ = _check_against_one_rank(pa, res, o, 1e-12, 1e-10, 1e-6, 1e-10)
+    assert s0["sync_timeouts"] == 0
+    obs = [sh.num_obs for _, sh, _ in res]
+    assert max(obs) / (sum(obs) / nranks) <= 1.1, obs
+
+
+def test_eight_shards_c2_match_one_rank(gpu_lib):
+    m = make_config("C2")
+    pa = ba.problem_from_map_frames(m, 48, 50, 2.0)
+    o = default_solver_options(max_num_iterations=5)
+    res = _sharded(pa, 8, o, timeout=300)
+    s0, _ = _check_against_one_rank(pa, res, o, 1e-12, 1e-10, 1e-6, 1e-10)
+    assert s0["sync_timeouts"] == 0
+
+
 def test_invalid_shard_fails_every_rank(gpu_lib):
     """A rank whose problem fails validation must not leave its peers blocked in the load-time all-reduce."""
     m = make_config("C1")

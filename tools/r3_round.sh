@@ -23,6 +23,14 @@ print("kernels", d["kernel_ms_per_iter"])
 o = d.get("other_workload") or {}
 if o: print("C5 %.1f it/s kernels %s" % (o["value"], o["kernel_ms_per_iter"]))
 PY
+if [ -n "$R3_DIAG" ]; then
+  [ -x tools/factor_bench2 ] && timeout -k 10 60 tools/factor_bench2 > gpurun_out/factor_bench2_$TAG.log 2>&1 && cat gpurun_out/factor_bench2_$TAG.log
+  timeout -k 10 300 python tools/chol_ab.py 40 > gpurun_out/chol_ab_$TAG.log 2>&1 || { echo "chol_ab failed"; tail -20 gpurun_out/chol_ab_$TAG.log; exit 1; }
+  cat gpurun_out/chol_ab_$TAG.log
+  timeout -k 10 120 python tools/phase_trace.py C2 > gpurun_out/phase_trace_C2_$TAG.log 2>&1 || { echo "trace C2 failed"; tail -5 gpurun_out/phase_trace_C2_$TAG.log; exit 1; }
+  tail -25 gpurun_out/phase_trace_C2_$TAG.log
+  timeout -k 10 180 python tools/phase_trace.py C5 > gpurun_out/phase_trace_C5_$TAG.log 2>&1 || { echo "trace C5 failed"; tail -5 gpurun_out/phase_trace_C5_$TAG.log; exit 1; }
+fi
 SG_HOST_TIMING=1 timeout -k 10 300 python tools/e2e_replay.py gpurun_out/e2e_replay_$TAG.json > gpurun_out/e2e_$TAG.log 2> gpurun_out/e2e_phases_$TAG.log \
   || { echo "replay failed"; tail -20 gpurun_out/e2e_phases_$TAG.log; exit 1; }
 tail -12 gpurun_out/e2e_$TAG.log
