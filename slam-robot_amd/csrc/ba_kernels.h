@@ -5,7 +5,7 @@
 // window BA):
 //   q[2][4F], t[2][3F], X[2][4P]   parameter state, two slots (current / candidate), switched by LmState::cur
 //   obs_pt[2M], obs_frame[M]       observations, CSR by point (poff[P+1])
-//   J[M][24]                       corrected, unscaled residual + Jacobian per observation
+//   J[M/64][12][64] (double2)      corrected, unscaled residual + Jacobian per observation, element pairs
 //                                  (r~ 2 | Jc 2x6 [rot_local 3, t 3] | Jp 2x4 | pad 2)
 //   V[P][10], g[P][4]              point normal-equation blocks (upper 4x4) and gradient
 //   Vinv[P][10], tp[P][4]          damped, scaled inverse and V^-1 g~ (per LM iteration)

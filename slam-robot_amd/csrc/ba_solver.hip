@@ -141,14 +141,22 @@ __device__ __forceinline__ int u4(int a, int c) { return a * (7 - a) / 2 + c; }
 // packed index of a window block pair (i <= j < nb)
 __device__ __forceinline__ int wp(int i, int j, int nb) { return i * nb - i * (i - 1) / 2 + (j - i); }
 
+// Observation records J (r~ 2 | Jc 12 | Jp 8 | cost, pad) in blocks of 64 observations, element pairs
+// interleaved: pair e2 (0..11) of observation o at double2 index ((o >> 6) * 12 + e2) * 64 + (o & 63).  A wave's
+// lanes reading (or writing) one element pair of 64 consecutive observations touch one contiguous KiB instead
+// of a 16-byte piece of 64 different 192-byte records.
+__device__ __forceinline__ size_t jidx2(int o, int e2) { return ((size_t)(o >> 6) * 12 + e2) * 64 + (o & 63); }
+__device__ __forceinline__ double2 jload2(const Dev& d, int o, int e2) {
+  return reinterpret_cast<const double2*>(d.J)[jidx2(o, e2)];
+}
+
 // Load the corrected Jacobian of observation o and apply Jacobi scaling.
 __device__ __forceinline__ void load_scaled_J(const Dev& d, int o, int b, const double* sp, double* r,
                                               double* Jc, double* Jp) {
-  const double2* J2 = reinterpret_cast<const double2*>(d.J + (size_t)o * kJStride);
   double buf[22];
 #pragma unroll
   for (int i = 0; i < 11; ++i) {
-    const double2 v = J2[i];
+    const double2 v = jload2(d, o, i);
     buf[2 * i] = v.x;
     buf[2 * i + 1] = v.y;
   }
@@ -257,12 +265,17 @@ __global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_linearize(Dev d) {
   const LinChunk ch = d.lchunks[blockIdx.x];
   __shared__ double pacc[kLinPts * 14];         // point blocks of the round: V (10) | g (4)
   __shared__ double camacc[kLinNbMax * kCamV];  // camera blocks of the window: upper Jc^T Jc (21) | Jc^T r (6)
+  // the rarely-touched per-lane sums (failures, the fixed cost and |X|^2 of iteration 0) live in LDS, one slot
+  // per lane, so they hold no registers across the projection (k_linearize's VGPR budget sets its occupancy)
+  __shared__ double lsum[4][kLinThreads];       // fail, fixed, ffail, xn2
   const int lane = threadIdx.x;
   const double4* X4 = reinterpret_cast<const double4*>(d.X[cur]);
   const int ncv = ch.nb * kCamV;
   for (int i = lane; i < ncv; i += kLinThreads) camacc[i] = 0.0;
   for (int i = lane; i < kLinPts * 14; i += kLinThreads) pacc[i] = 0.0;
-  double cost = 0.0, fail = 0.0, fixed = 0.0, ffail = 0.0, xn2 = 0.0, gmax = 0.0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) lsum[k][lane] = 0.0;
+  double cost = 0.0, gmax = 0.0;
   // per-observation inputs, software-pipelined one round ahead
   LinRound R = d.lrounds[ch.r0];
   int nobs = R.o1 - R.o0;
@@ -302,16 +315,16 @@ __global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_linearize(Dev d) {
       double rr[2], Jc[12], Jp[8], c;
       const bool ok = LinearizeObservation(d.q[cur] + 4 * f, d.t[cur] + 3 * f, d.k[cur] + 7 * meta_cam(m), X, pt,
                                            d.b, d.inv_b, rr, Jc, Jp, &c);
-      double2* Jo = reinterpret_cast<double2*>(d.J + (size_t)o * kJStride);
+      double2* Jo = reinterpret_cast<double2*>(d.J) + jidx2(o, 0);   // pair e2 at Jo[64 e2]
       if (!ok || fx) {
         if (!ok) {
-          if (fx) ffail += 1.0;
-          else fail += 1.0;
+          if (fx) lsum[2][lane] += 1.0;
+          else lsum[0][lane] += 1.0;
         } else if (first) {
-          fixed += c;
+          lsum[1][lane] += c;
         }
 #pragma unroll
-        for (int i = 0; i < kJStride / 2; ++i) Jo[i] = make_double2(0.0, 0.0);
+        for (int i = 0; i < kJStride / 2; ++i) Jo[64 * i] = make_double2(0.0, 0.0);
       } else {
         cost += c;
         const int b = meta_block(m);
@@ -328,10 +341,10 @@ __global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_linearize(Dev d) {
         }
         Jo[0] = make_double2(rr[0], rr[1]);
 #pragma unroll
-        for (int i = 0; i < 6; ++i) Jo[1 + i] = make_double2(Jc[2 * i], Jc[2 * i + 1]);
+        for (int i = 0; i < 6; ++i) Jo[64 * (1 + i)] = make_double2(Jc[2 * i], Jc[2 * i + 1]);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) Jo[7 + i] = make_double2(Jp[2 * i], Jp[2 * i + 1]);
-        Jo[11] = make_double2(c, 0.0);
+        for (int i = 0; i < 4; ++i) Jo[64 * (7 + i)] = make_double2(Jp[2 * i], Jp[2 * i + 1]);
+        Jo[64 * 11] = make_double2(c, 0.0);
         if (pf) {
           double* pa = pacc + (p - Rc.p0) * 14;
 #pragma unroll
@@ -384,7 +397,7 @@ __global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_linearize(Dev d) {
                 make_double4(1.0 / (1.0 + sqrt(V[0])), 1.0 / (1.0 + sqrt(V[4])), 1.0 / (1.0 + sqrt(V[7])),
                              1.0 / (1.0 + sqrt(V[9])));
             const double4 Xv = X4[pp];
-            xn2 += Xv.x * Xv.x + Xv.y * Xv.y + Xv.z * Xv.z + Xv.w * Xv.w;
+            lsum[3][lane] += Xv.x * Xv.x + Xv.y * Xv.y + Xv.z * Xv.z + Xv.w * Xv.w;
           }
         } else if (first) {
           reinterpret_cast<double4*>(d.scale_p)[pp] = make_double4(1.0, 1.0, 1.0, 1.0);
@@ -396,10 +409,10 @@ __global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_linearize(Dev d) {
   lds_fence_wave();
   for (int i = lane; i < ncv; i += kLinThreads) d.cam_slab[ch.cam_off + i] = camacc[i];
   cost = wave_sum_full(cost);
-  fail = wave_sum_full(fail);
-  fixed = wave_sum_full(fixed);
-  ffail = wave_sum_full(ffail);
-  xn2 = wave_sum_full(xn2);
+  const double fail = wave_sum_full(lsum[0][lane]);
+  const double fixed = wave_sum_full(lsum[1][lane]);
+  const double ffail = wave_sum_full(lsum[2][lane]);
+  const double xn2 = wave_sum_full(lsum[3][lane]);
   gmax = wave_max(gmax);
   if (lane == 0) {
     double* sc = d.lin_scal + blockIdx.x;   // structure of arrays: slot j at [j * nlin + chunk]
@@ -725,21 +738,19 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d) {
 // Points spanning more than kSegNbMax blocks take k_schur_wide (observation pairs, global atomics).
 
 __device__ __forceinline__ void load_Jc_scaled(const Dev& d, int o, int b, double* Jc) {
-  const double2* J2 = reinterpret_cast<const double2*>(d.J + (size_t)o * kJStride) + 1;   // skip r
   const double* sc = d.scale_c + 6 * b;
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
-    const double2 v = J2[i];
+    const double2 v = jload2(d, o, 1 + i);   // (pair 0: r)
     Jc[2 * i] = v.x * sc[(2 * i) % 6];
     Jc[2 * i + 1] = v.y * sc[(2 * i + 1) % 6];
   }
 }
 __device__ __forceinline__ void load_Jp_scaled(const Dev& d, int o, const double4& s4, double* Jp) {
-  const double2* J2 = reinterpret_cast<const double2*>(d.J + (size_t)o * kJStride) + 7;   // r 2 | Jc 12
   const double sp[4] = {s4.x, s4.y, s4.z, s4.w};
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const double2 v = J2[i];
+    const double2 v = jload2(d, o, 7 + i);   // (pairs 0-6: r, Jc)
     Jp[2 * i] = v.x * sp[(2 * i) % 4];
     Jp[2 * i + 1] = v.y * sp[(2 * i + 1) % 4];
   }
@@ -1419,7 +1430,12 @@ __global__ __launch_bounds__(128) void k_intr_schur(Dev d) {
       if ((m & kMetaFixed) || meta_cam(m) != c) continue;
       any = true;
       const double* Jk = d.Jk + 14 * (size_t)o;
-      const double* Jr = d.J + (size_t)o * kJStride + 14;   // corrected Jp (2x4)
+      double Jr[8];   // corrected Jp (2x4)
+      for (int i = 0; i < 4; ++i) {
+        const double2 v = jload2(d, o, 7 + i);
+        Jr[2 * i] = v.x;
+        Jr[2 * i + 1] = v.y;
+      }
       for (int j = 0; j < 7; ++j) {
         const double k0 = Jk[j] * d.scale_c[d.kc0 + 7 * c + j], k1 = Jk[7 + j] * d.scale_c[d.kc0 + 7 * c + j];
         for (int a = 0; a < 4; ++a) W[4 * j + a] += (k0 * Jr[a] + k1 * Jr[4 + a]) * sp[a];
@@ -3362,16 +3378,16 @@ __device__ __forceinline__ void pu_pass3(const Dev& d, const LinRound& R, int la
   }
   model -= m0 * (ob.r[0] + 0.5 * m0) + m1 * (ob.r[1] + 0.5 * m1);
   const double Xn[4] = {Xns[4 * lp], Xns[4 * lp + 1], Xns[4 * lp + 2], Xns[4 * lp + 3]};
-  double uv[2];
-  if (!Project(d.q[nxt] + 4 * ob.f, d.t[nxt] + 3 * ob.f, d.k[nxt] + 7 * ob.cam, Xn, uv)) {
-    candfail += 1.0;
-    return;
-  }
+  double uv[2] = {0.0, 0.0};
+  const bool okp = Project(d.q[nxt] + 4 * ob.f, d.t[nxt] + 3 * ob.f, d.k[nxt] + 7 * ob.cam, Xn, uv);
   const double2 pt = reinterpret_cast<const double2*>(d.obs_pt)[o];
   const double e0 = uv[0] - pt.x, e1 = uv[1] - pt.y;
   double rho0, rho1;
   Cauchy(e0 * e0 + e1 * e1, d.b, d.inv_b, &rho0, &rho1);
-  candcost += 0.5 * rho0;
+  // both accumulators updated unconditionally (selects, no early return): a conditional update of one of
+  // two references made the compiler keep them in an indexed stack slot (scratch traffic on every lane)
+  candfail += okp ? 0.0 : 1.0;
+  candcost += okp ? 0.5 * rho0 : 0.0;
 }
 
 // pass 2 for the points [p0, p1) of a round (lane per point): x_p, X+ into LDS and HBM.
@@ -4388,7 +4404,7 @@ void BaSolver::Load(const sg_problem& p) {
     stg.Add(fd_pair_, fd_pair);
     rdg_.Resize((size_t)std::max(n_, 1) + kCholNb);   // + padding rows of the last panel
   }
-  J_.Resize((size_t)std::max(M_, 1) * kJStride);
+  J_.Resize((size_t)((std::max(M_, 1) + 63) & ~63) * kJStride);   // whole 64-observation blocks (jidx2)
   V_.Resize(10 * (size_t)std::max(P_, 1));
   g_.Resize(4 * (size_t)std::max(P_, 1));
   scale_p_.Resize(4 * (size_t)std::max(P_, 1));
@@ -4455,7 +4471,7 @@ void BaSolver::Reserve(int F, int P, int M) {
   const size_t f = std::max(F, 1), pp = std::max(P, 1), m = std::max(M, 1);
   bool moved = false;
   // per observation (device order records, the Jacobian rows, the Schur cells)
-  moved |= J_.Reserve(m * kJStride);
+  moved |= J_.Reserve(((m + 63) & ~(size_t)63) * kJStride);
   moved |= obs_pt_.Reserve(2 * m);
   moved |= obs_frame_.Reserve(m);
   moved |= obs_fixed_.Reserve(m);
