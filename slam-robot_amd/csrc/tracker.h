@@ -21,7 +21,9 @@ struct TrackParams {
   float threshold, fb_max;
   int retry_levels;
   const float* mask;
+  unsigned long long* stamps = nullptr;   // diagnostics (SG_TRK_STAMP=1): per-phase cycles of the Newton loop
 };
+constexpr int kTrkStamps = 10;   // stage, probes, sums 1, score, sums 2 + differences, step, template, other, iters, waves
 
 class Tracker {
  public:
@@ -41,6 +43,8 @@ class Tracker {
   void SeedFeatures(int slot, const float* match_xy, int nmatch, int max_corners, double quality, double min_distance,
                     float* corners_xy, int* ncorners, float* added_xy, int* nadded);
   double track_ms() const { return track_ms_; }
+  // diagnostics: accumulated per-phase cycles of k_track_fb since the last call (SG_TRK_STAMP=1), kTrkStamps
+  std::vector<unsigned long long> Stamps();
   double pyramid_ms() const { return pyr_ms_; }
 
  private:
@@ -69,6 +73,8 @@ class Tracker {
   DBuf<uint8_t> brute_state_;
   int n_ = 0;
   bool ran_ = false;
+  bool stamp_on_ = false;
+  DBuf<unsigned long long> stamps_;
   double track_ms_ = 0.0, pyr_ms_ = 0.0;
 };
 

@@ -303,6 +303,21 @@ __device__ __forceinline__ void get_patch(const LevelDev& L, float px, float py,
   t.sumsq = q / len;
 }
 
+// Diagnostic per-phase cycle counters of the Newton loop (lane 0 of each wave; SG_TRK_STAMP=1), added to the
+// tracker's stamp buffer at the end of the kernel.  `on` is wave-uniform: production launches branch past it.
+struct TStamp {
+  unsigned long long acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long last = 0;
+  bool on = false;
+  __device__ __forceinline__ void mark(int slot) {
+    if (on) {
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      acc[slot] += now - last;
+      last = now;
+    }
+  }
+};
+
 struct TrackCtx {
   int W, len, max_it;
   int nk;              // patch pixels per lane actually used: ceil(len / 64) <= kNP
@@ -310,6 +325,7 @@ struct TrackCtx {
   int lane;
   float mk[kNP];       // this lane's mask values
   int pi[kNP], pj[kNP];   // this lane's patch pixels (row, column); pi = -1 past the patch
+  TStamp* ts = nullptr;
 };
 
 // NK: patch pixels per lane the launch's window needs, ceil(W^2 / 64) (the kernels are instantiated per NK:
@@ -341,6 +357,7 @@ template <int NK, bool kLds>
 __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev& L, const Tmpl& tp, float x, float y,
                                               float* mdx, float* mdy, float* mdxx, float* mdxy, float* mdyx,
                                               float* mdyy, const float* tile, const Stage& st) {
+  c.ts->mark(0);
   const double hh = 0.02;
   float px[6], py[6];
   px[0] = x;              py[0] = y;                // sad0
@@ -366,11 +383,13 @@ __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev&
     ps[r] = s;
     pq[r] = q;
   }
+  c.ts->mark(1);
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
     ps[r] = wave_tree_sum(ps[r]);
     pq[r] = wave_tree_sum(pq[r]);
   }
+  c.ts->mark(2);
   float sc[6];
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
@@ -391,6 +410,7 @@ __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev&
     }
     sc[r] = acc;
   }
+  c.ts->mark(3);
 #pragma unroll
   for (int r = 0; r < 6; ++r) sc[r] = wave_tree_sum(sc[r]);
   const double sad0 = sc[0], sadn1x = sc[1], sadn1y = sc[2], sadp1x = sc[3], sadp1y = sc[4], sadxy = sc[5];
@@ -400,6 +420,7 @@ __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev&
   *mdyy = (float)(((sadp1y - sad0) / hh - (sad0 - sadn1y) / hh) / hh);
   *mdxy = (float)(((sadxy - sadp1y) / hh - (sadp1x - sad0) / hh) / hh);
   *mdyx = (float)(((sadxy - sadp1x) / hh - (sadp1y - sad0) / hh) / hh);
+  c.ts->mark(4);
 }
 
 // One TrackFeature (hessian.h:243-264) pass: templates from `src` at (sx, sy) (GetPatches, 175-183), Newton
@@ -418,7 +439,9 @@ __device__ __forceinline__ int track_pass(const TrackCtx& c, const LevelDev* __r
     }
     const LevelDev Ls = src[i], Ld = dst[i];
     Tmpl tp;
+    c.ts->mark(7);
     get_patch_ctx<NK>(c, Ls, tx, ty, tp);
+    c.ts->mark(6);
     const float margin = 0.01f;
     int it = 0;
     bool oob = false;
@@ -448,6 +471,7 @@ __device__ __forceinline__ int track_pass(const TrackCtx& c, const LevelDev* __r
       const float cx = (dx < 1.f) ? dx : 1.f, cy = (dy < 1.f) ? dy : 1.f;   // std::min / std::max semantics
       x += (-1.f < cx) ? cx : -1.f;
       y += (-1.f < cy) ? cy : -1.f;
+      c.ts->mark(5);
       if (fabsf(dx) < c.threshold && fabsf(dy) < c.threshold) {
         ++it;
         break;
@@ -479,7 +503,11 @@ __global__ __launch_bounds__(64 * kTrackWaves) void k_track_fb(const LevelDev* _
   const int f = blockIdx.x * kTrackWaves + (threadIdx.x >> 6);
   if (f >= n) return;   // whole wave
   float* tile = stage_tiles[threadIdx.x >> 6];
+  TStamp tst;
+  tst.on = prm.stamps != nullptr && lane == 0;
+  if (tst.on) tst.last = __builtin_amdgcn_s_memtime();
   TrackCtx c;
+  c.ts = &tst;
   c.W = prm.window;
   c.len = prm.window * prm.window;
   c.nk = (c.len + 63) / 64;
@@ -534,6 +562,12 @@ __global__ __launch_bounds__(64 * kTrackWaves) void k_track_fb(const LevelDev* _
     accepted[f] = ok ? 1 : 0;
     if (iterations) iterations[f] = iters;
   }
+  if (tst.on) {
+    tst.mark(7);
+    for (int k = 0; k < 8; ++k) atomicAdd(prm.stamps + k, tst.acc[k]);
+    atomicAdd(prm.stamps + 8, (unsigned long long)iters);
+    atomicAdd(prm.stamps + 9, 1ull);
+  }
 }
 
 __global__ __launch_bounds__(64 * kTrackWaves) void k_get_patches(LevelDev L, int W, int n, const float* xy, float* out,
@@ -559,6 +593,7 @@ __global__ __launch_bounds__(64 * kTrackWaves) void k_get_patches(LevelDev L, in
 // One-directional TrackFeature of each FeatureTracker (sg_tracker_track_feature).
 
 __device__ __forceinline__ void init_ctx(TrackCtx& c, const TrackParams& prm, int lane) {
+  // (the one-directional kernels are not stamped: c.ts points at an off TStamp set by the caller)
   c.W = prm.window;
   c.len = prm.window * prm.window;
   c.nk = (c.len + 63) / 64;
@@ -588,7 +623,9 @@ __global__ __launch_bounds__(64 * kTrackWaves) void k_track_one(const LevelDev* 
   if (f >= n) return;
   float* tile = stage_tiles[threadIdx.x >> 6];
   TrackCtx c;
+  TStamp tst_off;
   init_ctx(c, prm, lane);
+  c.ts = &tst_off;
   const int lvls = min(depth, levels ? levels[f] : depth);
   float qx = to_xy[2 * f], qy = to_xy[2 * f + 1];
   int iters = 0;
@@ -695,7 +732,9 @@ __global__ __launch_bounds__(64 * kTrackWaves) void k_track_klt(const LevelDev* 
   const int f = blockIdx.x * kTrackWaves + (threadIdx.x >> 6);
   if (f >= n) return;
   TrackCtx c;
+  TStamp tst_off;
   init_ctx(c, prm, lane);
+  c.ts = &tst_off;
   const float sx = from_xy[2 * f], sy = from_xy[2 * f + 1];
   const double s = 1. / (1 << (depth - 1));
   float x = (float)(to_xy[2 * f] * s), y = (float)(to_xy[2 * f + 1] * s);
@@ -938,6 +977,7 @@ Tracker::Tracker(const sg_tracker_options& o, const sg_device_options& d) : opt_
   SG_HIP_CHECK(hipGetDeviceCount(&ndev));
   SG_REQUIRE(ndev > 0 && d.device >= 0 && d.device < ndev, SG_ENODEV, "no such HIP device");
   SG_HIP_CHECK(hipSetDevice(d.device));
+  stamp_on_ = getenv("SG_TRK_STAMP") && getenv("SG_TRK_STAMP")[0] == '1';
   SG_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   SG_HIP_CHECK(hipEventCreate(&ev_[0]));
   SG_HIP_CHECK(hipEventCreate(&ev_[1]));
@@ -1101,6 +1141,13 @@ void Tracker::Run(int from, int to, int repeats) {
   SG_REQUIRE(a.w == b.w && a.h == b.h, SG_EINVAL, "pyramids of different sizes");
   SG_HIP_CHECK(hipSetDevice(dev_.device));
   TrackParams prm{opt_.window, opt_.max_iterations, opt_.threshold, opt_.fb_max, opt_.retry_levels, mask_.ptr};
+  if (stamp_on_) {
+    if (stamps_.size == 0) {
+      stamps_.Resize(kTrkStamps);
+      stamps_.Zero(stream_);
+    }
+    prm.stamps = stamps_.ptr;
+  }
   SG_HIP_CHECK(hipEventRecord(ev_[0], stream_));
   if (n_ > 0)
     for (int r = 0; r < repeats; ++r)
@@ -1110,6 +1157,15 @@ void Tracker::Run(int from, int to, int repeats) {
   SG_HIP_CHECK(hipEventRecord(ev_[1], stream_));
   SG_HIP_CHECK(hipGetLastError());
   ran_ = true;
+}
+
+std::vector<unsigned long long> Tracker::Stamps() {
+  std::vector<unsigned long long> v(kTrkStamps, 0);
+  if (!stamp_on_ || stamps_.size == 0) return v;
+  SG_HIP_CHECK(hipMemcpyAsync(v.data(), stamps_.ptr, kTrkStamps * 8, hipMemcpyDeviceToHost, stream_));
+  SG_HIP_CHECK(hipStreamSynchronize(stream_));
+  stamps_.Zero(stream_);
+  return v;
 }
 
 void Tracker::Results(float* to_xy, int32_t* accepted, int32_t* iterations) {

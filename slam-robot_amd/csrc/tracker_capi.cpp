@@ -97,6 +97,17 @@ int sg_tracker_results(sg_tracker* t, float* to_xy, int32_t* accepted, int32_t* 
   SG_CAPI_END
 }
 
+// Diagnostic (not in the public header): per-phase Newton-loop cycles of k_track_fb (SG_TRK_STAMP=1), summed
+// over the waves since the last call: stage, probes, sums 1, score, sums 2, step, template, other, iterations,
+// waves.
+int sg_tracker_debug_stamps(sg_tracker* t, unsigned long long* out, int32_t n) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(t && out, SG_EINVAL, "null argument");
+  auto v = t->t->Stamps();
+  for (int32_t i = 0; i < n && i < (int32_t)v.size(); ++i) out[i] = v[i];
+  SG_CAPI_END
+}
+
 int sg_tracker_kernel_ms(sg_tracker* t, double* track_ms, double* pyramid_ms) {
   SG_CAPI_BEGIN
   SG_REQUIRE(t, SG_EINVAL, "null handle");

@@ -30,6 +30,10 @@ if [ -n "$R3_DIAG" ]; then
   timeout -k 10 120 python tools/phase_trace.py C2 > gpurun_out/phase_trace_C2_$TAG.log 2>&1 || { echo "trace C2 failed"; tail -5 gpurun_out/phase_trace_C2_$TAG.log; exit 1; }
   tail -25 gpurun_out/phase_trace_C2_$TAG.log
   timeout -k 10 180 python tools/phase_trace.py C5 > gpurun_out/phase_trace_C5_$TAG.log 2>&1 || { echo "trace C5 failed"; tail -5 gpurun_out/phase_trace_C5_$TAG.log; exit 1; }
+  timeout -k 10 120 python tools/tile_stamps.py C2 > gpurun_out/tile_stamps_C2_$TAG.log 2>&1 || { echo "tile stamps failed"; tail -5 gpurun_out/tile_stamps_C2_$TAG.log; exit 1; }
+  cat gpurun_out/tile_stamps_C2_$TAG.log
+  timeout -k 10 120 python tools/tracker_stamps.py 7 > gpurun_out/tracker_stamps_$TAG.log 2>&1 || { echo "tracker stamps failed"; tail -5 gpurun_out/tracker_stamps_$TAG.log; exit 1; }
+  cat gpurun_out/tracker_stamps_$TAG.log
 fi
 SG_HOST_TIMING=1 timeout -k 10 300 python tools/e2e_replay.py gpurun_out/e2e_replay_$TAG.json > gpurun_out/e2e_$TAG.log 2> gpurun_out/e2e_phases_$TAG.log \
   || { echo "replay failed"; tail -20 gpurun_out/e2e_phases_$TAG.log; exit 1; }
