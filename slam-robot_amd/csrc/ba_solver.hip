@@ -4702,12 +4702,12 @@ Dev BaSolver::MakeDev() {
 void BaSolver::Begin(const sg_solver_options& o) {
   SG_REQUIRE(loaded_, SG_EINVAL, "no problem loaded");
   SG_HIP_CHECK(hipSetDevice(dev_.device));
-  {
-    // restart from the current parameter slot: move it to slot 0
+  if (began_) {
+    // restart from the current parameter slot: move it to slot 0 (a fresh load starts in slot 0: no round trip)
     LmState h{};
     SG_HIP_CHECK(hipMemcpyAsync(&h, st_.ptr, sizeof(h), hipMemcpyDeviceToHost, stream_));
     SG_HIP_CHECK(hipStreamSynchronize(stream_));
-    if (began_ && h.cur == 1) {
+    if (h.cur == 1) {
       SG_HIP_CHECK(hipMemcpyAsync(q_.ptr, q_.ptr + 4 * (size_t)F_, 4 * (size_t)F_ * 8, hipMemcpyDeviceToDevice, stream_));
       SG_HIP_CHECK(hipMemcpyAsync(t_.ptr, t_.ptr + 3 * (size_t)F_, 3 * (size_t)F_ * 8, hipMemcpyDeviceToDevice, stream_));
       SG_HIP_CHECK(hipMemcpyAsync(X_.ptr, X_.ptr + 4 * (size_t)P_, 4 * (size_t)P_ * 8, hipMemcpyDeviceToDevice, stream_));
@@ -4715,8 +4715,8 @@ void BaSolver::Begin(const sg_solver_options& o) {
         SG_HIP_CHECK(hipMemcpyAsync(k_.ptr, k_.ptr + 7 * (size_t)ncam_, 7 * (size_t)ncam_ * 8, hipMemcpyDeviceToDevice,
                                     stream_));
     }
-    began_ = true;
   }
+  began_ = true;
   LmState s{};
   s.max_iter = o.max_num_iterations;
   s.max_invalid = o.max_num_consecutive_invalid_steps;
