@@ -3090,7 +3090,7 @@ __device__ __forceinline__ void bs_chain2(const double* __restrict__ Wb, const d
 //   the top one polls at most 256 times, so the time-out path runs deterministically.
 constexpr int kSepSpinMax = 1 << 22;
 constexpr int kSplitMinNT = 13;
-template <bool kStamp>
+template <bool kStamp, int kLa>
 __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_t* panel_jend,
                                                              double* __restrict__ Wg, int32_t* tflag, int nd,
                                                              int flags) {
@@ -3129,9 +3129,11 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
     sh.uflag = -1;
     sh.dflag = -1;
   }
-  // la bit 0: owner look-ahead (flags bit 3); bit 1: readlane factorisation (flags bit 4); bit 2: Dinv mode
-  // (flags bit 5: off-chain columns skip the TRSM)
-  const int la = ((flags & 8) ? 1 : 0) | ((flags & 16) ? 2 : 0) | ((flags & 32) ? 4 : 0);
+  // kLa bit 0: owner look-ahead; bit 1: readlane factorisation; bit 2: Dinv mode (off-chain columns skip the
+  // TRSM).  A template parameter, not a flag: each variant is its own kernel, so the default one carries none
+  // of the others' code (with all three as run-time branches the kernel grew to 93 KB, past the 64 KB
+  // instruction cache, and the C2 factorisation slowed from 69 to 77 us)
+  constexpr int la = kLa;
   bool bad = false, tmo = false;
   const int spin_max = (flags & 4) ? 256 : kSepSpinMax;
   if (bottom && (flags & 4))
@@ -3189,8 +3191,8 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
     }
     if (done) return;
     if (col == 0) {
-      bad |= (flags & 16) ? tile_diag<true>(D0, y0, sh, zp, 0, lane, li, lk)
-                          : tile_diag<false>(D0, y0, sh, zp, 0, lane, li, lk);
+      bad |= (la & 2) ? tile_diag<true>(D0, y0, sh, zp, 0, lane, li, lk)
+                      : tile_diag<false>(D0, y0, sh, zp, 0, lane, li, lk);
       if (la & 4)
         tile_dinv_post(sh, zp, 0, lane, li, lk);
       else
@@ -3724,6 +3726,24 @@ enum KernelId { kKLin = 0, kKCamReduce, kKCamFinal, kKSchur, kKSReduce, kKChol, 
 static const char* kKernelNames[kKNum] = {"linearize", "cam_reduce", "cam_finalize", "schur", "S_reduce",
                                           "cholesky", "point_update", "upd_reduce", "decide"};
 
+// The tiled Cholesky's instantiations: [0] the stamped build of the default (look-ahead), [1 + la] the variants (la bit 0
+// look-ahead, bit 1 readlane factor, bit 2 Dinv; SG_CHOL_LOOKAHEAD / SG_CHOL_FACTOR / SG_CHOL_DINV).
+static const void* const kCholTilesKernels[9] = {
+    (const void*)k_chol_tiles<true, 1>, (const void*)k_chol_tiles<false, 0>, (const void*)k_chol_tiles<false, 1>,
+    (const void*)k_chol_tiles<false, 2>, (const void*)k_chol_tiles<false, 3>, (const void*)k_chol_tiles<false, 4>,
+    (const void*)k_chol_tiles<false, 5>, (const void*)k_chol_tiles<false, 6>, (const void*)k_chol_tiles<false, 7>};
+
+void BaSolver::LaunchCholTiles(bool stamp, int la, dim3 grid, const Dev& d, int flags) {
+  const void* f = stamp ? kCholTilesKernels[0] : kCholTilesKernels[1 + (la & 7)];
+  Dev dd = d;
+  const int32_t* pj = (const int32_t*)work_i_.ptr;
+  double* wg = Wg_.ptr;
+  int32_t* tf = tflag_.ptr;
+  int nd = chol_nd_;
+  void* args[] = {&dd, &pj, &wg, &tf, &nd, &flags};
+  SG_HIP_CHECK(hipLaunchKernel(f, grid, dim3(kTileThreads), args, tile_lds_, stream_));
+}
+
 BaSolver::BaSolver(const sg_device_options& dev) : dev_(dev) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) throw Error(SG_ENODEV, "no HIP device available");
@@ -3742,6 +3762,19 @@ BaSolver::BaSolver(const sg_device_options& dev) : dev_(dev) {
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCholLds));
   SG_HIP_CHECK(hipFuncSetAttribute((const void*)k_cholesky_window<true>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCholLds));
+  {
+    // k_chol_tiles' dynamic LDS (x, z', band ends, staged candidate operands) grows with the map: grant the
+    // most the CU allows beside the kernel's static LDS once, here, so a load never changes the attribute
+    size_t lim = 160 * 1024;
+    for (const void* f : kCholTilesKernels) {
+      hipFuncAttributes fa;
+      SG_HIP_CHECK(hipFuncGetAttributes(&fa, f));
+      lim = std::min(lim, (size_t)160 * 1024 - fa.sharedSizeBytes);
+    }
+    for (const void* f : kCholTilesKernels)
+      SG_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lim));
+    tile_lds_set_ = lim;
+  }
   st_.Resize(1);
   timers_.resize(kKNum);
   for (int i = 0; i < kKNum; ++i) timers_[i].name = kKernelNames[i];
@@ -4338,8 +4371,13 @@ void BaSolver::Load(const sg_problem& p) {
     stager_->Add(Wg_, wz);
     stager_->Add(tflag_, std::vector<int32_t>(2, 0));
     tile_lds_ = (size_t)npanel * 32 * sizeof(double) + (size_t)(3 * npanel + 1) / 2 * sizeof(double);
-    chol_cand_lds_ = F_ <= kCandMax && D_ <= kCandMax && tile_lds_ + CandLds::bytes(F_, D_, n_) <= 100 * 1024;
+    chol_cand_lds_ = F_ <= kCandMax && D_ <= kCandMax && tile_lds_ + CandLds::bytes(F_, D_, n_) <= 100 * 1024 &&
+                     tile_lds_ + CandLds::bytes(F_, D_, n_) <= tile_lds_set_;
     if (chol_cand_lds_) tile_lds_ += CandLds::bytes(F_, D_, n_);
+    if (tile_lds_ > tile_lds_set_) {   // beyond the LDS granted at construction: the one-workgroup kernels
+      chol_tiles_ = false;
+      chol_nd_ = 0;
+    }
   }
   // k_S_reduce work: the band tiles (R <= C) of the frame columns, and per tile the segment tiles covering it
   // (segment order).  A segment tile outside the band is zero (no point couples its rows and columns).
@@ -4422,6 +4460,7 @@ void BaSolver::Load(const sg_problem& p) {
   chunk_scal_.Resize((size_t)std::max(npu_, 1) * kNScal);
   stg.Add(pu_units_, pu_units);
   stg.Flush(s);
+  lap("flush");
   cam_wide_.Resize((size_t)std::max(NB_, 1) * kCamV);
   S_wide_.Resize(nn * nn);
   xchg_cam_.Resize((size_t)NB_ * kCamV + kXNum + nranks());
@@ -4441,12 +4480,10 @@ void BaSolver::Load(const sg_problem& p) {
   }
   stamp_on_ = getenv("SG_STAMP") && getenv("SG_STAMP")[0] == '1';
   if (stamp_on_) stamps_.Resize(64 + 2 * 128 * 16);
+  lap("resize");
   ResetState(s);
-  if (chol_tiles_ && tile_lds_ > tile_lds_set_) {
-    for (const void* f : {(const void*)k_chol_tiles<false>, (const void*)k_chol_tiles<true>})
-      SG_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tile_lds_));
-    tile_lds_set_ = tile_lds_;
-  }
+  lap("reset");
+  // granted once at construction (a later hipFuncSetAttribute on a grown map cost 27 ms in the replay)
   SG_HIP_CHECK(hipStreamSynchronize(s));
   lap("uploads");
   if (host_timing) {
@@ -4804,16 +4841,10 @@ void BaSolver::Iterate(int n) {
                          (const int32_t*)pack_off_.ptr, npanel, Spk_.ptr, 1);
     }
     TimedLaunchBegin(kKChol);
-    if (chol_tiles_ && d.stamps)
-      hipLaunchKernelGGL(k_chol_tiles<true>, dim3(chol_nd_ > 0 ? 2 : 1), dim3(kTileThreads), tile_lds_, stream_, d,
-                         (const int32_t*)work_i_.ptr, Wg_.ptr, tflag_.ptr, chol_nd_,
-                         chol_simdmap_ | (chol_cand_lds_ ? 2 : 0) | (chol_force_tmo_ ? 4 : 0) |
-                         (chol_lookahead_ ? 8 : 0) | (chol_factor_rl_ ? 16 : 0) | (chol_dinv_ ? 32 : 0));
-    else if (chol_tiles_)
-      hipLaunchKernelGGL(k_chol_tiles<false>, dim3(chol_nd_ > 0 ? 2 : 1), dim3(kTileThreads), tile_lds_, stream_, d,
-                         (const int32_t*)work_i_.ptr, Wg_.ptr, tflag_.ptr, chol_nd_,
-                         chol_simdmap_ | (chol_cand_lds_ ? 2 : 0) | (chol_force_tmo_ ? 4 : 0) |
-                         (chol_lookahead_ ? 8 : 0) | (chol_factor_rl_ ? 16 : 0) | (chol_dinv_ ? 32 : 0));
+    if (chol_tiles_)
+      LaunchCholTiles(d.stamps != nullptr, (chol_lookahead_ ? 1 : 0) | (chol_factor_rl_ ? 2 : 0) | (chol_dinv_ ? 4 : 0),
+                      dim3(chol_nd_ > 0 ? 2 : 1), d,
+                      chol_simdmap_ | (chol_cand_lds_ ? 2 : 0) | (chol_force_tmo_ ? 4 : 0));
     else if (chol_window_ && d.stamps)
       hipLaunchKernelGGL(k_cholesky_window<true>, dim3(1), dim3(kCholThreads), kCholLds, stream_, d,
                          (const int32_t*)work_i_.ptr, rdg_.ptr);
