@@ -71,8 +71,9 @@ class BaSolver {
   // owner look-ahead of the tiled Cholesky (k_chol_tiles kLa bit 0; default on: C2 69.9 -> 67.8 us, C5 188.9 ->
   // 183.8 us, r3_v2 chol_ab); SG_CHOL_LOOKAHEAD=0 turns it off
   bool chol_lookahead_ = !(getenv("SG_CHOL_LOOKAHEAD") && atoi(getenv("SG_CHOL_LOOKAHEAD")) == 0);
-  // diagonal-tile factorisation with v_readlane pivot rows (k_chol_tiles flags bit 4): SG_CHOL_FACTOR=1
-  bool chol_factor_rl_ = getenv("SG_CHOL_FACTOR") && atoi(getenv("SG_CHOL_FACTOR")) == 1;
+  // diagonal-tile factorisation: 0 two pivots per LDS broadcast, 1 v_readlane pivot rows, 2 in registers with
+  // MFMA panel updates (tile_factor_mfma); SG_CHOL_FACTOR
+  int chol_factor_ = getenv("SG_CHOL_FACTOR") ? atoi(getenv("SG_CHOL_FACTOR")) : 0;
   // Dinv mode of the tiled Cholesky (k_chol_tiles flags bit 5): SG_CHOL_DINV=1
   bool chol_dinv_ = getenv("SG_CHOL_DINV") && atoi(getenv("SG_CHOL_DINV")) == 1;
   bool pack_force_ = getenv("SG_PACK_S") != nullptr;   // pack/unpack S on one rank too (tests the path)

@@ -2554,6 +2554,112 @@ __device__ __forceinline__ bool tile_factor_rl(const double* D, const double* Yk
   return bad;
 }
 
+// The four 16-lane rows' values of x at this lane's column: g[m] = x at lane li + 16 m (gfx950 permlane swaps,
+// as in sum_rows4: no LDS round trip).
+__device__ __forceinline__ void col_gather4(double x, double (&g)[4]) {
+  const int lo = __double2loint(x), hi = __double2hiint(x);
+  auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);   // [0]: lane l & 31, [1]: (l & 31) + 32
+  auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  auto c = __builtin_amdgcn_permlane16_swap(a[0], a[0], false, false);   // [0]: bit 4 clear, [1]: set
+  auto e = __builtin_amdgcn_permlane16_swap(b[0], b[0], false, false);
+  auto f = __builtin_amdgcn_permlane16_swap(a[1], a[1], false, false);
+  auto h = __builtin_amdgcn_permlane16_swap(b[1], b[1], false, false);
+  g[0] = __hiloint2double(e[0], c[0]);
+  g[1] = __hiloint2double(e[1], c[1]);
+  g[2] = __hiloint2double(h[0], f[0]);
+  g[3] = __hiloint2double(h[1], f[1]);
+}
+
+// The diagonal tile's factorisation in registers, in the MFMA layout it arrives in (no LDS staging, no
+// broadcast per pivot): four panels of four rows.  Panel p: the 4x4 block B of rows / columns 4p..4p+3 comes
+// to every lane by v_readlane and is factored wave-uniformly (B = R^T R); each lane transforms the four panel
+// rows at its column by R^-T (row-wise forward substitution; the rows' values at the column gathered by
+// permlane swaps) and keeps its own row's; the trailing rows then take the panel's rank-4 update as ONE
+// v_mfma_f64_16x16x4f64 (A = B = the new panel register: C -= U_pan^T U_pan).  The identity takes the same row
+// operations (-> Z = U^-T, one more MFMA per panel) and so does the rhs (y[li] on the lanes of column li).
+// In: D (acc layout: D[q] = D[lk + 4q][li], upper triangle meaningful), ys = y[li].  Out: Zt[q] =
+// Z[lk + 4q][li], ys = z[li] = (Z y)[li].  16 pivots = 4 uniform 4-pivot chains and 8 MFMAs, against 8 LDS
+// broadcast rounds in tile_factor.  Returns true on a non-positive pivot.
+__device__ __forceinline__ bool tile_factor_mfma(const f64x4& D, double& ys, f64x4& Zt, int li, int lk) {
+  f64x4 A, E;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    A[q] = (lk + 4 * q <= li) ? D[q] : 0.0;
+    E[q] = (lk + 4 * q == li) ? 1.0 : 0.0;
+  }
+  bool bad = false;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const double x = A[p], ex = E[p];
+    // the 4x4 diagonal block (upper) and the panel's rhs, wave-uniform
+    const double b00 = readlane_d(x, 4 * p), b01 = readlane_d(x, 4 * p + 1), b02 = readlane_d(x, 4 * p + 2),
+                 b03 = readlane_d(x, 4 * p + 3);
+    const double b11 = readlane_d(x, 16 + 4 * p + 1), b12 = readlane_d(x, 16 + 4 * p + 2),
+                 b13 = readlane_d(x, 16 + 4 * p + 3);
+    const double b22 = readlane_d(x, 32 + 4 * p + 2), b23 = readlane_d(x, 32 + 4 * p + 3);
+    const double b33 = readlane_d(x, 48 + 4 * p + 3);
+    const double yo[4] = {readlane_d(ys, 4 * p), readlane_d(ys, 4 * p + 1), readlane_d(ys, 4 * p + 2),
+                          readlane_d(ys, 4 * p + 3)};
+    double g[4], h[4];
+    col_gather4(x, g);
+    col_gather4(ex, h);
+    // B = R^T R (R upper), pivots by rsq + one Newton step as in tile_factor
+    bad |= !(b00 > 0.0);
+    const double i0 = rsq_nr1(b00);
+    const double r01 = b01 * i0, r02 = b02 * i0, r03 = b03 * i0;
+    const double c11 = fma(-r01, r01, b11);
+    bad |= !(c11 > 0.0);
+    const double i1 = rsq_nr1(c11);
+    const double r12 = fma(-r01, r02, b12) * i1, r13 = fma(-r01, r03, b13) * i1;
+    const double c22 = fma(-r12, r12, fma(-r02, r02, b22));
+    bad |= !(c22 > 0.0);
+    const double i2 = rsq_nr1(c22);
+    const double r23 = fma(-r12, r13, fma(-r02, r03, b23)) * i2;
+    const double c33 = fma(-r23, r23, fma(-r13, r13, fma(-r03, r03, b33)));
+    bad |= !(c33 > 0.0);
+    const double i3 = rsq_nr1(c33);
+    // new panel rows = R^-T (old panel rows): forward substitution
+    auto fs = [&](const double (&o)[4], double (&w)[4]) {
+      w[0] = o[0] * i0;
+      w[1] = fma(-r01, w[0], o[1]) * i1;
+      w[2] = fma(-r12, w[1], fma(-r02, w[0], o[2])) * i2;
+      w[3] = fma(-r23, w[2], fma(-r13, w[1], fma(-r03, w[0], o[3]))) * i3;
+    };
+    double gn[4], hn[4], yn[4];
+    fs(g, gn);
+    fs(h, hn);
+    fs(yo, yn);
+    const double gl = lk == 0 ? gn[0] : (lk == 1 ? gn[1] : (lk == 2 ? gn[2] : gn[3]));
+    const double xn = li >= 4 * p + lk ? gl : 0.0;   // row 4p + lk of U at column li (zero left of the diagonal)
+    const double en = lk == 0 ? hn[0] : (lk == 1 ? hn[1] : (lk == 2 ? hn[2] : hn[3]));
+    // rhs: the panel rows replaced, the trailing rows take the panel's column-li entries
+    const double yt = fma(-gn[3], yn[3], fma(-gn[2], yn[2], fma(-gn[1], yn[1], fma(-gn[0], yn[0], ys))));
+    const int dl = li - 4 * p;
+    const double yp = dl == 0 ? yn[0] : (dl == 1 ? yn[1] : (dl == 2 ? yn[2] : yn[3]));
+    ys = dl < 0 ? ys : (dl < 4 ? yp : yt);
+    // trailing rank-4 updates (rows of earlier panels see zero panel entries; row block p is replaced)
+    if (p < 3) A = __builtin_amdgcn_mfma_f64_16x16x4f64(-xn, xn, A, 0, 0, 0);
+    E = __builtin_amdgcn_mfma_f64_16x16x4f64(-xn, en, E, 0, 0, 0);
+    A[p] = xn;
+    E[p] = en;
+  }
+  Zt = E;
+  return bad;
+}
+
+// The owner of the next diagonal, register factorisation (kLa bit 3): D -> Z_K, z_K posted to the LDS ring.
+__device__ __forceinline__ bool tile_diag_mfma(const f64x4& D, double ypart, TileShared& sh, int K, int li,
+                                               int lk) {
+  double ys = sum_rows4(ypart);
+  f64x4 Zt;
+  const bool bad = tile_factor_mfma(D, ys, Zt, li, lk);
+  double* Zs = sh.Zs[K & 3];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) Zs[(lk + 4 * q) * kTLd + li] = Zt[q];
+  if (lk == 0) sh.zK[K & 3][li] = ys;
+  return bad;
+}
+
 // The owner of the next diagonal: D (acc layout) and its rhs partials -> Z, z and Z^T z of tile row K.
 template <bool kRl = false>
 __device__ __forceinline__ bool tile_diag(const f64x4& D, double ypart, TileShared& sh, double* zp, int K,
@@ -2825,8 +2931,9 @@ __device__ __forceinline__ void tile_phase(f64x4 (&acc)[kTB], double& ypart, int
     SG_TSTAMP(10)
     SG_PTRACE(K, 11)
     if (K + 1 < NT)
-      bad |= (la & 2) ? tile_diag<true>(acc[2], ypart, sh, zp, K + 1, lane, li, lk)
-                      : tile_diag<false>(acc[2], ypart, sh, zp, K + 1, lane, li, lk);
+      bad |= (la & 8) ? tile_diag_mfma(acc[2], ypart, sh, K + 1, li, lk)
+             : (la & 2) ? tile_diag<true>(acc[2], ypart, sh, zp, K + 1, lane, li, lk)
+                        : tile_diag<false>(acc[2], ypart, sh, zp, K + 1, lane, li, lk);
     SG_PTRACE(K, 12)
     late = true;
     SG_TSTAMP(11)
@@ -3191,8 +3298,9 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
     }
     if (done) return;
     if (col == 0) {
-      bad |= (la & 2) ? tile_diag<true>(D0, y0, sh, zp, 0, lane, li, lk)
-                      : tile_diag<false>(D0, y0, sh, zp, 0, lane, li, lk);
+      bad |= (la & 8) ? tile_diag_mfma(D0, y0, sh, 0, li, lk)
+             : (la & 2) ? tile_diag<true>(D0, y0, sh, zp, 0, lane, li, lk)
+                        : tile_diag<false>(D0, y0, sh, zp, 0, lane, li, lk);
       if (la & 4)
         tile_dinv_post(sh, zp, 0, lane, li, lk);
       else
@@ -3726,15 +3834,22 @@ enum KernelId { kKLin = 0, kKCamReduce, kKCamFinal, kKSchur, kKSReduce, kKChol, 
 static const char* kKernelNames[kKNum] = {"linearize", "cam_reduce", "cam_finalize", "schur", "S_reduce",
                                           "cholesky", "point_update", "upd_reduce", "decide"};
 
-// The tiled Cholesky's instantiations: [0] the stamped build of the default (look-ahead), [1 + la] the variants (la bit 0
-// look-ahead, bit 1 readlane factor, bit 2 Dinv; SG_CHOL_LOOKAHEAD / SG_CHOL_FACTOR / SG_CHOL_DINV).
-static const void* const kCholTilesKernels[9] = {
+// The tiled Cholesky's instantiations (kLa bit 0 look-ahead, bit 1 readlane factor, bit 2 Dinv, bit 3 register
+// / MFMA factor; SG_CHOL_LOOKAHEAD / SG_CHOL_FACTOR (1 readlane, 2 MFMA) / SG_CHOL_DINV): [0] the stamped build of
+// the default, then the variants in kCholTilesLa's order.
+static constexpr int kCholTilesLa[] = {0, 1, 3, 5, 8, 9};
+static const void* const kCholTilesStamped[] = {(const void*)k_chol_tiles<true, 1>, (const void*)k_chol_tiles<true, 9>};
+static const void* const kCholTilesKernels[] = {
     (const void*)k_chol_tiles<true, 1>, (const void*)k_chol_tiles<false, 0>, (const void*)k_chol_tiles<false, 1>,
-    (const void*)k_chol_tiles<false, 2>, (const void*)k_chol_tiles<false, 3>, (const void*)k_chol_tiles<false, 4>,
-    (const void*)k_chol_tiles<false, 5>, (const void*)k_chol_tiles<false, 6>, (const void*)k_chol_tiles<false, 7>};
+    (const void*)k_chol_tiles<false, 3>, (const void*)k_chol_tiles<false, 5>, (const void*)k_chol_tiles<false, 8>,
+    (const void*)k_chol_tiles<false, 9>};
 
 void BaSolver::LaunchCholTiles(bool stamp, int la, dim3 grid, const Dev& d, int flags) {
-  const void* f = stamp ? kCholTilesKernels[0] : kCholTilesKernels[1 + (la & 7)];
+  int idx = -1;
+  for (int i = 0; i < (int)(sizeof(kCholTilesLa) / sizeof(int)); ++i)
+    if (kCholTilesLa[i] == la) idx = i;
+  SG_REQUIRE(idx >= 0, SG_EINVAL, "this combination of SG_CHOL_* variants is not instantiated");
+  const void* f = stamp ? kCholTilesStamped[(la & 8) ? 1 : 0] : kCholTilesKernels[1 + idx];
   Dev dd = d;
   const int32_t* pj = (const int32_t*)work_i_.ptr;
   double* wg = Wg_.ptr;
@@ -3772,6 +3887,8 @@ BaSolver::BaSolver(const sg_device_options& dev) : dev_(dev) {
       lim = std::min(lim, (size_t)160 * 1024 - fa.sharedSizeBytes);
     }
     for (const void* f : kCholTilesKernels)
+      SG_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lim));
+    for (const void* f : kCholTilesStamped)
       SG_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lim));
     tile_lds_set_ = lim;
   }
@@ -4842,7 +4959,9 @@ void BaSolver::Iterate(int n) {
     }
     TimedLaunchBegin(kKChol);
     if (chol_tiles_)
-      LaunchCholTiles(d.stamps != nullptr, (chol_lookahead_ ? 1 : 0) | (chol_factor_rl_ ? 2 : 0) | (chol_dinv_ ? 4 : 0),
+      LaunchCholTiles(d.stamps != nullptr,
+                      (chol_lookahead_ ? 1 : 0) | (chol_factor_ == 1 ? 2 : 0) | (chol_dinv_ ? 4 : 0) |
+                          (chol_factor_ == 2 ? 8 : 0),
                       dim3(chol_nd_ > 0 ? 2 : 1), d,
                       chol_simdmap_ | (chol_cand_lds_ ? 2 : 0) | (chol_force_tmo_ ? 4 : 0));
     else if (chol_window_ && d.stamps)

@@ -19,10 +19,8 @@ steps = int(sys.argv[1]) if len(sys.argv) > 1 else 40
 VARIANTS = [
     ("base", {"SG_CHOL_LOOKAHEAD": "0", "SG_CHOL_FACTOR": "0", "SG_CHOL_DINV": "0"}),
     ("la", {"SG_CHOL_LOOKAHEAD": "1", "SG_CHOL_FACTOR": "0", "SG_CHOL_DINV": "0"}),
-    ("la+rl", {"SG_CHOL_LOOKAHEAD": "1", "SG_CHOL_FACTOR": "1", "SG_CHOL_DINV": "0"}),
-    ("la+dinv", {"SG_CHOL_LOOKAHEAD": "1", "SG_CHOL_FACTOR": "0", "SG_CHOL_DINV": "1"}),
-    ("la+rl+dinv", {"SG_CHOL_LOOKAHEAD": "1", "SG_CHOL_FACTOR": "1", "SG_CHOL_DINV": "1"}),
-    ("dinv", {"SG_CHOL_LOOKAHEAD": "0", "SG_CHOL_FACTOR": "0", "SG_CHOL_DINV": "1"}),
+    ("mf", {"SG_CHOL_LOOKAHEAD": "0", "SG_CHOL_FACTOR": "2", "SG_CHOL_DINV": "0"}),
+    ("la+mf", {"SG_CHOL_LOOKAHEAD": "1", "SG_CHOL_FACTOR": "2", "SG_CHOL_DINV": "0"}),
 ]
 out = {}
 for cfg in ("C2", "C5"):

@@ -28,7 +28,6 @@ o = d.get("other_workload") or {}
 if o: print("C5 %.1f it/s kernels %s" % (o["value"], o["kernel_ms_per_iter"]))
 PY
 if [ -n "$R3_DIAG" ]; then
-  [ -x tools/factor_bench2 ] && timeout -k 10 60 tools/factor_bench2 > gpurun_out/factor_bench2_$TAG.log 2>&1 && cat gpurun_out/factor_bench2_$TAG.log
   timeout -k 10 300 python tools/chol_ab.py 40 > gpurun_out/chol_ab_$TAG.log 2>&1 || { echo "chol_ab failed"; tail -20 gpurun_out/chol_ab_$TAG.log; exit 1; }
   cat gpurun_out/chol_ab_$TAG.log
   timeout -k 10 120 python tools/phase_trace.py C2 > gpurun_out/phase_trace_C2_$TAG.log 2>&1 || { echo "trace C2 failed"; tail -5 gpurun_out/phase_trace_C2_$TAG.log; exit 1; }
