@@ -55,6 +55,17 @@ class BaSolver {
  private:
   sg_device_options dev_;
   hipStream_t stream_ = nullptr;
+  // Schur elimination beside the camera reduction: after the first linearisation of a solve (the Jacobi scale
+  // of the camera columns is fixed from then on, slam.cpp's Ceres LM: jacobi_scaling), k_schur depends only on
+  // k_linearize, so it can run on side_ while k_cam_reduce, the camera all-reduce and k_cam_finalize run on
+  // stream_; k_S_reduce waits for both.  Measured slower on one GPU (C2 6042 -> 5690 it/s, C5 equal:
+  // tools/overlap_ab.sh, profiles/r3_v6_schur_overlap_ab.log): a k_schur workgroup's 140 KB of LDS leaves no
+  // room for the camera kernels on its CU, and the cross-stream event waits cost more than the overlap hides.
+  // Opt-in (SG_SCHUR_OVERLAP=1) for multi-GPU runs, where it hides the camera all-reduce behind k_schur.
+  hipStream_t side_ = nullptr;
+  hipEvent_t ev_lin_ = nullptr, ev_schur_ = nullptr;
+  bool overlap_ok_ = getenv("SG_SCHUR_OVERLAP") && atoi(getenv("SG_SCHUR_OVERLAP")) == 1;
+  bool need_seq_ = true;   // the next iteration is the first of a solve (it computes the camera scale)
   std::unique_ptr<Comm> comm_;
   bool loaded_ = false;
   bool began_ = false;
@@ -164,6 +175,8 @@ class BaSolver {
   void TimedLaunchBegin(int id);
   void LaunchCholTiles(bool stamp, int la, dim3 grid, const Dev& d, int flags);
   void TimedLaunchEnd(int id);
+  void TimedLaunchBegin(int id, hipStream_t s);
+  void TimedLaunchEnd(int id, hipStream_t s);
   void CollectTimes();
   Dev MakeDev();
   void AllReduceSum(double* buf, size_t n);

@@ -3867,6 +3867,9 @@ BaSolver::BaSolver(const sg_device_options& dev) : dev_(dev) {
              "sg_device_options.precision: only 0 (fp64, the reference's arithmetic) is implemented");
   SG_HIP_CHECK(hipSetDevice(dev.device));
   SG_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  SG_HIP_CHECK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+  SG_HIP_CHECK(hipEventCreateWithFlags(&ev_lin_, hipEventDisableTiming));
+  SG_HIP_CHECK(hipEventCreateWithFlags(&ev_schur_, hipEventDisableTiming));
   {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, dev.device) == hipSuccess && prop.multiProcessorCount > 0)
@@ -3900,6 +3903,9 @@ BaSolver::BaSolver(const sg_device_options& dev) : dev_(dev) {
 BaSolver::~BaSolver() {
   for (auto& t : timers_)
     for (auto e : t.ev) (void)hipEventDestroy(e);
+  if (ev_lin_) (void)hipEventDestroy(ev_lin_);
+  if (ev_schur_) (void)hipEventDestroy(ev_schur_);
+  if (side_) (void)hipStreamDestroy(side_);
   if (stream_) (void)hipStreamDestroy(stream_);
 }
 
@@ -4283,7 +4289,10 @@ void BaSolver::Load(const sg_problem& p) {
     // points per segment: one segment per CU (the workgroup's LDS holds one per CU; fewer, longer segments
     // write fewer partial tiles and keep the producer/consumer pipeline full; SG_SCHUR_SEGS: tuning)
     const int ncu = ncu_;
-    const int target = getenv("SG_SCHUR_SEGS") ? std::max(1, atoi(getenv("SG_SCHUR_SEGS"))) : ncu;
+    // (with k_schur beside the camera reduction, one CU per XCD stays free for k_cam_reduce / k_cam_finalize:
+    // a k_schur workgroup's 140 KB of LDS leaves no room for them on its CU)
+    const int target = getenv("SG_SCHUR_SEGS") ? std::max(1, atoi(getenv("SG_SCHUR_SEGS")))
+                                               : (overlap_ok_ ? std::max(1, ncu - 8) : ncu);
     const int maxpts = std::max(16, (P_ + target - 1) / target);
     int cnext = 0;
     for (int i = 0; i < P_;) {
@@ -4894,24 +4903,27 @@ void BaSolver::Begin(const sg_solver_options& o) {
   s.radius = o.initial_trust_region_radius;
   s.decrease_factor = 2.0;
   SG_HIP_CHECK(hipMemcpyAsync(st_.ptr, &s, sizeof(s), hipMemcpyHostToDevice, stream_));
+  need_seq_ = true;   // the first iteration fixes the camera scale: k_schur waits for it
   for (auto& t : timers_) {
     t.total_ms = 0.0;
     t.count = 0;
   }
 }
 
-void BaSolver::TimedLaunchBegin(int id) {
+void BaSolver::TimedLaunchBegin(int id) { TimedLaunchBegin(id, stream_); }
+void BaSolver::TimedLaunchEnd(int id) { TimedLaunchEnd(id, stream_); }
+void BaSolver::TimedLaunchBegin(int id, hipStream_t s) {
   if (!timing_) return;
   hipEvent_t a, b;
   SG_HIP_CHECK(hipEventCreate(&a));
   SG_HIP_CHECK(hipEventCreate(&b));
   timers_[id].ev.push_back(a);
   timers_[id].ev.push_back(b);
-  SG_HIP_CHECK(hipEventRecord(a, stream_));
+  SG_HIP_CHECK(hipEventRecord(a, s));
 }
-void BaSolver::TimedLaunchEnd(int id) {
+void BaSolver::TimedLaunchEnd(int id, hipStream_t s) {
   if (!timing_) return;
-  SG_HIP_CHECK(hipEventRecord(timers_[id].ev.back(), stream_));
+  SG_HIP_CHECK(hipEventRecord(timers_[id].ev.back(), s));
 }
 
 void BaSolver::Iterate(int n) {
@@ -4922,6 +4934,18 @@ void BaSolver::Iterate(int n) {
     TimedLaunchBegin(kKLin);
     hipLaunchKernelGGL(k_linearize, dim3(std::max(nlin_, 1)), dim3(kLinThreads), 0, stream_, d);
     TimedLaunchEnd(kKLin);
+    // k_schur beside the camera reduction (see side_ in ba_solver.h)
+    const bool overlap = overlap_ok_ && !need_seq_ && nk_ == 0;
+    need_seq_ = false;
+    if (overlap) {
+      SG_HIP_CHECK(hipEventRecord(ev_lin_, stream_));
+      SG_HIP_CHECK(hipStreamWaitEvent(side_, ev_lin_, 0));
+      TimedLaunchBegin(kKSchur, side_);
+      hipLaunchKernelGGL(k_schur, dim3(std::max(nseg_, 1)), dim3(kSchurThreads), 0, side_, d);
+      if (nwide_) hipLaunchKernelGGL(k_schur_wide, dim3(nwide_), dim3(kSchurThreads), 0, side_, d);
+      TimedLaunchEnd(kKSchur, side_);
+      SG_HIP_CHECK(hipEventRecord(ev_schur_, side_));
+    }
     TimedLaunchBegin(kKCamReduce);
     const int nv = NB_ * kCamV;
     hipLaunchKernelGGL(k_cam_reduce, dim3(NB_ + 1), dim3(kRedThreads), 0, stream_, d);
@@ -4935,10 +4959,14 @@ void BaSolver::Iterate(int n) {
     TimedLaunchBegin(kKCamFinal);
     hipLaunchKernelGGL(k_cam_finalize, dim3(1), dim3(256), 0, stream_, d);
     TimedLaunchEnd(kKCamFinal);
-    TimedLaunchBegin(kKSchur);
-    hipLaunchKernelGGL(k_schur, dim3(std::max(nseg_, 1)), dim3(kSchurThreads), 0, stream_, d);
-    if (nwide_) hipLaunchKernelGGL(k_schur_wide, dim3(nwide_), dim3(kSchurThreads), 0, stream_, d);
-    TimedLaunchEnd(kKSchur);
+    if (overlap) {
+      SG_HIP_CHECK(hipStreamWaitEvent(stream_, ev_schur_, 0));
+    } else {
+      TimedLaunchBegin(kKSchur);
+      hipLaunchKernelGGL(k_schur, dim3(std::max(nseg_, 1)), dim3(kSchurThreads), 0, stream_, d);
+      if (nwide_) hipLaunchKernelGGL(k_schur_wide, dim3(nwide_), dim3(kSchurThreads), 0, stream_, d);
+      TimedLaunchEnd(kKSchur);
+    }
     TimedLaunchBegin(kKSReduce);
     const int nwv = nstile_ + NB_;
     hipLaunchKernelGGL(k_S_reduce, dim3(std::max(nwv, 1)), dim3(256), 0, stream_, d);
