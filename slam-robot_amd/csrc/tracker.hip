@@ -431,70 +431,16 @@ __device__ __forceinline__ int track_pass(const TrackCtx& c, const LevelDev* __r
                                           float* py, int* iters, float* tile) {
   const double s = 1. / (1 << (lvls - 1));
   float x = (float)(*px * s), y = (float)(*py * s);
-  // The templates of the pass's first kPre levels (GetPatches, hessian.h:175-183) fetched together up front:
-  // every level's samples are in flight at once instead of one dependent round of image loads per level (the
-  // per-level fetch was a third of the Newton loop's cycles, tools/tracker_stamps.py).  Same samples, sums
-  // and order as get_patch_ctx, so the same bits.  Deeper levels (a 6-level retry) fetch in the loop.
-  constexpr int kPre = 4;
-  float pv[kPre][NK], pmean[kPre], psq[kPre];
-  c.ts->mark(7);
-  {
-    float txs = sx, tys = sy;
-#pragma unroll
-    for (int l = 0; l < kPre; ++l) {
-      const LevelDev Ls = src[l < lvls ? l : 0];   // (past lvls: level 0 again, unused)
-      Geo g;
-      make_geo(txs, tys, c.W, Ls.w, Ls.h, g);
-#pragma unroll
-      for (int k = 0; k < NK; ++k) pv[l][k] = k < c.nk ? sample(Ls.img, Ls.w, g, c.pi[k], c.pj[k]) : 0.f;
-      txs = l + 1 < lvls ? (float)(txs * 0.5) : sx;
-      tys = l + 1 < lvls ? (float)(tys * 0.5) : sy;
-    }
-#pragma unroll
-    for (int l = 0; l < kPre; ++l) {
-      float sm = 0.f, q = 0.f;
-#pragma unroll
-      for (int k = 0; k < NK; ++k) {
-        sm += pv[l][k];
-        q += pv[l][k] * pv[l][k];
-      }
-      if (l < lvls) {
-        sm = wave_tree_sum(sm);
-        q = wave_tree_sum(q);
-      }
-      pmean[l] = sm / c.len;
-      psq[l] = q / c.len;
-    }
-  }
   for (int i = lvls - 1; i >= 0; --i) {
-    const LevelDev Ld = dst[i];
-    Tmpl tp;
-#pragma unroll
-    for (int k = 0; k < kNP; ++k) tp.v[k] = 0.f;
-    if (i < kPre) {
-#pragma unroll
-      for (int k = 0; k < NK; ++k) {
-        float v = pv[0][k];
-#pragma unroll
-        for (int l = 1; l < kPre; ++l) v = i == l ? pv[l][k] : v;
-        tp.v[k] = v;
-      }
-      float mn = pmean[0], sq = psq[0];
-#pragma unroll
-      for (int l = 1; l < kPre; ++l) {
-        mn = i == l ? pmean[l] : mn;
-        sq = i == l ? psq[l] : sq;
-      }
-      tp.mean = mn;
-      tp.sumsq = sq;
-    } else {
-      float tx = sx, ty = sy;
-      for (int k = 0; k < i; ++k) {
-        tx = (float)(tx * 0.5);
-        ty = (float)(ty * 0.5);
-      }
-      get_patch_ctx<NK>(c, src[i], tx, ty, tp);
+    float tx = sx, ty = sy;
+    for (int k = 0; k < i; ++k) {
+      tx = (float)(tx * 0.5);
+      ty = (float)(ty * 0.5);
     }
+    const LevelDev Ls = src[i], Ld = dst[i];
+    Tmpl tp;
+    c.ts->mark(7);
+    get_patch_ctx<NK>(c, Ls, tx, ty, tp);
     c.ts->mark(6);
     const float margin = 0.01f;
     int it = 0;
