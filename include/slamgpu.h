@@ -204,8 +204,8 @@ int sg_ba_comm_init_local(sg_ba* h, sg_comm_group* g, int32_t rank);
 int sg_ba_load(sg_ba* h, const sg_problem* p);
 /* Pre-size the handle's device and pinned staging buffers for problems of up to max_frames frames, max_points
  * points and max_obs observations (a map's high-water mark), so loads that follow do not reallocate on their
- * critical path.  Reallocation drops the loaded problem (load again).  The Slam facade does this itself from
- * the map's size whenever the map outgrows its last reservation. */
+ * critical path.  Reallocation drops the loaded problem (load again).  The Slam facade does this itself,
+ * reserving twice the largest window problem it has loaded. */
 int sg_ba_reserve(sg_ba* h, int32_t max_frames, int32_t max_points, int32_t max_obs);
 /* Incremental problem update (replaces the per-call rebuild of slam.cpp:257-414): a
  * load whose structure equals the previous load's (frames, cameras, freedom flags, observation incidence,

@@ -12,6 +12,7 @@
 #include "ba_kernels.h"
 #include "common.h"
 #include "dbuf.h"
+#include "hostmirror.h"
 
 namespace sg {
 
@@ -63,6 +64,12 @@ class BaSolver {
   // room for the camera kernels on its CU, and the cross-stream event waits cost more than the overlap hides.
   // Opt-in (SG_SCHUR_OVERLAP=1) for multi-GPU runs, where it hides the camera all-reduce behind k_schur.
   hipStream_t side_ = nullptr;
+  HostMirror mb_;   // mapped mailbox: [0, 1 KB) the LM state read back, then the solution download
+  void ReadState(LmState* h);   // LmState via mb_ (a kernel writes it: no copy engine), stream synchronised
+  void WaitStream(hipStream_t s);   // spin-wait for the stream's work (see ba_solver.hip)
+  hipEvent_t ev_wait_ = nullptr;
+  hipEvent_t dev_marks_[4] = {nullptr, nullptr, nullptr, nullptr};   // SG_HOST_TIMING: device times in Load
+  void DevMark(hipStream_t s, int i);
   hipEvent_t ev_lin_ = nullptr, ev_schur_ = nullptr;
   bool overlap_ok_ = getenv("SG_SCHUR_OVERLAP") && atoi(getenv("SG_SCHUR_OVERLAP")) == 1;
   bool need_seq_ = true;   // the next iteration is the first of a solve (it computes the camera scale)

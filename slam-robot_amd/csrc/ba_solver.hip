@@ -46,6 +46,13 @@ namespace sg {
 // small device helpers
 
 
+// Word copy (8-byte words, grid-stride) between device and mapped host memory.
+__global__ __launch_bounds__(256) void k_copy_u64(const unsigned long long* __restrict__ src,
+                                                  unsigned long long* __restrict__ dst, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
@@ -3903,6 +3910,7 @@ BaSolver::BaSolver(const sg_device_options& dev) : dev_(dev) {
 BaSolver::~BaSolver() {
   for (auto& t : timers_)
     for (auto e : t.ev) (void)hipEventDestroy(e);
+  if (ev_wait_) (void)hipEventDestroy(ev_wait_);
   if (ev_lin_) (void)hipEventDestroy(ev_lin_);
   if (ev_schur_) (void)hipEventDestroy(ev_schur_);
   if (side_) (void)hipStreamDestroy(side_);
@@ -4121,10 +4129,14 @@ void BaSolver::Load(const sg_problem& p) {
   stg.Add(obs_frame_, obs_frame);
   stg.Add(obs_fixed_, obs_fixed);
   stg.Add(obs_meta_, obs_meta.empty() ? std::vector<int32_t>{0} : obs_meta);
+  if (host_timing) DevMark(s, 0);
   stg.Flush(s);
   {
     auto dup = [&](double* base, size_t half) {   // candidate slot = current slot
-      if (half) SG_HIP_CHECK(hipMemcpyAsync(base + half, base, half * sizeof(double), hipMemcpyDeviceToDevice, s));
+      if (half)   // a kernel, not a copy-engine hipMemcpyAsync (see hostmirror.h)
+        hipLaunchKernelGGL(k_copy_u64, dim3((unsigned)std::min<size_t>(256, (half + 255) / 256)), dim3(256), 0, s,
+                           reinterpret_cast<const unsigned long long*>(base),
+                           reinterpret_cast<unsigned long long*>(base + half), half);
     };
     dup(k_.ptr, 7 * (size_t)ncam_);
     dup(q_.ptr, 4 * (size_t)F_);
@@ -4585,7 +4597,9 @@ void BaSolver::Load(const sg_problem& p) {
   S_slab_.Resize(std::max(s_off, 1));
   chunk_scal_.Resize((size_t)std::max(npu_, 1) * kNScal);
   stg.Add(pu_units_, pu_units);
+  if (host_timing) DevMark(s, 1);
   stg.Flush(s);
+  if (host_timing) DevMark(s, 2);
   lap("flush");
   cam_wide_.Resize((size_t)std::max(NB_, 1) * kCamV);
   S_wide_.Resize(nn * nn);
@@ -4608,10 +4622,19 @@ void BaSolver::Load(const sg_problem& p) {
   if (stamp_on_) stamps_.Resize(64 + 2 * 128 * 16);
   lap("resize");
   ResetState(s);
+  if (host_timing) DevMark(s, 3);
   lap("reset");
-  // granted once at construction (a later hipFuncSetAttribute on a grown map cost 27 ms in the replay)
-  SG_HIP_CHECK(hipStreamSynchronize(s));
+  WaitStream(s);
   lap("uploads");
+  if (host_timing) {
+    float a = 0, b = 0, c = 0;
+    (void)hipEventElapsedTime(&a, dev_marks_[0], dev_marks_[1]);
+    (void)hipEventElapsedTime(&b, dev_marks_[1], dev_marks_[2]);
+    (void)hipEventElapsedTime(&c, dev_marks_[2], dev_marks_[3]);
+    char buf[128];
+    snprintf(buf, sizeof(buf), " [device: batch1..batch2 %.2f, scatter2 %.2f, reset %.2f]", a, b, c);
+    lap_log += buf;
+  }
   if (host_timing) {
     char buf[64];
     snprintf(buf, sizeof(buf), " (staged %.2f MB)", stg.staged_bytes() / 1e6);
@@ -4705,19 +4728,49 @@ void BaSolver::SaveStructure(const sg_problem& p) {
 }
 
 // LM state and accumulators a fresh solve starts from (zeroed on every Load)
-void BaSolver::ResetState(hipStream_t s) {
-  st_.Zero(s);          // LmState: slot 0 current, nothing pending (evaluate() may run before begin())
-  lin_scal_.Zero(s);
-  seg_fail_.Zero(s);
-  cam_wide_.Zero(s);
-  S_wide_.Zero(s);
-  rhs_.Zero(s);
-  chunk_scal_.Zero(s);
-  S_.Zero(s);
-  {
-    static const double kConst01[2] = {0.0, 1.0};   // k_chol_tiles: padding entries of the last tile
-    SG_HIP_CHECK(hipMemcpyAsync(S_.ptr + S_.size - 2, kConst01, sizeof(kConst01), hipMemcpyHostToDevice, s));
+// Zero a few device buffers and set the tiled Cholesky's {0, 1} constants (after S and its rhs) in one launch
+// (hipMemsetAsync / a pageable hipMemcpyAsync would go through the copy engine).
+struct ZeroList {
+  double* p[8];
+  size_t n[8];   // doubles
+  double* c01;   // two doubles: {0, 1}
+};
+__global__ __launch_bounds__(256) void k_reset_buffers(ZeroList z) {
+  for (int b = 0; b < 8; ++b) {
+    double* p = z.p[b];
+    const size_t n = z.n[b];
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+      p[i] = 0.0;
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && z.c01) {
+    z.c01[0] = 0.0;
+    z.c01[1] = 1.0;
+  }
+}
+
+void BaSolver::ResetState(hipStream_t s) {
+  // LmState (slot 0 current, nothing pending: evaluate() may run before begin()), the accumulators, S; one
+  // launch, no copy engine (hostmirror.h)
+  ZeroList z{};
+  auto put = [&](int i, void* ptr, size_t bytes) {
+    z.p[i] = static_cast<double*>(ptr);
+    z.n[i] = ptr ? bytes / 8 : 0;
+  };
+  static_assert(sizeof(LmState) % 8 == 0, "LmState is zeroed in 8-byte words");
+  put(0, st_.ptr, st_.size * sizeof(LmState));
+  put(1, lin_scal_.ptr, lin_scal_.size * sizeof(double));
+  put(2, seg_fail_.ptr, seg_fail_.size * sizeof(*seg_fail_.ptr));
+  put(3, cam_wide_.ptr, cam_wide_.size * sizeof(double));
+  put(4, S_wide_.ptr, S_wide_.size * sizeof(double));
+  put(5, rhs_.ptr, rhs_.size * sizeof(double));
+  put(6, chunk_scal_.ptr, chunk_scal_.size * sizeof(double));
+  put(7, S_.ptr, (S_.size - 2) * sizeof(double));
+  z.c01 = S_.ptr + S_.size - 2;   // k_chol_tiles: padding entries of the last tile
+  size_t mx = 0;
+  for (int i = 0; i < 8; ++i) mx = std::max(mx, z.n[i]);
+  const unsigned g = (unsigned)std::min<size_t>(512, std::max<size_t>(1, (mx + 255) / 256));
+  hipLaunchKernelGGL(k_reset_buffers, dim3(g), dim3(256), 0, s, z);
+  SG_HIP_CHECK(hipGetLastError());
   if (stamp_on_) stamps_.Zero(s);
 }
 
@@ -4862,14 +4915,68 @@ Dev BaSolver::MakeDev() {
   return d;
 }
 
+// The LM state handed over as a kernel argument (no host buffer, no copy engine: see hostmirror.h).
+__global__ void k_set_state(LmState s, LmState* st) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) *st = s;
+}
+
+// The current parameter slot's poses, points and intrinsics into the mapped download buffer
+// [q 4F | t 3F | X 4P | k 7 ncam] (the slot is read on the device: no state round trip first).
+__global__ __launch_bounds__(256) void k_download(const double* __restrict__ q, const double* __restrict__ t,
+                                                  const double* __restrict__ X, const double* __restrict__ k,
+                                                  const LmState* st, int F, int P, int ncam, double* __restrict__ out) {
+  const int cur = st->cur;
+  const size_t nq = 4 * (size_t)F, nt = 3 * (size_t)F, nx = 4 * (size_t)P, nk = 7 * (size_t)ncam;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nq + nt + nx + nk;
+       i += (size_t)gridDim.x * blockDim.x) {
+    double v;
+    if (i < nq) v = q[nq * cur + i];
+    else if (i < nq + nt) v = t[nt * cur + (i - nq)];
+    else if (i < nq + nt + nx) v = X[nx * cur + (i - nq - nt)];
+    else v = k[nk * cur + (i - nq - nt - nx)];
+    out[i] = v;
+  }
+}
+
+// Wait for stream s by spinning on an event query.  hipStreamSynchronize's blocking wait returned 13-28 ms
+// late in a few percent of the main.cpp replay's loads, all of whose work had been three small kernels
+// (tools/e2e_replay.py, profiles/r3_v8_*); the solver's waits are short (a load, an LM batch), so the host
+// spins on them, falling back to the blocking wait after SG_SPIN_MS (default 200 ms).
+void BaSolver::WaitStream(hipStream_t s) {
+  static const double spin_ms = getenv("SG_SPIN_MS") ? atof(getenv("SG_SPIN_MS")) : 200.0;
+  if (!ev_wait_) SG_HIP_CHECK(hipEventCreateWithFlags(&ev_wait_, hipEventDisableTiming));
+  SG_HIP_CHECK(hipEventRecord(ev_wait_, s));
+  const auto t0 = std::chrono::steady_clock::now();
+  while (true) {
+    const hipError_t e = hipEventQuery(ev_wait_);
+    if (e == hipSuccess) return;
+    if (e != hipErrorNotReady) SG_HIP_CHECK(e);
+    if (std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() > spin_ms) break;
+  }
+  SG_HIP_CHECK(hipEventSynchronize(ev_wait_));
+}
+
+void BaSolver::DevMark(hipStream_t s, int i) {
+  if (!dev_marks_[i]) SG_HIP_CHECK(hipEventCreate(&dev_marks_[i]));
+  SG_HIP_CHECK(hipEventRecord(dev_marks_[i], s));
+}
+
+void BaSolver::ReadState(LmState* h) {
+  static_assert(sizeof(LmState) % 8 == 0, "LmState is copied in 8-byte words");
+  mb_.Reserve(1024);
+  hipLaunchKernelGGL(k_copy_u64, dim3(1), dim3(64), 0, stream_, reinterpret_cast<const unsigned long long*>(st_.ptr),
+                     reinterpret_cast<unsigned long long*>(mb_.d), sizeof(LmState) / 8);
+  WaitStream(stream_);
+  std::memcpy(h, mb_.h, sizeof(LmState));
+}
+
 void BaSolver::Begin(const sg_solver_options& o) {
   SG_REQUIRE(loaded_, SG_EINVAL, "no problem loaded");
   SG_HIP_CHECK(hipSetDevice(dev_.device));
   if (began_) {
     // restart from the current parameter slot: move it to slot 0 (a fresh load starts in slot 0: no round trip)
     LmState h{};
-    SG_HIP_CHECK(hipMemcpyAsync(&h, st_.ptr, sizeof(h), hipMemcpyDeviceToHost, stream_));
-    SG_HIP_CHECK(hipStreamSynchronize(stream_));
+    ReadState(&h);
     if (h.cur == 1) {
       SG_HIP_CHECK(hipMemcpyAsync(q_.ptr, q_.ptr + 4 * (size_t)F_, 4 * (size_t)F_ * 8, hipMemcpyDeviceToDevice, stream_));
       SG_HIP_CHECK(hipMemcpyAsync(t_.ptr, t_.ptr + 3 * (size_t)F_, 3 * (size_t)F_ * 8, hipMemcpyDeviceToDevice, stream_));
@@ -4902,7 +5009,7 @@ void BaSolver::Begin(const sg_solver_options& o) {
   s.termination = s.done ? SG_FUNCTION_TOLERANCE : SG_NO_CONVERGENCE;
   s.radius = o.initial_trust_region_radius;
   s.decrease_factor = 2.0;
-  SG_HIP_CHECK(hipMemcpyAsync(st_.ptr, &s, sizeof(s), hipMemcpyHostToDevice, stream_));
+  hipLaunchKernelGGL(k_set_state, dim3(1), dim3(64), 0, stream_, s, st_.ptr);
   need_seq_ = true;   // the first iteration fixes the camera scale: k_schur waits for it
   for (auto& t : timers_) {
     t.total_ms = 0.0;
@@ -5052,8 +5159,7 @@ void BaSolver::Sync() { SG_HIP_CHECK(hipStreamSynchronize(stream_)); }
 
 void BaSolver::Summary(sg_solver_summary* s) {
   LmState h{};
-  SG_HIP_CHECK(hipMemcpyAsync(&h, st_.ptr, sizeof(h), hipMemcpyDeviceToHost, stream_));
-  SG_HIP_CHECK(hipStreamSynchronize(stream_));
+  ReadState(&h);
   std::memset(s, 0, sizeof(*s));
   s->num_iterations = h.pushed;
   s->num_successful_steps = h.n_succ;
@@ -5070,25 +5176,23 @@ void BaSolver::Summary(sg_solver_summary* s) {
 }
 
 void BaSolver::Download(sg_problem* p) {
-  LmState h{};
-  SG_HIP_CHECK(hipMemcpyAsync(&h, st_.ptr, sizeof(h), hipMemcpyDeviceToHost, stream_));
-  SG_HIP_CHECK(hipStreamSynchronize(stream_));
-  std::vector<double> q(4 * (size_t)F_), t(3 * (size_t)F_), X(4 * (size_t)P_);
-  SG_HIP_CHECK(hipMemcpyAsync(q.data(), q_.ptr + 4 * (size_t)F_ * h.cur, q.size() * 8, hipMemcpyDeviceToHost, stream_));
-  SG_HIP_CHECK(hipMemcpyAsync(t.data(), t_.ptr + 3 * (size_t)F_ * h.cur, t.size() * 8, hipMemcpyDeviceToHost, stream_));
-  SG_HIP_CHECK(hipMemcpyAsync(X.data(), X_.ptr + 4 * (size_t)P_ * h.cur, X.size() * 8, hipMemcpyDeviceToHost, stream_));
-  SG_HIP_CHECK(hipStreamSynchronize(stream_));
-  std::copy(q.begin(), q.end(), p->q);
-  std::copy(t.begin(), t.end(), p->t);
-  if (nk_) {
-    SG_HIP_CHECK(hipMemcpyAsync(p->k, k_.ptr + 7 * (size_t)ncam_ * h.cur, 7 * (size_t)ncam_ * 8,
-                                hipMemcpyDeviceToHost, stream_));
-    SG_HIP_CHECK(hipStreamSynchronize(stream_));
-  }
+  const size_t nq = 4 * (size_t)F_, nt = 3 * (size_t)F_, nx = 4 * (size_t)P_, nk = nk_ ? 7 * (size_t)ncam_ : 0;
+  const size_t tot = nq + nt + nx + nk;
+  mb_.Reserve(1024 + 8 * std::max<size_t>(tot, 1));
+  double* out_d = reinterpret_cast<double*>(mb_.d + 1024);
+  const double* out = reinterpret_cast<const double*>(mb_.h + 1024);
+  const unsigned g = (unsigned)std::min<size_t>(1024, std::max<size_t>(1, (tot + 255) / 256));
+  hipLaunchKernelGGL(k_download, dim3(g), dim3(256), 0, stream_, q_.ptr, t_.ptr, X_.ptr, nk ? k_.ptr : q_.ptr,
+                     (const LmState*)st_.ptr, F_, P_, nk ? ncam_ : 0, out_d);
+  WaitStream(stream_);
+  std::copy(out, out + nq, p->q);
+  std::copy(out + nq, out + nq + nt, p->t);
+  const double* X = out + nq + nt;
   for (int i = 0; i < P_; ++i) {
     const int pt = point_perm_[i];
     for (int a = 0; a < 4; ++a) p->X[4 * pt + a] = X[4 * i + a];
   }
+  if (nk) std::copy(out + nq + nt + nx, out + tot, p->k);
 }
 
 void BaSolver::Solve(const sg_solver_options& o, sg_problem* p, sg_solver_summary* s) {
@@ -5100,8 +5204,7 @@ void BaSolver::Solve(const sg_solver_options& o, sg_problem* p, sg_solver_summar
   while (true) {
     Iterate(batch);
     launched += batch;
-    SG_HIP_CHECK(hipMemcpyAsync(&h, st_.ptr, sizeof(h), hipMemcpyDeviceToHost, stream_));
-    SG_HIP_CHECK(hipStreamSynchronize(stream_));
+    ReadState(&h);
     if (h.done) break;
     SG_REQUIRE(launched < cap, SG_EDEVICE, "LM loop did not terminate on the device");
   }

@@ -3,8 +3,10 @@
 // A full sg_ba_load uploads some forty index lists and value arrays.  Issued one hipMemcpyAsync each from
 // pageable vectors, every copy is staged synchronously by the runtime, which dominated the load of the small
 // problems main.cpp solves every frame (SolveFrames(2, 5): tools/e2e_replay.py).  The Stager packs them into
-// one pinned host buffer (16-byte aligned pieces), copies it with one hipMemcpyAsync into a device staging
-// buffer and scatters the pieces to their buffers with one kernel launch.
+// one pinned, device-mapped host buffer (16-byte aligned pieces) and one kernel launch reads the pieces
+// straight from host memory into their device buffers (zero-copy): no copy engine on the load's path.  (A
+// hipMemcpyAsync into a device staging buffer went through the SDMA engine, whose copies stalled 13-28 ms in
+// about one load in six of the main.cpp replay; HSA_ENABLE_SDMA=0 removed most of those stalls.)
 #ifndef SG_STAGER_H_
 #define SG_STAGER_H_
 
@@ -52,7 +54,7 @@ class Stager {
   // pinned allocation (milliseconds for tens of MB) on the load's critical path.
   bool ReserveBytes(size_t bytes) {
     if (bytes > cap_) Grow(bytes);
-    return dev_.Reserve(bytes);
+    return false;   // (no device buffer: the scatter reads host memory)
   }
   size_t staged_bytes() const { return last_bytes_; }
 
@@ -83,25 +85,21 @@ class Stager {
     max_bytes_ = 0;
   }
 
-  // One pinned copy of this batch's region and one scatter launch on stream s.  The batch's pinned region
-  // is not rewritten before the next load's Clear() waits for the copy.
+  // One scatter launch on stream s reading this batch's pieces from the mapped pinned buffer.  The batch's
+  // region is not rewritten before the next load's Clear() waits for the launch.
   void Flush(hipStream_t s) {
     if (pieces_.empty()) return;
-    const size_t tbl = used_;
     const size_t tbytes = pieces_.size() * sizeof(StagePiece);
     const size_t tbl_off = Reserve(tbytes);
     std::memcpy(host_ + tbl_off, pieces_.data(), tbytes);
-    (void)tbl;
-    dev_.Resize(used_);   // (reserved: no reallocation; a reallocation would synchronise the device first)
-    SG_HIP_CHECK(hipMemcpyAsync(dev_.ptr + batch0_, host_ + batch0_, used_ - batch0_, hipMemcpyHostToDevice, s));
     if (!copied_) SG_HIP_CHECK(hipEventCreateWithFlags(&copied_, hipEventDisableTiming));
-    SG_HIP_CHECK(hipEventRecord(copied_, s));
-    pending_ = true;
     last_bytes_ += used_ - batch0_;
     const unsigned gx = (unsigned)std::min<size_t>(64, std::max<size_t>(1, (max_bytes_ / 16 + 255) / 256));
     hipLaunchKernelGGL(k_stage_scatter, dim3(gx, (unsigned)pieces_.size()), dim3(256), 0, s,
-                       reinterpret_cast<const StagePiece*>(dev_.ptr + tbl_off), dev_.ptr);
+                       reinterpret_cast<const StagePiece*>(hdev_ + tbl_off), hdev_);
     SG_HIP_CHECK(hipGetLastError());
+    SG_HIP_CHECK(hipEventRecord(copied_, s));
+    pending_ = true;
     pieces_.clear();
     batch0_ = (used_ + 15) & ~(size_t)15;
     used_ = batch0_;
@@ -131,21 +129,24 @@ class Stager {
     WaitCopy();
     const size_t ncap = (std::max<size_t>(want, 8u << 20) + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);
     unsigned char* nh = nullptr;
-    SG_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&nh), ncap, hipHostMallocDefault));
+    SG_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&nh), ncap, hipHostMallocMapped));
+    void* dp = nullptr;
+    SG_HIP_CHECK(hipHostGetDevicePointer(&dp, nh, 0));
     if (host_) {
       std::memcpy(nh, host_, used_);
       (void)hipHostFree(host_);
     }
     host_ = nh;
+    hdev_ = static_cast<unsigned char*>(dp);
     cap_ = ncap;
   }
 
-  unsigned char* host_ = nullptr;
+  unsigned char* host_ = nullptr;   // pinned, mapped into the device's address space
+  unsigned char* hdev_ = nullptr;   // its device-side address
   size_t cap_ = 0, used_ = 0, batch0_ = 0, max_bytes_ = 0, last_bytes_ = 0;
-  hipEvent_t copied_ = nullptr;
+  hipEvent_t copied_ = nullptr;     // the last scatter launch (it reads host_)
   bool pending_ = false;
   std::vector<StagePiece> pieces_;
-  DBuf<unsigned char> dev_;
 };
 
 }  // namespace sg
