@@ -200,6 +200,12 @@ typedef struct sg_comm_group sg_comm_group;
 int sg_comm_group_create(sg_comm_group** out, int32_t nranks);
 void sg_comm_group_destroy(sg_comm_group* g);
 int sg_ba_comm_init_local(sg_ba* h, sg_comm_group* g, int32_t rank);
+/* Host-callback communicator: one process per rank over any host collective (gloo, MPI).  Each of the solver's
+ * all-reduces copies its device buffer to host memory, calls fn(buf, n, op, user) (op 0 = sum, 1 = max; return
+ * 0 on success, nonzero fails the call with SG_ECOMM) and copies the result back — the call sequence of the
+ * RCCL communicator (sg_ba_comm_init), with the transport on the host.  Must precede sg_ba_load. */
+typedef int (*sg_allreduce_fn)(double* buf, long long n, int32_t op, void* user);
+int sg_ba_comm_init_host(sg_ba* h, int32_t nranks, int32_t rank, sg_allreduce_fn fn, void* user);
 /* Upload a problem (the problem's q/t/X are read now and written back by sg_ba_download). */
 int sg_ba_load(sg_ba* h, const sg_problem* p);
 /* Pre-size the handle's device and pinned staging buffers for problems of up to max_frames frames, max_points

@@ -43,6 +43,7 @@ class BaSolver {
   int KernelWork(double* bytes, double* flops, int max);
   void CommInit(const void* id128, int nranks, int rank);
   void CommInitLocal(std::shared_ptr<struct LocalGroup> g, int rank);   // in-process test group (comm.h)
+  void CommInitHost(int nranks, int rank, int (*fn)(double*, long long, int, void*), void* user);   // comm.h
   static void UniqueId(void* id128);
 
   void Info(sg_ba_info* out) const;

@@ -3935,6 +3935,14 @@ void BaSolver::CommInitLocal(std::shared_ptr<LocalGroup> g, int rank) {
   dev_.rank = rank;
 }
 
+void BaSolver::CommInitHost(int nranks, int rank, int (*fn)(double*, long long, int, void*), void* user) {
+  SG_REQUIRE(!loaded_, SG_EINVAL, "sg_ba_comm_init_host must precede sg_ba_load");
+  SG_HIP_CHECK(hipSetDevice(dev_.device));
+  comm_.reset(new HostComm(nranks, rank, fn, user));
+  dev_.nranks = comm_->nranks();
+  dev_.rank = rank;
+}
+
 int BaSolver::nranks() const { return comm_ ? comm_->nranks() : 1; }
 
 void BaSolver::AllReduceSum(double* buf, size_t n) {

@@ -82,6 +82,13 @@ int sg_ba_comm_init_local(sg_ba* h, sg_comm_group* g, int32_t rank) {
   SG_CAPI_END
 }
 
+int sg_ba_comm_init_host(sg_ba* h, int32_t nranks, int32_t rank, sg_allreduce_fn fn, void* user) {
+  SG_CAPI_BEGIN
+  SG_REQUIRE(h && fn, SG_EINVAL, "null argument");
+  h->solver->CommInitHost(nranks, rank, fn, user);
+  SG_CAPI_END
+}
+
 int sg_ba_load(sg_ba* h, const sg_problem* p) {
   SG_CAPI_BEGIN
   SG_REQUIRE(h && p, SG_EINVAL, "null argument");

@@ -49,6 +49,27 @@ class RcclComm : public Comm {
   void* comm_ = nullptr;  // ncclComm_t
 };
 
+// A host transport behind a callback (sg_ba_comm_init_host): every all-reduce copies the device buffer to
+// pinned host memory, calls fn(buf, n, op, user) (op 0 sum, 1 max; nonzero return = failure) and copies the
+// result back, in the solver's stream order.  The same call sequence as RcclComm, so a multi-process run over
+// any host collective (gloo in tests/test_multirank_gloo_gpu.py, MPI) exercises the solver's exchange path
+// with one process per rank on a one-GPU box.
+typedef int (*HostAllReduceFn)(double* buf, long long n, int op, void* user);
+class HostComm : public Comm {
+ public:
+  HostComm(int nranks, int rank, HostAllReduceFn fn, void* user);
+  ~HostComm() override;
+  void AllReduceSum(double* buf, size_t n, hipStream_t s) override { Reduce(buf, n, s, 0); }
+  void AllReduceMax(double* buf, size_t n, hipStream_t s) override { Reduce(buf, n, s, 1); }
+
+ private:
+  void Reduce(double* buf, size_t n, hipStream_t s, int op);
+  HostAllReduceFn fn_;
+  void* user_;
+  double* host_ = nullptr;
+  size_t cap_ = 0;
+};
+
 // Shared state of an in-process group (sg_comm_group in the C-ABI).
 struct LocalGroup {
   static constexpr int kMaxRanks = 8;

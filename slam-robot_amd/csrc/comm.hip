@@ -46,6 +46,37 @@ void RcclComm::AllReduceMax(double* buf, size_t n, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// Host-callback transport
+
+HostComm::HostComm(int nranks, int rank, HostAllReduceFn fn, void* user) : fn_(fn), user_(user) {
+  SG_REQUIRE(fn && nranks >= 1 && rank >= 0 && rank < nranks, SG_EINVAL, "bad host communicator");
+  nranks_ = nranks;
+  rank_ = rank;
+}
+
+HostComm::~HostComm() {
+  if (host_) (void)hipHostFree(host_);
+}
+
+void HostComm::Reduce(double* buf, size_t n, hipStream_t s, int op) {
+  if (n == 0) return;
+  if (n > cap_) {
+    SG_HIP_CHECK(hipStreamSynchronize(s));
+    if (host_) (void)hipHostFree(host_);
+    host_ = nullptr;
+    cap_ = 0;
+    SG_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&host_), n * sizeof(double), hipHostMallocDefault));
+    cap_ = n;
+  }
+  SG_HIP_CHECK(hipMemcpyAsync(host_, buf, n * sizeof(double), hipMemcpyDeviceToHost, s));
+  SG_HIP_CHECK(hipStreamSynchronize(s));
+  const int rc = fn_(host_, (long long)n, op, user_);
+  if (rc != 0) throw Error(SG_ECOMM, "host communicator callback failed (" + std::to_string(rc) + ")");
+  SG_HIP_CHECK(hipMemcpyAsync(buf, host_, n * sizeof(double), hipMemcpyHostToDevice, s));
+  SG_HIP_CHECK(hipStreamSynchronize(s));   // host_ is reused by the next all-reduce
+}
+
+// ------------------------------------------------------------------------------------------------
 // In-process group
 
 void LocalGroup::Barrier() {

@@ -108,6 +108,23 @@ class BundleAdjuster:
         """Join an in-process communicator group (one device, one host thread per rank; tests)."""
         check(self.lib.sg_ba_comm_init_local(self.h, group.h, rank), "sg_ba_comm_init_local")
 
+    def comm_init_host(self, nranks: int, rank: int, allreduce):
+        """Join a host-transport communicator (sg_ba_comm_init_host): allreduce(array, op) receives each of the
+        solver's all-reduce buffers as a float64 numpy view of pinned host memory (op "sum" or "max") and
+        reduces it in place across the ranks (e.g. torch.distributed over gloo, one process per rank)."""
+        import numpy as np
+        from .capi import ALLREDUCE_FN
+
+        def cb(buf, n, op, user):
+            try:
+                allreduce(np.ctypeslib.as_array(buf, shape=(int(n),)), "max" if op == 1 else "sum")
+                return 0
+            except Exception:   # noqa: BLE001 - reported to the solver as SG_ECOMM
+                return 1
+        self._allreduce_cb = ALLREDUCE_FN(cb)   # kept alive as long as the handle
+        check(self.lib.sg_ba_comm_init_host(self.h, nranks, rank, C.cast(self._allreduce_cb, C.c_void_p), None),
+              "sg_ba_comm_init_host")
+
     @staticmethod
     def unique_id() -> bytes:
         lib = load_library()

@@ -235,6 +235,9 @@ class SgFrontendStats(C.Structure):
         return {n: getattr(self, n) for n, _ in self._fields_}
 
 
+# sg_allreduce_fn: int (*)(double* buf, long long n, int32_t op, void* user)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_longlong, C.c_int32, C.c_void_p)
+
 SYMBOLS = {
     "sg_version": (C.c_char_p, []),
     "sg_last_error": (C.c_char_p, []),
@@ -254,6 +257,7 @@ SYMBOLS = {
     "sg_comm_group_create": (C.c_int, [C.POINTER(C.c_void_p), C.c_int32]),
     "sg_comm_group_destroy": (None, [C.c_void_p]),
     "sg_ba_comm_init_local": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32]),
+    "sg_ba_comm_init_host": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p]),
     "sg_ba_load": (C.c_int, [C.c_void_p, C.POINTER(SgProblem)]),
     "sg_ba_reserve": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32]),
     "sg_ba_load_counts": (C.c_int, [C.c_void_p, _ip, _ip]),

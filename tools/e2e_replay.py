@@ -66,6 +66,7 @@ def merge(mm, sel, F):
 slam = ba.Slam(device=0)
 stats = {"2/5": [], "10/20": []}
 t_all = time.perf_counter()
+t_last = t_all   # when the last call into the library returned (gap_ms: host-only time before a SolveFrames)
 for F in range(F0, NF + 1):
     mm, sel = view(F)
     calls = [("2/5", 2, 5)]
@@ -77,15 +78,18 @@ for F in range(F0, NF + 1):
         ok = slam.SolveFrames(mm, ns, npres, 2.0)
         wall = 1e3 * (time.perf_counter() - t0)
         ph = slam.last_phase_ms()
-        ph.update(wall=wall, iterations=slam.iterations() - it0, ok=bool(ok), frame=F)
+        ph.update(wall=wall, iterations=slam.iterations() - it0, ok=bool(ok), frame=F,
+                  gap_ms=1e3 * (t0 - t_last))
         stats[name].append(ph)
         if ok:
             slam.ReprojectMap(mm)
             slam.Clean(mm, 2.0)
+        t_last = time.perf_counter()
     slam.ApplyEpipolarConstraint(mm)
     slam.ReprojectMap(mm)
     slam.Normalize(mm)
     slam.ReprojectMap(mm)
+    t_last = time.perf_counter()
     merge(mm, sel, F)
 t_all = time.perf_counter() - t_all
 
@@ -110,6 +114,12 @@ for name, rows in stats.items():
     if rows:
         crit["median_load_ms_%s" % name] = float(np.median([r["load"] for r in rows]))
         crit["median_solve_ms_%s" % name] = float(np.median([r["solve"] for r in rows]))
+# host-only time before each call (view / merge of the growing map) against its load: device idle gaps
+gaps = np.array([r["gap_ms"] for r in later]) if later else np.zeros(0)
+loads = np.array([r["load"] for r in later]) if later else np.zeros(0)
+if len(gaps) > 2:
+    crit["gap_ms_median"] = float(np.median(gaps))
+    crit["gap_ms_of_loads_over_5ms"] = [round(float(g), 2) for g, l in zip(gaps, loads) if l > 5]
 summary["criteria"] = crit
 print("criteria:", json.dumps(crit))
 print("load counts (full, values):", slam.load_counts())
