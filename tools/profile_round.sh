@@ -6,6 +6,8 @@
 #   profiles/<tag>_kernel_stats_<workload>.csv   rocprofv3 kernel statistics
 #   profiles/<tag>_pmc_traffic_<workload>.json   HBM bytes per launch (tools/pmc_traffic.py)
 # bench.py's traffic fields read the newest *_pmc_traffic_<workload>.json.  Usage: profile_round.sh <tag> [workloads]
+# On a gpurun box only gpurun_out/ comes back: the summaries are written to gpurun_out/prof_<tag>/profiles/ as
+# well; copy them into profiles/ after the call (cp gpurun_out/prof_<tag>/profiles/* profiles/).
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"
 TAG=${1:?tag}
@@ -20,7 +22,8 @@ for W in $WLS; do
     -- python3 "$R/bench.py" --only "$W" --steps 20 --warmup 5 > "$OUT/kt_$W.json" 2> "$OUT/kt_$W.log" \
     || { echo "kernel trace $W failed"; tail -5 "$OUT/kt_$W.log"; exit 1; }
   f=$(ls "$OUT"/kt_$W/run_kernel_stats.csv "$OUT"/kt_$W/*/run_kernel_stats.csv "$OUT"/kt_$W/*/*/run_kernel_stats.csv 2>/dev/null | head -1)
-  [ -n "$f" ] && cp "$f" "$R/profiles/${TAG}_kernel_stats_${W}.csv"
+  mkdir -p "$OUT/profiles"
+  [ -n "$f" ] && cp "$f" "$R/profiles/${TAG}_kernel_stats_${W}.csv" && cp "$f" "$OUT/profiles/${TAG}_kernel_stats_${W}.csv"
   i=0
   for c in FETCH_SIZE WRITE_SIZE; do
     i=$((i+1))
@@ -32,4 +35,5 @@ for W in $WLS; do
   done
   python3 "$R/tools/pmc_traffic.py" "$OUT/pmc_$W" "$R/profiles/${TAG}_pmc_traffic_${W}.json" \
     "bench.py --only $W --steps 20 --warmup 5" || exit 1
+  cp "$R/profiles/${TAG}_pmc_traffic_${W}.json" "$OUT/profiles/"
 done
