@@ -865,74 +865,135 @@ __device__ __forceinline__ double schur_points(const Dev& d, const LmState* st, 
 // goes to tile c >> 4, lane (c & 15) + 16 k.  A point observed once in every block of its span (obs sorted by
 // block at load) finds its observation at a fixed offset; others read the cell records.  The first and last
 // cell of a point also zero the columns of its tiles 0 .. jhi outside its span.
+// Each thread takes two cells per round and issues the loads of both (the common single-observation cells:
+// J pairs and scales) before either's arithmetic, so two cells' memory latencies overlap (the same
+// arithmetic in the same order as one cell at a time: the same bits).
+struct CellOps {
+  double2 jp[4], jc[6];
+  double4 s4;
+  double sc[6];
+};
+__device__ __forceinline__ void cell_load(const Dev& d, int o, int b, int p, CellOps& c) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) c.jp[i] = jload2(d, o, 7 + i);   // (pairs 0-6: r, Jc)
+#pragma unroll
+  for (int i = 0; i < 6; ++i) c.jc[i] = jload2(d, o, 1 + i);   // (pair 0: r)
+  c.s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) c.sc[i] = d.scale_c[6 * b + i];
+}
+// E_{p,b} += (or =) the observation's G J~c from preloaded operands (load_Jp_scaled / load_Jc_scaled's
+// arithmetic)
+template <typename At>
+__device__ __forceinline__ void cell_apply(const CellOps& c, const double* L, int col0, bool first, At at) {
+  double G[4][2];
+  {
+    const double sp[4] = {c.s4.x, c.s4.y, c.s4.z, c.s4.w};
+    double Jp[8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      Jp[2 * i] = c.jp[i].x * sp[(2 * i) % 4];
+      Jp[2 * i + 1] = c.jp[i].y * sp[(2 * i + 1) % 4];
+    }
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      double g0 = 0.0, g1 = 0.0;
+#pragma unroll
+      for (int m = 0; m <= kk; ++m) {
+        g0 += L[l4(kk, m)] * Jp[m];
+        g1 += L[l4(kk, m)] * Jp[4 + m];
+      }
+      G[kk][0] = g0;
+      G[kk][1] = g1;
+    }
+  }
+  double Jc[12];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    Jc[2 * i] = c.jc[i].x * c.sc[(2 * i) % 6];
+    Jc[2 * i + 1] = c.jc[i].y * c.sc[(2 * i + 1) % 6];
+  }
+  if (first) {
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+      for (int a = 0; a < 6; ++a) at(col0 + a, kk) = G[kk][0] * Jc[a] + G[kk][1] * Jc[6 + a];
+  } else {
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+      for (int a = 0; a < 6; ++a) at(col0 + a, kk) += G[kk][0] * Jc[a] + G[kk][1] * Jc[6 + a];
+  }
+}
 __device__ __forceinline__ void schur_cells(const Dev& d, const SchurBatch& B, int tid, int c0w, const double* Lsh,
                                             const int4* pinf, const int2* pob, const uint8_t* cmap, double* Xb) {
   const int ncell = B.c1 - B.c0;
-  for (int lc = tid; lc < ncell; lc += 64 * kSchurCellWaves) {
-    const int t = cmap[lc];
-    const int4 pi = pinf[t];
-    const int2 po = pob[t];
-    const int b = pi.x + (lc - po.y);
-    const double* L = Lsh + 10 * t;
-    double* xp = Xb + pi.z;
-    const int col0 = 6 * b - c0w;
-    auto at = [&](int col, int k) -> double& { return xp[64 * (col >> 4) + 16 * k + (col & 15)]; };
-    if (b == pi.x)   // left margin: the columns of tiles 0 .. jhi before the span (the consumer reads them all)
-      for (int col = 0; col < col0; ++col)
+  constexpr int kStride = 64 * kSchurCellWaves;
+  for (int lc0 = tid; lc0 < ncell; lc0 += 2 * kStride) {
+    // both cells' table entries and, for single-observation cells, their operand loads first
+    int tc[2], bc[2], oc[2];
+    bool simple[2];
+    CellOps ops[2];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) at(col, k) = 0.0;
-    if (b == pi.x + pi.y - 1)   // right margin: after the span, to the end of tile jhi
-      for (int col = col0 + 6; col < 16 * (pi.w + 1); ++col)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) at(col, k) = 0.0;
-    int o0, k1 = 0, k2 = 0;
-    if (po.x >= 0) {
-      o0 = po.x + (b - pi.x);
-    } else {
-      const int4 ci = d.cells[B.c0 + lc];   // first observation (-1: none), point, (block << 16) | further, offset
-      o0 = ci.x;
-      k1 = ci.w;
-      k2 = ci.w + (ci.z & 0xffff);
-    }
-    if (o0 < 0) {
-#pragma unroll
-      for (int a = 0; a < 6; ++a)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) at(col0 + a, k) = 0.0;
-      continue;
-    }
-    const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[B.p0 + t];
-#pragma unroll 1
-    for (int k = k1 - 1; k < k2; ++k) {
-      const int o = k < k1 ? o0 : d.cell_obs[k];
-      double G[4][2];
-      {
-        double Jp[8];
-        load_Jp_scaled(d, o, s4, Jp);
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-          double g0 = 0.0, g1 = 0.0;
-#pragma unroll
-          for (int m = 0; m <= kk; ++m) {
-            g0 += L[l4(kk, m)] * Jp[m];
-            g1 += L[l4(kk, m)] * Jp[4 + m];
-          }
-          G[kk][0] = g0;
-          G[kk][1] = g1;
+    for (int h = 0; h < 2; ++h) {
+      const int lc = lc0 + h * kStride;
+      simple[h] = false;
+      oc[h] = -1;
+      tc[h] = 0;
+      bc[h] = 0;
+      if (lc < ncell) {
+        const int t = cmap[lc];
+        const int4 pi = pinf[t];
+        const int2 po = pob[t];
+        tc[h] = t;
+        bc[h] = pi.x + (lc - po.y);
+        if (po.x >= 0) {
+          simple[h] = true;
+          oc[h] = po.x + (bc[h] - pi.x);
+          cell_load(d, oc[h], bc[h], B.p0 + t, ops[h]);
         }
       }
-      double Jc[12];
-      load_Jc_scaled(d, o, b, Jc);
-      if (k < k1) {
+    }
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk)
+    for (int h = 0; h < 2; ++h) {
+      const int lc = lc0 + h * kStride;
+      if (lc >= ncell) break;
+      const int t = tc[h];
+      const int4 pi = pinf[t];
+      const int b = bc[h];
+      const double* L = Lsh + 10 * t;
+      double* xp = Xb + pi.z;
+      const int col0 = 6 * b - c0w;
+      auto at = [&](int col, int k) -> double& { return xp[64 * (col >> 4) + 16 * k + (col & 15)]; };
+      if (b == pi.x)   // left margin: the columns of tiles 0 .. jhi before the span (the consumer reads them all)
+        for (int col = 0; col < col0; ++col)
 #pragma unroll
-          for (int a = 0; a < 6; ++a) at(col0 + a, kk) = G[kk][0] * Jc[a] + G[kk][1] * Jc[6 + a];
-      } else {
+          for (int k = 0; k < 4; ++k) at(col, k) = 0.0;
+      if (b == pi.x + pi.y - 1)   // right margin: after the span, to the end of tile jhi
+        for (int col = col0 + 6; col < 16 * (pi.w + 1); ++col)
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk)
+          for (int k = 0; k < 4; ++k) at(col, k) = 0.0;
+      if (simple[h]) {
+        cell_apply(ops[h], L, col0, true, at);
+        continue;
+      }
+      const int4 ci = d.cells[B.c0 + lc];   // first observation (-1: none), point, (block << 16) | further, offset
+      const int o0 = ci.x;
+      const int k1 = ci.w;
+      const int k2 = ci.w + (ci.z & 0xffff);
+      if (o0 < 0) {
 #pragma unroll
-          for (int a = 0; a < 6; ++a) at(col0 + a, kk) += G[kk][0] * Jc[a] + G[kk][1] * Jc[6 + a];
+        for (int a = 0; a < 6; ++a)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) at(col0 + a, k) = 0.0;
+        continue;
+      }
+#pragma unroll 1
+      for (int k = k1 - 1; k < k2; ++k) {
+        const int o = k < k1 ? o0 : d.cell_obs[k];
+        CellOps c;
+        cell_load(d, o, b, B.p0 + t, c);
+        cell_apply(c, L, col0, k < k1, at);
       }
     }
   }
