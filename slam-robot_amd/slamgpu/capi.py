@@ -12,7 +12,8 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC_DIR = os.path.join(os.path.dirname(PKG_DIR), "csrc")
-LIB_PATH = os.path.join(CSRC_DIR, "libslamgpu.so")
+# SG_LIB_PATH: an alternative in-tree build of the same library (A/B of kernel variants: tools/)
+LIB_PATH = os.environ.get("SG_LIB_PATH") or os.path.join(CSRC_DIR, "libslamgpu.so")
 
 SG_OK = 0
 TERMINATION = {0: "NO_CONVERGENCE", 1: "FUNCTION_TOLERANCE", 2: "GRADIENT_TOLERANCE",

@@ -103,3 +103,25 @@ def test_two_processes_gloo_c2_match_one_rank(tmp_path, gpu_lib):
             X[4 * i:4 * i + 4] = x["X"][4 * j:4 * j + 4]
     assert not np.isnan(X).any()
     np.testing.assert_allclose(X, one.X, rtol=0, atol=1e-10)
+
+
+def test_host_communicator_failure_is_reported(gpu_lib):
+    """A transport that fails (the callback returns nonzero) fails the call with SG_ECOMM instead of hanging or
+    solving with a partial sum; the handle stays usable for a one-rank problem afterwards."""
+    from slamgpu import ba
+    from slamgpu.capi import SlamGpuError
+    from slamgpu.scene import make_config
+
+    m = make_config("C1")
+    pa = ba.problem_from_map_frames(m, m.num_frames - 2, m.num_frames, 2.0)
+    shard = ba.shard_problem(pa, 0, 2)
+
+    def broken(arr, op):
+        raise RuntimeError("transport down")
+
+    g = ba.BundleAdjuster()
+    g.comm_init_host(2, 0, broken)
+    with pytest.raises(SlamGpuError) as e:
+        g.load(shard)
+    assert "code -71" in str(e.value) and "communicator" in str(e.value)
+    g.close()
