@@ -62,6 +62,9 @@ def parse():
                          "Hamming matcher (config 4)")
     ap.add_argument("--model-scaling", type=int, default=1,
                     help="N = 1: model C5 strong scaling over 2/4/8 landmark shards from measured kernel times")
+    ap.add_argument("--comm", choices=("rccl", "host"), default="rccl",
+                    help="N > 1: rccl (one GPU per rank, the product path) or host (torch.distributed gloo through "
+                         "sg_ba_comm_init_host: rehearses the multi-rank bench with several ranks on one GPU)")
     ap.add_argument("--only", choices=("all", "C2", "C5", "sweep", "frontend"), default="all",
                     help="profiling runs: one workload alone (its kernels are then the only ones launched)")
     args = ap.parse_args()
@@ -266,12 +269,17 @@ def make_workload(cfg, n_gpus, rank, points_per_gpu, frames):
 class Runner:
     """One BA workload on this rank: its solver (and RCCL communicator for N > 1)."""
 
-    def __init__(self, prob, local, rank, n_gpus, dist):
+    def __init__(self, prob, local, rank, n_gpus, dist, comm="rccl"):
         import torch
         from slamgpu import ba
         self.prob, self.dist, self.local, self.rank, self.n = prob, dist, local, rank, n_gpus
+        self.tdev = f"cuda:{local}" if comm == "rccl" else "cpu"   # gloo reduces host tensors
         self.solver = ba.BundleAdjuster(device=local)
-        if n_gpus > 1:
+        if n_gpus > 1 and comm == "host":
+            def allreduce(arr, op):
+                dist.all_reduce(torch.from_numpy(arr), op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+            self.solver.comm_init_host(n_gpus, rank, allreduce)
+        elif n_gpus > 1:
             uid = ba.BundleAdjuster.unique_id() if rank == 0 else bytes(128)
             t = torch.tensor(list(uid), dtype=torch.uint8, device=f"cuda:{local}")
             dist.broadcast(t, 0)
@@ -287,7 +295,7 @@ class Runner:
         if self.dist is None:
             return x
         import torch
-        e = torch.tensor([x], dtype=torch.float64, device=f"cuda:{self.local}")
+        e = torch.tensor([x], dtype=torch.float64, device=self.tdev)
         self.dist.all_reduce(e, op=self.dist.ReduceOp.MAX)
         return float(e.item())
 
@@ -391,7 +399,7 @@ def kernel_report(res, steps, n_text, workload):
 
 def run_workload(cfg, args, n_gpus, rank, local, dist, steps, warmup):
     full, prob, desc = make_workload(cfg, n_gpus, rank, args.points, args.frames)
-    r = Runner(prob, local, rank, n_gpus, dist)
+    r = Runner(prob, local, rank, n_gpus, dist, args.comm)
     res = r.timed(steps, warmup)
     info = r.solver.info()
     start = r.solve_from_start()
@@ -400,7 +408,7 @@ def run_workload(cfg, args, n_gpus, rank, local, dist, steps, warmup):
     if dist is not None:
         import torch
         v = torch.tensor([prob.num_points, prob.num_obs, info["num_pairs"]], dtype=torch.float64,
-                         device=f"cuda:{local}")
+                         device=r.tdev)
         allv = [torch.zeros_like(v) for _ in range(n_gpus)]
         dist.all_gather(allv, v)
         rows = [[int(x) for x in t.cpu().tolist()] for t in allv]
@@ -499,12 +507,14 @@ def main():
         print(json.dumps({"only": args.only, "result": out}), flush=True)
         return
 
+    if args.comm == "host":   # rehearsal: several ranks may share the box's GPUs
+        local = local % max(1, torch.cuda.device_count())
     dist = None
     if ws > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=ws)
+        dist.init_process_group("nccl" if args.comm == "rccl" else "gloo", rank=rank, world_size=ws)
     n_gpus = ws
     strong = args.config == "C5"
 
@@ -566,8 +576,10 @@ def main():
         "config": {"workload": desc, "keyframes": full.num_frames, "landmarks": full.num_points,
                    "observations": full.num_obs, "landmarks_per_gpu": prob.num_points,
                    "observations_per_gpu": prob.num_obs, "free_frames": int(full.frame_rot_free.sum()),
-                   "parallelism": "landmark-shard x%d (RCCL all-reduce of the camera system)" % n_gpus
-                   if n_gpus > 1 else "single GPU"},
+                   "parallelism": ("landmark-shard x%d (RCCL all-reduce of the camera system)" % n_gpus
+                                   if args.comm == "rccl" else
+                                   "landmark-shard x%d ranks over a host transport (gloo; rehearsal, not a "
+                                   "multi-GPU measurement)" % n_gpus) if n_gpus > 1 else "single GPU"},
         "accepted_frac": res["accepted"] / args.steps,
         "timed_regime": "every LM iteration linearizes (sg_solver_options.always_linearize; SURVEY.md 8d unit)",
         "lm_regime": res["lm_regime"],
