@@ -95,6 +95,9 @@ class BaSolver {
   int chol_factor_ = getenv("SG_CHOL_FACTOR") ? atoi(getenv("SG_CHOL_FACTOR")) : 0;
   // Dinv mode of the tiled Cholesky (k_chol_tiles flags bit 5): SG_CHOL_DINV=1
   bool chol_dinv_ = getenv("SG_CHOL_DINV") && atoi(getenv("SG_CHOL_DINV")) == 1;
+  // dataflow phase sync of the tiled Cholesky (k_chol_tiles kLa bit 4: per-row counters instead of a barrier
+  // per tile row; needs the look-ahead): SG_CHOL_DATAFLOW=1
+  bool chol_dataflow_ = getenv("SG_CHOL_DATAFLOW") && atoi(getenv("SG_CHOL_DATAFLOW")) == 1;
   bool pack_force_ = getenv("SG_PACK_S") != nullptr;   // pack/unpack S on one rank too (tests the path)
   size_t npack_ = 0;                                      // band of S + rhs, doubles (all-reduce size)
   bool stamp_on_ = false;

@@ -2447,6 +2447,8 @@ struct TileShared {
   int tmo;                     // a hand-off wait hit its spin limit (kCTimeout)
   int uflag;                   // look-ahead: the last phase whose owner has posted U_{K,K+1} (Ur[K & 1][0])
   int dflag;                   // Dinv mode: the last phase whose D_K^-1 and z'_K are posted (Dv, zp)
+  int uposted;                 // dataflow mode: U tiles posted so far (all rows, monotonic)
+  int zflag;                   // dataflow mode: the last K whose Z_K and z_K are posted
   double Dv[16 * kTLd];        // Dinv mode: D_K^-1 = Z_K^T Z_K, row-major
   int simd[kTB];               // SIMD of each wave
   double Id[16 * kTLd];        // the identity (the factor's augmented columns)
@@ -2960,6 +2962,11 @@ __device__ __forceinline__ void tile_phase(f64x4 (&acc)[kTB], double& ypart, int
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&sh.uflag, K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
+    if ((la & 16) && !(la & 4)) {
+      // dataflow mode: this column's U_{K,J} is in the ring (counted; the next phase waits for the whole row)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) __hip_atomic_fetch_add(&sh.uposted, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     const double* zk = sh.zK[K & 3];
 #pragma unroll
     for (int q = 0; q < 4; ++q) ypart = fma(-U[q], zk[lk + 4 * q], ypart);
@@ -2998,10 +3005,15 @@ __device__ __forceinline__ void tile_phase(f64x4 (&acc)[kTB], double& ypart, int
     }
     SG_TSTAMP(10)
     SG_PTRACE(K, 11)
-    if (K + 1 < NT)
+    if (K + 1 < NT) {
       bad |= (la & 8) ? tile_diag_mfma(acc[2], ypart, sh, K + 1, li, lk)
              : (la & 2) ? tile_diag<true>(acc[2], ypart, sh, zp, K + 1, lane, li, lk)
                         : tile_diag<false>(acc[2], ypart, sh, zp, K + 1, lane, li, lk);
+      if (la & 16) {   // dataflow mode: Z_{K+1}, z_{K+1} posted
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_store(&sh.zflag, K + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
     SG_PTRACE(K, 12)
     late = true;
     SG_TSTAMP(11)
@@ -3303,6 +3315,8 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
     sh.tmo = 0;
     sh.uflag = -1;
     sh.dflag = -1;
+    sh.uposted = 0;
+    sh.zflag = 0;   // Z_0 is posted before the first barrier
   }
   // kLa bit 0: owner look-ahead; bit 1: readlane factorisation; bit 2: Dinv mode (off-chain columns skip the
   // TRSM).  A template parameter, not a flag: each variant is its own kernel, so the default one carries none
@@ -3379,8 +3393,26 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
     SG_TSTAMP(0)
     __syncthreads();
     SG_TSTAMP(1)
+    // Dataflow mode (kLa bit 4): no barrier between phases.  Phase K needs row K-1's U tiles (all of them: the
+    // trailing updates) and Z_K / z_K (the TRSM); each wave waits for exactly those (a monotonic count of posted
+    // U tiles against the running total of row sizes, and the Z flag), so the next owner starts its TRSM the
+    // moment Z_K is posted instead of at a barrier that also waits for every trailing update.  Ring safety: a
+    // wave that has seen all of row K-1 posted knows every wave has finished reading row K-2 (the U ring is two
+    // deep) and has passed phase K-2 (the Z ring is four deep).  Bounded waits (kCTimeout on expiry).
+    int uexp = 0;
+    auto df_wait = [&](int K) {
+      uexp += max(0, tend[K - 1] - K);   // row K-1's U tiles: columns K .. tend[K-1]-1
+      int spin = 0;
+      while ((__hip_atomic_load(&sh.uposted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < uexp ||
+              __hip_atomic_load(&sh.zflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < K) &&
+             ++spin < kLaSpinMax)
+        __builtin_amdgcn_s_sleep(0);
+      tmo |= spin >= kLaSpinMax;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    };
 #pragma nounroll
     for (int K = 0; K < NTf; ++K) {
+      if ((la & 16) && K >= 1) df_wait(K);
       if (nd > 0 && !bottom && K == m - 1) {
         // relaxed polls, one acquire (an acquiring poll would invalidate the cache on every round)
         int spin = 0;
@@ -3397,12 +3429,21 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
       // the owner of the next diagonal (now late) is on the critical path until the barrier: it rotates after
       if (!late) tile_rotate(acc);
       SG_PTRACE(K, wave)
-      lds_barrier();
+      if (!(la & 16)) lds_barrier();
       if (late) tile_rotate(acc);
       SG_TSTAMP(3)
     }
     if (bottom) {
       // row nd-1's updates of the separator columns (slots of phase nd), then the hand-off
+      if (la & 16) {   // row nd-1 complete (no Z_nd: the bottom does not factor the separator)
+        uexp += max(0, tend[nd - 1] - nd);
+        int spin = 0;
+        while (__hip_atomic_load(&sh.uposted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < uexp &&
+               ++spin < kLaSpinMax)
+          __builtin_amdgcn_s_sleep(0);
+        tmo |= spin >= kLaSpinMax;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      }
       tile_final(acc, J, late, la, sh, Wb, tend, nd, lane, li, lk);
       sep_write(acc, ypart, J, nd, NT, m, sepb, sepy, li, lk);
     }
@@ -3905,19 +3946,20 @@ static const char* kKernelNames[kKNum] = {"linearize", "cam_reduce", "cam_finali
 // The tiled Cholesky's instantiations (kLa bit 0 look-ahead, bit 1 readlane factor, bit 2 Dinv, bit 3 register
 // / MFMA factor; SG_CHOL_LOOKAHEAD / SG_CHOL_FACTOR (1 readlane, 2 MFMA) / SG_CHOL_DINV): [0] the stamped build of
 // the default, then the variants in kCholTilesLa's order.
-static constexpr int kCholTilesLa[] = {0, 1, 3, 5, 8, 9};
-static const void* const kCholTilesStamped[] = {(const void*)k_chol_tiles<true, 1>, (const void*)k_chol_tiles<true, 9>};
+static constexpr int kCholTilesLa[] = {0, 1, 3, 5, 8, 9, 17};
+static const void* const kCholTilesStamped[] = {(const void*)k_chol_tiles<true, 1>, (const void*)k_chol_tiles<true, 9>,
+                                                (const void*)k_chol_tiles<true, 17>};
 static const void* const kCholTilesKernels[] = {
     (const void*)k_chol_tiles<true, 1>, (const void*)k_chol_tiles<false, 0>, (const void*)k_chol_tiles<false, 1>,
     (const void*)k_chol_tiles<false, 3>, (const void*)k_chol_tiles<false, 5>, (const void*)k_chol_tiles<false, 8>,
-    (const void*)k_chol_tiles<false, 9>};
+    (const void*)k_chol_tiles<false, 9>, (const void*)k_chol_tiles<false, 17>};
 
 void BaSolver::LaunchCholTiles(bool stamp, int la, dim3 grid, const Dev& d, int flags) {
   int idx = -1;
   for (int i = 0; i < (int)(sizeof(kCholTilesLa) / sizeof(int)); ++i)
     if (kCholTilesLa[i] == la) idx = i;
   SG_REQUIRE(idx >= 0, SG_EINVAL, "this combination of SG_CHOL_* variants is not instantiated");
-  const void* f = stamp ? kCholTilesStamped[(la & 8) ? 1 : 0] : kCholTilesKernels[1 + idx];
+  const void* f = stamp ? kCholTilesStamped[(la & 16) ? 2 : (la & 8) ? 1 : 0] : kCholTilesKernels[1 + idx];
   Dev dd = d;
   const int32_t* pj = (const int32_t*)work_i_.ptr;
   double* wg = Wg_.ptr;
@@ -5165,7 +5207,7 @@ void BaSolver::Iterate(int n) {
     if (chol_tiles_)
       LaunchCholTiles(d.stamps != nullptr,
                       (chol_lookahead_ ? 1 : 0) | (chol_factor_ == 1 ? 2 : 0) | (chol_dinv_ ? 4 : 0) |
-                          (chol_factor_ == 2 ? 8 : 0),
+                          (chol_factor_ == 2 ? 8 : 0) | (chol_dataflow_ ? 16 : 0),
                       dim3(chol_nd_ > 0 ? 2 : 1), d,
                       chol_simdmap_ | (chol_cand_lds_ ? 2 : 0) | (chol_force_tmo_ ? 4 : 0));
     else if (chol_window_ && d.stamps)

@@ -17,10 +17,9 @@ from slamgpu.scene import make_config  # noqa: E402
 
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 40
 VARIANTS = [
-    ("base", {"SG_CHOL_LOOKAHEAD": "0", "SG_CHOL_FACTOR": "0", "SG_CHOL_DINV": "0"}),
-    ("la", {"SG_CHOL_LOOKAHEAD": "1", "SG_CHOL_FACTOR": "0", "SG_CHOL_DINV": "0"}),
-    ("mf", {"SG_CHOL_LOOKAHEAD": "0", "SG_CHOL_FACTOR": "2", "SG_CHOL_DINV": "0"}),
-    ("la+mf", {"SG_CHOL_LOOKAHEAD": "1", "SG_CHOL_FACTOR": "2", "SG_CHOL_DINV": "0"}),
+    ("la", {"SG_CHOL_LOOKAHEAD": "1", "SG_CHOL_FACTOR": "0", "SG_CHOL_DINV": "0", "SG_CHOL_DATAFLOW": "0"}),
+    ("la+df", {"SG_CHOL_LOOKAHEAD": "1", "SG_CHOL_FACTOR": "0", "SG_CHOL_DINV": "0", "SG_CHOL_DATAFLOW": "1"}),
+    ("base", {"SG_CHOL_LOOKAHEAD": "0", "SG_CHOL_FACTOR": "0", "SG_CHOL_DINV": "0", "SG_CHOL_DATAFLOW": "0"}),
 ]
 out = {}
 for cfg in ("C2", "C5"):
