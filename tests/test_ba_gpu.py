@@ -481,8 +481,8 @@ def test_cholesky_handoff_timeout_is_reported(gpu_lib, monkeypatch):
 
 
 @pytest.mark.parametrize("env", [{"SG_CHOL_LOOKAHEAD": "0"}, {"SG_CHOL_FACTOR": "1"}, {"SG_CHOL_FACTOR": "2"},
-                                 {"SG_CHOL_DINV": "1"}, {"SG_SCHUR_OVERLAP": "1"}],
-                         ids=["no-lookahead", "readlane-factor", "mfma-factor", "dinv", "schur-overlap"])
+                                 {"SG_CHOL_DINV": "1"}, {"SG_CHOL_DATAFLOW": "1"}, {"SG_SCHUR_OVERLAP": "1"}],
+                         ids=["no-lookahead", "readlane-factor", "mfma-factor", "dinv", "dataflow", "schur-overlap"])
 def test_solver_variants_match_default(gpu_lib, monkeypatch, env):
     """The measured-and-not-default variants stay correct: the tiled Cholesky without the
     owner look-ahead, with v_readlane pivot rows, with the register / MFMA-panel diagonal factorisation, in
