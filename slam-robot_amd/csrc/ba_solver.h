@@ -69,6 +69,11 @@ class BaSolver {
   void ReadState(LmState* h);   // LmState via mb_ (a kernel writes it: no copy engine), stream synchronised
   void WaitStream(hipStream_t s);   // spin-wait for the stream's work (see ba_solver.hip)
   hipEvent_t ev_wait_ = nullptr;
+  // graph mode (SG_GRAPH=1): the captured LM iteration (ba_solver.hip, Iterate)
+  bool graph_ok_ = getenv("SG_GRAPH") && atoi(getenv("SG_GRAPH")) == 1;
+  hipGraphExec_t iter_exec_ = nullptr;
+  void DropGraph();
+  void EnqueueIterations(int n);
   hipEvent_t dev_marks_[4] = {nullptr, nullptr, nullptr, nullptr};   // SG_HOST_TIMING: device times in Load
   void DevMark(hipStream_t s, int i);
   hipEvent_t ev_lin_ = nullptr, ev_schur_ = nullptr;

@@ -4011,6 +4011,7 @@ BaSolver::BaSolver(const sg_device_options& dev) : dev_(dev) {
 }
 
 BaSolver::~BaSolver() {
+  DropGraph();
   for (auto& t : timers_)
     for (auto e : t.ev) (void)hipEventDestroy(e);
   if (ev_wait_) (void)hipEventDestroy(ev_wait_);
@@ -4060,6 +4061,7 @@ __global__ __launch_bounds__(256) void k_fill_obs_pnt(const int32_t* __restrict_
 }
 
 void BaSolver::Load(const sg_problem& p) {
+  DropGraph();   // the captured iteration holds this load's device pointers and sizes
   static const bool host_timing = getenv("SG_HOST_TIMING") != nullptr;   // development aid: phase times
   auto lt0 = std::chrono::steady_clock::now();
   std::string lap_log;
@@ -4763,6 +4765,7 @@ void BaSolver::Load(const sg_problem& p) {
 }
 
 void BaSolver::Reserve(int F, int P, int M) {
+  DropGraph();
   SG_REQUIRE(F >= 0 && P >= 0 && M >= 0, SG_EINVAL, "negative reservation");
   SG_HIP_CHECK(hipSetDevice(dev_.device));
   const size_t f = std::max(F, 1), pp = std::max(P, 1), m = std::max(M, 1);
@@ -5147,6 +5150,34 @@ void BaSolver::TimedLaunchEnd(int id, hipStream_t s) {
 void BaSolver::Iterate(int n) {
   SG_REQUIRE(loaded_, SG_EINVAL, "no problem loaded");
   SG_HIP_CHECK(hipSetDevice(dev_.device));
+  // Graph mode (SG_GRAPH=1): one LM iteration's chain captured once per load into a hipGraph and replayed;
+  // the kernels' arguments (device pointers, sizes, variant flags) are fixed between loads.  One rank, no
+  // per-kernel timing, no stamps, no side stream.
+  const bool graphable = graph_ok_ && !timing_ && !stamp_on_ && !(comm_ && comm_->nranks() > 1) && !pack_force_ &&
+                         nk_ == 0 && !overlap_ok_;
+  if (graphable && n > 0) {
+    if (!iter_exec_) {
+      hipGraph_t g = nullptr;
+      SG_HIP_CHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+      EnqueueIterations(1);
+      SG_HIP_CHECK(hipStreamEndCapture(stream_, &g));
+      const hipError_t e = hipGraphInstantiate(&iter_exec_, g, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(g);
+      SG_HIP_CHECK(e);
+    }
+    for (int it = 0; it < n; ++it) SG_HIP_CHECK(hipGraphLaunch(iter_exec_, stream_));
+    need_seq_ = false;
+    return;
+  }
+  EnqueueIterations(n);
+}
+
+void BaSolver::DropGraph() {
+  if (iter_exec_) (void)hipGraphExecDestroy(iter_exec_);
+  iter_exec_ = nullptr;
+}
+
+void BaSolver::EnqueueIterations(int n) {
   Dev d = MakeDev();
   for (int it = 0; it < n; ++it) {
     TimedLaunchBegin(kKLin);
