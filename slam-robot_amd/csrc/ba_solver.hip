@@ -550,6 +550,10 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d) {
     e1 = d.fd_boff[b0 + 1];
   }
   const int dd0 = tid < d.D ? tid : 0;
+  // thread 0 runs the minimizer bookkeeping on a register copy of LmState (loaded beside the prefetches, written
+  // back once): no chain of dependent global round trips through st->
+  LmState s0;
+  if (tid == 0) s0 = *st;
   const int fa0 = d.D > 0 ? d.fd_a[dd0] : 0, fb0 = d.D > 0 ? d.fd_b[dd0] : 0;
   // read once, before thread 0 updates them below (no other thread re-reads LmState flags afterwards)
   const int cur = st->cur;
@@ -665,52 +669,53 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d) {
       double gmax = gm;
       for (int r = 0; r < d.nranks; ++r) gmax = fmax(gmax, xs[kXNum + r]);
       if (first) {
-        st->fixed_cost = xs[kXFixed];
+        s0.fixed_cost = xs[kXFixed];
         if (xs[kXFixedFail] > 0.0) {
-          st->done = 1; st->ok = 0; st->termination = SG_DID_NOT_RUN;
+          s0.done = 1; s0.ok = 0; s0.termination = SG_DID_NOT_RUN;
         } else if (xs[kXFail] > 0.0) {
-          st->done = 1; st->ok = 0; st->termination = SG_NUMERICAL_FAILURE;
+          s0.done = 1; s0.ok = 0; s0.termination = SG_NUMERICAL_FAILURE;
         } else {
-          st->cost = cost;
-          st->initial_cost = cost + st->fixed_cost;
-          st->abs_gtol = st->gtol * gmax;
-          st->pushed = 1;
-          st->min_pushed_cost = cost;
-          st->x_norm = sqrt(xs[kXXnorm2] + xn2c);
-          if (gmax <= st->abs_gtol && !st->disable_term) {
-            st->done = 1; st->ok = 1; st->termination = SG_GRADIENT_TOLERANCE;
+          s0.cost = cost;
+          s0.initial_cost = cost + s0.fixed_cost;
+          s0.abs_gtol = s0.gtol * gmax;
+          s0.pushed = 1;
+          s0.min_pushed_cost = cost;
+          s0.x_norm = sqrt(xs[kXXnorm2] + xn2c);
+          if (gmax <= s0.abs_gtol && !s0.disable_term) {
+            s0.done = 1; s0.ok = 1; s0.termination = SG_GRADIENT_TOLERANCE;
           }
         }
-        st->first = 0;
+        s0.first = 0;
       } else {
         if (xs[kXFail] > 0.0) {
-          st->done = 1; st->ok = 0; st->termination = SG_NUMERICAL_FAILURE;
+          s0.done = 1; s0.ok = 0; s0.termination = SG_NUMERICAL_FAILURE;
         } else {
-          st->cost = cost;
-          if (!st->disable_term && gmax <= st->abs_gtol) {
-            st->done = 1; st->ok = 1; st->termination = SG_GRADIENT_TOLERANCE;
-          } else if (!st->disable_term && st->radius < st->min_radius) {
-            st->done = 1; st->ok = 1; st->termination = SG_PARAMETER_TOLERANCE;
+          s0.cost = cost;
+          if (!s0.disable_term && gmax <= s0.abs_gtol) {
+            s0.done = 1; s0.ok = 1; s0.termination = SG_GRADIENT_TOLERANCE;
+          } else if (!s0.disable_term && s0.radius < s0.min_radius) {
+            s0.done = 1; s0.ok = 1; s0.termination = SG_PARAMETER_TOLERANCE;
           } else {
-            st->pushed += 1;
-            st->min_pushed_cost = fmin(st->min_pushed_cost, cost);
+            s0.pushed += 1;
+            s0.min_pushed_cost = fmin(s0.min_pushed_cost, cost);
           }
         }
       }
-      st->need_lin = 0;
+      s0.need_lin = 0;
     }
   }
   __syncthreads();
   if (tid == 0) {
-    if (!st->done) {
-      if (!st->disable_term && st->pushed - 1 >= st->max_iter) {
-        st->done = 1; st->ok = 1; st->termination = SG_NO_CONVERGENCE;
-      } else if (st->disable_term && st->lm_iters >= st->max_iter) {
-        st->done = 1; st->ok = 1; st->termination = SG_NO_CONVERGENCE;
+    if (!s0.done) {
+      if (!s0.disable_term && s0.pushed - 1 >= s0.max_iter) {
+        s0.done = 1; s0.ok = 1; s0.termination = SG_NO_CONVERGENCE;
+      } else if (s0.disable_term && s0.lm_iters >= s0.max_iter) {
+        s0.done = 1; s0.ok = 1; s0.termination = SG_NO_CONVERGENCE;
       }
     }
-    if (!st->done) st->lm_iters += 1;
-    done_sh = st->done;
+    if (!s0.done) s0.lm_iters += 1;
+    done_sh = s0.done;
+    *st = s0;
   }
   __syncthreads();
   if (done_sh) return;
