@@ -60,6 +60,8 @@ def parse():
     ap.add_argument("--frontend", type=int, default=1,
                     help="also measure the front end at N=1: KLT tracks/sec (config 3) and the 256-bit "
                          "Hamming matcher (config 4)")
+    ap.add_argument("--solve-all", type=int, default=1,
+                    help="N = 1: also time SolveAllFrames(C2 map, 2, false/true) (whole map; dense with cameras)")
     ap.add_argument("--model-scaling", type=int, default=1,
                     help="N = 1: model C5 strong scaling over 2/4/8 landmark shards from measured kernel times")
     ap.add_argument("--comm", choices=("rccl", "host"), default="rccl",
@@ -69,6 +71,7 @@ def parse():
                     help="profiling runs: one workload alone (its kernels are then the only ones launched)")
     args = ap.parse_args()
     if args.only != "all":
+        args.solve_all = 0
         args.cpu_runs = 0
         args.cpu_seconds = 0
         args.other = 0
@@ -443,6 +446,42 @@ def bench_sweep(local, sweep_obs):
             "ms_per_launch": kt[0], "bytes_per_launch": wb, **traffic_fields("k_linearize", "sweep", wb)}
 
 
+def bench_solve_all(local, steps=20, warmup=3):
+    """Whole-map refinements of main.cpp's calibration step (SolveAllFrames(map, 2, false / true), main.cpp:282,
+    327; slam.cpp:447-480) on the config-2 map: every frame free but the gauge, and with solve_cameras the 7
+    intrinsics of each camera couple every frame, so the reduced system is dense and takes the one-workgroup
+    global-memory Cholesky (k_cholesky_global) instead of the tiled band.  LM iterations per second over K
+    always-linearize iterations (termination off) and the per-kernel times."""
+    from slamgpu import ba
+    from slamgpu.capi import default_solver_options
+    from slamgpu.scene import make_config
+    m = make_config("C2")
+    out = {}
+    for cams in (False, True):
+        p = ba.problem_from_map_all(m, 2.0, cams)
+        g = ba.BundleAdjuster(device=local)
+        g.load(p)
+        info = g.info()
+        g.begin(default_solver_options(max_num_iterations=warmup + 2 * steps + 8, disable_termination=1,
+                                       always_linearize=1))
+        g.iterate(warmup)
+        g.sync()
+        t0 = time.perf_counter()
+        g.iterate(steps)
+        g.sync()
+        el = time.perf_counter() - t0
+        g.set_timing(True)
+        g.iterate(steps)
+        g.sync()
+        kt = g.kernel_times()
+        g.close()
+        out["solve_cameras" if cams else "poses_points"] = {
+            "iters_per_s": steps / el, "ms_per_iter": 1e3 * el / steps, "n": info["n"],
+            "cholesky": info["cholesky"], "band_tiles": info["band_tiles"],
+            "kernel_ms_per_iter": {k: round(v[0] * v[1] / steps, 5) for k, v in kt.items()}}
+    return out
+
+
 REPLICATED = ("cam_finalize", "cholesky", "decide")   # every landmark shard runs these on the whole system
 
 
@@ -549,6 +588,7 @@ def main():
                                              args.config)
 
     sweep_scaled = bench_sweep(local, args.sweep_obs) if args.sweep_obs > 0 and n_gpus == 1 else None
+    solve_all = bench_solve_all(local) if args.solve_all and n_gpus == 1 else None
 
     cpu = None
     if args.cpu_runs > 0 and n_gpus == 1:
@@ -588,6 +628,7 @@ def main():
         "roofline": roof,
         "roofline_sweep": sweep,
         "roofline_sweep_scaled": sweep_scaled,
+        "solve_all_frames": solve_all,
         "kernel_ms_per_iter": per_iter_ms,
         "cpu_baseline": cpu,
         "speedup_vs_cpu": (value / cpu["value"]) if cpu else None,

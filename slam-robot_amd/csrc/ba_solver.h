@@ -108,6 +108,8 @@ class BaSolver {
   bool stamp_on_ = false;
   int ncu_ = 256;                       // compute units (Schur segment count), queried once
   size_t tile_lds_set_ = 0;             // dynamic LDS last granted to k_chol_tiles
+  size_t gchol_lds_max_ = 0;            // dynamic LDS granted to k_cholesky_global
+  bool chol_gstage_ = false;            // k_cholesky_global stages panel rows in LDS
   std::unique_ptr<class Stager> stager_;   // batched structure uploads (stager.h)
   DBuf<unsigned long long> stamps_;
 

@@ -1358,41 +1358,95 @@ __global__ __launch_bounds__(256) void k_intr_zero(Dev d) {
 
 // One thread per observation: J_k (the same corrected projection Jacobian as k_linearize) and its
 // J^T J / J^T r terms.
+// The per-camera sums (upper 7x7 of Jk^T Jk, gradient, diagonal: 42 values per camera, all observations of
+// the camera add into them) go through LDS per workgroup and then one global atomic per value and workgroup:
+// a global atomic per observation on 42 shared addresses serialised the launch (9.5 ms at config 2).  The
+// frame-intrinsics block KU_fk likewise accumulates in LDS over a window of kIntrWin frame blocks from the
+// workgroup's first point's first block (observations are point-major, points in device order by first
+// block); observations in blocks outside the window add globally.
+constexpr int kIntrCamV = 42;
+constexpr int kIntrKMax = 7 * kMaxIntrCams;
+constexpr int kIntrWin = 32;
 __global__ __launch_bounds__(256) void k_intr_lin(Dev d) {
   const LmState* st = d.st;
   if (st->done || !st->need_lin) return;
-  const int o = blockIdx.x * blockDim.x + threadIdx.x;
-  if (o >= d.M) return;
+  __shared__ double kacc[kMaxIntrCams * kIntrCamV];
+  __shared__ double kfw[kIntrWin * 6 * kIntrKMax];
+  __shared__ int b_lo_sh;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < kMaxIntrCams * kIntrCamV; i += blockDim.x) kacc[i] = 0.0;
+  for (int i = tid; i < kIntrWin * 6 * kIntrKMax; i += blockDim.x) kfw[i] = 0.0;
+  if (tid == 0) {
+    const int o0 = min((int)(blockIdx.x * blockDim.x), d.M - 1);
+    b_lo_sh = o0 >= 0 ? max(0, d.pinfo[d.obs_pnt[o0]].y >> 8) : 0;
+  }
+  __syncthreads();
+  const int b_lo = b_lo_sh;
+  const int o = blockIdx.x * blockDim.x + tid;
   const int cur = st->cur;
-  const int m = d.obs_meta[o], f = d.obs_frame[o], p = d.obs_pnt[o], cam = meta_cam(m);
-  double* Jko = d.Jk + 14 * (size_t)o;
-  const double4 Xv = reinterpret_cast<const double4*>(d.X[cur])[p];
-  const double X[4] = {Xv.x, Xv.y, Xv.z, Xv.w};
-  const double pt[2] = {d.obs_pt[2 * o], d.obs_pt[2 * o + 1]};
-  double rr[2], Jc[12], Jp[8], Jk[14], c;
-  if ((m & kMetaFixed) || !LinearizeObservation(d.q[cur] + 4 * f, d.t[cur] + 3 * f, d.k[cur] + 7 * cam, X, pt,
-                                                d.b, d.inv_b, rr, Jc, Jp, &c, Jk)) {
-    for (int i = 0; i < 14; ++i) Jko[i] = 0.0;   // a failed projection fails the linearization (k_linearize)
-    return;
+  const int nk = d.nk;
+  if (o < d.M) {
+    const int m = d.obs_meta[o], f = d.obs_frame[o], p = d.obs_pnt[o], cam = meta_cam(m);
+    double* Jko = d.Jk + 14 * (size_t)o;
+    const double4 Xv = reinterpret_cast<const double4*>(d.X[cur])[p];
+    const double X[4] = {Xv.x, Xv.y, Xv.z, Xv.w};
+    const double pt[2] = {d.obs_pt[2 * o], d.obs_pt[2 * o + 1]};
+    double rr[2], Jc[12], Jp[8], Jk[14], c;
+    if ((m & kMetaFixed) || !LinearizeObservation(d.q[cur] + 4 * f, d.t[cur] + 3 * f, d.k[cur] + 7 * cam, X, pt,
+                                                  d.b, d.inv_b, rr, Jc, Jp, &c, Jk)) {
+      for (int i = 0; i < 14; ++i) Jko[i] = 0.0;   // a failed projection fails the linearization (k_linearize)
+    } else {
+      for (int i = 0; i < 14; ++i) Jko[i] = Jk[i];
+      double* ka = kacc + cam * kIntrCamV;
+      int u = 0;
+      for (int a = 0; a < 7; ++a) {
+        for (int j = a; j < 7; ++j) atomicAdd(ka + u++, Jk[a] * Jk[j] + Jk[7 + a] * Jk[7 + j]);
+        atomicAdd(ka + 28 + a, Jk[a] * rr[0] + Jk[7 + a] * rr[1]);
+        atomicAdd(ka + 35 + a, Jk[a] * Jk[a] + Jk[7 + a] * Jk[7 + a]);
+      }
+      const int b = meta_block(m);
+      if (b >= 0) {
+        if (!(m & kMetaRot)) { Jc[0] = Jc[1] = Jc[2] = Jc[6] = Jc[7] = Jc[8] = 0.0; }
+        if (!(m & kMetaTrans)) { Jc[3] = Jc[4] = Jc[5] = Jc[9] = Jc[10] = Jc[11] = 0.0; }
+        const int wb = b - b_lo;
+        if (wb >= 0 && wb < kIntrWin) {
+          double* Kf = kfw + (6 * wb) * kIntrKMax + 7 * cam;
+          for (int a = 0; a < 6; ++a)
+            for (int j = 0; j < 7; ++j) atomicAdd(Kf + a * kIntrKMax + j, Jc[a] * Jk[j] + Jc[6 + a] * Jk[7 + j]);
+        } else {
+          double* Kf = d.KU + (size_t)(6 * b) * nk + 7 * cam;
+          for (int a = 0; a < 6; ++a)
+            for (int j = 0; j < 7; ++j) atomicAdd(Kf + (size_t)a * nk + j, Jc[a] * Jk[j] + Jc[6 + a] * Jk[7 + j]);
+        }
+      }
+    }
   }
-  for (int i = 0; i < 14; ++i) Jko[i] = Jk[i];
-  const int kc = 7 * cam, nk = d.nk;
-  double* Kk = d.KU + (size_t)(d.kc0 + kc) * nk;
-  for (int a = 0; a < 7; ++a) {
-    for (int j = a; j < 7; ++j) atomicAdd(Kk + (size_t)a * nk + kc + j, Jk[a] * Jk[j] + Jk[7 + a] * Jk[7 + j]);
-    atomicAdd(d.camg + d.kc0 + kc + a, Jk[a] * rr[0] + Jk[7 + a] * rr[1]);
-    atomicAdd(d.camdiag + d.kc0 + kc + a, Jk[a] * Jk[a] + Jk[7 + a] * Jk[7 + a]);
+  __syncthreads();
+  for (int i = tid; i < d.ncam * kIntrCamV; i += blockDim.x) {
+    const double v = kacc[i];
+    if (v == 0.0) continue;
+    const int cam = i / kIntrCamV, e = i - cam * kIntrCamV, kc = 7 * cam;
+    if (e < 28) {
+      int a = 0, u = e;
+      while (u >= 7 - a) {
+        u -= 7 - a;
+        ++a;
+      }
+      atomicAdd(d.KU + (size_t)(d.kc0 + kc + a) * nk + kc + a + u, v);
+    } else if (e < 35) {
+      atomicAdd(d.camg + d.kc0 + kc + (e - 28), v);
+    } else {
+      atomicAdd(d.camdiag + d.kc0 + kc + (e - 35), v);
+    }
   }
-  const int b = meta_block(m);
-  if (b < 0) return;
-  if (!(m & kMetaRot)) { Jc[0] = Jc[1] = Jc[2] = Jc[6] = Jc[7] = Jc[8] = 0.0; }
-  if (!(m & kMetaTrans)) { Jc[3] = Jc[4] = Jc[5] = Jc[9] = Jc[10] = Jc[11] = 0.0; }
-  double* Kf = d.KU + (size_t)(6 * b) * nk + kc;
-  for (int a = 0; a < 6; ++a)
-    for (int j = 0; j < 7; ++j) atomicAdd(Kf + (size_t)a * nk + j, Jc[a] * Jk[j] + Jc[6 + a] * Jk[7 + j]);
+  for (int i = tid; i < kIntrWin * 6 * nk; i += blockDim.x) {
+    const int row = i / nk, j = i - row * nk;   // row = 6 (b - b_lo) + a
+    const int b = b_lo + row / 6;
+    const double v = kfw[row * kIntrKMax + j];
+    if (b < d.NB && v != 0.0) atomicAdd(d.KU + (size_t)(6 * b + row % 6) * nk + j, v);
+  }
 }
 
-// CameraStabilization residual of camera c (slam.cpp:107-124) and its exact Jacobian.
 __device__ __forceinline__ void stab_residual(const double* k, double* res, double* J) {
   res[0] = 1000.0 * k[0] * k[0];
   res[1] = 1000.0 * k[1] * k[1];
@@ -1482,11 +1536,51 @@ __global__ __launch_bounds__(256) void k_intr_assemble(Dev d) {
 
 // Thread per free point p: W_kp = A_k^T A_p over its observations of camera c (scaled), Y = W_kp V~p^-1, then
 // S_kk -= Y W_kp'^T, rhs_k -= W_kp t_p, and for each observation (frame block b) S_bk -= A_c^T (A_p Y^T).
+// The k-k block of S and the k rhs (shared by every point) accumulate in LDS per workgroup, then one global
+// atomic per entry and workgroup (a global atomic per point on ~120 shared addresses took 1.9 ms at config 2).
+// The frame-intrinsics coupling S_fk of the workgroup's points accumulates in LDS too, over a window of
+// kIntrWin frame blocks from the workgroup's first point's first block (points are in device order, by first
+// block, so a workgroup's points touch a narrow band of blocks); blocks outside the window add globally.
+struct IntrSchurLds {
+  double skk[kIntrKMax * kIntrKMax], sxk[kIntrKMax];
+  double sfk[kIntrWin * 6 * kIntrKMax];
+  int b_lo;
+};
+__device__ __forceinline__ void intr_schur_point(const Dev& d, int p, IntrSchurLds& sh);
 __global__ __launch_bounds__(128) void k_intr_schur(Dev d) {
   const LmState* st = d.st;
   if (st->done) return;
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= d.P || !d.pfree[p]) return;
+  __shared__ IntrSchurLds sh;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < kIntrKMax * kIntrKMax; i += blockDim.x) sh.skk[i] = 0.0;
+  for (int i = tid; i < kIntrWin * 6 * kIntrKMax; i += blockDim.x) sh.sfk[i] = 0.0;
+  if (tid < kIntrKMax) sh.sxk[tid] = 0.0;
+  if (tid == 0) {
+    const int p0 = min((int)(blockIdx.x * blockDim.x), d.P - 1);
+    sh.b_lo = p0 >= 0 ? max(0, d.pinfo[p0].y >> 8) : 0;
+  }
+  __syncthreads();
+  const int p = blockIdx.x * blockDim.x + tid;
+  if (p < d.P && d.pfree[p]) intr_schur_point(d, p, sh);
+  __syncthreads();
+  const int K = d.nk, n = d.n;
+  for (int i = tid; i < K * K; i += blockDim.x) {
+    const int r = i / K, c = i - r * K;
+    const double v = sh.skk[r * kIntrKMax + c];
+    if (c >= r && v != 0.0) atomicAdd(d.S + (size_t)(d.kc0 + r) * n + d.kc0 + c, v);
+  }
+  if (tid < K && sh.sxk[tid] != 0.0) atomicAdd(d.xc + d.kc0 + tid, sh.sxk[tid]);
+  for (int i = tid; i < kIntrWin * 6 * K; i += blockDim.x) {
+    const int row = i / K, j = i - row * K;   // row = 6 (b - b_lo) + a
+    const int b = sh.b_lo + row / 6;
+    const double v = sh.sfk[row * kIntrKMax + j];
+    if (b < d.NB && v != 0.0) atomicAdd(d.S + (size_t)(6 * b + row % 6) * n + d.kc0 + j, v);
+  }
+}
+
+__device__ __forceinline__ void intr_schur_point(const Dev& d, int p, IntrSchurLds& sh) {
+  double* skk = sh.skk;
+  double* sxk = sh.sxk;
   const int o0 = d.poff[p], o1 = d.poff[p + 1], n = d.n;
   const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
   const double sp[4] = {s4.x, s4.y, s4.z, s4.w};
@@ -1528,7 +1622,7 @@ __global__ __launch_bounds__(128) void k_intr_schur(Dev d) {
         Y[4 * j + a] = y;
         r += W[4 * j + a] * tpv[a];
       }
-      atomicAdd(d.xc + kc + j, -r);
+      atomicAdd(sxk + 7 * c + j, -r);
     }
     // S_kk blocks (c, c2 >= c), upper triangle
     for (int c2 = c; c2 < d.ncam; ++c2) {
@@ -1538,12 +1632,11 @@ __global__ __launch_bounds__(128) void k_intr_schur(Dev d) {
       } else if (!build_W(c2, W2)) {
         continue;
       }
-      const int kc2 = d.kc0 + 7 * c2;
       for (int j = 0; j < 7; ++j)
         for (int j2 = (c2 == c ? j : 0); j2 < 7; ++j2) {
           double v = 0.0;
           for (int a = 0; a < 4; ++a) v += Y[4 * j + a] * W2[4 * j2 + a];
-          atomicAdd(d.S + (size_t)(kc + j) * n + kc2 + j2, -v);
+          atomicAdd(skk + (7 * c + j) * kIntrKMax + 7 * c2 + j2, -v);
         }
     }
     // S_fk: every observation of the point in a free frame block
@@ -1559,9 +1652,16 @@ __global__ __launch_bounds__(128) void k_intr_schur(Dev d) {
           for (int a = 0; a < 4; ++a) v += Jp[4 * rr + a] * Y[4 * j + a];
           Mx[7 * rr + j] = v;
         }
-      for (int a = 0; a < 6; ++a)
-        for (int j = 0; j < 7; ++j)
-          atomicAdd(d.S + (size_t)(6 * b + a) * n + kc + j, -(Jc[a] * Mx[j] + Jc[6 + a] * Mx[7 + j]));
+      const int wb = b - sh.b_lo;
+      if (wb >= 0 && wb < kIntrWin) {
+        double* dst = sh.sfk + (6 * wb) * kIntrKMax + 7 * c;
+        for (int a = 0; a < 6; ++a)
+          for (int j = 0; j < 7; ++j) atomicAdd(dst + a * kIntrKMax + j, -(Jc[a] * Mx[j] + Jc[6 + a] * Mx[7 + j]));
+      } else {
+        for (int a = 0; a < 6; ++a)
+          for (int j = 0; j < 7; ++j)
+            atomicAdd(d.S + (size_t)(6 * b + a) * n + kc + j, -(Jc[a] * Mx[j] + Jc[6 + a] * Mx[7 + j]));
+      }
     }
   }
 }
@@ -2332,12 +2432,19 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
   SG_STAMP_FLUSH()
 }
 
-// Global-memory path for bands wider than the LDS window.
+// Global-memory path for bands wider than the LDS window (a dense S: free intrinsics couple every frame).
+// Right-looking over 16-row panels: wave 0 factors the diagonal block, a thread per column does the panel's
+// TRSM, and the trailing update A_IJ -= U_KI^T U_KJ runs over 16 x 16 tiles (I <= J), four
+// v_mfma_f64_16x16x4f64 a tile with the tile in the accumulator, a wave per tile.  kStage: the panel's
+// factored rows are staged in LDS (after xs, pitch n) so the update reads its operands from LDS; the launch
+// takes the <false> instance when 17 n doubles do not fit.
+template <bool kStage>
 __global__ __launch_bounds__(kCholThreads) void k_cholesky_global(Dev d, const int32_t* panel_jend, double* rdg) {
   LmState* st = d.st;
   if (st->done) return;
-  extern __shared__ double xs[];   // n doubles: back-substitution solution
+  extern __shared__ double xs[];   // n doubles: back-substitution solution (then the staged panel rows)
   const int n = d.n, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lk = lane >> 4, li = lane & 15;
   const int nwaves = kCholThreads / 64;
   double* A = d.S;
   double* y = d.work;
@@ -2372,40 +2479,65 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_global(Dev d, const i
       if (lane == 0 && bad) fail_sh = 1;
     }
     __syncthreads();
-    const int ncol = jmax - (kb + w);
-    for (int ci = tid; ci < ncol + 1; ci += kCholThreads) {
-      const bool isy = ci == ncol;
-      const int c = kb + w + ci;
+    const int m = jmax - (kb + w);   // trailing columns [kb + w, jmax)
+    const size_t c0 = (size_t)kb + w;
+    double* P = xs + n;              // staged panel rows: P[r n + ci], column kb + w + ci
+    // U_K row r, trailing column ci (LDS when staged; never a pointer that may be either: flat accesses)
+    auto U = [&](int r, int ci) -> double {
+      if constexpr (kStage) return P[r * n + ci];
+      else return A[(size_t)(kb + r) * n + c0 + ci];
+    };
+    for (int ci = tid; ci < m + 1; ci += kCholThreads) {
+      const bool isy = ci == m;
       double a[kCholNb];
 #pragma unroll
-      for (int r = 0; r < kCholNb; ++r) a[r] = (r < w) ? (isy ? y[kb + r] : A[(size_t)(kb + r) * n + c]) : 0.0;
+      for (int r = 0; r < kCholNb; ++r) a[r] = (r < w) ? (isy ? y[kb + r] : A[(size_t)(kb + r) * n + c0 + ci]) : 0.0;
       chol_trsm16(a, U11, rdiag, w);
 #pragma unroll
       for (int r = 0; r < kCholNb; ++r)
         if (r < w) {
-          if (isy) y[kb + r] = a[r];
-          else A[(size_t)(kb + r) * n + c] = a[r];
+          if (isy) {
+            y[kb + r] = a[r];
+          } else {
+            A[(size_t)(kb + r) * n + c0 + ci] = a[r];
+            if constexpr (kStage) P[r * n + ci] = a[r];
+          }
         }
     }
     __syncthreads();
-    for (int i = kb + w + wave; i < jmax; i += nwaves) {
-      double ui[kCholNb];
+    const int T = (m + 15) >> 4;
+    const int ntiles = T * (T + 1) / 2;
+    for (int tile = wave; tile < ntiles; tile += nwaves) {
+      int ti = 0, rem = tile;
+      while (rem >= T - ti) { rem -= T - ti; ++ti; }
+      const int tj = ti + rem;
+      const int i0 = 16 * ti, j0 = 16 * tj;
+      f64x4 acc;
 #pragma unroll
-      for (int r = 0; r < kCholNb; ++r) ui[r] = (r < w) ? A[(size_t)(kb + r) * n + i] : 0.0;
-      for (int j = i + lane; j < jmax; j += 64) {
-        double s = 0.0;
-#pragma unroll
-        for (int r = 0; r < kCholNb; ++r)
-          if (r < w) s += ui[r] * A[(size_t)(kb + r) * n + j];
-        A[(size_t)i * n + j] -= s;
+      for (int qq = 0; qq < 4; ++qq) {
+        const int row = i0 + lk + 4 * qq, col = j0 + li;
+        acc[qq] = (row < m && col < m && row <= col) ? A[(c0 + row) * n + c0 + col] : 0.0;
       }
-      if (lane == 0) {
-        double s = 0.0;
 #pragma unroll
-        for (int r = 0; r < kCholNb; ++r)
-          if (r < w) s += ui[r] * y[kb + r];
-        y[i] -= s;
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const int r = 4 * s4 + lk;
+        const bool kin = r < w;
+        const double av = (kin && i0 + li < m) ? -U(r, i0 + li) : 0.0;
+        const double bv = (kin && j0 + li < m) ? U(r, j0 + li) : 0.0;
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
       }
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq) {
+        const int row = i0 + lk + 4 * qq, col = j0 + li;
+        if (row < m && col < m && row <= col) A[(c0 + row) * n + c0 + col] = acc[qq];
+      }
+    }
+    for (int ci = tid; ci < m; ci += kCholThreads) {
+      double s = 0.0;
+#pragma unroll
+      for (int r = 0; r < kCholNb; ++r)
+        if (r < w) s += U(r, ci) * y[kb + r];
+      y[c0 + ci] -= s;
     }
     __syncthreads();
   }
@@ -4009,6 +4141,11 @@ BaSolver::BaSolver(const sg_device_options& dev) : dev_(dev) {
     for (const void* f : kCholTilesStamped)
       SG_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lim));
     tile_lds_set_ = lim;
+    hipFuncAttributes ga;
+    SG_HIP_CHECK(hipFuncGetAttributes(&ga, (const void*)k_cholesky_global<true>));
+    gchol_lds_max_ = (size_t)160 * 1024 - ga.sharedSizeBytes;
+    for (const void* f : {(const void*)k_cholesky_global<true>, (const void*)k_cholesky_global<false>})
+      SG_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)gchol_lds_max_));
   }
   st_.Resize(1);
   timers_.resize(kKNum);
@@ -4603,6 +4740,8 @@ void BaSolver::Load(const sg_problem& p) {
     stager_->Add(pack_off_, off);
     Spk_.Resize(std::max<size_t>(npack_, 1));
   }
+  // k_cholesky_global stages each panel's rows in LDS when x and 16 rows of S fit
+  chol_gstage_ = (size_t)std::max(n_, 1) * 8 * (1 + kCholNb) <= gchol_lds_max_;
   chol_window_ = npanel <= kJendSh;   // band ends cached in LDS
   for (int pk = 0; pk < npanel; ++pk)
     if (panel_jmax[pk] - pk * kCholNb > kCholWS) chol_window_ = false;
@@ -5253,8 +5392,9 @@ void BaSolver::EnqueueIterations(int n) {
       hipLaunchKernelGGL(k_cholesky_window<false>, dim3(1), dim3(kCholThreads), kCholLds, stream_, d,
                          (const int32_t*)work_i_.ptr, rdg_.ptr);
     else
-      hipLaunchKernelGGL(k_cholesky_global, dim3(1), dim3(kCholThreads), (size_t)std::max(n_, 1) * 8, stream_, d,
-                         (const int32_t*)work_i_.ptr, rdg_.ptr);
+      hipLaunchKernelGGL(chol_gstage_ ? k_cholesky_global<true> : k_cholesky_global<false>, dim3(1),
+                         dim3(kCholThreads), (size_t)std::max(n_, 1) * 8 * (chol_gstage_ ? 1 + kCholNb : 1), stream_,
+                         d, (const int32_t*)work_i_.ptr, rdg_.ptr);
     TimedLaunchEnd(kKChol);
     if (nk_) hipLaunchKernelGGL(k_intr_step, dim3(1), dim3(64), 0, stream_, d);
     TimedLaunchBegin(kKPointUpd);

@@ -26,6 +26,8 @@ print("C2 %.1f it/s (%.4f ms), roofline frac %.5f, lm_regime %.1f it/s" % (d["va
 print("kernels", d["kernel_ms_per_iter"])
 o = d.get("other_workload") or {}
 if o: print("C5 %.1f it/s kernels %s" % (o["value"], o["kernel_ms_per_iter"]))
+for k, v in (d.get("solve_all_frames") or {}).items():
+    print("solve_all %s: %.1f it/s (%.3f ms), n %d, %s" % (k, v["iters_per_s"], v["ms_per_iter"], v["n"], v["cholesky"]))
 PY
 if [ -n "$R3_DIAG" ]; then
   timeout -k 10 300 python tools/chol_ab.py 40 > gpurun_out/chol_ab_$TAG.log 2>&1 || { echo "chol_ab failed"; tail -20 gpurun_out/chol_ab_$TAG.log; exit 1; }
