@@ -1546,10 +1546,10 @@ struct IntrSchurLds {
   double sfk[kIntrWin * 6 * kIntrKMax];
   int b_lo;
 };
-__device__ __forceinline__ void intr_schur_point(const Dev& d, int p, IntrSchurLds& sh);
+__device__ __forceinline__ void intr_schur_point(const Dev& d, int p, bool act, IntrSchurLds& sh);
 __global__ __launch_bounds__(128) void k_intr_schur(Dev d) {
   const LmState* st = d.st;
-  if (st->done) return;
+  if (st->done || d.P == 0) return;
   __shared__ IntrSchurLds sh;
   const int tid = threadIdx.x;
   for (int i = tid; i < kIntrKMax * kIntrKMax; i += blockDim.x) sh.skk[i] = 0.0;
@@ -1561,7 +1561,7 @@ __global__ __launch_bounds__(128) void k_intr_schur(Dev d) {
   }
   __syncthreads();
   const int p = blockIdx.x * blockDim.x + tid;
-  if (p < d.P && d.pfree[p]) intr_schur_point(d, p, sh);
+  intr_schur_point(d, min(p, d.P - 1), p < d.P && d.pfree[p], sh);   // every lane: wave sums inside
   __syncthreads();
   const int K = d.nk, n = d.n;
   for (int i = tid; i < K * K; i += blockDim.x) {
@@ -1578,10 +1578,13 @@ __global__ __launch_bounds__(128) void k_intr_schur(Dev d) {
   }
 }
 
-__device__ __forceinline__ void intr_schur_point(const Dev& d, int p, IntrSchurLds& sh) {
+// Called by every lane (inactive ones with no observations, so W = 0): the S_kk and rhs terms, shared by all
+// points, are summed over the wave first (one LDS atomic a value and wave, not 64 on one address).
+__device__ __forceinline__ void intr_schur_point(const Dev& d, int p, bool act, IntrSchurLds& sh) {
   double* skk = sh.skk;
   double* sxk = sh.sxk;
-  const int o0 = d.poff[p], o1 = d.poff[p + 1], n = d.n;
+  const bool lane0 = (threadIdx.x & 63) == 0;
+  const int o0 = act ? d.poff[p] : 0, o1 = act ? d.poff[p + 1] : 0, n = d.n;
   const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
   const double sp[4] = {s4.x, s4.y, s4.z, s4.w};
   double Vi[10];
@@ -1612,35 +1615,37 @@ __device__ __forceinline__ void intr_schur_point(const Dev& d, int p, IntrSchurL
   };
   for (int c = 0; c < d.ncam; ++c) {
     double W[28], Y[28];
-    if (!build_W(c, W)) continue;
+    const bool has = build_W(c, W);
     const int kc = d.kc0 + 7 * c;
     for (int j = 0; j < 7; ++j) {
       double r = 0.0;
       for (int a = 0; a < 4; ++a) {
         double y = 0.0;
         for (int e = 0; e < 4; ++e) y += W[4 * j + e] * sym4(Vi, e, a);
-        Y[4 * j + a] = y;
+        Y[4 * j + a] = has ? y : 0.0;   // (a lane without observations of c adds exact zeros)
         r += W[4 * j + a] * tpv[a];
       }
-      atomicAdd(sxk + 7 * c + j, -r);
+      const double rs = wave_sum_full(has ? -r : 0.0);
+      if (lane0) atomicAdd(sxk + 7 * c + j, rs);
     }
     // S_kk blocks (c, c2 >= c), upper triangle
     for (int c2 = c; c2 < d.ncam; ++c2) {
       double W2[28];
       if (c2 == c) {
         for (int i = 0; i < 28; ++i) W2[i] = W[i];
-      } else if (!build_W(c2, W2)) {
-        continue;
+      } else {
+        build_W(c2, W2);
       }
       for (int j = 0; j < 7; ++j)
         for (int j2 = (c2 == c ? j : 0); j2 < 7; ++j2) {
           double v = 0.0;
           for (int a = 0; a < 4; ++a) v += Y[4 * j + a] * W2[4 * j2 + a];
-          atomicAdd(skk + (7 * c + j) * kIntrKMax + 7 * c2 + j2, -v);
+          const double vs = wave_sum_full(-v);
+          if (lane0) atomicAdd(skk + (7 * c + j) * kIntrKMax + 7 * c2 + j2, vs);
         }
     }
-    // S_fk: every observation of the point in a free frame block
-    for (int o = o0; o < o1; ++o) {
+    // S_fk: every observation of the point in a free frame block (none without observations of camera c)
+    for (int o = has ? o0 : o1; o < o1; ++o) {
       const int m = d.obs_meta[o], b = meta_block(m);
       if ((m & kMetaFixed) || b < 0) continue;
       double r[2], Jc[12], Jp[8];
@@ -2438,6 +2443,10 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_window(Dev d, const i
 // v_mfma_f64_16x16x4f64 a tile with the tile in the accumulator, a wave per tile.  kStage: the panel's
 // factored rows are staged in LDS (after xs, pitch n) so the update reads its operands from LDS; the launch
 // takes the <false> instance when 17 n doubles do not fit.
+// With free intrinsics S is an arrowhead: the frame columns keep their band and only the nk intrinsics columns
+// are dense, so a panel's trailing columns are [kb + w, bend) (the frame band end, panel_jend[npanel + pk])
+// followed by [max(kc0, kb + w), n); the factor has no fill outside them (a frame column's envelope starts
+// after the panel's rows).  The update runs over that compact index space (ci -> column).
 template <bool kStage>
 __global__ __launch_bounds__(kCholThreads) void k_cholesky_global(Dev d, const int32_t* panel_jend, double* rdg) {
   LmState* st = d.st;
@@ -2479,19 +2488,25 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_global(Dev d, const i
       if (lane == 0 && bad) fail_sh = 1;
     }
     __syncthreads();
-    const int m = jmax - (kb + w);   // trailing columns [kb + w, jmax)
-    const size_t c0 = (size_t)kb + w;
-    double* P = xs + n;              // staged panel rows: P[r n + ci], column kb + w + ci
+    const int c0 = kb + w;
+    int m1 = jmax - c0, klo = n;     // trailing columns: [c0, c0 + m1) then [klo, n)
+    if (d.nk > 0) {
+      m1 = max(0, panel_jend[npanel + pk] - c0);
+      klo = max(d.kc0, c0);
+    }
+    const int m = m1 + (n - klo);
+    auto colof = [&](int ci) -> size_t { return (size_t)(ci < m1 ? c0 + ci : klo + (ci - m1)); };
+    double* P = xs + n;              // staged panel rows: P[r n + ci], column colof(ci)
     // U_K row r, trailing column ci (LDS when staged; never a pointer that may be either: flat accesses)
     auto U = [&](int r, int ci) -> double {
       if constexpr (kStage) return P[r * n + ci];
-      else return A[(size_t)(kb + r) * n + c0 + ci];
+      else return A[(size_t)(kb + r) * n + colof(ci)];
     };
     for (int ci = tid; ci < m + 1; ci += kCholThreads) {
       const bool isy = ci == m;
       double a[kCholNb];
 #pragma unroll
-      for (int r = 0; r < kCholNb; ++r) a[r] = (r < w) ? (isy ? y[kb + r] : A[(size_t)(kb + r) * n + c0 + ci]) : 0.0;
+      for (int r = 0; r < kCholNb; ++r) a[r] = (r < w) ? (isy ? y[kb + r] : A[(size_t)(kb + r) * n + colof(ci)]) : 0.0;
       chol_trsm16(a, U11, rdiag, w);
 #pragma unroll
       for (int r = 0; r < kCholNb; ++r)
@@ -2499,7 +2514,7 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_global(Dev d, const i
           if (isy) {
             y[kb + r] = a[r];
           } else {
-            A[(size_t)(kb + r) * n + c0 + ci] = a[r];
+            A[(size_t)(kb + r) * n + colof(ci)] = a[r];
             if constexpr (kStage) P[r * n + ci] = a[r];
           }
         }
@@ -2507,37 +2522,54 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_global(Dev d, const i
     __syncthreads();
     const int T = (m + 15) >> 4;
     const int ntiles = T * (T + 1) / 2;
-    for (int tile = wave; tile < ntiles; tile += nwaves) {
-      int ti = 0, rem = tile;
-      while (rem >= T - ti) { rem -= T - ti; ++ti; }
-      const int tj = ti + rem;
-      const int i0 = 16 * ti, j0 = 16 * tj;
-      f64x4 acc;
+    // kTU consecutive tiles (row-major over I <= J) a wave at a time: their loads in flight together
+    constexpr int kTU = 4;
+    for (int t0 = wave * kTU; t0 < ntiles; t0 += nwaves * kTU) {
+      int i0[kTU], j0[kTU];
+      {
+        int ti = 0, rem = t0;
+        while (rem >= T - ti) { rem -= T - ti; ++ti; }
 #pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
-        const int row = i0 + lk + 4 * qq, col = j0 + li;
-        acc[qq] = (row < m && col < m && row <= col) ? A[(c0 + row) * n + c0 + col] : 0.0;
+        for (int u = 0; u < kTU; ++u) {
+          const bool ok = t0 + u < ntiles;
+          i0[u] = ok ? 16 * ti : m;   // an absent tile is masked out by row < m
+          j0[u] = ok ? 16 * (ti + rem) : m;
+          if (++rem >= T - ti) { ++ti; rem = 0; }
+        }
       }
+      f64x4 acc[kTU];
+#pragma unroll
+      for (int u = 0; u < kTU; ++u)
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const int row = i0[u] + lk + 4 * qq, col = j0[u] + li;
+          acc[u][qq] = (row < m && col < m && row <= col) ? A[colof(row) * n + colof(col)] : 0.0;
+        }
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4) {
         const int r = 4 * s4 + lk;
         const bool kin = r < w;
-        const double av = (kin && i0 + li < m) ? -U(r, i0 + li) : 0.0;
-        const double bv = (kin && j0 + li < m) ? U(r, j0 + li) : 0.0;
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+#pragma unroll
+        for (int u = 0; u < kTU; ++u) {
+          const double av = (kin && i0[u] + li < m) ? -U(r, i0[u] + li) : 0.0;
+          const double bv = (kin && j0[u] + li < m) ? U(r, j0[u] + li) : 0.0;
+          acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[u], 0, 0, 0);
+        }
       }
 #pragma unroll
-      for (int qq = 0; qq < 4; ++qq) {
-        const int row = i0 + lk + 4 * qq, col = j0 + li;
-        if (row < m && col < m && row <= col) A[(c0 + row) * n + c0 + col] = acc[qq];
-      }
+      for (int u = 0; u < kTU; ++u)
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const int row = i0[u] + lk + 4 * qq, col = j0[u] + li;
+          if (row < m && col < m && row <= col) A[colof(row) * n + colof(col)] = acc[u][qq];
+        }
     }
     for (int ci = tid; ci < m; ci += kCholThreads) {
       double s = 0.0;
 #pragma unroll
       for (int r = 0; r < kCholNb; ++r)
         if (r < w) s += U(r, ci) * y[kb + r];
-      y[c0 + ci] -= s;
+      y[colof(ci)] -= s;
     }
     __syncthreads();
   }
@@ -4720,7 +4752,7 @@ void BaSolver::Load(const sg_problem& p) {
     for (int b = 0; b < NB_; ++b) lo_blk[b] = (int)(-neg[b]);
   }
   const int npanel = (n_ + kCholNb - 1) / kCholNb;
-  std::vector<int32_t> panel_jmax(std::max(npanel, 1), 0);
+  std::vector<int32_t> panel_jmax(std::max(npanel, 1), 0), panel_bend(std::max(npanel, 1), 0);
   for (int pk = 0; pk < npanel; ++pk) {
     const int row_hi = std::min(n_, (pk + 1) * kCholNb) - 1;   // last row of the panel
     const int blk_hi = row_hi / 6;
@@ -4730,8 +4762,12 @@ void BaSolver::Load(const sg_problem& p) {
       if (lo_blk[b] <= blk_hi) jmax = std::max(jmax, 6 * b + 6);
     jmax = std::min(jmax, n_);
     panel_jmax[pk] = std::min(n_, (jmax + kCholNb - 1) / kCholNb * kCholNb);   // band end, 16-aligned
-    if (nk_) panel_jmax[pk] = n_;   // the intrinsics columns couple every frame: S is dense
+    if (nk_) {   // the intrinsics columns couple every frame: S is dense (k_cholesky_global: arrowhead)
+      panel_bend[pk] = std::min(jmax, 6 * NB_);
+      panel_jmax[pk] = n_;
+    }
   }
+  if (nk_) panel_jmax.insert(panel_jmax.end(), panel_bend.begin(), panel_bend.end());   // work_i_ tail
   {
     std::vector<int32_t> off(npanel + 1, 0);
     for (int pk = 0; pk < npanel; ++pk)
