@@ -1798,18 +1798,26 @@ __device__ __forceinline__ void chol_trsm16(double (&a)[kCholNb], const double (
 // Back substitution U x = y.  U rows in global A (band end per panel), 1/U_jj in rdg, forward solution
 // in y (global); the solution goes to xs (LDS, n doubles) and y.  Blocked by 16 from the end; the
 // 16x16 triangle runs in one wave with readlane broadcasts.
+// kc0 < n: the arrowhead layout of k_cholesky_global (row panel pk's columns [kb + w, panel_jend[npanel + pk])
+// then [max(kc0, kb + w), n)).
 __device__ __noinline__ void chol_backsub(const double* A, const double* rdg, double* y, double* xs, int n,
-                                          const int32_t* panel_jend) {
+                                          const int32_t* panel_jend, int kc0) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
   const int npanel = (n + kCholNb - 1) / kCholNb;
   __shared__ double rpart[kCholNb];
   for (int pk = npanel - 1; pk >= 0; --pk) {
     const int kb = pk * kCholNb;
     const int w = min(kCholNb, n - kb);
-    const int jend = panel_jend[pk];
+    const int c0 = kb + w;
+    const int bend = kc0 < n ? max(c0, panel_jend[npanel + pk]) : panel_jend[pk];
+    const int klo = kc0 < n ? max(kc0, c0) : n;
+    const int m1 = bend - c0, m = m1 + (n - klo);
     for (int r = wave; r < w; r += nwaves) {
       double s = 0.0;
-      for (int j = kb + w + lane; j < jend; j += 64) s += A[(size_t)(kb + r) * n + j] * xs[j];
+      for (int ci = lane; ci < m; ci += 64) {
+        const int j = ci < m1 ? c0 + ci : klo + (ci - m1);
+        s += A[(size_t)(kb + r) * n + j] * xs[j];
+      }
       s = wave_sum(s);
       if (lane == 0) rpart[r] = s;
     }
@@ -2573,7 +2581,7 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_global(Dev d, const i
     }
     __syncthreads();
   }
-  chol_backsub(A, rdg, y, xs, n, panel_jend);
+  chol_backsub(A, rdg, y, xs, n, panel_jend, d.nk > 0 ? d.kc0 : n);
   for (int i = tid; i < n; i += kCholThreads) d.xc[i] = xs[i];
   __syncthreads();
   chol_candidates<kCholThreads>(d, y, fail_sh);
