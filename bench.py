@@ -7,9 +7,10 @@ complement, reduced camera Cholesky, back-substitution, candidate cost, accept/r
 
 Workloads (synthetic scenes, slamgpu/scene.py; fp64 arithmetic, the reference's own precision):
   --config C2 (default): BASELINE config 2 — 50 keyframes / ~19.4k landmarks / ~148k observations (seed 2),
-      SolveFrames(map, 48, 50, 2.0).  N > 1 (torchrun, one rank per GPU): weak scaling — 50 keyframes and
-      N x 20k landmarks sharded over the ranks (sg_problem_shard), RCCL all-reduce of the camera system per
-      iteration; value = N * K / time (the unit is one LM iteration's worth of config-2 work).
+      SolveFrames(map, 48, 50, 2.0).  N > 1 (torchrun, one rank per GPU): strong scaling — the same 20k-landmark
+      problem's landmarks sharded over the ranks (sg_problem_shard), RCCL all-reduces of the camera system per
+      iteration; value = K / time.  The weak-scaling figure (50 keyframes and N x 20k landmarks, value =
+      N * K / time in units of config-2 iterations) is reported beside it as `weak_scaling`.
   --config C5: BASELINE config 5 — 200 keyframes / ~194k landmarks / ~1.95M observations (seed 5),
       SolveFrames(map, 198, 200, 2.0); N > 1: strong scaling, the same problem's landmarks sharded over the
       ranks; value = K / time.
@@ -49,11 +50,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--points", type=int, default=20000, help="landmarks per GPU")
+    ap.add_argument("--points", type=int, default=20000, help="landmarks of the config-2 scene")
     ap.add_argument("--frames", type=int, default=50)
     ap.add_argument("--config", choices=("C2", "C5"), default="C2", help="headline workload")
     ap.add_argument("--other", type=int, default=1, help="also measure the other BA workload (C5 / C2)")
-    ap.add_argument("--cpu-runs", type=int, default=20, help="CPU-baseline timed runs per leg (0: skip)")
+    ap.add_argument("--cpu-runs", type=int, default=7, help="CPU-baseline timed runs per leg (0: skip)")
     ap.add_argument("--cpu-seconds", type=float, default=4.0, help="front-end CPU-baseline sample (0: skip)")
     ap.add_argument("--sweep-obs", type=int, default=2_000_000,
                     help="observations in the scaled Jacobian-sweep measurement (0: skip)")
@@ -63,7 +64,10 @@ def parse():
     ap.add_argument("--solve-all", type=int, default=1,
                     help="N = 1: also time SolveAllFrames(C2 map, 2, false/true) (whole map; dense with cameras)")
     ap.add_argument("--model-scaling", type=int, default=1,
-                    help="N = 1: model C5 strong scaling over 2/4/8 landmark shards from measured kernel times")
+                    help="N = 1: model C2 and C5 strong scaling over 2/4/8 landmark shards from measured kernel "
+                         "times")
+    ap.add_argument("--weak", type=int, default=1,
+                    help="N > 1: also measure C2 weak scaling (N x 20k landmarks) beside the strong headline")
     ap.add_argument("--comm", choices=("rccl", "host"), default="rccl",
                     help="N > 1: rccl (one GPU per rank, the product path) or host (torch.distributed gloo through "
                          "sg_ba_comm_init_host: rehearses the multi-rank bench with several ranks on one GPU)")
@@ -219,48 +223,58 @@ def dist_env():
 
 
 def cpu_legs(full, runs, ba_iters_note):
-    """CPU baseline of one LM iteration (oracle/oracle_ba.cpp, the Ceres-1.8 LM + SPARSE_SCHUR restatement):
-    each run solves the config from its perturbed start with max_num_iterations = 1 (iteration 0's
-    residual pass + one LM iteration: linearize, Schur, Cholesky, candidate), 3 warm-up runs, median of
-    `runs` timed runs.  Legs: 1 thread (the reference's Ceres num_threads default, slam.cpp:504), 1 thread
-    with -ffast-math (the reference's Makefile:4 flags), and this process's CPU share on OpenMP."""
+    """CPU baseline of one LM iteration (oracle/oracle_ba.cpp, the Ceres-1.8 LM + SPARSE_SCHUR restatement).
+    A solve from the perturbed start with max_num_iterations = k pays the set-up, iteration 0's residual and
+    Jacobian pass and k LM iterations; one LM iteration is timed as the difference T(2) - T(1) of the medians of
+    `runs` timed runs each (1 warm-up run each; both accepted steps on this problem, so each iteration
+    linearizes — the same unit as the device figure).  Legs: 1 thread (the reference's Ceres num_threads
+    default, slam.cpp:504), 1 thread with -ffast-math (the reference's Makefile:4 flags), and this process's CPU
+    share on OpenMP."""
     import statistics
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     from slamgpu.capi import default_solver_options
     nproc = os.cpu_count() or 1
-    share = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else nproc
-    share = min(share, int(os.environ.get("OMP_NUM_THREADS", share)))
-    o1 = default_solver_options(max_num_iterations=1)
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else nproc
+    share = min(affinity, int(os.environ.get("OMP_NUM_THREADS", affinity)))
     legs = []
     for name, nt, fm in (("1 thread, -O3", 1, False), ("1 thread, -O3 -ffast-math", 1, True),
                          ("%d threads (OpenMP), -O3" % share, share, False)):
-        ts = []
-        for r in range(3 + runs):
-            po = full.copy()
-            t0 = time.perf_counter()
-            oracle.solve(po, o1, nthreads=nt, fastmath=fm)
-            if r >= 3:
-                ts.append(time.perf_counter() - t0)
-        med = statistics.median(ts)
-        legs.append({"leg": name, "threads": nt, "fastmath": fm, "value": 1.0 / med, "unit": "iters/s",
-                     "median_s_per_iteration": med, "runs": len(ts)})
+        med = {}
+        for k in (1, 2):
+            o = default_solver_options(max_num_iterations=k)
+            ts = []
+            for r in range(1 + runs):
+                po = full.copy()
+                t0 = time.perf_counter()
+                s = oracle.solve(po, o, nthreads=nt, fastmath=fm)
+                if r >= 1:
+                    ts.append(time.perf_counter() - t0)
+            assert s["num_successful_steps"] == k, s
+            med[k] = statistics.median(ts)
+        per_it = med[2] - med[1]
+        legs.append({"leg": name, "threads": nt, "fastmath": fm, "value": 1.0 / per_it, "unit": "iters/s",
+                     "s_per_iteration": per_it, "median_s_1_iteration_solve": med[1],
+                     "median_s_2_iteration_solve": med[2], "runs": runs})
     best = max(legs, key=lambda l: l["value"])
     return {"value": best["value"], "unit": "iters/s", "cores": best["threads"], "kind": "port",
-            "sample": "median of %d runs per leg: SolveFrames(%s) from the perturbed start, max_num_iterations=1 "
-                      "(oracle/oracle_ba.cpp, dual-number Jacobians); nproc=%d, CPU share %d"
-                      % (runs, ba_iters_note, nproc, share),
-            "legs": legs}
+            "sample": "one LM iteration = T(2 iterations) - T(1 iteration), medians of %d runs each: "
+                      "SolveFrames(%s) from the perturbed start (oracle/oracle_ba.cpp, dual-number Jacobians); "
+                      "nproc=%d, affinity share %d, OpenMP threads %d" % (runs, ba_iters_note, nproc, affinity, share),
+            "nproc": nproc, "affinity_share": affinity, "legs": legs}
 
 
-def make_workload(cfg, n_gpus, rank, points_per_gpu, frames):
-    """(full problem, this rank's shard, description) of a BA workload."""
+def make_workload(cfg, n_gpus, rank, points, frames, weak=False):
+    """(full problem, this rank's shard, description) of a BA workload.  C2 is the `points`-landmark problem
+    sharded over the ranks (strong scaling); weak=True builds n_gpus x `points` landmarks instead."""
     from slamgpu import ba
     from slamgpu.scene import make_config, make_scene
     if cfg == "C2":
-        scene = make_scene(num_frames=frames, num_points=points_per_gpu * n_gpus, seed=2, run_max=14, run_min=4)
+        npts = points * n_gpus if weak else points
+        scene = make_scene(num_frames=frames, num_points=npts, seed=2, run_max=14, run_min=4)
         full = ba.problem_from_map_frames(scene, frames - 2, frames, 2.0)
-        desc = "config 2: SolveFrames(%d of %d KF) local BA, LM iteration" % (frames - 2, frames)
+        desc = "config 2: SolveFrames(%d of %d KF) local BA, LM iteration%s" % (
+            frames - 2, frames, " (weak scaling: %d x %d landmarks)" % (n_gpus, points) if weak else "")
     else:
         scene = make_config("C5")
         full = ba.problem_from_map_frames(scene, scene.num_frames - 2, scene.num_frames, 2.0)
@@ -400,8 +414,8 @@ def kernel_report(res, steps, n_text, workload):
     return {k: round(v, 5) for k, v in per_iter_ms.items()}, roof, sweep
 
 
-def run_workload(cfg, args, n_gpus, rank, local, dist, steps, warmup):
-    full, prob, desc = make_workload(cfg, n_gpus, rank, args.points, args.frames)
+def run_workload(cfg, args, n_gpus, rank, local, dist, steps, warmup, weak=False):
+    full, prob, desc = make_workload(cfg, n_gpus, rank, args.points, args.frames, weak)
     r = Runner(prob, local, rank, n_gpus, dist, args.comm)
     res = r.timed(steps, warmup)
     info = r.solver.info()
@@ -470,10 +484,14 @@ def bench_solve_all(local, steps=20, warmup=3):
         g.iterate(steps)
         g.sync()
         el = time.perf_counter() - t0
+        s1 = g.summary()   # a solve that ended early would time no-op launches: refuse the figure
+        assert s1["ok"] == 1 and s1["sync_timeouts"] == 0 and s1["num_lm_iterations"] == warmup + steps, s1
         g.set_timing(True)
         g.iterate(steps)
         g.sync()
         kt = g.kernel_times()
+        s2 = g.summary()
+        assert s2["ok"] == 1 and s2["sync_timeouts"] == 0 and s2["num_lm_iterations"] == warmup + 2 * steps, s2
         g.close()
         out["solve_cameras" if cams else "poses_points"] = {
             "iters_per_s": steps / el, "ms_per_iter": 1e3 * el / steps, "n": info["n"],
@@ -555,28 +573,39 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl" if args.comm == "rccl" else "gloo", rank=rank, world_size=ws)
     n_gpus = ws
-    strong = args.config == "C5"
+    c5 = args.config == "C5"
 
     full, prob, desc, res, info, start, bal = run_workload(args.config, args, n_gpus, rank, local, dist,
                                                            args.steps, args.warmup)
     other = None
     if args.other:
-        ocfg = "C2" if strong else "C5"
+        ocfg = "C2" if c5 else "C5"
         k2 = min(args.steps, 50)
         f2, p2, d2, r2, i2, st2, b2 = run_workload(ocfg, args, n_gpus, rank, local, dist, k2, min(args.warmup, 10))
         if rank == 0:
             pk2, roof2, sw2 = kernel_report(r2, k2, "n=%d, band %d tiles" % (i2["n"], i2["band_tiles"]), ocfg)
-            val2 = (n_gpus if ocfg == "C2" else 1) * k2 / r2["elapsed"]
+            val2 = k2 / r2["elapsed"]
             scal = None
-            if ocfg == "C5" and n_gpus == 1 and args.model_scaling:
+            if n_gpus == 1 and args.model_scaling:
                 scal = model_scaling(local, f2, pk2)
-            other = {"workload": d2, "scaling": "weak" if ocfg == "C2" else "strong", "value": val2,
+            other = {"workload": d2, "scaling": "strong", "value": val2,
                      "unit": "iters/s", "steps": k2, "ms_per_step": 1e3 * r2["elapsed"] / k2,
                      "accepted_frac": r2["accepted"] / k2, "lm_regime": r2["lm_regime"], "keyframes": f2.num_frames,
                      "landmarks": f2.num_points, "observations": f2.num_obs, "per_rank": {
                          "landmarks": p2.num_points, "observations": p2.num_obs}, "solver": i2,
                      "kernel_ms_per_iter": pk2, "roofline": roof2, "roofline_sweep": sw2,
                      "solve_from_start": st2, "shard_balance": b2, "strong_scaling_model": scal}
+
+    weak = None
+    if n_gpus > 1 and args.weak and not c5:
+        # C2 weak scaling beside the strong headline: 50 keyframes and N x 20k landmarks, N x K / time
+        kw = min(args.steps, 50)
+        fw, pw, dw, rw, iw, stw, bw = run_workload("C2", args, n_gpus, rank, local, dist, kw, min(args.warmup, 10),
+                                                   weak=True)
+        weak = {"workload": dw, "scaling": "weak", "value": n_gpus * kw / rw["elapsed"],
+                "unit": "iters/s (config-2 iterations: N x K / time)", "steps": kw,
+                "ms_per_step": 1e3 * rw["elapsed"] / kw, "landmarks": fw.num_points, "observations": fw.num_obs,
+                "per_rank": {"landmarks": pw.num_points, "observations": pw.num_obs}, "shard_balance": bw}
 
     if rank != 0:
         if dist is not None:
@@ -586,22 +615,23 @@ def main():
 
     per_iter_ms, roof, sweep = kernel_report(res, args.steps, "n=%d, band %d tiles" % (info["n"], info["band_tiles"]),
                                              args.config)
+    scal1 = model_scaling(local, full, per_iter_ms) if n_gpus == 1 and args.model_scaling else None
 
     sweep_scaled = bench_sweep(local, args.sweep_obs) if args.sweep_obs > 0 and n_gpus == 1 else None
     solve_all = bench_solve_all(local) if args.solve_all and n_gpus == 1 else None
 
     cpu = None
     if args.cpu_runs > 0 and n_gpus == 1:
-        cpu = cpu_legs(full, args.cpu_runs, "48, 50, 2.0" if args.config == "C2" else "198, 200, 2.0")
+        cpu = cpu_legs(full, args.cpu_runs, "48, 50, 2.0" if not c5 else "198, 200, 2.0")
 
     frontend = None
     if args.frontend and n_gpus == 1:
         cs = args.cpu_seconds
         frontend = {"tracker": bench_tracker(local, cs), "hamming": bench_hamming(local, cs)}
 
-    value = (1 if strong else n_gpus) * args.steps / res["elapsed"]
+    value = args.steps / res["elapsed"]
     line = {
-        "metric": "local-BA iters/sec (%s)" % ("200 KF, 200k pts" if strong else "50 KF, 20k pts"),
+        "metric": "local-BA iters/sec (%s)" % ("200 KF, 200k pts" if c5 else "50 KF, 20k pts"),
         "value": value,
         "unit": "iters/s",
         "n_gpus": n_gpus,
@@ -609,7 +639,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": 1e3 * res["elapsed"] / args.steps,
         "higher_is_better": True,
-        "scaling": "strong" if strong else "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (seeded scene generator, slamgpu/scene.py)",
@@ -635,6 +665,8 @@ def main():
         "speedup_vs_cpu_from_start": (start["iters_per_s_wall"] / cpu["value"]) if cpu and start["iters_per_s_wall"] else None,
         "lm_state": {"final_cost": res["summary"]["final_cost"], "radius": res["summary"]["trust_region_radius"]},
         "shard_balance": bal,
+        "strong_scaling_model": scal1,
+        "weak_scaling": weak,
         "other_workload": other,
         "frontend": frontend,
         "traffic_source": "HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes over "

@@ -192,6 +192,7 @@ class BaSolver {
   std::vector<KTimer> timers_;
   void TimedLaunchBegin(int id);
   void LaunchCholTiles(bool stamp, int la, dim3 grid, const Dev& d, int flags);
+  int CholTilesLa() const;
   void TimedLaunchEnd(int id);
   void TimedLaunchBegin(int id, hipStream_t s);
   void TimedLaunchEnd(int id, hipStream_t s);

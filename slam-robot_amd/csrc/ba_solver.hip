@@ -22,6 +22,7 @@
 
 #include <chrono>
 #include <string>
+#include <thread>
 
 #include <algorithm>
 #include <cfloat>
@@ -4131,11 +4132,21 @@ static const void* const kCholTilesKernels[] = {
     (const void*)k_chol_tiles<false, 3>, (const void*)k_chol_tiles<false, 5>, (const void*)k_chol_tiles<false, 8>,
     (const void*)k_chol_tiles<false, 9>, (const void*)k_chol_tiles<false, 17>};
 
-void BaSolver::LaunchCholTiles(bool stamp, int la, dim3 grid, const Dev& d, int flags) {
-  int idx = -1;
+// The SG_CHOL_* variant flags as k_chol_tiles' kLa, and its index in kCholTilesLa (-1: not instantiated).
+int BaSolver::CholTilesLa() const {
+  return (chol_lookahead_ ? 1 : 0) | (chol_factor_ == 1 ? 2 : 0) | (chol_dinv_ ? 4 : 0) | (chol_factor_ == 2 ? 8 : 0) |
+         (chol_dataflow_ ? 16 : 0);
+}
+static int chol_tiles_index(int la) {
   for (int i = 0; i < (int)(sizeof(kCholTilesLa) / sizeof(int)); ++i)
-    if (kCholTilesLa[i] == la) idx = i;
-  SG_REQUIRE(idx >= 0, SG_EINVAL, "this combination of SG_CHOL_* variants is not instantiated");
+    if (kCholTilesLa[i] == la) return i;
+  return -1;
+}
+// stamped builds exist for the default (look-ahead), the MFMA factor and the dataflow sync only
+static bool chol_tiles_stamped(int la) { return la == 1 || la == 9 || la == 17; }
+
+void BaSolver::LaunchCholTiles(bool stamp, int la, dim3 grid, const Dev& d, int flags) {
+  const int idx = chol_tiles_index(la);   // validated in the constructor (CheckCholVariant)
   const void* f = stamp ? kCholTilesStamped[(la & 16) ? 2 : (la & 8) ? 1 : 0] : kCholTilesKernels[1 + idx];
   Dev dd = d;
   const int32_t* pj = (const int32_t*)work_i_.ptr;
@@ -4161,6 +4172,17 @@ BaSolver::BaSolver(const sg_device_options& dev) : dev_(dev) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, dev.device) == hipSuccess && prop.multiProcessorCount > 0)
       ncu_ = prop.multiProcessorCount;
+  }
+  // the SG_CHOL_* / SG_STAMP development switches are fixed per process: refuse a combination without a build
+  // here, not in the middle of a solve (and never launch a stamped build of a different variant)
+  {
+    const int la = CholTilesLa();
+    SG_REQUIRE(chol_tiles_index(la) >= 0, SG_EINVAL,
+               "this combination of SG_CHOL_* variants is not instantiated (SG_CHOL_LOOKAHEAD=0 runs alone)");
+    const bool stamp = getenv("SG_STAMP") && getenv("SG_STAMP")[0] == '1';
+    SG_REQUIRE(!stamp || chol_tiles_stamped(la), SG_EINVAL,
+               "SG_STAMP=1 has no stamped build of this SG_CHOL_* variant (the default, SG_CHOL_FACTOR=2 and "
+               "SG_CHOL_DATAFLOW=1 have one)");
   }
   stager_.reset(new Stager());
   SG_HIP_CHECK(hipFuncSetAttribute((const void*)k_cholesky_window<false>,
@@ -4785,7 +4807,9 @@ void BaSolver::Load(const sg_problem& p) {
     Spk_.Resize(std::max<size_t>(npack_, 1));
   }
   // k_cholesky_global stages each panel's rows in LDS when x and 16 rows of S fit
-  chol_gstage_ = (size_t)std::max(n_, 1) * 8 * (1 + kCholNb) <= gchol_lds_max_;
+  // (SG_CHOL_GSTAGE=0: never, so tests reach the unstaged instance at any size)
+  chol_gstage_ = (size_t)std::max(n_, 1) * 8 * (1 + kCholNb) <= gchol_lds_max_ &&
+                 !(getenv("SG_CHOL_GSTAGE") && atoi(getenv("SG_CHOL_GSTAGE")) == 0);
   chol_window_ = npanel <= kJendSh;   // band ends cached in LDS
   for (int pk = 0; pk < npanel; ++pk)
     if (panel_jmax[pk] - pk * kCholNb > kCholWS) chol_window_ = false;
@@ -5243,9 +5267,13 @@ __global__ __launch_bounds__(256) void k_download(const double* __restrict__ q, 
 // Wait for stream s by spinning on an event query.  hipStreamSynchronize's blocking wait returned 13-28 ms
 // late in a few percent of the main.cpp replay's loads, all of whose work had been three small kernels
 // (tools/e2e_replay.py, profiles/r3_v8_*); the solver's waits are short (a load, an LM batch), so the host
-// spins on them, falling back to the blocking wait after SG_SPIN_MS (default 200 ms).
+// spins on them, falling back to the blocking wait after SG_SPIN_MS (default 200 ms).  A sharded solver (several
+// ranks, possibly rank threads or processes sharing the host's cores with the threads that run the host
+// all-reduces) yields between polls and spins at most 1 ms.
 void BaSolver::WaitStream(hipStream_t s) {
   static const double spin_ms = getenv("SG_SPIN_MS") ? atof(getenv("SG_SPIN_MS")) : 200.0;
+  const bool shared = nranks() > 1;
+  const double limit = shared ? std::min(spin_ms, 1.0) : spin_ms;
   if (!ev_wait_) SG_HIP_CHECK(hipEventCreateWithFlags(&ev_wait_, hipEventDisableTiming));
   SG_HIP_CHECK(hipEventRecord(ev_wait_, s));
   const auto t0 = std::chrono::steady_clock::now();
@@ -5253,7 +5281,8 @@ void BaSolver::WaitStream(hipStream_t s) {
     const hipError_t e = hipEventQuery(ev_wait_);
     if (e == hipSuccess) return;
     if (e != hipErrorNotReady) SG_HIP_CHECK(e);
-    if (std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() > spin_ms) break;
+    if (std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() > limit) break;
+    if (shared) std::this_thread::yield();
   }
   SG_HIP_CHECK(hipEventSynchronize(ev_wait_));
 }
@@ -5424,10 +5453,7 @@ void BaSolver::EnqueueIterations(int n) {
     }
     TimedLaunchBegin(kKChol);
     if (chol_tiles_)
-      LaunchCholTiles(d.stamps != nullptr,
-                      (chol_lookahead_ ? 1 : 0) | (chol_factor_ == 1 ? 2 : 0) | (chol_dinv_ ? 4 : 0) |
-                          (chol_factor_ == 2 ? 8 : 0) | (chol_dataflow_ ? 16 : 0),
-                      dim3(chol_nd_ > 0 ? 2 : 1), d,
+      LaunchCholTiles(d.stamps != nullptr, CholTilesLa(), dim3(chol_nd_ > 0 ? 2 : 1), d,
                       chol_simdmap_ | (chol_cand_lds_ ? 2 : 0) | (chol_force_tmo_ ? 4 : 0));
     else if (chol_window_ && d.stamps)
       hipLaunchKernelGGL(k_cholesky_window<true>, dim3(1), dim3(kCholThreads), kCholLds, stream_, d,
@@ -5641,7 +5667,7 @@ void BaSolver::Info(sg_ba_info* o) const {
   o->num_blocks = NB_;
   o->n = n_;
   o->band_tiles = band_tiles_;
-  o->cholesky_path = chol_tiles_ ? 0 : (chol_window_ ? 1 : 2);
+  o->cholesky_path = chol_tiles_ ? 0 : (chol_window_ ? 1 : (chol_gstage_ ? 2 : 3));
   o->cholesky_split = chol_tiles_ ? chol_nd_ : 0;
   o->num_pairs = (int32_t)std::min<size_t>(npairs_, INT32_MAX);
   o->rank = comm_ ? comm_->rank() : 0;

@@ -510,3 +510,38 @@ def test_solver_variants_match_default(gpu_lib, monkeypatch, env):
     assert abs(s0["final_cost"] - s1["final_cost"]) <= 1e-12 * s0["final_cost"]
     np.testing.assert_allclose(p1.q, p0.q, rtol=0, atol=1e-10)
     np.testing.assert_allclose(p1.t, p0.t, rtol=0, atol=1e-6)
+
+
+@pytest.mark.parametrize("stage", ["1", "0"], ids=["staged", "unstaged"])
+def test_free_intrinsics_c2_global_cholesky_matches_oracle(gpu_lib, oracle_lib, monkeypatch, stage):
+    """SolveAllFrames(C2 map, 2.0, true) (slam.cpp:447-480) at the size where the free-intrinsics path runs its
+    global-memory pieces: n = 314 > kCholWS, so S (dense through the 14 intrinsics columns) is factored by
+    k_cholesky_global (arrowhead trailing update, MFMA tiles; with and without the LDS-staged panel rows,
+    SG_CHOL_GSTAGE=0), and 48 free frame blocks > kIntrWin = 32, so k_intr_lin / k_intr_schur take their
+    out-of-window global-atomic branches.  Three LM iterations against the oracle's dense solve: the same
+    steps, cost to 1e-8 relative, intrinsics to 1e-7, translations to 1e-5 mm."""
+    import os
+    monkeypatch.setenv("SG_CHOL_GSTAGE", stage)
+    m = make_config("C2")
+    for c in range(len(m.k) // 7):
+        k = m.k[7 * c:7 * c + 7]
+        k[3] *= 1.002
+        k[4] *= 1.002
+        k[5] += 1.0
+    pa = ba.problem_from_map_all(m, 2.0, solve_cameras=True)
+    pg, po = pa.copy(), pa.copy()
+    g = ba.BundleAdjuster()
+    g.load(pg)
+    info = g.info()
+    assert info["n"] > 128 and info["num_blocks"] > 32
+    assert info["cholesky_path"] == (2 if stage == "1" else 3), info
+    o = default_solver_options(max_num_iterations=3)
+    sg = g.solve(o)
+    so = oracle_lib.solve(po, o, nthreads=min(16, os.cpu_count() or 1))
+    assert sg["ok"] == so["ok"] == 1 and sg["sync_timeouts"] == 0
+    assert sg["num_iterations"] == so["num_iterations"]
+    assert sg["num_successful_steps"] == so["num_successful_steps"] >= 2
+    assert abs(sg["initial_cost"] - so["initial_cost"]) <= 1e-10 * so["initial_cost"]
+    assert abs(sg["final_cost"] - so["final_cost"]) <= 1e-8 * so["final_cost"]
+    np.testing.assert_allclose(pg.k, po.k, rtol=1e-7, atol=1e-9)
+    np.testing.assert_allclose(pg.t, po.t, atol=1e-5)
