@@ -70,11 +70,43 @@ def test_residual_sweep_matches_oracle(gpu_lib, oracle_lib):
         assert abs(cost - co) <= 1e-12 * co
 
 
-def test_golden_c1_first_20_iterations(gpu_lib):
-    """The C1 golden's first 20 LM iterations, iteration for iteration: the same accepted steps, cost to 1e-9
-    relative, rotations and points to 1e-9, translations to 1e-5 mm.  (From about iteration 25 the trust radius passes 1e15, where the
-    homogeneous 4x4 point blocks — rank 3: X and lambda X project alike — are singular to rounding and steps
-    turn invalid by rounding-level differences; see test_golden_c1_solve.)"""
+def test_c1_first_10_iterations_match_oracle(gpu_lib, oracle_lib):
+    """The C1 golden problem's first 10 LM iterations (trust radius up to 6e8) against the oracle, iteration for
+    iteration: the same accepted steps, cost to 1e-12 relative, rotations and point directions to 1e-9,
+    translations to 1e-9 mm, per-observation residuals to 1e-9 px (measured on MI355X: cost 5e-15, rotations
+    5e-15, point directions 3e-13, translations 3e-11 mm, residuals 2.5e-10 px: tools/parity_pins.py)."""
+    pa, _ = _golden()
+    o = default_solver_options(max_num_iterations=10)
+    b = ba.BundleAdjuster()
+    pg, po = pa.copy(), pa.copy()
+    b.load(pg)
+    s = b.solve(o)
+    so = oracle_lib.solve(po, o)
+    assert s["num_successful_steps"] == so["num_successful_steps"] == 10
+    assert abs(s["final_cost"] - so["final_cost"]) <= 1e-12 * so["final_cost"]
+    np.testing.assert_allclose(pg.q, po.q, rtol=0, atol=1e-9)
+    np.testing.assert_allclose(pg.t, po.t, rtol=0, atol=1e-9)
+    # points: their directions to 1e-9 (measured 3e-13); their scale |X| (the gauge of the rank-3 point block)
+    # is already drifting by rounding at radius 6e8 (5e-10 relative measured), so X itself is held to 5e-9
+    xg, xo = pg.X.reshape(-1, 4), po.X.reshape(-1, 4)
+    np.testing.assert_allclose(xg / np.linalg.norm(xg, axis=1, keepdims=True),
+                               xo / np.linalg.norm(xo, axis=1, keepdims=True), rtol=0, atol=1e-9)
+    np.testing.assert_allclose(pg.X, po.X, rtol=0, atol=5e-9)
+    rg, _, _ = oracle_lib.evaluate(pg)
+    ro, _, _ = oracle_lib.evaluate(po)
+    np.testing.assert_allclose(rg, ro, rtol=0, atol=1e-9)
+
+
+def test_golden_c1_first_20_iterations(gpu_lib, oracle_lib):
+    """The C1 golden's first 20 LM iterations against the committed oracle state: the same accepted steps, and
+    the comparison made through gauge-invariant quantities.  By iteration 20 the trust radius is 3.5e13; the
+    homogeneous 4x4 point blocks are rank 3 (X and lambda X project alike, project.h:33-34), so the LM damping
+    D/radius ~ 1e-14 |V| is below the rounding of V itself and the scale |X| of each point drifts by rounding
+    (measured 2.3e-5 relative between the two solvers); the damping metric then moves the other directions at
+    the 1e-8 level.  The gauge-invariant figures are the per-observation residuals (what the solve minimises)
+    and the cost.  Measured on MI355X (tools/parity_pins.py): cost 2e-10 relative, residuals RMS 2.6e-7 px /
+    max 8.7e-6 px, rotations 6.3e-10, translations 2.4e-6 mm; bounds: cost 1e-9, residual RMS 1e-6 px and max
+    5e-5 px, rotations 5e-9, translations 1e-5 mm (4x-8x the measured values)."""
     pa, g = _golden()
     b = ba.BundleAdjuster()
     pg = pa.copy()
@@ -82,25 +114,23 @@ def test_golden_c1_first_20_iterations(gpu_lib):
     s = b.solve(default_solver_options(max_num_iterations=20))
     assert s["num_successful_steps"] == int(g["oracle20_num_successful"]) == 20
     assert abs(s["final_cost"] - float(g["oracle20_final_cost"])) <= 1e-9 * float(g["oracle20_final_cost"])
-    np.testing.assert_allclose(pg.q, g["oracle20_q"], rtol=0, atol=1e-9)
-    np.testing.assert_allclose(pg.t, g["oracle20_t"], rtol=0, atol=1e-5)   # mm (radius 3.5e13 by then)
-    # the homogeneous points up to their scale: X and lambda X project alike (project.h:33-34), so the 4x4
-    # point blocks are rank 3 and the step along X itself is set only by the LM damping at trust radii ~1e13;
-    # that gauge direction drifts by rounding (measured 2e-5 relative between the two solvers).  The unit
-    # directions agree to 1e-9 for 99.7 % of the entries and to 8e-9 (0.05 um at 6 m) for the rest, so the
-    # bound is 1e-8 with the 1e-9 share asserted separately
-    xg, xo = pg.X.reshape(-1, 4), g["oracle20_X"].reshape(-1, 4)
-    ug = xg / np.linalg.norm(xg, axis=1, keepdims=True)
-    uo = xo / np.linalg.norm(xo, axis=1, keepdims=True)
-    np.testing.assert_allclose(ug, uo, rtol=0, atol=1e-8)
-    assert (np.abs(ug - uo) <= 1e-9).mean() >= 0.99
+    np.testing.assert_allclose(pg.q, g["oracle20_q"], rtol=0, atol=5e-9)
+    np.testing.assert_allclose(pg.t, g["oracle20_t"], rtol=0, atol=1e-5)   # mm
+    po = pa.copy()
+    po.q[:], po.t[:], po.X[:] = g["oracle20_q"], g["oracle20_t"], g["oracle20_X"]
+    rg, _, fg = oracle_lib.evaluate(pg)
+    ro, _, fo = oracle_lib.evaluate(po)
+    assert fg == fo == 0
+    dr = np.abs(rg - ro)
+    assert np.sqrt((dr ** 2).mean()) <= 1e-6 and dr.max() <= 5e-5, (np.sqrt((dr ** 2).mean()), dr.max())
 
 
 def test_golden_c1_solve(gpu_lib, oracle_lib):
-    """The full C1 solve.  The oracle takes 158 iterations, 72 of them invalid steps at trust radii >= 1e15
-    where the homogeneous point blocks are singular to rounding (test_golden_c1_first_20_iterations): the two
-    solvers' invalid-step counts there differ with rounding, so the iteration count is compared within 20
-    and the minimum to 1e-6 relative cost, 1e-2 mm, 1e-6."""
+    """The full C1 solve.  The oracle takes 158 iterations: 85 successful, 72 invalid steps at trust radii
+    >= 1e15 where the homogeneous point blocks are singular to rounding (test_golden_c1_first_20_iterations), 1
+    unsuccessful.  How many invalid steps each solver takes in that regime depends on rounding (measured: the
+    device takes 159 with the same 85 successful steps and 73 invalid), so the successful steps are compared
+    within 2 and the total within 5, and the minimum to 1e-6 relative cost, 1e-2 mm, 1e-6."""
     pa, g = _golden()
     b = ba.BundleAdjuster()
     pg = pa.copy()
@@ -109,7 +139,8 @@ def test_golden_c1_solve(gpu_lib, oracle_lib):
     assert s["ok"] == 1 and s["termination"] == "FUNCTION_TOLERANCE"
     assert abs(s["final_cost"] - float(g["oracle_final_cost"])) <= 1e-6 * float(g["oracle_final_cost"])
     assert abs(s["initial_cost"] - float(g["oracle_initial_cost"])) <= 1e-10 * float(g["oracle_initial_cost"])
-    assert abs(s["num_iterations"] - int(g["oracle_num_iterations"])) <= 20
+    assert abs(s["num_successful_steps"] - int(g["oracle_num_successful"])) <= 2
+    assert abs(s["num_iterations"] - int(g["oracle_num_iterations"])) <= 5
     np.testing.assert_allclose(pg.t, g["oracle_t"], atol=1e-2)
     np.testing.assert_allclose(pg.q, g["oracle_q"], atol=1e-6)
     # scipy started at the oracle's minimum stays there (local-minimum check)
