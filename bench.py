@@ -503,53 +503,69 @@ def bench_solve_all(local, steps=20, warmup=3):
 REPLICATED = ("cam_finalize", "cholesky", "decide")   # every landmark shard runs these on the whole system
 
 
-def model_scaling(local, full, full_kernel_ms, ns=(2, 4, 8), steps=20, warmup=3,
-                  allreduce_us=20.0, band_gbs=50.0):
-    """Modelled strong scaling of a BA workload over N landmark shards, from measured kernel times: every
-    shard of the N-way split (sg_problem_shard) is loaded alone on this GPU and timed (always-linearize
-    iterations, HIP events); a shard's iteration = its shardable kernels (linearize, camera reduce, Schur,
-    S reduce, point update, update reduce) + the replicated ones measured on the whole problem (camera
-    finalize, Cholesky, decision: every rank runs them on the full reduced system) + three all-reduces per
-    iteration (camera blocks, the packed band of S, the update scalars) priced at `allreduce_us` each plus the
-    band at `band_gbs` (assumptions, not measurements: RCCL over xGMI is not measurable on this 1-GPU box).
-    The slowest shard sets the pace."""
+def model_scaling(local, full, full_kernel_ms, ns=(2, 4, 8), steps=20, warmup=3, allreduce_us=20.0, band_gbs=50.0,
+                  decide_us=4.0):
+    """Modelled strong scaling of a BA workload over N landmark shards, from measured kernel times.  Every shard of
+    the N-way split (sg_problem_shard) is loaded alone on this GPU and timed with the multi-rank chain forced
+    (SG_XCHG_MERGE=force: each rank assembles its own camera blocks into its partial S, the band of S travels
+    packed with the camera gradient / diagonal / cost scalars in its tail, and the bookkeeping and damping follow
+    the exchange; the pack and unpack kernels are timed as 'exchange').  A shard's iteration = its shardable
+    kernels (linearize, camera reduce, Schur, S reduce, point update + next linearization, update reduce, pack /
+    unpack) + the replicated ones measured on the whole problem in the same chain (camera finalize, Cholesky)
+    + the separate decision launch of a multi-rank chain (`decide_us`) + two all-reduces per iteration (the
+    packed band with its tail, the step scalars) priced at `allreduce_us` each plus the band at `band_gbs`
+    (assumptions, not measurements: RCCL over xGMI is not measurable on this 1-GPU box).  The slowest shard sets
+    the pace."""
     from slamgpu import ba
     from slamgpu.capi import default_solver_options
-    rep_ms = sum(full_kernel_ms.get(k, 0.0) for k in REPLICATED)
-    one_ms = sum(full_kernel_ms.values())
-    out = {"n": [1], "ms_per_iter": [one_ms], "speedup": [1.0], "replicated_ms": rep_ms,
-           "shard_compute_ms": [one_ms - rep_ms], "allreduce_ms": [0.0]}
-    for n in ns:
-        worst = 0.0
-        band = None
-        for r in range(n):
-            sh = ba.shard_problem(full, r, n)
-            g = ba.BundleAdjuster(device=local)
-            g.load(sh)
-            if band is None:
-                info = g.info()
-                band = 8.0 * info["n"] * min(info["n"], 16 * (info["band_tiles"] + 1))
-            g.begin(default_solver_options(max_num_iterations=warmup + steps + 4, disable_termination=1,
-                                           always_linearize=1))
-            g.iterate(warmup)
-            g.sync()
-            g.set_timing(True)
-            g.iterate(steps)
-            g.sync()
-            kt = g.kernel_times()
-            g.close()
-            shard_ms = sum(v[0] * v[1] for k, v in kt.items() if k not in REPLICATED) / steps
-            worst = max(worst, shard_ms)
-        ar_ms = 3 * allreduce_us * 1e-3 + band / (band_gbs * 1e9) * 1e3
-        t = worst + rep_ms + ar_ms
-        out["n"].append(n)
-        out["shard_compute_ms"].append(worst)
-        out["allreduce_ms"].append(ar_ms)
-        out["ms_per_iter"].append(t)
-        out["speedup"].append(one_ms / t)
-    out["assumptions"] = ("all-reduce %.0f us each (3 per iteration) + the packed band at %.0f GB/s; the slowest "
-                          "shard's measured shardable kernels + the whole problem's replicated kernels (%s)"
-                          % (allreduce_us, band_gbs, ", ".join(REPLICATED)))
+
+    def per_iter(prob):
+        g = ba.BundleAdjuster(device=local)
+        g.load(prob)
+        info = g.info()
+        g.begin(default_solver_options(max_num_iterations=warmup + steps + 4, disable_termination=1,
+                                       always_linearize=1))
+        g.iterate(warmup)
+        g.sync()
+        g.set_timing(True)
+        g.iterate(steps)
+        g.sync()
+        kt = g.kernel_times()
+        g.close()
+        return {k: v[0] * v[1] / steps for k, v in kt.items()}, info
+
+    old = os.environ.get("SG_XCHG_MERGE")
+    os.environ["SG_XCHG_MERGE"] = "force"
+    try:
+        full_ms, info = per_iter(full)
+        rep_ms = sum(full_ms.get(k, 0.0) for k in REPLICATED) + decide_us * 1e-3
+        band = 8.0 * info["n"] * min(info["n"], 16 * (info["band_tiles"] + 1)) + 8.0 * 2 * info["n"]
+        one_ms = sum(full_kernel_ms.values())
+        out = {"n": [1], "ms_per_iter": [one_ms], "speedup": [1.0], "replicated_ms": rep_ms,
+               "replicated_kernels_ms": {k: full_ms.get(k, 0.0) for k in REPLICATED},
+               "shard_compute_ms": [one_ms - sum(full_kernel_ms.get(k, 0.0) for k in REPLICATED)],
+               "allreduce_ms": [0.0], "exchanges_per_iteration": 2}
+        for n in ns:
+            worst = 0.0
+            for r in range(n):
+                ms, _ = per_iter(ba.shard_problem(full, r, n))
+                worst = max(worst, sum(v for k, v in ms.items() if k not in REPLICATED))
+            ar_ms = 2 * allreduce_us * 1e-3 + band / (band_gbs * 1e9) * 1e3
+            t = worst + rep_ms + ar_ms
+            out["n"].append(n)
+            out["shard_compute_ms"].append(worst)
+            out["allreduce_ms"].append(ar_ms)
+            out["ms_per_iter"].append(t)
+            out["speedup"].append(one_ms / t)
+    finally:
+        if old is None:
+            del os.environ["SG_XCHG_MERGE"]
+        else:
+            os.environ["SG_XCHG_MERGE"] = old
+    out["assumptions"] = ("2 all-reduces per iteration at %.0f us each + the packed band and tail at %.0f GB/s, a "
+                          "separate decision launch of %.0f us; the slowest shard's measured shardable kernels "
+                          "(multi-rank chain forced on one rank) + the whole problem's replicated kernels (%s)"
+                          % (allreduce_us, band_gbs, decide_us, ", ".join(REPLICATED)))
     return out
 
 

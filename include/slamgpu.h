@@ -245,6 +245,8 @@ typedef struct sg_ba_info {
   int32_t rank, nranks;
   int32_t cholesky_split;                    /* tiled path: tile rows factored bottom-up by a second workgroup
                                                 (dissected band; 0: one workgroup) */
+  int32_t num_allreduces;                    /* landmark-shard sum all-reduces this handle has issued in LM
+                                                iterations (0 on one rank) */
 } sg_ba_info;
 int sg_ba_info_get(const sg_ba* h, sg_ba_info* out);
 

@@ -5,9 +5,11 @@
 // window BA):
 //   q[2][4F], t[2][3F], X[2][4P]   parameter state, two slots (current / candidate), switched by LmState::cur
 //   obs_pt[2M], obs_frame[M]       observations, CSR by point (poff[P+1])
-//   J[M/64][12][64] (double2)      corrected, unscaled residual + Jacobian per observation, element pairs
-//                                  (r~ 2 | Jc 2x6 [rot_local 3, t 3] | Jp 2x4 | pad 2)
-//   V[P][10], g[P][4]              point normal-equation blocks (upper 4x4) and gradient
+//   J[2][M/64][12][64] (double2)   corrected, unscaled residual + Jacobian per observation, element pairs
+//                                  (r~ 2 | Jc 2x6 [rot_local 3, t 3] | Jp 2x4 | pad 2), one slot per parameter
+//                                  slot: the linearization at x[cur], and the one k_update_lin forms at the
+//                                  candidate x[cur ^ 1] (it becomes current when the step is accepted)
+//   V[2][P][10], g[2][P][4]        point normal-equation blocks (upper 4x4) and gradient, slotted like J
 //   Vinv[P][10], tp[P][4]          damped, scaled inverse and V^-1 g~ (per LM iteration)
 //   cam_slab / S_slab              per-chunk partial camera blocks / per-segment Schur tiles (deterministic
 //                                  reduce)
@@ -113,6 +115,7 @@ struct LinChunk {
   int32_t cam_off;    // offset of this chunk's camera partials in cam_slab (doubles)
   int32_t wide;       // one point: camera terms by global atomics, point block reduced over the workgroup
   int32_t p0, p1;
+  int32_t u0;         // its first k_point_update work unit (one per round; one for a wide chunk)
 };
 
 struct LmState {
@@ -162,10 +165,11 @@ struct Dev {
   double* fd_J;                  // [D][6] corrected, unscaled: d/dt_a, d/dt_b
   double* fd_D;                  // [NB][9] FD diagonal (trans) block, unscaled
   double* fd_X;                  // [D][9] FD cross block J_a J_b^T, unscaled
-  // linearization
-  double* J;
-  double* V;
-  double* g;
+  // linearization, two slots (s = LmState::cur: the current point; cur ^ 1: k_update_lin's candidate)
+  double* J[2];
+  double* V[2];
+  double* g[2];
+  int32_t spec;                  // speculative linearization: k_update_lin linearizes at every candidate
   double* scale_p;
   double* diag_p;
   double* Vinv;
@@ -183,13 +187,18 @@ struct Dev {
   int32_t nstile;
   const int32_t* r_loff;         // [NB+1] CSR: per block, offsets of its rhs partials in S_slab
   const int32_t* r_lidx;
-  double* cam_slab;
+  double* cam_slab[2];
   double* S_slab;
   double* chunk_scal;            // [npu][kNScal] k_point_update scalars (per work unit)
-  double* cam_wide;              // [NB][27] (wide chunks, global atomics)
+  double* cam_wide[2];           // [NB][27] (wide chunks, global atomics)
   double* S_wide;                // [n][n]   (wide chunks, global atomics)
   // exchange buffers (all-reduced across landmark shards)
   double* xchg_cam;              // [NB*27 + kXNum + nranks]: camera blocks, scalars, per-rank max |g| slots
+                                 // (summed over the shards by the camera-block all-reduce)
+  double* xcam_loc;              // the same, this rank's own (never all-reduced)
+  double* xtail;                 // merged exchange tail after the packed band of S (k_cam_finalize modes 1, 2):
+                                 // camera gradient [6 NB] | diagonal [6 NB] | scalars [kXNum] | max |g| [nranks]
+                                 // | FrameDistance cost
   int32_t rank, nranks;          // landmark shard of this solver
   double* S;                     // [n][n] reduced system (upper blocks), then its factor
   double* rhs;                   // [n]
@@ -206,7 +215,7 @@ struct Dev {
   const LinRound* lrounds;
   const uint16_t* llist;         // per round: window-block offsets + local observation indices by block
   int32_t nlin;
-  double* lin_scal;              // [nlin][kNScal] k_linearize scalars (cost, failures, |x|^2, max |g|)
+  double* lin_scal[2];           // [nlin][kNScal] k_linearize scalars (cost, failures, |x|^2, max |g|)
   const int32_t* pu_units;       // [npu] k_point_update work units: round index, or -(chunk + 1) (wide chunk)
   int32_t npu;
   const struct SchurSeg* segs;   // [nseg] Schur work units

@@ -104,6 +104,16 @@ class BaSolver {
   // per tile row; needs the look-ahead): SG_CHOL_DATAFLOW=1
   bool chol_dataflow_ = getenv("SG_CHOL_DATAFLOW") && atoi(getenv("SG_CHOL_DATAFLOW")) == 1;
   bool pack_force_ = getenv("SG_PACK_S") != nullptr;   // pack/unpack S on one rank too (tests the path)
+  // speculative linearization (k_update_lin: the candidate pass linearizes at the candidate; k_linearize runs
+  // only in a solve's first iteration); SG_SPEC=0: k_point_update + k_linearize every iteration
+  bool spec_ = !(getenv("SG_SPEC") && atoi(getenv("SG_SPEC")) == 0);
+  size_t jslot_ = 0, cslot_ = 0;   // doubles per slot of J and cam_slab
+  // merged exchange of landmark shards (ba_solver.hip, EnqueueIterations): 1 default (shards), 0 off (SG_XCHG_MERGE=0),
+  // 2 forced on one rank too (SG_XCHG_MERGE=force, tests)
+  int merge_ = getenv("SG_XCHG_MERGE") ? (std::string(getenv("SG_XCHG_MERGE")) == "force" ? 2 : atoi(getenv("SG_XCHG_MERGE")) != 0)
+                                       : 1;
+  size_t ntail_ = 0;   // doubles of the merged exchange's tail
+  int32_t nallreduce_ = 0;   // landmark-shard all-reduces issued (sg_ba_info.num_allreduces)
   size_t npack_ = 0;                                      // band of S + rhs, doubles (all-reduce size)
   bool stamp_on_ = false;
   int ncu_ = 256;                       // compute units (Schur segment count), queried once

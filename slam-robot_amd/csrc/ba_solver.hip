@@ -154,17 +154,17 @@ __device__ __forceinline__ int wp(int i, int j, int nb) { return i * nb - i * (i
 // lanes reading (or writing) one element pair of 64 consecutive observations touch one contiguous KiB instead
 // of a 16-byte piece of 64 different 192-byte records.
 __device__ __forceinline__ size_t jidx2(int o, int e2) { return ((size_t)(o >> 6) * 12 + e2) * 64 + (o & 63); }
-__device__ __forceinline__ double2 jload2(const Dev& d, int o, int e2) {
-  return reinterpret_cast<const double2*>(d.J)[jidx2(o, e2)];
+__device__ __forceinline__ double2 jload2(const double* J, int o, int e2) {
+  return reinterpret_cast<const double2*>(J)[jidx2(o, e2)];
 }
 
 // Load the corrected Jacobian of observation o and apply Jacobi scaling.
-__device__ __forceinline__ void load_scaled_J(const Dev& d, int o, int b, const double* sp, double* r,
-                                              double* Jc, double* Jp) {
+__device__ __forceinline__ void load_scaled_J(const Dev& d, const double* J, int o, int b, const double* sp,
+                                              double* r, double* Jc, double* Jp) {
   double buf[22];
 #pragma unroll
   for (int i = 0; i < 11; ++i) {
-    const double2 v = jload2(d, o, i);
+    const double2 v = jload2(J, o, i);
     buf[2 * i] = v.x;
     buf[2 * i + 1] = v.y;
   }
@@ -323,7 +323,7 @@ __global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_linearize(Dev d) {
       double rr[2], Jc[12], Jp[8], c;
       const bool ok = LinearizeObservation(d.q[cur] + 4 * f, d.t[cur] + 3 * f, d.k[cur] + 7 * meta_cam(m), X, pt,
                                            d.b, d.inv_b, rr, Jc, Jp, &c);
-      double2* Jo = reinterpret_cast<double2*>(d.J) + jidx2(o, 0);   // pair e2 at Jo[64 e2]
+      double2* Jo = reinterpret_cast<double2*>(d.J[cur]) + jidx2(o, 0);   // pair e2 at Jo[64 e2]
       if (!ok || fx) {
         if (!ok) {
           if (fx) lsum[2][lane] += 1.0;
@@ -374,7 +374,7 @@ __global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_linearize(Dev d) {
               atomicAdd(dst + 21 + a, Jc[a] * rr[0] + Jc[6 + a] * rr[1]);
             }
           };
-          if (ch.wide) add_cam(d.cam_wide + (size_t)b * kCamV);
+          if (ch.wide) add_cam(d.cam_wide[cur] + (size_t)b * kCamV);
           else add_cam(camacc + (b - ch.b_lo) * kCamV);
         }
       }
@@ -394,10 +394,10 @@ __global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_linearize(Dev d) {
 #pragma unroll
         for (int i = 0; i < 14; ++i) pa[i] = 0.0;
         const bool pf = d.pfree[pp] != 0;
-        double2* Vd = reinterpret_cast<double2*>(d.V + 10 * (size_t)pp);
+        double2* Vd = reinterpret_cast<double2*>(d.V[cur] + 10 * (size_t)pp);
 #pragma unroll
         for (int k = 0; k < 5; ++k) Vd[k] = make_double2(V[2 * k], V[2 * k + 1]);
-        reinterpret_cast<double4*>(d.g)[pp] = make_double4(g[0], g[1], g[2], g[3]);
+        reinterpret_cast<double4*>(d.g[cur])[pp] = make_double4(g[0], g[1], g[2], g[3]);
         if (pf) {
           gmax = fmax(gmax, fmax(fmax(fabs(g[0]), fabs(g[1])), fmax(fabs(g[2]), fabs(g[3]))));
           if (first) {
@@ -415,7 +415,7 @@ __global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_linearize(Dev d) {
     }
   }
   lds_fence_wave();
-  for (int i = lane; i < ncv; i += kLinThreads) d.cam_slab[ch.cam_off + i] = camacc[i];
+  for (int i = lane; i < ncv; i += kLinThreads) d.cam_slab[cur][ch.cam_off + i] = camacc[i];
   cost = wave_sum_full(cost);
   const double fail = wave_sum_full(lsum[0][lane]);
   const double fixed = wave_sum_full(lsum[1][lane]);
@@ -423,7 +423,7 @@ __global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_linearize(Dev d) {
   const double xn2 = wave_sum_full(lsum[3][lane]);
   gmax = wave_max(gmax);
   if (lane == 0) {
-    double* sc = d.lin_scal + blockIdx.x;   // structure of arrays: slot j at [j * nlin + chunk]
+    double* sc = d.lin_scal[cur] + blockIdx.x;   // structure of arrays: slot j at [j * nlin + chunk]
     const size_t ns = d.nlin;
     sc[kCost * ns] = cost;
     sc[kFail * ns] = fail;
@@ -445,6 +445,7 @@ __global__ __launch_bounds__(kRedThreads) void k_cam_reduce(Dev d) {
   if (st->done || !st->need_lin) return;
   const int tid = threadIdx.x;
   const int nv = d.NB * kCamV;
+  const int cur = st->cur;
   if ((int)blockIdx.x < d.NB) {
     const int b = blockIdx.x;
     __shared__ double part[kCamSlices][kCamV];
@@ -459,7 +460,7 @@ __global__ __launch_bounds__(kRedThreads) void k_cam_reduce(Dev d) {
 #pragma unroll
         for (int u = 0; u < kU; ++u) ix[u] = d.cam_lidx[jb + u * kCamSlices < j1 ? jb + u * kCamSlices : 0];   // unconditional
 #pragma unroll
-        for (int u = 0; u < kU; ++u) v[u] = d.cam_slab[ix[u] + e];
+        for (int u = 0; u < kU; ++u) v[u] = d.cam_slab[cur][ix[u] + e];
 #pragma unroll
         for (int u = 0; u < kU; ++u)
           if (jb + u * kCamSlices < j1) acc += v[u];
@@ -469,11 +470,14 @@ __global__ __launch_bounds__(kRedThreads) void k_cam_reduce(Dev d) {
     __syncthreads();
     if (tid < kCamV) {
       const int i = b * kCamV + tid;
-      double s = d.cam_wide[i];
-      d.cam_wide[i] = 0.0;
+      double s = d.cam_wide[cur][i];
+      // (speculative mode: kept, a re-reduce after a rejected step reads it again; k_S_reduce clears the
+      // candidate slot before k_update_lin accumulates into it)
+      if (!d.spec) d.cam_wide[cur][i] = 0.0;
 #pragma unroll
       for (int k = 0; k < kCamSlices; ++k) s += part[k][tid];
-      d.xchg_cam[i] = s;
+      d.xchg_cam[i] = s;   // summed over the shards (camera-block all-reduce) or left as this rank's
+      d.xcam_loc[i] = s;   // this rank's own (k_S_reduce's local assembly, k_cam_finalize mode 1)
     }
     return;
   }
@@ -489,7 +493,7 @@ __global__ __launch_bounds__(kRedThreads) void k_cam_reduce(Dev d) {
 #pragma unroll
     for (int u = 0; u < kScalU; ++u) {
       const int c = c0 + u * kRedThreads;
-      const double* sc = d.lin_scal + (c < d.nlin ? c : 0);   // coalesced: slot j at [j * nlin + chunk]
+      const double* sc = d.lin_scal[cur] + (c < d.nlin ? c : 0);   // coalesced: slot j at [j * nlin + chunk]
       const size_t ns = d.nlin;
       t[u][kXCost] = sc[kCost * ns];
       t[u][kXFail] = sc[kFail * ns];
@@ -510,9 +514,9 @@ __global__ __launch_bounds__(kRedThreads) void k_cam_reduce(Dev d) {
   gm = block_max<kRedThreads>(gm, redm);
   if (tid == 0) {
 #pragma unroll
-    for (int j = 0; j < kXNum; ++j) d.xchg_cam[nv + j] = v[j];
+    for (int j = 0; j < kXNum; ++j) d.xchg_cam[nv + j] = d.xcam_loc[nv + j] = v[j];
     // max |g| travels in the same sum all-reduce: one slot per rank, zeros in the others' slots
-    for (int r = 0; r < d.nranks; ++r) d.xchg_cam[nv + kXNum + r] = (r == d.rank) ? gm : 0.0;
+    for (int r = 0; r < d.nranks; ++r) d.xchg_cam[nv + kXNum + r] = d.xcam_loc[nv + kXNum + r] = (r == d.rank) ? gm : 0.0;
   }
 }
 
@@ -524,7 +528,66 @@ __global__ __launch_bounds__(kRedThreads) void k_cam_reduce(Dev d) {
 // pass's exchange-buffer operands are loaded before the FrameDistance pass.
 constexpr int kFinFdSh = 256;    // FrameDistance residuals held in LDS (more: re-read from global)
 constexpr int kFinNSh = 1536;    // frame columns held in LDS (more: re-read from global)
-__global__ __launch_bounds__(256) void k_cam_finalize(Dev d) {
+// Ceres TrustRegionMinimizer bookkeeping of a linearized iteration (thread 0, on a register copy of LmState):
+// iteration 0's cost / fixed cost / failures / gradient tolerance, or a later iteration's push.
+__device__ __forceinline__ void fin_push(LmState& s0, bool first, double cost, double gmax, const double* xs,
+                                         double xn2c) {
+  if (first) {
+    s0.fixed_cost = xs[kXFixed];
+    if (xs[kXFixedFail] > 0.0) {
+      s0.done = 1; s0.ok = 0; s0.termination = SG_DID_NOT_RUN;
+    } else if (xs[kXFail] > 0.0) {
+      s0.done = 1; s0.ok = 0; s0.termination = SG_NUMERICAL_FAILURE;
+    } else {
+      s0.cost = cost;
+      s0.initial_cost = cost + s0.fixed_cost;
+      s0.abs_gtol = s0.gtol * gmax;
+      s0.pushed = 1;
+      s0.min_pushed_cost = cost;
+      s0.x_norm = sqrt(xs[kXXnorm2] + xn2c);
+      if (gmax <= s0.abs_gtol && !s0.disable_term) {
+        s0.done = 1; s0.ok = 1; s0.termination = SG_GRADIENT_TOLERANCE;
+      }
+    }
+    s0.first = 0;
+  } else {
+    if (xs[kXFail] > 0.0) {
+      s0.done = 1; s0.ok = 0; s0.termination = SG_NUMERICAL_FAILURE;
+    } else {
+      s0.cost = cost;
+      if (!s0.disable_term && gmax <= s0.abs_gtol) {
+        s0.done = 1; s0.ok = 1; s0.termination = SG_GRADIENT_TOLERANCE;
+      } else if (!s0.disable_term && s0.radius < s0.min_radius) {
+        s0.done = 1; s0.ok = 1; s0.termination = SG_PARAMETER_TOLERANCE;
+      } else {
+        s0.pushed += 1;
+        s0.min_pushed_cost = fmin(s0.min_pushed_cost, cost);
+      }
+    }
+  }
+  s0.need_lin = 0;
+}
+
+// The max-iteration tests and the LM iteration count (every iteration, linearized or not).
+__device__ __forceinline__ void fin_count(LmState& s0) {
+  if (!s0.done) {
+    if (!s0.disable_term && s0.pushed - 1 >= s0.max_iter) {
+      s0.done = 1; s0.ok = 1; s0.termination = SG_NO_CONVERGENCE;
+    } else if (s0.disable_term && s0.lm_iters >= s0.max_iter) {
+      s0.done = 1; s0.ok = 1; s0.termination = SG_NO_CONVERGENCE;
+    }
+  }
+  if (!s0.done) s0.lm_iters += 1;
+}
+
+// mode 0: everything, on the summed camera blocks (one rank, or landmark shards after the camera-block
+//         all-reduce: a solve's first iteration, which fixes the Jacobi scale);
+// mode 1: landmark shards after the first iteration, before the merged exchange — this rank's camera gradient
+//         and diagonal (its own blocks; the FrameDistance terms on rank 0) for k_S_reduce's local assembly and
+//         into the exchange tail with the cost scalars; no bookkeeping;
+// mode 2: after the merged exchange (every rank, identically): the bookkeeping on the summed tail, the LM
+//         diagonal, and the damping D^2 / radius added to the summed S (k_S_reduce's local assembly leaves it out).
+__global__ __launch_bounds__(256) void k_cam_finalize(Dev d, int mode) {
   LmState* st = d.st;
   __shared__ double red[4];
   __shared__ double fdcost[256];
@@ -535,13 +598,19 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d) {
   const int nv = d.NB * kCamV;
   const int nf = 6 * d.NB;
   const bool fd_lds = d.D <= kFinFdSh, n_lds = nf <= kFinNSh;
+  // exchange tail (modes 1, 2): camera gradient [nf] | camera diagonal [nf] | scalars [kXNum] | per-rank max |g|
+  // [nranks] | FrameDistance cost
+  double* tg = d.xtail;
+  double* tdg = d.xtail + nf;
+  double* txs = d.xtail + 2 * nf;
+  const double* U0 = mode == 1 ? d.xcam_loc : d.xchg_cam;
   // block pass operands of block tid (the common case NB <= 256) and the first FrameDistance pair: their
   // loads go out beside LmState's (see k_S_reduce) and stay in flight during the FrameDistance pass
   double Ug[6], Ud[6];
   int e0 = 0, e1 = 0;
   const int b0 = tid < d.NB ? tid : 0;
-  {
-    const double* U = d.xchg_cam + (size_t)b0 * kCamV;
+  if (mode != 2) {
+    const double* U = U0 + (size_t)b0 * kCamV;
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
       Ug[a] = U[21 + a];
@@ -560,10 +629,53 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d) {
   const int cur = st->cur;
   const bool lin = st->need_lin, first = st->first, jacobi = st->jacobi;
   if (st->done) return;
+  if (mode == 2) {
+    if (lin) {
+      // gradient max-norm over the free camera columns of the summed gradient, and the per-rank point maxima
+      double gm = 0.0;
+      for (int f = tid; f < d.F; f += blockDim.x) {
+        const int b = d.frame_block[f];
+        if (b < 0) continue;
+        if (d.rot_free[f])
+          for (int a = 0; a < 3; ++a) gm = fmax(gm, fabs(tg[6 * b + a]));
+        if (d.trans_free[f])
+          for (int a = 3; a < 6; ++a) gm = fmax(gm, fabs(tg[6 * b + a]));
+      }
+      gm = block_max<256>(gm, red);
+      if (tid == 0) {
+        double gmax = gm;
+        for (int r = 0; r < d.nranks; ++r) gmax = fmax(gmax, txs[kXNum + r]);
+        fin_push(s0, false, txs[kXCost] + txs[kXNum + d.nranks], gmax, txs, 0.0);
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      fin_count(s0);
+      done_sh = s0.done;
+      *st = s0;
+    }
+    __syncthreads();
+    if (done_sh) return;
+    const double radius = st->radius;
+    const bool reuse = st->reuse_diag;
+    for (int i = tid; i < d.n; i += blockDim.x) {
+      double dg;
+      if (!reuse) {
+        const double s = d.scale_c[i];
+        dg = fmin(fmax(s * s * tdg[i], st->min_diag), st->max_diag);
+        d.diag_c[i] = dg;
+      } else {
+        dg = d.diag_c[i];
+      }
+      d.S[(size_t)i * d.n + i] += dg / radius;
+    }
+    return;
+  }
+  const bool fd_here = mode == 0 || d.rank == 0;   // mode 1: the FrameDistance terms enter on rank 0 only
   if (lin) {
     // FrameDistance residuals at x[cur]
     double myfd = 0.0;
-    for (int dd = tid; dd < d.D; dd += blockDim.x) {
+    for (int dd = tid; dd < (fd_here ? d.D : 0); dd += blockDim.x) {
       const int fa = dd == tid ? fa0 : d.fd_a[dd], fb = dd == tid ? fb0 : d.fd_b[dd];
       const double* ta = d.t[cur] + 3 * fa;
       const double* tb = d.t[cur] + 3 * fb;
@@ -605,7 +717,7 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d) {
     double gm = 0.0, xn2c = 0.0;
     for (int b = tid; b < d.NB; b += blockDim.x) {
       if (b != tid) {   // NB > 256: operands not prefetched
-        const double* U = d.xchg_cam + (size_t)b * kCamV;
+        const double* U = U0 + (size_t)b * kCamV;
         for (int a = 0; a < 6; ++a) {
           Ug[a] = U[21 + a];
           Ud[a] = U[u6(a, a)];
@@ -615,7 +727,7 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d) {
       }
       double fdD[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
       double gfd[3] = {0, 0, 0};
-      for (int e = e0; e < e1; ++e) {
+      for (int e = fd_here ? e0 : e1; e < e1; ++e) {
         const int dd = d.fd_bidx[e] >> 1, side = d.fd_bidx[e] & 1;
         const double* Jd = fd_lds ? fdJs + 6 * dd + 3 * side : d.fd_J + 6 * dd + 3 * side;
         const double rr = fd_lds ? fdrs[dd] : d.fd_r[dd];
@@ -624,17 +736,28 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d) {
           for (int j = 0; j < 3; ++j) fdD[3 * i + j] += Jd[i] * Jd[j];
         }
       }
-      for (int i = 0; i < 9; ++i) d.fd_D[9 * b + i] = fdD[i];
+      if (fd_here)
+        for (int i = 0; i < 9; ++i) d.fd_D[9 * b + i] = fdD[i];
       for (int a = 0; a < 6; ++a) {
         const double gg = Ug[a] + (a >= 3 ? gfd[a - 3] : 0.0);
         const double dg = Ud[a] + (a >= 3 ? fdD[4 * (a - 3)] : 0.0);
         d.camg[6 * b + a] = gg;
         d.camdiag[6 * b + a] = dg;
+        if (mode == 1) {
+          tg[6 * b + a] = gg;
+          tdg[6 * b + a] = dg;
+        }
         if (n_lds) {
           gsh[6 * b + a] = gg;
           dgsh[6 * b + a] = dg;
         }
       }
+    }
+    if (mode == 1) {
+      // this rank's cost scalars and max |g| slots, and the FrameDistance cost (rank 0), into the tail
+      if (tid < kXNum + d.nranks) txs[tid] = d.xcam_loc[nv + tid];
+      if (tid == 0) txs[kXNum + d.nranks] = fd_total;
+      return;
     }
     __syncthreads();
     // gradient max-norm over free camera columns; camera part of |x| at iteration 0
@@ -664,57 +787,20 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d) {
       }
     }
     if (tid == 0) {
-      const double fd = fd_total;
       const double* xs = d.xchg_cam + nv;
-      const double cost = xs[kXCost] + fd;
       double gmax = gm;
       for (int r = 0; r < d.nranks; ++r) gmax = fmax(gmax, xs[kXNum + r]);
-      if (first) {
-        s0.fixed_cost = xs[kXFixed];
-        if (xs[kXFixedFail] > 0.0) {
-          s0.done = 1; s0.ok = 0; s0.termination = SG_DID_NOT_RUN;
-        } else if (xs[kXFail] > 0.0) {
-          s0.done = 1; s0.ok = 0; s0.termination = SG_NUMERICAL_FAILURE;
-        } else {
-          s0.cost = cost;
-          s0.initial_cost = cost + s0.fixed_cost;
-          s0.abs_gtol = s0.gtol * gmax;
-          s0.pushed = 1;
-          s0.min_pushed_cost = cost;
-          s0.x_norm = sqrt(xs[kXXnorm2] + xn2c);
-          if (gmax <= s0.abs_gtol && !s0.disable_term) {
-            s0.done = 1; s0.ok = 1; s0.termination = SG_GRADIENT_TOLERANCE;
-          }
-        }
-        s0.first = 0;
-      } else {
-        if (xs[kXFail] > 0.0) {
-          s0.done = 1; s0.ok = 0; s0.termination = SG_NUMERICAL_FAILURE;
-        } else {
-          s0.cost = cost;
-          if (!s0.disable_term && gmax <= s0.abs_gtol) {
-            s0.done = 1; s0.ok = 1; s0.termination = SG_GRADIENT_TOLERANCE;
-          } else if (!s0.disable_term && s0.radius < s0.min_radius) {
-            s0.done = 1; s0.ok = 1; s0.termination = SG_PARAMETER_TOLERANCE;
-          } else {
-            s0.pushed += 1;
-            s0.min_pushed_cost = fmin(s0.min_pushed_cost, cost);
-          }
-        }
-      }
-      s0.need_lin = 0;
+      fin_push(s0, first, xs[kXCost] + fd_total, gmax, xs, xn2c);
     }
+  }
+  if (mode == 1) {
+    // not linearized (a rejected step): the tail is not read after the exchange; keep it finite
+    for (int i = tid; i < 2 * nf + kXNum + d.nranks + 1; i += blockDim.x) d.xtail[i] = 0.0;
+    return;
   }
   __syncthreads();
   if (tid == 0) {
-    if (!s0.done) {
-      if (!s0.disable_term && s0.pushed - 1 >= s0.max_iter) {
-        s0.done = 1; s0.ok = 1; s0.termination = SG_NO_CONVERGENCE;
-      } else if (s0.disable_term && s0.lm_iters >= s0.max_iter) {
-        s0.done = 1; s0.ok = 1; s0.termination = SG_NO_CONVERGENCE;
-      }
-    }
-    if (!s0.done) s0.lm_iters += 1;
+    fin_count(s0);
     done_sh = s0.done;
     *st = s0;
   }
@@ -750,20 +836,20 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d) {
 //      segment) add the cells' rhs terms.
 // Points spanning more than kSegNbMax blocks take k_schur_wide (observation pairs, global atomics).
 
-__device__ __forceinline__ void load_Jc_scaled(const Dev& d, int o, int b, double* Jc) {
+__device__ __forceinline__ void load_Jc_scaled(const Dev& d, const double* J, int o, int b, double* Jc) {
   const double* sc = d.scale_c + 6 * b;
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
-    const double2 v = jload2(d, o, 1 + i);   // (pair 0: r)
+    const double2 v = jload2(J, o, 1 + i);   // (pair 0: r)
     Jc[2 * i] = v.x * sc[(2 * i) % 6];
     Jc[2 * i + 1] = v.y * sc[(2 * i + 1) % 6];
   }
 }
-__device__ __forceinline__ void load_Jp_scaled(const Dev& d, int o, const double4& s4, double* Jp) {
+__device__ __forceinline__ void load_Jp_scaled(const double* J, int o, const double4& s4, double* Jp) {
   const double sp[4] = {s4.x, s4.y, s4.z, s4.w};
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const double2 v = jload2(d, o, 7 + i);   // (pairs 0-6: r, Jc)
+    const double2 v = jload2(J, o, 7 + i);   // (pairs 0-6: r, Jc)
     Jp[2 * i] = v.x * sp[(2 * i) % 4];
     Jp[2 * i + 1] = v.y * sp[(2 * i + 1) % 4];
   }
@@ -774,13 +860,13 @@ __device__ __forceinline__ void load_Jp_scaled(const Dev& d, int o, const double
 // diag_p go to global memory for k_point_update.  Returns false when V~ is not positive definite (Vi, Li NaN).
 __device__ __forceinline__ bool point_block(const Dev& d, const LmState* st, int p, double* Vi, double* Li,
                                             double* w) {
-  const double* Vp = d.V + 10 * (size_t)p;
+  const double* Vp = d.V[st->cur] + 10 * (size_t)p;
   double V[10];
 #pragma unroll
   for (int i = 0; i < 10; ++i) V[i] = Vp[i];
   const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
   const double sp[4] = {s4.x, s4.y, s4.z, s4.w};
-  const double4 g4 = reinterpret_cast<const double4*>(d.g)[p];
+  const double4 g4 = reinterpret_cast<const double4*>(d.g[st->cur])[p];
   const double gs[4] = {g4.x * sp[0], g4.y * sp[1], g4.z * sp[2], g4.w * sp[3]};
   double dp[4];
   if (!st->reuse_diag) {
@@ -879,11 +965,11 @@ struct CellOps {
   double4 s4;
   double sc[6];
 };
-__device__ __forceinline__ void cell_load(const Dev& d, int o, int b, int p, CellOps& c) {
+__device__ __forceinline__ void cell_load(const Dev& d, const double* J, int o, int b, int p, CellOps& c) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) c.jp[i] = jload2(d, o, 7 + i);   // (pairs 0-6: r, Jc)
+  for (int i = 0; i < 4; ++i) c.jp[i] = jload2(J, o, 7 + i);   // (pairs 0-6: r, Jc)
 #pragma unroll
-  for (int i = 0; i < 6; ++i) c.jc[i] = jload2(d, o, 1 + i);   // (pair 0: r)
+  for (int i = 0; i < 6; ++i) c.jc[i] = jload2(J, o, 1 + i);   // (pair 0: r)
   c.s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
 #pragma unroll
   for (int i = 0; i < 6; ++i) c.sc[i] = d.scale_c[6 * b + i];
@@ -931,7 +1017,8 @@ __device__ __forceinline__ void cell_apply(const CellOps& c, const double* L, in
       for (int a = 0; a < 6; ++a) at(col0 + a, kk) += G[kk][0] * Jc[a] + G[kk][1] * Jc[6 + a];
   }
 }
-__device__ __forceinline__ void schur_cells(const Dev& d, const SchurBatch& B, int tid, int c0w, const double* Lsh,
+__device__ __forceinline__ void schur_cells(const Dev& d, const double* J, const SchurBatch& B, int tid, int c0w,
+                                            const double* Lsh,
                                             const int4* pinf, const int2* pob, const uint8_t* cmap, double* Xb) {
   const int ncell = B.c1 - B.c0;
   constexpr int kStride = 64 * kSchurCellWaves;
@@ -956,7 +1043,7 @@ __device__ __forceinline__ void schur_cells(const Dev& d, const SchurBatch& B, i
         if (po.x >= 0) {
           simple[h] = true;
           oc[h] = po.x + (bc[h] - pi.x);
-          cell_load(d, oc[h], bc[h], B.p0 + t, ops[h]);
+          cell_load(d, J, oc[h], bc[h], B.p0 + t, ops[h]);
         }
       }
     }
@@ -998,7 +1085,7 @@ __device__ __forceinline__ void schur_cells(const Dev& d, const SchurBatch& B, i
       for (int k = k1 - 1; k < k2; ++k) {
         const int o = k < k1 ? o0 : d.cell_obs[k];
         CellOps c;
-        cell_load(d, o, b, B.p0 + t, c);
+        cell_load(d, J, o, b, B.p0 + t, c);
         cell_apply(c, L, col0, k < k1, at);
       }
     }
@@ -1032,7 +1119,7 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d) {
     SG_SSTAMP(33)
     for (int s = 0; s <= nbt; ++s) {
       if (s < nbt)
-        schur_cells(d, d.sbatch[sg.bt0 + s], tid, c0w, sh.L[s % 3], sh.pinf[s % 3], sh.pob[s % 3], sh.cmap[s % 3],
+        schur_cells(d, d.J[st->cur], d.sbatch[sg.bt0 + s], tid, c0w, sh.L[s % 3], sh.pinf[s % 3], sh.pob[s % 3], sh.cmap[s % 3],
                     sh.X[s & 1]);
       SG_SSTAMP(34)
       __syncthreads();
@@ -1143,12 +1230,13 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur_wide(Dev d) {
   __syncthreads();
   const int obs_lo = d.poff[p], obs_hi = d.poff[p + 1];
   const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
+  const double* Jw = d.J[st->cur];
   for (int o = obs_lo + tid; o < obs_hi; o += kSchurThreads) {
     const int b = d.frame_block[d.obs_frame[o]];
     if (b < 0) continue;
     double Jp[8], Jc[12];
-    load_Jp_scaled(d, o, s4, Jp);
-    load_Jc_scaled(d, o, b, Jc);
+    load_Jp_scaled(Jw, o, s4, Jp);
+    load_Jc_scaled(d, Jw, o, b, Jc);
     const double e0 = Jp[0] * tpv[0] + Jp[1] * tpv[1] + Jp[2] * tpv[2] + Jp[3] * tpv[3];
     const double e1 = Jp[4] * tpv[0] + Jp[5] * tpv[1] + Jp[6] * tpv[2] + Jp[7] * tpv[3];
 #pragma unroll
@@ -1159,10 +1247,10 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur_wide(Dev d) {
     const int os = obs_lo + (pr.x >> 16), ot = obs_lo + (pr.x & 0xffff);
     const int bs = pr.y >> 16, bt = pr.y & 0xffff;
     double Jcs[12], Jct[12], Jpt[8], Jps[8], Ps[8];
-    load_Jc_scaled(d, os, bs, Jcs);
-    load_Jc_scaled(d, ot, bt, Jct);
-    load_Jp_scaled(d, ot, s4, Jpt);
-    load_Jp_scaled(d, os, s4, Jps);
+    load_Jc_scaled(d, Jw, os, bs, Jcs);
+    load_Jc_scaled(d, Jw, ot, bt, Jct);
+    load_Jp_scaled(Jw, ot, s4, Jpt);
+    load_Jp_scaled(Jw, os, s4, Jps);
 #pragma unroll
     for (int rr = 0; rr < 2; ++rr)
 #pragma unroll
@@ -1189,7 +1277,11 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur_wide(Dev d) {
 // and, on the assembling rank, the camera-only terms.  S leaves here damped; elements below the diagonal of a
 // diagonal tile are written as 0 (no factorisation reads them).  Tiles outside the band are never written
 // (zero since the load).
-__global__ __launch_bounds__(256) void k_S_reduce(Dev d) {
+// amode: 0 this rank adds no camera-only terms (landmark shards: ranks > 0 in a solve's first iteration);
+// 1 blockdiag(U) of the summed camera blocks + FrameDistance + damping (one rank; rank 0 of shards in the
+// first iteration); 2 this rank's own camera blocks, the FrameDistance terms on rank 0, no damping (landmark
+// shards after the first iteration: summed with S in one exchange, k_cam_finalize mode 2 adds the damping).
+__global__ __launch_bounds__(256) void k_S_reduce(Dev d, int amode) {
   // LmState is read beside the first work-list loads, not ahead of them: the done test comes after the
   // partial walk (a finished solve's trailing launches walk once more; every other launch saves a round trip)
   const LmState* st = d.st;
@@ -1210,14 +1302,15 @@ __global__ __launch_bounds__(256) void k_S_reduce(Dev d) {
     const double e_acc = (up && d.nwide) ? d.S_wide[gi] : 0.0;
     const int I = i / 6, a = i - 6 * (i / 6), Jb = j / 6, c = j - 6 * (j / 6);
     double e_si = 0.0, e_sj = 0.0, e_u = 0.0, e_fd = 0.0, e_dg = 0.0, e_x = 0.0;
-    if (d.assemble && up) {
+    const bool fd_here = amode == 1 || (amode == 2 && d.rank == 0);
+    if (amode != 0 && up) {
       e_si = d.scale_c[i];
       e_sj = d.scale_c[j];
       if (I == Jb) {
-        e_u = d.xchg_cam[(size_t)I * kCamV + u6(a, c)];
-        e_fd = (a >= 3 && c >= 3) ? d.fd_D[9 * I + 3 * (a - 3) + (c - 3)] : 0.0;
-        e_dg = a == c ? d.diag_c[i] : 0.0;
-      } else if (a >= 3 && c >= 3) {
+        e_u = (amode == 2 ? d.xcam_loc : d.xchg_cam)[(size_t)I * kCamV + u6(a, c)];
+        e_fd = (fd_here && a >= 3 && c >= 3) ? d.fd_D[9 * I + 3 * (a - 3) + (c - 3)] : 0.0;
+        e_dg = (amode == 1 && a == c) ? d.diag_c[i] : 0.0;
+      } else if (fd_here && a >= 3 && c >= 3) {
         const int dd = d.fd_pair[I * d.NB + Jb];
         if (dd >= 0) {
           const double* Xd = d.fd_X + 9 * dd;   // J_a J_b^T, rows: frame a's translation
@@ -1259,7 +1352,7 @@ __global__ __launch_bounds__(256) void k_S_reduce(Dev d) {
     double t = ((wsum[0][tid] + wsum[1][tid]) + wsum[2][tid]) + wsum[3][tid];
     t += e_acc;
     if (d.nwide) d.S_wide[gi] = 0.0;
-    if (d.assemble) {   // assembly_term, from the prefetched operands
+    if (amode != 0) {   // assembly_term, from the prefetched operands
       double v;
       if (I == Jb) {
         v = (e_u + e_fd) * (e_si * e_sj);
@@ -1274,11 +1367,14 @@ __global__ __launch_bounds__(256) void k_S_reduce(Dev d) {
   }
   // rhs block I: one wave per 64-entry chunk of its partial list (in list order), lanes 0..5
   const int I = wv - d.nstile;
+  // speculative linearization: clear block I of the candidate slot's wide-chunk camera accumulator before
+  // k_update_lin adds to it (k_cam_reduce keeps the current slot's)
+  if (d.spec && part == 1 && lane < kCamV) d.cam_wide[st->cur ^ 1][(size_t)I * kCamV + lane] = 0.0;
   const int j0 = d.r_loff[I], j1 = d.r_loff[I + 1];
   const int el = lane < 6 ? lane : 0;
   const int ei = 6 * I + el;
   const double e_acc = d.rhs[ei];
-  const double e_si = d.assemble ? d.scale_c[ei] : 0.0, e_g = d.assemble ? d.camg[ei] : 0.0;
+  const double e_si = amode != 0 ? d.scale_c[ei] : 0.0, e_g = amode != 0 ? d.camg[ei] : 0.0;
   __shared__ double rsum[4][6];
   constexpr int kSR = 32;
   double s = 0.0;
@@ -1301,7 +1397,7 @@ __global__ __launch_bounds__(256) void k_S_reduce(Dev d) {
   if (done || part != 0 || lane >= 6) return;
   s = ((rsum[0][lane] + rsum[1][lane]) + rsum[2][lane]) + rsum[3][lane];
   s += e_acc;
-  if (d.assemble) s += e_si * e_g;   // y = rhs_sub + S g_c
+  if (amode != 0) s += e_si * e_g;   // y = rhs_sub + S g_c
   d.xc[ei] = s;       // local rhs partial (all-reduced with S); the wide accumulator is reset
   d.rhs[ei] = 0.0;
 }
@@ -1603,7 +1699,7 @@ __device__ __forceinline__ void intr_schur_point(const Dev& d, int p, bool act, 
       const double* Jk = d.Jk + 14 * (size_t)o;
       double Jr[8];   // corrected Jp (2x4)
       for (int i = 0; i < 4; ++i) {
-        const double2 v = jload2(d, o, 7 + i);
+        const double2 v = jload2(d.J[d.st->cur], o, 7 + i);
         Jr[2 * i] = v.x;
         Jr[2 * i + 1] = v.y;
       }
@@ -1650,7 +1746,7 @@ __device__ __forceinline__ void intr_schur_point(const Dev& d, int p, bool act, 
       const int m = d.obs_meta[o], b = meta_block(m);
       if ((m & kMetaFixed) || b < 0) continue;
       double r[2], Jc[12], Jp[8];
-      load_scaled_J(d, o, b, sp, r, Jc, Jp);
+      load_scaled_J(d, d.J[d.st->cur], o, b, sp, r, Jc, Jp);
       double Mx[14];   // A_p Y^T (2x7)
       for (int rr = 0; rr < 2; ++rr)
         for (int j = 0; j < 7; ++j) {
@@ -3717,7 +3813,7 @@ struct PuObs {
 };
 
 // pacc == nullptr: the records only (a wide chunk's second walk).
-__device__ __forceinline__ void pu_pass1(const Dev& d, const LinRound& R, int lane, double* pacc, PuObs& ob) {
+__device__ __forceinline__ void pu_pass1(const Dev& d, int cur, const LinRound& R, int lane, double* pacc, PuObs& ob) {
   ob.on = false;
   const int nc = R.o1 - R.o0;
   if (lane >= nc) return;
@@ -3732,7 +3828,7 @@ __device__ __forceinline__ void pu_pass1(const Dev& d, const LinRound& R, int la
   const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
   const double sp[4] = {s4.x, s4.y, s4.z, s4.w};
   double Jc[12];
-  load_scaled_J(d, o, ob.b, sp, ob.r, Jc, ob.Jp);
+  load_scaled_J(d, d.J[cur], o, ob.b, sp, ob.r, Jc, ob.Jp);
   ob.u[0] = ob.u[1] = 0.0;
   if (ob.b >= 0) {
     const double* xc = d.xc + 6 * ob.b;
@@ -3800,7 +3896,7 @@ __device__ __forceinline__ void pu_pass2(const Dev& d, int p0, int p1, int lane,
   if (pf) {
     const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
     const double sp[4] = {s4.x, s4.y, s4.z, s4.w};
-    const double4 g4 = reinterpret_cast<const double4*>(d.g)[p];
+    const double4 g4 = reinterpret_cast<const double4*>(d.g[cur])[p];
     const double rhs[4] = {g4.x * sp[0] - pa[0], g4.y * sp[1] - pa[1], g4.z * sp[2] - pa[2], g4.w * sp[3] - pa[3]};
     const double* Vi = d.Vinv + 10 * (size_t)p;
     double Vl[10];
@@ -3854,7 +3950,7 @@ __global__ __launch_bounds__(kLinThreads) void k_point_update(Dev d) {
     for (int r = ch.r0; r < ch.r1; ++r) {
       const LinRound R = d.lrounds[r];
       PuObs ob;
-      pu_pass1(d, R, lane, pacc, ob);
+      pu_pass1(d, cur, R, lane, pacc, ob);
       lds_fence_wave();
       pu_pass2(d, R.p0, R.p1, lane, cur, nxt, pacc, xps, Xns, step2, candx2);
       lds_fence_wave();
@@ -3864,7 +3960,7 @@ __global__ __launch_bounds__(kLinThreads) void k_point_update(Dev d) {
   } else {
     for (int r = ch.r0; r < ch.r1; ++r) {
       PuObs ob;
-      pu_pass1(d, d.lrounds[r], lane, pacc, ob);
+      pu_pass1(d, cur, d.lrounds[r], lane, pacc, ob);
     }
     lds_fence_wave();
     pu_pass2(d, ch.p0, ch.p1, lane, cur, nxt, pacc, xps, Xns, step2, candx2);
@@ -3872,7 +3968,7 @@ __global__ __launch_bounds__(kLinThreads) void k_point_update(Dev d) {
     for (int r = ch.r0; r < ch.r1; ++r) {
       const LinRound R = d.lrounds[r];
       PuObs ob;
-      pu_pass1(d, R, lane, nullptr, ob);
+      pu_pass1(d, cur, R, lane, nullptr, ob);
       pu_pass3(d, R, lane, nxt, xps, Xns, ob, model, candcost, candfail);
     }
   }
@@ -3889,6 +3985,212 @@ __global__ __launch_bounds__(kLinThreads) void k_point_update(Dev d) {
     sc[kCandFail * ns] = candfail;
     sc[kStep2 * ns] = step2;
     sc[kCandX2 * ns] = candx2;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_update_lin: k_point_update fused with the next linearization (speculative linearization).  The candidate
+// pass projects every observation at x+ = x[cur ^ 1] anyway; here it evaluates the analytic Jacobian there too
+// and writes the candidate's J records, point blocks V / g and camera partials into the other slot (J, V, g,
+// cam_slab, cam_wide, lin_scal [cur ^ 1]).  When the decision accepts the step, cur flips and that slot is the
+// current linearization — Ceres evaluates the Jacobian at the accepted x (slam.cpp:482-521), the same arithmetic
+// at the same point — so no k_linearize launch and no second sweep over the observations follow; a rejected
+// step leaves slot cur as it was (the next iteration re-reduces it when it must re-linearize).
+// Work decomposition: k_linearize's chunks (the candidate camera partials in k_linearize's order), and the
+// update scalars per round (k_point_update's units, in its lane order), so the solve is bitwise the one of
+// k_point_update + k_linearize (test_ba_gpu.py::test_speculative_linearization_is_bitwise_identical).
+
+// One lane's observation of round R: the model term of the current linearization (ob, from pass 1), then
+// project.h + analytic Jacobian + Cauchy corrector at the candidate (k_linearize's body at x[nxt]): the J
+// record into slot nxt, the candidate's point and camera terms into LDS, its cost.
+__device__ __forceinline__ void ul_obs(const Dev& d, const LinRound& R, const LinChunk& ch, int lane, int nxt,
+                                       const PuObs& ob, const double* xps, const double* Xns, double* pacc,
+                                       double* camacc, double (*lsum)[kLinThreads], double& model, double& cost,
+                                       double& candcost, double& candfail) {
+  if (lane >= R.o1 - R.o0) return;
+  const int o = R.o0 + lane;
+  const int m = d.obs_meta[o];
+  const int lp = d.obs_pnt[o] - R.p0;
+  const int f = d.obs_frame[o];
+  const bool fx = (m & kMetaFixed) != 0;
+  if (ob.on) {   // k_point_update pass 3: -(A s).(r + A s / 2)
+    const double* xp = xps + 4 * lp;
+    double m0 = -ob.u[0], m1 = -ob.u[1];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      m0 -= ob.Jp[c] * xp[c];
+      m1 -= ob.Jp[4 + c] * xp[c];
+    }
+    model -= m0 * (ob.r[0] + 0.5 * m0) + m1 * (ob.r[1] + 0.5 * m1);
+  }
+  const double X[4] = {Xns[4 * lp], Xns[4 * lp + 1], Xns[4 * lp + 2], Xns[4 * lp + 3]};
+  const double2 uv = reinterpret_cast<const double2*>(d.obs_pt)[o];
+  const double pt[2] = {uv.x, uv.y};
+  double rr[2], Jc[12], Jp[8], c;
+  const bool ok = LinearizeObservation(d.q[nxt] + 4 * f, d.t[nxt] + 3 * f, d.k[nxt] + 7 * meta_cam(m), X, pt, d.b,
+                                       d.inv_b, rr, Jc, Jp, &c);
+  // the candidate cost as k_point_update sums it (c is project.h's forward value: the same bits as Project)
+  if (!fx) {
+    candfail += ok ? 0.0 : 1.0;
+    candcost += ok ? c : 0.0;
+  }
+  double2* Jo = reinterpret_cast<double2*>(d.J[nxt]) + jidx2(o, 0);   // pair e2 at Jo[64 e2]
+  if (!ok || fx) {
+    if (!ok) lsum[fx ? 1 : 0][lane] += 1.0;   // (a fixed observation's cost counts at iteration 0 only)
+#pragma unroll
+    for (int i = 0; i < kJStride / 2; ++i) Jo[64 * i] = make_double2(0.0, 0.0);
+    return;
+  }
+  cost += c;
+  const bool pf = (m & kMetaPfree) != 0;
+  const int b = meta_block(m);
+  if (b < 0) {
+#pragma unroll
+    for (int i = 0; i < 12; ++i) Jc[i] = 0.0;
+  } else {
+    if (!(m & kMetaRot)) { Jc[0] = Jc[1] = Jc[2] = Jc[6] = Jc[7] = Jc[8] = 0.0; }
+    if (!(m & kMetaTrans)) { Jc[3] = Jc[4] = Jc[5] = Jc[9] = Jc[10] = Jc[11] = 0.0; }
+  }
+  if (!pf) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) Jp[i] = 0.0;
+  }
+  Jo[0] = make_double2(rr[0], rr[1]);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) Jo[64 * (1 + i)] = make_double2(Jc[2 * i], Jc[2 * i + 1]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) Jo[64 * (7 + i)] = make_double2(Jp[2 * i], Jp[2 * i + 1]);
+  Jo[64 * 11] = make_double2(c, 0.0);
+  if (pf) {
+    double* pa = pacc + lp * 14;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc)
+        if (cc >= a) atomicAdd(pa + u4(a, cc), Jp[a] * Jp[cc] + Jp[4 + a] * Jp[4 + cc]);
+      atomicAdd(pa + 10 + a, Jp[a] * rr[0] + Jp[4 + a] * rr[1]);
+    }
+  }
+  if (b >= 0) {
+    auto add_cam = [&](double* dst) {
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+#pragma unroll
+        for (int cc = 0; cc < 6; ++cc)
+          if (cc >= a) atomicAdd(dst + u6(a, cc), Jc[a] * Jc[cc] + Jc[6 + a] * Jc[6 + cc]);
+        atomicAdd(dst + 21 + a, Jc[a] * rr[0] + Jc[6 + a] * rr[1]);
+      }
+    };
+    if (ch.wide) add_cam(d.cam_wide[nxt] + (size_t)b * kCamV);
+    else add_cam(camacc + (b - ch.b_lo) * kCamV);
+  }
+}
+
+// The candidate point blocks of the points [p0, p1) (lane per point) into slot nxt (k_linearize's point pass).
+__device__ __forceinline__ void ul_points(const Dev& d, int p0, int p1, int lane, int nxt, double* pacc,
+                                          double& gmax) {
+  if (lane >= p1 - p0) return;
+  const int pp = p0 + lane;
+  double* pa = pacc + lane * 14;
+  double V[10], g[4];
+#pragma unroll
+  for (int i = 0; i < 10; ++i) V[i] = pa[i];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) g[i] = pa[10 + i];
+#pragma unroll
+  for (int i = 0; i < 14; ++i) pa[i] = 0.0;
+  double2* Vd = reinterpret_cast<double2*>(d.V[nxt] + 10 * (size_t)pp);
+#pragma unroll
+  for (int k = 0; k < 5; ++k) Vd[k] = make_double2(V[2 * k], V[2 * k + 1]);
+  reinterpret_cast<double4*>(d.g[nxt])[pp] = make_double4(g[0], g[1], g[2], g[3]);
+  if (d.pfree[pp]) gmax = fmax(gmax, fmax(fmax(fabs(g[0]), fabs(g[1])), fmax(fabs(g[2]), fabs(g[3]))));
+}
+
+// k_point_update's per-unit scalars (its wave sums, in its order), then reset for the next unit.
+__device__ __forceinline__ void ul_unit_scalars(const Dev& d, int unit, int lane, double& model, double& candcost,
+                                                double& candfail, double& step2, double& candx2) {
+  const double m = wave_sum_full(model), cc = wave_sum_full(candcost), cf = wave_sum_full(candfail);
+  const double s2 = wave_sum_full(step2), x2 = wave_sum_full(candx2);
+  if (lane == 0) {
+    double* sc = d.chunk_scal + unit;   // structure of arrays: slot j at [j * npu + unit]
+    const size_t ns = d.npu;
+    sc[kModel * ns] = m;
+    sc[kCandCost * ns] = cc;
+    sc[kCandFail * ns] = cf;
+    sc[kStep2 * ns] = s2;
+    sc[kCandX2 * ns] = x2;
+  }
+  model = candcost = candfail = step2 = candx2 = 0.0;
+}
+
+__global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_update_lin(Dev d) {
+  const LmState* st = d.st;
+  if (st->done) return;
+  const int cur = st->cur, nxt = cur ^ 1;
+  const LinChunk ch = d.lchunks[blockIdx.x];
+  __shared__ double pacc[kLinPts * 14];         // candidate point blocks of the round: V (10) | g (4)
+  __shared__ double camacc[kLinNbMax * kCamV];  // candidate camera blocks of the window
+  __shared__ double lsum[2][kLinThreads];       // candidate failures: free, fixed observations
+  __shared__ double ua[kLinPts * 4], xps[kLinPts * 4], Xns[kLinPts * 4];   // A_p^T A_c x_c, x_p, X+ per point
+  const int lane = threadIdx.x;
+  const int ncv = ch.nb * kCamV;
+  for (int i = lane; i < ncv; i += kLinThreads) camacc[i] = 0.0;
+  for (int i = lane; i < kLinPts * 14; i += kLinThreads) pacc[i] = 0.0;
+  for (int i = lane; i < kLinPts * 4; i += kLinThreads) ua[i] = 0.0;
+  lsum[0][lane] = 0.0;
+  lsum[1][lane] = 0.0;
+  lds_fence_wave();
+  double cost = 0.0, gmax = 0.0;
+  double model = 0.0, candcost = 0.0, candfail = 0.0, step2 = 0.0, candx2 = 0.0;
+  if (!ch.wide) {
+    for (int r = ch.r0; r < ch.r1; ++r) {
+      const LinRound R = d.lrounds[r];
+      PuObs ob;
+      pu_pass1(d, cur, R, lane, ua, ob);
+      lds_fence_wave();
+      pu_pass2(d, R.p0, R.p1, lane, cur, nxt, ua, xps, Xns, step2, candx2);
+      lds_fence_wave();
+      ul_obs(d, R, ch, lane, nxt, ob, xps, Xns, pacc, camacc, lsum, model, cost, candcost, candfail);
+      lds_fence_wave();
+      ul_points(d, R.p0, R.p1, lane, nxt, pacc, gmax);
+      lds_fence_wave();
+      ul_unit_scalars(d, ch.u0 + (r - ch.r0), lane, model, candcost, candfail, step2, candx2);
+    }
+  } else {
+    // one point over several rounds: its back substitution needs every piece's A_p^T u first
+    for (int r = ch.r0; r < ch.r1; ++r) {
+      PuObs ob;
+      pu_pass1(d, cur, d.lrounds[r], lane, ua, ob);
+    }
+    lds_fence_wave();
+    pu_pass2(d, ch.p0, ch.p1, lane, cur, nxt, ua, xps, Xns, step2, candx2);
+    lds_fence_wave();
+    for (int r = ch.r0; r < ch.r1; ++r) {
+      const LinRound R = d.lrounds[r];
+      PuObs ob;
+      pu_pass1(d, cur, R, lane, nullptr, ob);
+      ul_obs(d, R, ch, lane, nxt, ob, xps, Xns, pacc, camacc, lsum, model, cost, candcost, candfail);
+    }
+    lds_fence_wave();
+    ul_points(d, ch.p0, ch.p1, lane, nxt, pacc, gmax);
+    lds_fence_wave();
+    ul_unit_scalars(d, ch.u0, lane, model, candcost, candfail, step2, candx2);
+  }
+  lds_fence_wave();
+  for (int i = lane; i < ncv; i += kLinThreads) d.cam_slab[nxt][ch.cam_off + i] = camacc[i];
+  cost = wave_sum_full(cost);
+  const double fail = wave_sum_full(lsum[0][lane]);
+  const double ffail = wave_sum_full(lsum[1][lane]);
+  gmax = wave_max(gmax);
+  if (lane == 0) {
+    double* sc = d.lin_scal[nxt] + blockIdx.x;   // k_linearize's scalars of the candidate (never iteration 0)
+    const size_t ns = d.nlin;
+    sc[kCost * ns] = cost;
+    sc[kFail * ns] = fail;
+    sc[kFixed * ns] = 0.0;
+    sc[kFixedFail * ns] = ffail;
+    sc[kXnorm2 * ns] = 0.0;
+    sc[kGmax * ns] = gmax;
   }
 }
 
@@ -4117,9 +4419,9 @@ __global__ __launch_bounds__(64) void k_reproject_reduce(const double* partial, 
 // Host driver
 
 enum KernelId { kKLin = 0, kKCamReduce, kKCamFinal, kKSchur, kKSReduce, kKChol, kKPointUpd, kKUpdRed, kKDecide,
-                kKNum };
+                kKXchg, kKNum };
 static const char* kKernelNames[kKNum] = {"linearize", "cam_reduce", "cam_finalize", "schur", "S_reduce",
-                                          "cholesky", "point_update", "upd_reduce", "decide"};
+                                          "cholesky", "point_update", "upd_reduce", "decide", "exchange"};
 
 // The tiled Cholesky's instantiations (kLa bit 0 look-ahead, bit 1 readlane factor, bit 2 Dinv, bit 3 register
 // / MFMA factor; SG_CHOL_LOOKAHEAD / SG_CHOL_FACTOR (1 readlane, 2 MFMA) / SG_CHOL_DINV): [0] the stamped build of
@@ -4254,7 +4556,10 @@ void BaSolver::CommInitHost(int nranks, int rank, int (*fn)(double*, long long, 
 int BaSolver::nranks() const { return comm_ ? comm_->nranks() : 1; }
 
 void BaSolver::AllReduceSum(double* buf, size_t n) {
-  if (comm_ && comm_->nranks() > 1) comm_->AllReduceSum(buf, n, stream_);
+  if (comm_ && comm_->nranks() > 1) {
+    comm_->AllReduceSum(buf, n, stream_);
+    ++nallreduce_;
+  }
 }
 
 __global__ __launch_bounds__(256) void k_fill_obs_pnt(const int32_t* __restrict__ poff, int32_t* __restrict__ obs_pnt,
@@ -4550,6 +4855,7 @@ void BaSolver::Load(const sg_problem& p) {
   nlin_ = (int)lchunks.size();
   std::vector<int32_t> pu_units;   // k_point_update work units: a round index, or -(chunk + 1) for wide chunks
   for (int c = 0; c < nlin_; ++c) {
+    lchunks[c].u0 = (int)pu_units.size();   // k_update_lin writes the units' scalars
     if (lchunks[c].wide)
       pu_units.push_back(-(c + 1));
     else
@@ -4804,7 +5110,9 @@ void BaSolver::Load(const sg_problem& p) {
       off[pk + 1] = off[pk] + std::min(kCholNb, n_ - pk * kCholNb) * (panel_jmax[pk] - pk * kCholNb);
     npack_ = (size_t)off[npanel] + n_;
     stager_->Add(pack_off_, off);
-    Spk_.Resize(std::max<size_t>(npack_, 1));
+    // + the merged exchange's tail (k_cam_finalize modes 1, 2)
+    ntail_ = 2 * (size_t)6 * NB_ + kXNum + nranks() + 1;
+    Spk_.Resize(npack_ + ntail_);
   }
   // k_cholesky_global stages each panel's rows in LDS when x and 16 rows of S fit
   // (SG_CHOL_GSTAGE=0: never, so tests reach the unstaged instance at any size)
@@ -4905,9 +5213,11 @@ void BaSolver::Load(const sg_problem& p) {
     stg.Add(fd_pair_, fd_pair);
     rdg_.Resize((size_t)std::max(n_, 1) + kCholNb);   // + padding rows of the last panel
   }
-  J_.Resize((size_t)((std::max(M_, 1) + 63) & ~63) * kJStride);   // whole 64-observation blocks (jidx2)
-  V_.Resize(10 * (size_t)std::max(P_, 1));
-  g_.Resize(4 * (size_t)std::max(P_, 1));
+  // the linearization's buffers hold two slots (current point, k_update_lin's candidate)
+  jslot_ = (size_t)((std::max(M_, 1) + 63) & ~63) * kJStride;   // whole 64-observation blocks (jidx2)
+  J_.Resize(2 * jslot_);
+  V_.Resize(2 * 10 * (size_t)std::max(P_, 1));
+  g_.Resize(2 * 4 * (size_t)std::max(P_, 1));
   scale_p_.Resize(4 * (size_t)std::max(P_, 1));
   diag_p_.Resize(4 * (size_t)std::max(P_, 1));
   Vinv_.Resize(10 * (size_t)std::max(P_, 1));
@@ -4917,8 +5227,9 @@ void BaSolver::Load(const sg_problem& p) {
   diag_c_.Resize(nn);
   camdiag_.Resize(nn);
   camg_.Resize(nn);
-  cam_slab_.Resize(std::max(lcam_off, 1));
-  lin_scal_.Resize((size_t)std::max(nlin_, 1) * kNScal);
+  cslot_ = std::max(lcam_off, 1);
+  cam_slab_.Resize(2 * cslot_);
+  lin_scal_.Resize(2 * (size_t)std::max(nlin_, 1) * kNScal);
   S_slab_.Resize(std::max(s_off, 1));
   chunk_scal_.Resize((size_t)std::max(npu_, 1) * kNScal);
   stg.Add(pu_units_, pu_units);
@@ -4926,9 +5237,9 @@ void BaSolver::Load(const sg_problem& p) {
   stg.Flush(s);
   if (host_timing) DevMark(s, 2);
   lap("flush");
-  cam_wide_.Resize((size_t)std::max(NB_, 1) * kCamV);
+  cam_wide_.Resize(2 * (size_t)std::max(NB_, 1) * kCamV);
   S_wide_.Resize(nn * nn);
-  xchg_cam_.Resize((size_t)NB_ * kCamV + kXNum + nranks());
+  xchg_cam_.Resize(2 * ((size_t)NB_ * kCamV + kXNum + nranks()));   // summed | this rank's
   S_.Resize(nn * nn + nn + 2);   // S, then the rhs partial xc (one all-reduce covers both), then {0, 1}
   rhs_.Resize(nn);
   xchg_upd_.Resize(kUNum);
@@ -4983,7 +5294,7 @@ void BaSolver::Reserve(int F, int P, int M) {
   const size_t f = std::max(F, 1), pp = std::max(P, 1), m = std::max(M, 1);
   bool moved = false;
   // per observation (device order records, the Jacobian rows, the Schur cells)
-  moved |= J_.Reserve(((m + 63) & ~(size_t)63) * kJStride);
+  moved |= J_.Reserve(2 * ((m + 63) & ~(size_t)63) * kJStride);
   moved |= obs_pt_.Reserve(2 * m);
   moved |= obs_frame_.Reserve(m);
   moved |= obs_fixed_.Reserve(m);
@@ -4994,9 +5305,9 @@ void BaSolver::Reserve(int F, int P, int M) {
   moved |= llist_d_.Reserve(2 * m);
   // per point
   moved |= X_.Reserve(8 * pp);
-  moved |= V_.Reserve(10 * pp);
+  moved |= V_.Reserve(2 * 10 * pp);
   moved |= Vinv_.Reserve(10 * pp);
-  moved |= g_.Reserve(4 * pp);
+  moved |= g_.Reserve(2 * 4 * pp);
   moved |= tp_.Reserve(4 * pp);
   moved |= scale_p_.Reserve(4 * pp);
   moved |= diag_p_.Reserve(4 * pp);
@@ -5182,9 +5493,18 @@ Dev BaSolver::MakeDev() {
   d.fd_J = fd_J_.ptr;
   d.fd_D = fd_D_.ptr;
   d.fd_X = fd_X_.ptr;
-  d.J = J_.ptr;
-  d.V = V_.ptr;
-  d.g = g_.ptr;
+  {
+    const size_t pp = std::max(P_, 1);
+    for (int sl = 0; sl < 2; ++sl) {
+      d.J[sl] = J_.ptr + sl * jslot_;
+      d.V[sl] = V_.ptr + sl * 10 * pp;
+      d.g[sl] = g_.ptr + sl * 4 * pp;
+      d.cam_slab[sl] = cam_slab_.ptr + sl * cslot_;
+      d.cam_wide[sl] = cam_wide_.ptr + sl * (size_t)std::max(NB_, 1) * kCamV;
+      d.lin_scal[sl] = lin_scal_.ptr + sl * (size_t)std::max(nlin_, 1) * kNScal;
+    }
+  }
+  d.spec = spec_ ? 1 : 0;
   d.scale_p = scale_p_.ptr;
   d.diag_p = diag_p_.ptr;
   d.Vinv = Vinv_.ptr;
@@ -5199,12 +5519,12 @@ Dev BaSolver::MakeDev() {
   d.s_lidx = s_lidx_.ptr;
   d.r_loff = r_loff_.ptr;
   d.r_lidx = r_lidx_.ptr;
-  d.cam_slab = cam_slab_.ptr;
   d.S_slab = S_slab_.ptr;
   d.chunk_scal = chunk_scal_.ptr;
-  d.cam_wide = cam_wide_.ptr;
   d.S_wide = S_wide_.ptr;
   d.xchg_cam = xchg_cam_.ptr;
+  d.xcam_loc = xchg_cam_.ptr + (size_t)NB_ * kCamV + kXNum + nranks();
+  d.xtail = Spk_.ptr + npack_;
   d.rank = comm_ ? comm_->rank() : 0;
   d.nranks = nranks();
   d.S = S_.ptr;
@@ -5222,7 +5542,6 @@ Dev BaSolver::MakeDev() {
   d.nlin = nlin_;
   d.npu = npu_;
   d.pu_units = pu_units_.ptr;
-  d.lin_scal = lin_scal_.ptr;
   d.segs = segs_.ptr;
   d.nseg = nseg_;
   d.sbatch = sbatch_.ptr;
@@ -5304,6 +5623,7 @@ void BaSolver::ReadState(LmState* h) {
 void BaSolver::Begin(const sg_solver_options& o) {
   SG_REQUIRE(loaded_, SG_EINVAL, "no problem loaded");
   SG_HIP_CHECK(hipSetDevice(dev_.device));
+  const bool began_again = began_;
   if (began_) {
     // restart from the current parameter slot: move it to slot 0 (a fresh load starts in slot 0: no round trip)
     LmState h{};
@@ -5341,6 +5661,14 @@ void BaSolver::Begin(const sg_solver_options& o) {
   s.radius = o.initial_trust_region_radius;
   s.decrease_factor = 2.0;
   hipLaunchKernelGGL(k_set_state, dim3(1), dim3(64), 0, stream_, s, st_.ptr);
+  if (began_again && spec_) {
+    // k_cam_reduce keeps the wide-chunk camera accumulators in speculative mode: clear both slots for the
+    // restart's first k_linearize (a fresh Load has zeroed them)
+    ZeroList z{};
+    z.p[0] = cam_wide_.ptr;
+    z.n[0] = cam_wide_.size;
+    hipLaunchKernelGGL(k_reset_buffers, dim3(1), dim3(256), 0, stream_, z);
+  }
   need_seq_ = true;   // the first iteration fixes the camera scale: k_schur waits for it
   for (auto& t : timers_) {
     t.total_ms = 0.0;
@@ -5372,6 +5700,10 @@ void BaSolver::Iterate(int n) {
   // per-kernel timing, no stamps, no side stream.
   const bool graphable = graph_ok_ && !timing_ && !stamp_on_ && !(comm_ && comm_->nranks() > 1) && !pack_force_ &&
                          nk_ == 0 && !overlap_ok_;
+  if (graphable && n > 0 && need_seq_) {   // a solve's first iteration (it linearizes) outside the graph
+    EnqueueIterations(1);
+    --n;
+  }
   if (graphable && n > 0) {
     if (!iter_exec_) {
       hipGraph_t g = nullptr;
@@ -5397,10 +5729,15 @@ void BaSolver::DropGraph() {
 void BaSolver::EnqueueIterations(int n) {
   Dev d = MakeDev();
   for (int it = 0; it < n; ++it) {
-    TimedLaunchBegin(kKLin);
-    hipLaunchKernelGGL(k_linearize, dim3(std::max(nlin_, 1)), dim3(kLinThreads), 0, stream_, d);
-    TimedLaunchEnd(kKLin);
+    // speculative mode: only a solve's first iteration linearizes here; later ones find the linearization of
+    // the accepted point in the slot k_update_lin filled (k_linearize would exit at once: no launch)
+    if (!spec_ || need_seq_) {
+      TimedLaunchBegin(kKLin);
+      hipLaunchKernelGGL(k_linearize, dim3(std::max(nlin_, 1)), dim3(kLinThreads), 0, stream_, d);
+      TimedLaunchEnd(kKLin);
+    }
     // k_schur beside the camera reduction (see side_ in ba_solver.h)
+    const bool first_it = need_seq_;
     const bool overlap = overlap_ok_ && !need_seq_ && nk_ == 0;
     need_seq_ = false;
     if (overlap) {
@@ -5412,18 +5749,26 @@ void BaSolver::EnqueueIterations(int n) {
       TimedLaunchEnd(kKSchur, side_);
       SG_HIP_CHECK(hipEventRecord(ev_schur_, side_));
     }
+    // Landmark shards exchange twice per LM iteration after a solve's first: k_S_reduce assembles each rank's
+    // own camera blocks (and, on rank 0, the FrameDistance terms) into its partial S, and the camera gradient,
+    // diagonal and cost scalars ride in the same all-reduce as the band of S (k_cam_finalize modes 1 and 2);
+    // the first iteration sums the camera blocks first (the Jacobi scale of the camera columns comes from
+    // them), then S.  SG_XCHG_MERGE=0: the three-exchange chain every iteration; =force: the merged chain on
+    // one rank too (tests the path).
+    const bool multi_x = (comm_ && comm_->nranks() > 1);
+    const bool merged = !first_it && nk_ == 0 && (merge_ == 2 || (multi_x && merge_ == 1));
     TimedLaunchBegin(kKCamReduce);
     const int nv = NB_ * kCamV;
     hipLaunchKernelGGL(k_cam_reduce, dim3(NB_ + 1), dim3(kRedThreads), 0, stream_, d);
     TimedLaunchEnd(kKCamReduce);
-    AllReduceSum(xchg_cam_.ptr, (size_t)nv + kXNum + nranks());
+    if (!merged) AllReduceSum(xchg_cam_.ptr, (size_t)nv + kXNum + nranks());
     if (nk_) {
       hipLaunchKernelGGL(k_intr_zero, dim3((n_ * nk_ + 255) / 256), dim3(256), 0, stream_, d);
       hipLaunchKernelGGL(k_intr_lin, dim3((std::max(M_, 1) + 255) / 256), dim3(256), 0, stream_, d);
       hipLaunchKernelGGL(k_intr_fin, dim3(1), dim3(64), 0, stream_, d);
     }
     TimedLaunchBegin(kKCamFinal);
-    hipLaunchKernelGGL(k_cam_finalize, dim3(1), dim3(256), 0, stream_, d);
+    hipLaunchKernelGGL(k_cam_finalize, dim3(1), dim3(256), 0, stream_, d, merged ? 1 : 0);
     TimedLaunchEnd(kKCamFinal);
     if (overlap) {
       SG_HIP_CHECK(hipStreamWaitEvent(stream_, ev_schur_, 0));
@@ -5435,21 +5780,30 @@ void BaSolver::EnqueueIterations(int n) {
     }
     TimedLaunchBegin(kKSReduce);
     const int nwv = nstile_ + NB_;
-    hipLaunchKernelGGL(k_S_reduce, dim3(std::max(nwv, 1)), dim3(256), 0, stream_, d);
+    hipLaunchKernelGGL(k_S_reduce, dim3(std::max(nwv, 1)), dim3(256), 0, stream_, d,
+                       merged ? 2 : (d.assemble ? 1 : 0));
     TimedLaunchEnd(kKSReduce);
     if (nk_) {
       hipLaunchKernelGGL(k_intr_assemble, dim3((n_ * nk_ + 255) / 256), dim3(256), 0, stream_, d);
       hipLaunchKernelGGL(k_intr_schur, dim3((std::max(P_, 1) + 127) / 128), dim3(128), 0, stream_, d);
     }
-    if ((comm_ && comm_->nranks() > 1) || pack_force_) {
-      // the band of S and the rhs partial are summed over landmark shards (packed: the band only)
+    if (multi_x || pack_force_ || merged) {
+      // the band of S and the rhs partial are summed over landmark shards (packed: the band only), with the
+      // merged tail after them
       const int npanel = (n_ + kCholNb - 1) / kCholNb;
       const dim3 pg(npanel + 1, 4);
+      TimedLaunchBegin(kKXchg);   // pack, all-reduce, unpack
       hipLaunchKernelGGL(k_S_pack, pg, dim3(256), 0, stream_, S_.ptr, n_, (const int32_t*)work_i_.ptr,
                          (const int32_t*)pack_off_.ptr, npanel, Spk_.ptr, 0);
-      AllReduceSum(Spk_.ptr, npack_);
+      AllReduceSum(Spk_.ptr, npack_ + (merged ? ntail_ : 0));
       hipLaunchKernelGGL(k_S_pack, pg, dim3(256), 0, stream_, S_.ptr, n_, (const int32_t*)work_i_.ptr,
                          (const int32_t*)pack_off_.ptr, npanel, Spk_.ptr, 1);
+      TimedLaunchEnd(kKXchg);
+      if (merged) {
+        TimedLaunchBegin(kKCamFinal);
+        hipLaunchKernelGGL(k_cam_finalize, dim3(1), dim3(256), 0, stream_, d, 2);
+        TimedLaunchEnd(kKCamFinal);
+      }
     }
     TimedLaunchBegin(kKChol);
     if (chol_tiles_)
@@ -5468,7 +5822,10 @@ void BaSolver::EnqueueIterations(int n) {
     TimedLaunchEnd(kKChol);
     if (nk_) hipLaunchKernelGGL(k_intr_step, dim3(1), dim3(64), 0, stream_, d);
     TimedLaunchBegin(kKPointUpd);
-    hipLaunchKernelGGL(k_point_update, dim3(std::max(npu_, 1)), dim3(kLinThreads), 0, stream_, d);
+    if (spec_)
+      hipLaunchKernelGGL(k_update_lin, dim3(std::max(nlin_, 1)), dim3(kLinThreads), 0, stream_, d);
+    else
+      hipLaunchKernelGGL(k_point_update, dim3(std::max(npu_, 1)), dim3(kLinThreads), 0, stream_, d);
     TimedLaunchEnd(kKPointUpd);
     const bool multi = comm_ && comm_->nranks() > 1;
     TimedLaunchBegin(kKUpdRed);
@@ -5649,6 +6006,10 @@ int BaSolver::KernelWork(double* bytes, double* flops, int max) {
   by[kKSchur] = M * 192 + P * (80 + 32 + 32 + 32 + 80 + 32);
   fl[kKSchur] = 2048.0 * schur_mfma_;   // v_mfma_f64_16x16x4f64 tile updates
   by[kKPointUpd] = M * (192 + 16 + 4) + P * (32 + 32 + 80 + 32 + 32);
+  if (spec_) {   // k_update_lin: the update's traffic plus the candidate's linearization (a second J record, V, g)
+    by[kKPointUpd] = M * (192 + 192 + 16 + 4 + 4 + 4) + P * (32 + 32 + 80 + 32 + 32 + 80 + 32) + NB * kCamV * 8;
+    fl[kKPointUpd] = M * 420.0;
+  }
   by[kKChol] = n * n * 8 * 2;
   fl[kKChol] = n * n * n / 3.0;
   int k = 0;
@@ -5672,6 +6033,7 @@ void BaSolver::Info(sg_ba_info* o) const {
   o->num_pairs = (int32_t)std::min<size_t>(npairs_, INT32_MAX);
   o->rank = comm_ ? comm_->rank() : 0;
   o->nranks = comm_ ? comm_->nranks() : 1;
+  o->num_allreduces = nallreduce_;
 }
 
 double BaSolver::ReprojectMap(sg_map* m) {

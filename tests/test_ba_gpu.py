@@ -576,3 +576,87 @@ def test_free_intrinsics_c2_global_cholesky_matches_oracle(gpu_lib, oracle_lib, 
     assert abs(sg["final_cost"] - so["final_cost"]) <= 1e-8 * so["final_cost"]
     np.testing.assert_allclose(pg.k, po.k, rtol=1e-7, atol=1e-9)
     np.testing.assert_allclose(pg.t, po.t, atol=1e-5)
+
+
+def _solve_env(pa, env, monkeypatch, options=None, bench=None):
+    """Solve pa.copy() on a fresh handle with the environment switches env; bench = (W, K): begin with
+    termination off and always-linearize, W + K iterations, download (the benchmark's regime)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    p = pa.copy()
+    g = ba.BundleAdjuster()
+    g.load(p)
+    if bench is None:
+        s = g.solve(options)
+    else:
+        g.begin(default_solver_options(max_num_iterations=10 ** 6, disable_termination=1, always_linearize=1))
+        g.iterate(bench[0])
+        g.iterate(bench[1])
+        g.sync()
+        s = g.summary()
+        g.download()
+    g.close()
+    for k in env:
+        monkeypatch.delenv(k, raising=False)
+    return s, p
+
+
+@pytest.mark.parametrize("regime", ["solve", "bench"])
+def test_speculative_linearization_is_bitwise_identical(gpu_lib, monkeypatch, regime):
+    """k_update_lin (the candidate pass linearizes at the candidate into the other slot; k_linearize only in a
+    solve's first iteration) against k_point_update + k_linearize every iteration (SG_SPEC=0): the same
+    arithmetic at the same points, the camera partials in k_linearize's chunk order and the update scalars per
+    k_point_update unit, so the C2 solve is the same bit for bit — a full solve from the perturbed start, and
+    60 iterations of the benchmark regime (termination off, a rejected step re-reduces the current slot
+    instead of re-linearizing), which runs past convergence into rejected steps."""
+    m = make_config("C2")
+    pa = ba.problem_from_map_frames(m, 48, 50, 2.0)
+    bench = None if regime == "solve" else (20, 40)
+    s0, p0 = _solve_env(pa, {"SG_SPEC": "0"}, monkeypatch, bench=bench)
+    s1, p1 = _solve_env(pa, {}, monkeypatch, bench=bench)
+    assert s0["ok"] == 1 and s0["sync_timeouts"] == 0
+    if bench:
+        assert s0["num_unsuccessful_steps"] > 0   # the regime reached rejected steps
+    assert s0 == s1
+    np.testing.assert_array_equal(p0.q, p1.q)
+    np.testing.assert_array_equal(p0.t, p1.t)
+    np.testing.assert_array_equal(p0.X, p1.X)
+
+
+def test_speculative_linearization_wide_chunks(gpu_lib, oracle_lib, monkeypatch):
+    """Points with more than 64 observations or wider than 24 blocks (k_linearize's wide chunks: one point over
+    several rounds, camera terms by global atomics into the slotted cam_wide) on the edge-structure scene, with
+    rejected steps (tight tolerances): speculative and non-speculative solves agree to rounding (the wide
+    chunks' atomics sum in arrival order) and match the oracle's minimum."""
+    m = make_scene(num_frames=40, num_points=400, seed=21, run_max=40)
+    rng = np.random.default_rng(0)
+    m.obs_disabled[rng.random(m.num_obs) < 0.05] = 1
+    m.point_uncertainty[:] = 1.0
+    pa = ba.problem_from_map_frames(m, 38, 40, 2.0)
+    tight = default_solver_options(function_tolerance=1e-13, parameter_tolerance=1e-13, max_num_iterations=200)
+    s0, p0 = _solve_env(pa, {"SG_SPEC": "0"}, monkeypatch, options=tight)
+    s1, p1 = _solve_env(pa, {}, monkeypatch, options=tight)
+    assert s1["ok"] == 1 and s1["num_unsuccessful_steps"] > 0
+    assert abs(s0["final_cost"] - s1["final_cost"]) <= 1e-10 * s0["final_cost"]
+    np.testing.assert_allclose(p1.q, p0.q, atol=1e-7)
+    po = pa.copy()
+    so = oracle_lib.solve(po, tight)
+    _assert_same_minimum(oracle_lib, p1, s1, po, so)
+
+
+def test_merged_exchange_chain_on_one_rank(gpu_lib, monkeypatch):
+    """The landmark shards' merged exchange chain forced on one rank (SG_XCHG_MERGE=force: k_S_reduce assembles
+    the rank's own camera blocks and FrameDistance terms without the damping, S travels packed with the camera
+    gradient / diagonal / cost scalars in its tail, k_cam_finalize mode 2 does the bookkeeping and adds the
+    damping after the exchange) against the default chain on C2: the same solve up to the rounding of adding the
+    damping last (same steps, cost 1e-12 relative, rotations 1e-10, translations 1e-6 mm)."""
+    m = make_config("C2")
+    pa = ba.problem_from_map_frames(m, 48, 50, 2.0)
+    s0, p0 = _solve_env(pa, {}, monkeypatch)
+    s1, p1 = _solve_env(pa, {"SG_XCHG_MERGE": "force"}, monkeypatch)
+    assert s1["ok"] == 1 and s1["sync_timeouts"] == 0
+    assert s0["num_iterations"] == s1["num_iterations"]
+    assert s0["num_successful_steps"] == s1["num_successful_steps"]
+    assert abs(s0["final_cost"] - s1["final_cost"]) <= 1e-12 * s0["final_cost"]
+    np.testing.assert_allclose(p1.q, p0.q, rtol=0, atol=1e-10)
+    np.testing.assert_allclose(p1.t, p0.t, rtol=0, atol=1e-6)

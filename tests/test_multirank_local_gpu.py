@@ -238,3 +238,66 @@ def test_failed_load_then_reload(gpu_lib):
     assert s1 == s2
     np.testing.assert_array_equal(p1.X, p2.X)
     np.testing.assert_array_equal(p1.q, p2.q)
+
+
+def _sharded_counts(pa, nranks, first, more):
+    """Begin + `first` iterations, then `more` iterations on every shard; per rank (all-reduces issued during
+    the `more` iterations, summary, shard after download)."""
+    group = ba.LocalCommGroup(nranks)
+    shards = [ba.shard_problem(pa, r, nranks) for r in range(nranks)]
+    out = [None] * nranks
+
+    def work(r):
+        try:
+            g = ba.BundleAdjuster()
+            g.comm_init_local(group, r)
+            g.load(shards[r])
+            g.begin(default_solver_options(max_num_iterations=first + more))
+            g.iterate(first)
+            g.sync()
+            c0 = g.info()["num_allreduces"]
+            g.iterate(more)
+            g.sync()
+            c1 = g.info()["num_allreduces"]
+            s = g.summary()
+            g.download()
+            out[r] = (c1 - c0, s, shards[r])
+            g.close()
+        except Exception as e:   # noqa: BLE001 - reported per rank
+            out[r] = e
+
+    th = [threading.Thread(target=work, args=(r,)) for r in range(nranks)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(300)
+    assert not any(t.is_alive() for t in th), "a rank did not finish"
+    group.close()
+    for r in out:
+        assert not isinstance(r, Exception), r
+    return out
+
+
+@pytest.mark.parametrize("merge", ["1", "0"], ids=["merged", "three-exchange"])
+def test_exchanges_per_iteration(gpu_lib, monkeypatch, merge):
+    """After a solve's first iteration (which sums the camera blocks, then S, then the step scalars: three
+    all-reduces) the shards exchange twice per LM iteration: the band of S with the camera gradient, diagonal and
+    cost scalars in its tail, then the step scalars (SG_XCHG_MERGE=0 keeps three).  Both chains give
+    the one-rank solve of C2 to rounding: 4 shards, 6 iterations."""
+    monkeypatch.setenv("SG_XCHG_MERGE", merge)
+    m = make_config("C2")
+    pa = ba.problem_from_map_frames(m, 48, 50, 2.0)
+    out = _sharded_counts(pa, 4, 1, 5)
+    for n_ar, s, _ in out:
+        assert n_ar == 5 * (2 if merge == "1" else 3), n_ar
+        assert s == out[0][1]
+    monkeypatch.delenv("SG_XCHG_MERGE")
+    one = pa.copy()
+    g = ba.BundleAdjuster()
+    g.load(one)
+    s1 = g.solve(default_solver_options(max_num_iterations=6))
+    s0 = out[0][1]
+    assert s0["num_successful_steps"] == s1["num_successful_steps"]
+    assert abs(s0["final_cost"] - s1["final_cost"]) <= 1e-12 * s1["final_cost"]
+    np.testing.assert_allclose(out[0][2].q, one.q, rtol=0, atol=1e-10)
+    np.testing.assert_allclose(out[0][2].t, one.t, rtol=0, atol=1e-6)
