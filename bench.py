@@ -215,6 +215,81 @@ def bench_hamming(local, cpu_seconds):
     return res
 
 
+def bench_matcher_sequence(local, cpu):
+    """Matcher::Track per frame (matcher.cpp:301-405) over the 11-frame sequence the front-end parity test uses
+    (slamgpu.video.matcher_sequence: 320x240, 13x13 window, 6-level pyramid; seeding, tracking frames, scene
+    cuts, view expiry): the device front end (pyramid, FindMatches as one launch per pass, corner seeding, the
+    bookkeeping in host C++, the map through Python callbacks) timed per Track call after one warm-up pass of
+    the whole sequence, beside the sequential restatement (oracle/oracle_matcher.py over the C++ tracker
+    oracle) on the same frames."""
+    import statistics
+    from slamgpu.frontend import Matcher, add_frame
+    from slamgpu.scene import MapArrays
+    from slamgpu.video import SEQ_K, matcher_sequence, sequence_mark, sequence_pose, sequence_true_t
+    frames, _ = matcher_sequence()
+
+    def run():
+        z = lambda dt: np.zeros(0, dt)  # noqa: E731
+        m = MapArrays(k=SEQ_K.copy(), q=z(np.float64), t=z(np.float64), frame_camera=z(np.int32),
+                      frame_prev=z(np.int32), X=z(np.float64), point_flags=z(np.int32),
+                      point_uncertainty=z(np.float64), obs_pt=z(np.float64), obs_frame=z(np.int32),
+                      obs_point=z(np.int32), obs_disabled=z(np.int32), obs_error=z(np.float64),
+                      frame_keyframe=z(np.int32))
+        mt = Matcher(device=local, window=13, depth=6)
+        ms, batches, stats = [], [], []
+        for i, img in enumerate(frames):
+            q, t = sequence_pose(i)
+            add_frame(m, 0, q, t)
+            sequence_mark(i, m.point_flags, m.point_uncertainty, m.num_points)
+
+            def upd(i=i):
+                m.t[3 * i:3 * i + 3] = sequence_true_t(i)
+                return i % 2 == 1
+            t0 = time.perf_counter()
+            mt.Track(img, i, 0, m, upd)
+            ms.append(1e3 * (time.perf_counter() - t0))
+            batches.append(mt.last_stats["track_batches"])
+            stats.append((mt.last_stats["matches"], mt.last_stats["keyframe"]))
+        mt.close()
+        return ms, batches, stats
+
+    run()
+    ms, batches, stats = run()
+    res = {"metric": "Matcher::Track ms per frame (11-frame sequence, 320x240, 13x13, 6 levels)",
+           "ms_per_frame_median": statistics.median(ms), "ms_per_frame_mean": sum(ms) / len(ms),
+           "ms_per_frame": [round(x, 3) for x in ms], "track_launches_per_frame": batches,
+           "matches_keyframe": stats,
+           "note": "wall time of sg_frontend_track through the Python mirror (map callbacks in Python): pyramid, "
+                   "FindMatches (one k_find_matches launch per pass: a wave per feature walks its views), corner "
+                   "seeding on keyframes, bookkeeping"}
+    if cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle_matcher as om
+        omap = om.OracleMap(SEQ_K, [], [], [])
+        mt = om.OracleMatcher()
+        oms = []
+        for i, img in enumerate(frames):
+            q, t = sequence_pose(i)
+            omap.q.append(list(q))
+            omap.t.append(list(t))
+            omap.frame_camera.append(0)
+            omap.obs[i] = []
+            omap.keyframe.append(0)
+            sequence_mark(i, omap.flags, omap.uncertainty, len(omap.X))
+
+            def oupd(i=i):
+                omap.t[i] = list(sequence_true_t(i))
+                return i % 2 == 1
+            t0 = time.perf_counter()
+            mt.Track(img, i, omap, oupd)
+            oms.append(1e3 * (time.perf_counter() - t0))
+        res["cpu_baseline"] = {"value": statistics.median(oms), "unit": "ms/frame (median)", "cores": 1,
+                               "kind": "port", "ms_per_frame": [round(x, 2) for x in oms],
+                               "sample": "oracle/oracle_matcher.py (features one at a time, C++ tracker oracle) "
+                                         "over the same 11 frames"}
+    return res
+
+
 def dist_env():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -643,7 +718,8 @@ def main():
     frontend = None
     if args.frontend and n_gpus == 1:
         cs = args.cpu_seconds
-        frontend = {"tracker": bench_tracker(local, cs), "hamming": bench_hamming(local, cs)}
+        frontend = {"tracker": bench_tracker(local, cs), "hamming": bench_hamming(local, cs),
+                    "matcher": bench_matcher_sequence(local, cs > 0)}
 
     value = args.steps / res["elapsed"]
     line = {

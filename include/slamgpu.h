@@ -409,7 +409,7 @@ typedef struct sg_frontend_stats {
   int32_t added;           /* new features / points ("Added %d new features") */
   int32_t features;        /* live features after the call */
   int32_t views;           /* keyframe views after the call */
-  int32_t track_batches;   /* device tracking launches (FindMatches rounds x source views) */
+  int32_t track_batches;   /* device FindMatches launches (one per pass; a second after update_frames) */
 } sg_frontend_stats;
 
 typedef struct sg_frontend sg_frontend;

@@ -64,7 +64,10 @@ enum CholX { kCStep2 = 0, kCCandX2, kCModel, kCCandCost, kCFail, kCTimeout, kCNu
 constexpr int kSegNbMax = SG_SEG_NB;
 static_assert(kSegNbMax <= 24, "cells of a batch: kSchurBatchCells");
 constexpr int kSchurCellWaves = 3;   // operand-tile waves (a batch has <= 64 kSchurCellWaves cells)
-constexpr int kSchurCWaves = 4;      // MFMA waves (one per SIMD); a point wave between the two groups
+#ifndef SG_SCHUR_CW
+#define SG_SCHUR_CW 4
+#endif
+constexpr int kSchurCWaves = SG_SCHUR_CW;   // MFMA waves (4: one per SIMD; 8: two); a point wave between the groups
 constexpr int kSchurWaves = kSchurCellWaves + 1 + kSchurCWaves;
 constexpr int kSchurThreads = 64 * kSchurWaves;
 constexpr int kSchurTW = 10;

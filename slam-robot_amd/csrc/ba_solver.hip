@@ -1022,13 +1022,16 @@ __device__ __forceinline__ void schur_cells(const Dev& d, const double* J, const
                                             const int4* pinf, const int2* pob, const uint8_t* cmap, double* Xb) {
   const int ncell = B.c1 - B.c0;
   constexpr int kStride = 64 * kSchurCellWaves;
-  for (int lc0 = tid; lc0 < ncell; lc0 += 2 * kStride) {
+  // cells per thread and round: 2 with four MFMA waves (their loads overlap); 1 with eight, whose register budget
+  // (three waves per SIMD) does not hold two cells' operands
+  constexpr int kCpt = kSchurCWaves > 4 ? 1 : 2;
+  for (int lc0 = tid; lc0 < ncell; lc0 += kCpt * kStride) {
     // both cells' table entries and, for single-observation cells, their operand loads first
-    int tc[2], bc[2], oc[2];
-    bool simple[2];
-    CellOps ops[2];
+    int tc[kCpt], bc[kCpt], oc[kCpt];
+    bool simple[kCpt];
+    CellOps ops[kCpt];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < kCpt; ++h) {
       const int lc = lc0 + h * kStride;
       simple[h] = false;
       oc[h] = -1;
@@ -1048,7 +1051,7 @@ __device__ __forceinline__ void schur_cells(const Dev& d, const double* J, const
       }
     }
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < kCpt; ++h) {
       const int lc = lc0 + h * kStride;
       if (lc >= ncell) break;
       const int t = tc[h];
@@ -1159,6 +1162,9 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d) {
 #define SG_SCHUR_CASE(W) \
           case W: schur_wave_batch<W>(acc, Xb, wsh, pinf, npts, lane); break;
           SG_SCHUR_CASE(0) SG_SCHUR_CASE(1) SG_SCHUR_CASE(2) SG_SCHUR_CASE(3)
+#if SG_SCHUR_CW > 4
+          SG_SCHUR_CASE(4) SG_SCHUR_CASE(5) SG_SCHUR_CASE(6) SG_SCHUR_CASE(7)
+#endif
 #undef SG_SCHUR_CASE
         }
         SG_SSTAMP(42)
@@ -1171,6 +1177,9 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d) {
 #define SG_SCHUR_CASE(W) \
       case W: schur_store<W>(acc, slab, sg.ntw, lane); break;
       SG_SCHUR_CASE(0) SG_SCHUR_CASE(1) SG_SCHUR_CASE(2) SG_SCHUR_CASE(3)
+#if SG_SCHUR_CW > 4
+      SG_SCHUR_CASE(4) SG_SCHUR_CASE(5) SG_SCHUR_CASE(6) SG_SCHUR_CASE(7)
+#endif
 #undef SG_SCHUR_CASE
     }
     SG_SSTAMP(45)

@@ -4,9 +4,9 @@
 //
 // The reference walks its live features one at a time (FindMatches, matcher.cpp:210-271): for each
 // feature not yet matched, try its stored views in order and keep the first forward/backward-consistent
-// track.  Features are independent, so here FindMatches runs in rounds: round r tries every still
-// unmatched feature's r-th remaining view, all of them in one device launch per source view.  The
-// observations are then appended in feature order, which is the order the reference's loop adds them.
+// track.  Features are independent, so here FindMatches is one device launch: a wave per feature walks that
+// feature's attempts (its views, in order) and stops at the first accepted track.  The observations are
+// then appended in feature order, which is the order the reference's loop adds them.
 //
 // Defined orders where the reference's are implementation details:
 //   * Feature::matches is a map<View*, Point2f> (matcher.cpp:43): ordered by pointer value.  Here views are
@@ -245,7 +245,6 @@ class Frontend {
     Call(cb_->frame_pose(cb_->user, to.frame, pose.q, pose.t, pose.k), "frame_pose");
     struct Cand {
       int id;
-      size_t next;        // next index into the feature's matches
       int levels;
       bool projected;
       float px, py;       // projected starting point
@@ -256,7 +255,7 @@ class Frontend {
       double X[4], unc;
       int32_t usable;
       Call(cb_->point_state(cb_->user, f.second.point, X, &unc, &usable), "point_state");
-      Cand c{f.first, 0, unc > 100 ? 6 : 3, false, 0.f, 0.f};
+      Cand c{f.first, unc > 100 ? 6 : 3, false, 0.f, 0.f};
       if (unc < 100) {
         double uv[2];
         if (Project(pose.q, pose.t, pose.k, X, uv)) {
@@ -268,79 +267,33 @@ class Frontend {
       active.push_back(c);
     }
 
+    // Every feature's attempts in its view order (the out-of-bounds test of matcher.cpp:245-247 — note '>' for y
+    // — drops a start before the device sees it), all features in one device launch (Tracker::FindMatches: a
+    // wave per feature stops at its first forward/backward-consistent track).
+    std::vector<int32_t> aoff(1, 0), aslot, lv;
+    std::vector<float> axy;
+    for (auto& c : active) {
+      for (const Match& m : features_[c.id].matches) {
+        const View* from = FindView(m.view_seq);
+        SG_REQUIRE(from, SG_EINVAL, "feature refers to an expired view");
+        const float tx = c.projected ? c.px : m.x, ty = c.projected ? c.py : m.y;
+        if (tx < 0 || ty < 0 || tx >= (float)to.w || ty > (float)to.h) continue;
+        aslot.push_back(from->slot);
+        axy.insert(axy.end(), {m.x, m.y, tx, ty});
+      }
+      aoff.push_back((int32_t)aslot.size());
+      lv.push_back(c.levels);
+    }
     std::map<int, std::pair<float, float>> found;
-    std::vector<float> from_xy, to_xy;
-    std::vector<int32_t> lv, acc;
-    while (!active.empty()) {
-      // This round's attempt per feature: its next view whose starting point is in bounds.
-      struct Try {
-        size_t cand;
-        int slot;
-        float fx, fy, tx, ty;
-      };
-      std::vector<Try> tries;
-      std::vector<Cand> keep;
-      for (auto& c : active) {
-        const auto& ms = features_[c.id].matches;
-        bool queued = false;
-        while (c.next < ms.size()) {
-          const Match& m = ms[c.next++];
-          const View* from = FindView(m.view_seq);
-          SG_REQUIRE(from, SG_EINVAL, "feature refers to an expired view");
-          float tx = m.x, ty = m.y;
-          if (c.projected) {
-            tx = c.px;
-            ty = c.py;
-          }
-          // OOB test of matcher.cpp:245-247 (note '>' for y).
-          if (tx < 0 || ty < 0 || tx >= (float)to.w || ty > (float)to.h) continue;
-          tries.push_back({keep.size(), from->slot, m.x, m.y, tx, ty});
-          queued = true;
-          break;
-        }
-        if (queued) keep.push_back(c);
-      }
-      if (tries.empty()) break;
-      std::vector<char> ok(tries.size(), 0);
-      std::vector<std::pair<float, float>> res(tries.size());
-      // One device launch per source view.
-      std::vector<int> slots;
-      for (auto& t : tries)
-        if (std::find(slots.begin(), slots.end(), t.slot) == slots.end()) slots.push_back(t.slot);
-      for (int slot : slots) {
-        std::vector<size_t> idx;
-        from_xy.clear();
-        to_xy.clear();
-        lv.clear();
-        for (size_t i = 0; i < tries.size(); ++i)
-          if (tries[i].slot == slot) {
-            idx.push_back(i);
-            from_xy.push_back(tries[i].fx);
-            from_xy.push_back(tries[i].fy);
-            to_xy.push_back(tries[i].tx);
-            to_xy.push_back(tries[i].ty);
-            lv.push_back(keep[tries[i].cand].levels);
-          }
-        acc.assign(idx.size(), 0);
-        const int n = (int)idx.size();
-        trk_->LoadFeatures(n, from_xy.data(), to_xy.data(), lv.data());
-        trk_->Run(slot, to.slot, 1);
-        trk_->Results(to_xy.data(), acc.data(), nullptr);
-        ++batches_;
-        for (int j = 0; j < n; ++j) {
-          ok[idx[j]] = acc[j] != 0;
-          res[idx[j]] = {to_xy[2 * j], to_xy[2 * j + 1]};
-        }
-      }
-      std::vector<Cand> next;
-      for (size_t i = 0; i < tries.size(); ++i) {
-        const Cand& c = keep[tries[i].cand];
-        if (ok[i])
-          found[c.id] = res[i];
-        else
-          next.push_back(c);
-      }
-      active.swap(next);
+    const int n = (int)active.size();
+    if (n > 0 && aoff.back() > 0) {
+      std::vector<float> to_xy(2 * (size_t)n);
+      std::vector<int32_t> which(n, -1);
+      trk_->FindMatches(to.slot, n, aoff.data(), aslot.data(), axy.data(), lv.data(), to_xy.data(), which.data(),
+                        nullptr);
+      ++batches_;
+      for (int i = 0; i < n; ++i)
+        if (which[i] >= 0) found[active[i].id] = {to_xy[2 * i], to_xy[2 * i + 1]};
     }
     // Add the new observations in the reference's loop order (features by id).
     for (auto& m : found) {

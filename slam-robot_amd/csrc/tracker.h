@@ -36,6 +36,11 @@ class Tracker {
   void LoadFeatures(int n, const float* from_xy, const float* to_xy, const int32_t* levels);
   void Run(int from, int to, int repeats);
   void Results(float* to_xy, int32_t* accepted, int32_t* iterations);
+  // FindMatches (matcher.cpp:210-271) of n features into slot `to` in one launch: feature f's attempts are
+  // aoff[f] .. aoff[f+1]-1, attempt a from slot aslot[a], match point axy[4a..4a+1], start axy[4a+2..4a+3];
+  // which[f] = the accepted attempt's index in the feature's list or -1, to_xy its track.
+  void FindMatches(int to, int n, const int32_t* aoff, const int32_t* aslot, const float* axy, const int32_t* levels,
+                   float* to_xy, int32_t* which, int32_t* iterations);
   // One-directional TrackFeature of the configured FeatureTracker (hessian.h / klt.h / brute.h).
   void TrackFeature(int from, int to, int n, const float* from_xy, float* to_xy, const int32_t* levels,
                     int32_t* status, int32_t* iterations);
@@ -65,6 +70,10 @@ class Tracker {
   DBuf<uint8_t> img_;
   DBuf<float> from_, init_, out_;
   DBuf<int32_t> levels_, acc_, its_;
+  std::vector<uint8_t> tabs_h_;   // every slot's level table [max_images][kTrkMaxDepth] (k_find_matches)
+  DBuf<uint8_t> tabs_;
+  DBuf<int32_t> aoff_, aslot_;
+  DBuf<float> axy_;
   DBuf<float> seed_dx_, seed_dy_, seed_eig_, seed_val_, seed_val2_;
   DBuf<uint8_t> seed_flag_, seed_tmp_;
   DBuf<int> seed_idx_, seed_idx2_, seed_misc_;

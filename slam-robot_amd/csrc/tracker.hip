@@ -489,9 +489,57 @@ __device__ __forceinline__ int track_pass(const TrackCtx& c, const LevelDev* __r
   return 0;
 }
 
+// matcher.cpp TrackFeature (173-206) + FindMatches' retry with more levels (247-251) of one feature (one wave):
+// forward from (fx, fy) starting at (*tx, *ty), backward, the forward/backward check; *tx, *ty hold the last
+// forward result (the retry starts from the forward-mutated to_pt, matcher.cpp:176, 247-248).  The backward pass
+// is skipped when the forward pass failed: the matcher rejects the feature either way and the backward pass
+// does not touch to_pt.
+template <int NK>
+__device__ __forceinline__ bool fb_track(const TrackCtx& c, const LevelDev* __restrict__ from_lv,
+                                         const LevelDev* __restrict__ to_lv, int depth, const TrackParams& prm,
+                                         float fx, float fy, int lv0, float* ptx, float* pty, int* piters,
+                                         float* tile) {
+  float tx = *ptx, ty = *pty;
+  int iters = *piters;
+  bool ok = false;
+  for (int attempt = 0; attempt < 2 && !ok; ++attempt) {
+    int lv = lv0;
+    if (attempt == 1) {
+      if (prm.retry_levels <= 0 || lv0 == prm.retry_levels) break;
+      lv = prm.retry_levels;
+    }
+    const int lvls = min(depth, lv);
+    int st = 0;
+    float bx = fx, by = fy;
+    for (int pass = 0; pass < 2; ++pass) {
+      const LevelDev* src = pass ? to_lv : from_lv;
+      const LevelDev* dst = pass ? from_lv : to_lv;
+      const float sx = pass ? tx : fx, sy = pass ? ty : fy;
+      float qx = pass ? bx : tx, qy = pass ? by : ty;
+      st = track_pass<NK>(c, src, dst, lvls, sx, sy, &qx, &qy, &iters, tile);
+      if (st != 0) break;
+      if (pass == 0) {
+        tx = qx;
+        ty = qy;
+      } else {
+        bx = qx;
+        by = qy;
+      }
+    }
+    if (st == 0) {
+      const float ex = fx - bx, ey = fy - by;
+      ok = !(sqrt((double)ex * ex + (double)ey * ey) > (double)prm.fb_max);
+    }
+  }
+  *ptx = tx;
+  *pty = ty;
+  *piters = iters;
+  return ok;
+}
+
+__device__ __forceinline__ void init_ctx(TrackCtx& c, const TrackParams& prm, int lane);
+
 // matcher.cpp TrackFeature (173-206) + FindMatches' retry with more levels (247-251), one wave per feature.
-// The attempt and pass loops share one inlined body.  The backward pass is skipped when the forward pass
-// failed: the matcher rejects the feature either way and the backward pass does not touch to_pt.
 template <int NK>
 __global__ __launch_bounds__(64 * kTrackWaves) void k_track_fb(const LevelDev* __restrict__ from_lv,
                                                                const LevelDev* __restrict__ to_lv, int depth,
@@ -526,36 +574,7 @@ __global__ __launch_bounds__(64 * kTrackWaves) void k_track_fb(const LevelDev* _
   float tx = to_init[2 * f], ty = to_init[2 * f + 1];
   const int lv0 = levels ? levels[f] : 3;
   int iters = 0;
-  bool ok = false;
-  for (int attempt = 0; attempt < 2 && !ok; ++attempt) {
-    int lv = lv0;
-    if (attempt == 1) {
-      if (prm.retry_levels <= 0 || lv0 == prm.retry_levels) break;
-      lv = prm.retry_levels;
-    }
-    const int lvls = min(depth, lv);
-    int st = 0;
-    float bx = fx, by = fy;
-    for (int pass = 0; pass < 2; ++pass) {
-      const LevelDev* src = pass ? to_lv : from_lv;
-      const LevelDev* dst = pass ? from_lv : to_lv;
-      const float sx = pass ? tx : fx, sy = pass ? ty : fy;
-      float qx = pass ? bx : tx, qy = pass ? by : ty;
-      st = track_pass<NK>(c, src, dst, lvls, sx, sy, &qx, &qy, &iters, tile);
-      if (st != 0) break;
-      if (pass == 0) {
-        tx = qx;
-        ty = qy;
-      } else {
-        bx = qx;
-        by = qy;
-      }
-    }
-    if (st == 0) {
-      const float ex = fx - bx, ey = fy - by;
-      ok = !(sqrt((double)ex * ex + (double)ey * ey) > (double)prm.fb_max);
-    }
-  }
+  const bool ok = fb_track<NK>(c, from_lv, to_lv, depth, prm, fx, fy, lv0, &tx, &ty, &iters, tile);
   if (lane == 0) {
     to_xy[2 * f] = tx;
     to_xy[2 * f + 1] = ty;
@@ -636,6 +655,48 @@ __global__ __launch_bounds__(64 * kTrackWaves) void k_track_one(const LevelDev* 
       to_xy[2 * f] = qx;
       to_xy[2 * f + 1] = qy;
     }
+    if (iterations) iterations[f] = iters;
+  }
+}
+
+// matcher.cpp FindMatches (210-271) over a batch of features into one view: one wave per feature walks the
+// feature's attempts — a stored view (pyramid slot) and its match point, the starting point in the new view, in
+// the feature's view order, out-of-bounds starts already dropped (matcher.cpp:245-247) — and stops at the first
+// forward/backward-consistent track (fb_track, with the retry).  which[f]: the accepted attempt (-1: none), to_xy
+// its track.  A frame's matching is one launch instead of a host round trip per view and round.
+template <int NK>
+__global__ __launch_bounds__(64 * kTrackWaves) void k_find_matches(const LevelDev* __restrict__ tabs, int to_slot,
+                                                                   int depth, TrackParams prm, int n,
+                                                                   const int32_t* __restrict__ aoff,
+                                                                   const int32_t* __restrict__ aslot,
+                                                                   const float4* __restrict__ axy,
+                                                                   const int32_t* __restrict__ levels, float* to_xy,
+                                                                   int32_t* which, int32_t* iterations) {
+  __shared__ float stage_tiles[kTrackWaves][kStT * kStT];
+  const int lane = threadIdx.x & 63;
+  const int f = blockIdx.x * kTrackWaves + (threadIdx.x >> 6);
+  if (f >= n) return;   // whole wave
+  float* tile = stage_tiles[threadIdx.x >> 6];
+  TrackCtx c;
+  TStamp tst_off;
+  init_ctx(c, prm, lane);
+  c.ts = &tst_off;
+  const LevelDev* to_lv = tabs + (size_t)to_slot * kTrkMaxDepth;
+  const int a0 = aoff[f], a1 = aoff[f + 1], lv0 = levels[f];
+  int iters = 0, hit = -1;
+  float tx = 0.f, ty = 0.f;
+  for (int a = a0; a < a1 && hit < 0; ++a) {
+    const float4 xy = axy[a];
+    tx = xy.z;
+    ty = xy.w;
+    if (fb_track<NK>(c, tabs + (size_t)aslot[a] * kTrkMaxDepth, to_lv, depth, prm, xy.x, xy.y, lv0, &tx, &ty, &iters,
+                     tile))
+      hit = a - a0;
+  }
+  if (lane == 0) {
+    to_xy[2 * f] = tx;
+    to_xy[2 * f + 1] = ty;
+    which[f] = hit;
     if (iterations) iterations[f] = iters;
   }
 }
@@ -1065,6 +1126,9 @@ void Tracker::SetImage(int slot, const uint8_t* bgr, int w, int h, int stride) {
     std::memcpy(tab.data() + sizeof(LevelDev) * l, &L, sizeof(L));
   }
   s.table.Upload(tab, stream_);
+  tabs_h_.resize(sizeof(LevelDev) * kTrkMaxDepth * slots_.size());
+  std::memcpy(tabs_h_.data() + sizeof(LevelDev) * kTrkMaxDepth * slot, tab.data(), tab.size());
+  tabs_.Upload(tabs_h_, stream_);
   SG_HIP_CHECK(hipStreamSynchronize(stream_));   // the host image buffer may be reused by the caller
   float ms = 0.f;
   SG_HIP_CHECK(hipEventElapsedTime(&ms, ev_[2], ev_[3]));
@@ -1157,6 +1221,47 @@ void Tracker::Run(int from, int to, int repeats) {
   SG_HIP_CHECK(hipEventRecord(ev_[1], stream_));
   SG_HIP_CHECK(hipGetLastError());
   ran_ = true;
+}
+
+void Tracker::FindMatches(int to, int n, const int32_t* aoff, const int32_t* aslot, const float* axy,
+                          const int32_t* levels, float* to_xy, int32_t* which, int32_t* iterations) {
+  SG_REQUIRE(to >= 0 && to < (int)slots_.size() && slots_[to].valid, SG_EINVAL, "empty 'to' slot");
+  SG_REQUIRE(n >= 0, SG_EINVAL, "bad feature count");
+  if (n == 0) return;
+  SG_REQUIRE(aoff && levels && to_xy && which && aoff[0] == 0, SG_EINVAL, "bad attempt lists");
+  const int na = aoff[n];
+  for (int f = 0; f < n; ++f) SG_REQUIRE(aoff[f + 1] >= aoff[f] && levels[f] >= 1, SG_EINVAL, "bad attempt lists");
+  for (int a = 0; a < na; ++a) {
+    SG_REQUIRE(aslot[a] >= 0 && aslot[a] < (int)slots_.size() && slots_[aslot[a]].valid, SG_EINVAL,
+               "attempt from an empty slot");
+    SG_REQUIRE(slots_[aslot[a]].w == slots_[to].w && slots_[aslot[a]].h == slots_[to].h, SG_EINVAL,
+               "pyramids of different sizes");
+  }
+  SG_HIP_CHECK(hipSetDevice(dev_.device));
+  aoff_.Upload(std::vector<int32_t>(aoff, aoff + n + 1), stream_);
+  aslot_.Upload(std::vector<int32_t>(aslot, aslot + std::max(na, 1)), stream_);
+  axy_.Upload(std::vector<float>(axy, axy + 4 * (size_t)std::max(na, 1)), stream_);
+  levels_.Upload(std::vector<int32_t>(levels, levels + n), stream_);
+  out_.Resize(2 * (size_t)n);
+  acc_.Resize(n);
+  its_.Resize(n);
+  TrackParams prm{opt_.window, opt_.max_iterations, opt_.threshold, opt_.fb_max, opt_.retry_levels, mask_.ptr};
+  SG_HIP_CHECK(hipEventRecord(ev_[0], stream_));
+  SG_TRK_NK(opt_.window, k_find_matches, dim3((n + kTrackWaves - 1) / kTrackWaves), dim3(64 * kTrackWaves), 0,
+            stream_, (const LevelDev*)tabs_.ptr, to, opt_.depth, prm, n, aoff_.ptr, aslot_.ptr,
+            reinterpret_cast<const float4*>(axy_.ptr), levels_.ptr, out_.ptr, acc_.ptr, its_.ptr);
+  SG_HIP_CHECK(hipEventRecord(ev_[1], stream_));
+  SG_HIP_CHECK(hipGetLastError());
+  SG_HIP_CHECK(hipMemcpyAsync(to_xy, out_.ptr, sizeof(float) * 2 * n, hipMemcpyDeviceToHost, stream_));
+  SG_HIP_CHECK(hipMemcpyAsync(which, acc_.ptr, sizeof(int32_t) * n, hipMemcpyDeviceToHost, stream_));
+  if (iterations)
+    SG_HIP_CHECK(hipMemcpyAsync(iterations, its_.ptr, sizeof(int32_t) * n, hipMemcpyDeviceToHost, stream_));
+  SG_HIP_CHECK(hipStreamSynchronize(stream_));
+  float ms = 0.f;
+  SG_HIP_CHECK(hipEventElapsedTime(&ms, ev_[0], ev_[1]));
+  track_ms_ = ms;
+  ran_ = false;   // the batch buffers now hold this call's lists, not a LoadFeatures batch
+  n_ = 0;
 }
 
 std::vector<unsigned long long> Tracker::Stamps() {

@@ -13,73 +13,13 @@ import sys
 
 import numpy as np
 import pytest
-from scipy import ndimage
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(os.path.dirname(HERE), "oracle"))
 import oracle_matcher as om  # noqa: E402
 
-W, H = 320, 240
-K = np.array([0.0, 0.0, 0.0, 416.0, -416.0, 160.0, 120.0])     # main.cpp:474-482 intrinsics, centred
-
-
-def _texture(seed, margin=48):
-    rng = np.random.default_rng(seed)
-    t = rng.uniform(0.0, 255.0, size=(H + 2 * margin, W + 2 * margin))
-    return ndimage.gaussian_filter(t, 2.0), margin
-
-
-def _warp(tex, m, dx, dy):
-    ys, xs = np.mgrid[0:H, 0:W].astype(np.float64)
-    return ndimage.map_coordinates(tex, [ys - dy + m, xs - dx + m], order=1, mode="nearest")
-
-
-# (texture seed of the right part, fraction of the width [from the left] covered by a fresh texture)
-SCHEDULE = [(None, 0.0), (None, 0.0), (None, 0.0), (11, 0.8), (11, 0.8), (12, 0.85), (13, 0.9), (13, 0.9),
-            (14, 0.9), (15, 0.9), (None, 0.0)]
-
-
-def make_sequence():
-    base, m = _texture(3)
-    frames, shifts = [], []
-    for i, (seed, frac) in enumerate(SCHEDULE):
-        dx, dy = 0.7 * i, -0.4 * i
-        img = _warp(base, m, dx, dy)
-        if seed is not None:
-            other, m2 = _texture(seed)
-            cut = int(frac * W)
-            img[:, :cut] = _warp(other, m2, 0.5 * i, 0.3 * i)[:, :cut]
-        g = np.clip(np.rint(img), 0, 255).astype(np.uint8)
-        frames.append(np.repeat(g[:, :, None], 3, axis=2))
-        shifts.append((dx, dy))
-    return frames, shifts
-
-
-def _true_t(i):
-    """Camera translation that moves a point 2000 mm ahead by the base texture's image shift (0.7, -0.4) px
-    per frame (fx = 416, fy = -416)."""
-    return np.array([-0.7 * i * 2000 / 416, -0.4 * i * 2000 / 416, 0.0])
-
-
-def _pose(i):
-    """Initial pose guess: identity rotation; odd frames from 3 on start 100 mm off (about 20 px), which
-    update_frames then corrects (the role SolveFramePose would have)."""
-    t = _true_t(i)
-    if i >= 3 and i % 2 == 1:
-        t = t + np.array([100.0, 0.0, 0.0])
-    return np.array([0.0, 0.0, 0.0, 1.0]), t
-
-
-def _mark(step, flags, unc, npts):
-    """Between frames: mark some points MISMATCHED and give some an uncertainty below 100 (Clean's role)."""
-    if step == 5 and npts > 10:
-        flags[3] |= 1 << om.MISMATCHED
-        flags[7] |= 1 << om.MISMATCHED
-    if step in (2, 6):
-        for p in range(0, npts, 3):
-            unc[p] = 3.0
-        for p in range(1, npts, 6):
-            unc[p] = 100.0
+from slamgpu.video import SEQ_K as K, matcher_sequence as make_sequence  # noqa: E402
+from slamgpu.video import sequence_mark as _mark, sequence_pose as _pose, sequence_true_t as _true_t  # noqa: E402
 
 
 def run_oracle(frames):
