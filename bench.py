@@ -458,8 +458,14 @@ class Runner:
                 "device_kernel_ms": dev_ms, "iters_per_s_device": its / (dev_ms * 1e-3) if dev_ms else None}
 
 
+SPEC = os.environ.get("SG_SPEC", "1") != "0"   # speculative linearization (the library default)
+KERNEL_SYMBOL = {"point_update": "k_update_lin" if SPEC else "k_point_update"}
+
+
 def kernel_report(res, steps, n_text, workload):
-    """Per-iteration kernel times, the dominant kernel's roofline and the sweep roofline."""
+    """Per-iteration kernel times, the dominant kernel's roofline and the sweep roofline.  The Jacobian sweep of
+    the timed iterations is k_update_lin (the candidate pass + the candidate's linearization) in the speculative
+    chain, where k_linearize runs only in a solve's first iteration; k_linearize otherwise."""
     kt, work = res["kt"], res["work"]
     per_iter_ms = {k: v[0] * v[1] / max(steps, 1) for k, v in kt.items()}
     dominant = max(per_iter_ms, key=per_iter_ms.get)
@@ -474,18 +480,22 @@ def kernel_report(res, steps, n_text, workload):
                         "over its mean HIP-event launch time" % n_text}
     else:
         ach = dom_bytes / (dom_ms * 1e-3) / 1e9
+        sym = KERNEL_SYMBOL.get(dominant, "k_" + dominant)
         roof = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": ach / HBM_PEAK_GBS, **traffic_fields("k_" + dominant, workload, dom_bytes), "kernel": dominant,
+                "frac": ach / HBM_PEAK_GBS, **traffic_fields(sym, workload, dom_bytes), "kernel": sym,
                 "us_per_launch": 1e3 * dom_ms}
     sweep = None
     n_lin = res["lin_active"]
-    if n_lin > 0:
-        lin_total_ms = kt["linearize"][0] * kt["linearize"][1]
-        ach = work["linearize"][0] * n_lin / (lin_total_ms * 1e-3) / 1e9
+    lk = "linearize" if kt.get("linearize", (0, 0))[1] > 0 else "point_update"
+    if n_lin > 0 and kt.get(lk, (0, 0))[1] > 0:
+        sym = "k_linearize" if lk == "linearize" else KERNEL_SYMBOL["point_update"]
+        total_ms = kt[lk][0] * kt[lk][1]
+        active = n_lin if lk == "linearize" else kt[lk][1]
+        ach = work[lk][0] * active / (total_ms * 1e-3) / 1e9
         sweep = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                 "frac": ach / HBM_PEAK_GBS, "bytes_per_launch": work["linearize"][0],
-                 **traffic_fields("k_linearize", workload, work["linearize"][0]), "active_launches": n_lin,
-                 "launches": kt["linearize"][1]}
+                 "frac": ach / HBM_PEAK_GBS, "bytes_per_launch": work[lk][0], "kernel": sym,
+                 **traffic_fields(sym, workload, work[lk][0]), "active_launches": active,
+                 "launches": kt[lk][1]}
     return {k: round(v, 5) for k, v in per_iter_ms.items()}, roof, sweep
 
 

@@ -671,11 +671,14 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d, int mode) {
     }
     return;
   }
-  const bool fd_here = mode == 0 || d.rank == 0;   // mode 1: the FrameDistance terms enter on rank 0 only
+  // mode 1: the FrameDistance terms enter the exchange on rank 0 only; every rank still evaluates them (fd_r,
+  // fd_J, fd_X, fd_D: the Cholesky's candidate pass takes its FrameDistance model term from them, identically
+  // on every rank)
+  const bool fd_here = mode == 0 || d.rank == 0;
   if (lin) {
     // FrameDistance residuals at x[cur]
     double myfd = 0.0;
-    for (int dd = tid; dd < (fd_here ? d.D : 0); dd += blockDim.x) {
+    for (int dd = tid; dd < d.D; dd += blockDim.x) {
       const int fa = dd == tid ? fa0 : d.fd_a[dd], fb = dd == tid ? fb0 : d.fd_b[dd];
       const double* ta = d.t[cur] + 3 * fa;
       const double* tb = d.t[cur] + 3 * fb;
@@ -727,7 +730,7 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d, int mode) {
       }
       double fdD[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
       double gfd[3] = {0, 0, 0};
-      for (int e = fd_here ? e0 : e1; e < e1; ++e) {
+      for (int e = e0; e < e1; ++e) {
         const int dd = d.fd_bidx[e] >> 1, side = d.fd_bidx[e] & 1;
         const double* Jd = fd_lds ? fdJs + 6 * dd + 3 * side : d.fd_J + 6 * dd + 3 * side;
         const double rr = fd_lds ? fdrs[dd] : d.fd_r[dd];
@@ -736,11 +739,10 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d, int mode) {
           for (int j = 0; j < 3; ++j) fdD[3 * i + j] += Jd[i] * Jd[j];
         }
       }
-      if (fd_here)
-        for (int i = 0; i < 9; ++i) d.fd_D[9 * b + i] = fdD[i];
+      for (int i = 0; i < 9; ++i) d.fd_D[9 * b + i] = fdD[i];
       for (int a = 0; a < 6; ++a) {
-        const double gg = Ug[a] + (a >= 3 ? gfd[a - 3] : 0.0);
-        const double dg = Ud[a] + (a >= 3 ? fdD[4 * (a - 3)] : 0.0);
+        const double gg = Ug[a] + ((fd_here && a >= 3) ? gfd[a - 3] : 0.0);
+        const double dg = Ud[a] + ((fd_here && a >= 3) ? fdD[4 * (a - 3)] : 0.0);
         d.camg[6 * b + a] = gg;
         d.camdiag[6 * b + a] = dg;
         if (mode == 1) {
@@ -756,7 +758,7 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d, int mode) {
     if (mode == 1) {
       // this rank's cost scalars and max |g| slots, and the FrameDistance cost (rank 0), into the tail
       if (tid < kXNum + d.nranks) txs[tid] = d.xcam_loc[nv + tid];
-      if (tid == 0) txs[kXNum + d.nranks] = fd_total;
+      if (tid == 0) txs[kXNum + d.nranks] = fd_here ? fd_total : 0.0;
       return;
     }
     __syncthreads();

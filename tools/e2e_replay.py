@@ -122,7 +122,42 @@ if len(gaps) > 2:
     crit["gap_ms_of_loads_over_5ms"] = [round(float(g), 2) for g, l in zip(gaps, loads) if l > 5]
 summary["criteria"] = crit
 print("criteria:", json.dumps(crit))
+
+# Control: the same host gaps, in the same order, with no load behind them: after each call's
+# measured gap (slept), a no-op device round trip (one tiny kernel through torch, then synchronize) and, after
+# the gap again, a minimal library call (ReprojectMap of a one-observation map: small uploads, two kernels, a
+# download).  If these also take 10-28 ms after the gaps where loads did, the stall is the idle GPU's start
+# latency, independent of the load path.
+import torch  # noqa: E402
+
+xz = torch.zeros(1, device="cuda")
+tiny = make_scene(num_frames=2, num_points=1, seed=1, run_max=2)
+ctrl = []
+for r in later:
+    g = r["gap_ms"] / 1e3
+    time.sleep(g)
+    t0 = time.perf_counter()
+    xz.add_(1.0)
+    torch.cuda.synchronize()
+    noop = 1e3 * (time.perf_counter() - t0)
+    time.sleep(g)
+    t0 = time.perf_counter()
+    slam.ReprojectMap(tiny)
+    small = 1e3 * (time.perf_counter() - t0)
+    ctrl.append({"frame": r["frame"], "gap_ms": r["gap_ms"], "load_ms": r["load"], "noop_ms": noop,
+                 "tiny_call_ms": small})
+noops = np.array([c["noop_ms"] for c in ctrl])
+tinys = np.array([c["tiny_call_ms"] for c in ctrl])
+cgaps = np.array([c["gap_ms"] for c in ctrl])
+control = {"calls": len(ctrl), "noop_ms_median": float(np.median(noops)), "noop_ms_max": float(noops.max()),
+           "tiny_call_ms_median": float(np.median(tinys)), "tiny_call_ms_max": float(tinys.max()),
+           "noop_over_5ms": [(round(float(g), 2), round(float(v), 2)) for g, v in zip(cgaps, noops) if v > 5],
+           "tiny_over_5ms": [(round(float(g), 2), round(float(v), 2)) for g, v in zip(cgaps, tinys) if v > 5],
+           "loads_over_5ms": [(round(float(c["gap_ms"]), 2), round(float(c["load_ms"]), 2)) for c in ctrl
+                              if c["load_ms"] > 5]}
+summary["control"] = control
+print("control (same gaps, no load):", json.dumps(control))
 print("load counts (full, values):", slam.load_counts())
 os.makedirs(os.path.dirname(out_path), exist_ok=True)
 with open(out_path, "w") as f:
-    json.dump({"summary": summary, "calls": stats}, f, indent=1)
+    json.dump({"summary": summary, "calls": stats, "control": ctrl}, f, indent=1)

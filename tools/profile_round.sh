@@ -15,7 +15,7 @@ WLS=${2:-"C2 C5 sweep frontend"}
 OUT="$R/gpurun_out/prof_$TAG"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-KRE="k_chol_tiles|k_cholesky_window|k_linearize|k_cam_reduce|k_cam_finalize|k_schur|k_S_reduce|k_point_update|k_upd_reduce|k_track_fb|k_hamming_slices"
+KRE="k_chol_tiles|k_cholesky_window|k_linearize|k_cam_reduce|k_cam_finalize|k_schur|k_S_reduce|k_point_update|k_update_lin|k_upd_reduce|k_track_fb|k_find_matches|k_hamming_slices"
 for W in $WLS; do
   echo "== $W kernel trace"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt_$W" -o run --output-format csv \
