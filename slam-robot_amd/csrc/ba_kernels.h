@@ -199,6 +199,7 @@ struct Dev {
   double* xchg_cam;              // [NB*27 + kXNum + nranks]: camera blocks, scalars, per-rank max |g| slots
                                  // (summed over the shards by the camera-block all-reduce)
   double* xcam_loc;              // the same, this rank's own (never all-reduced)
+  double* xchg_cand;             // the same for the candidate (speculative chain: k_cam_reduce mode 1), local
   double* xtail;                 // merged exchange tail after the packed band of S (k_cam_finalize modes 1, 2):
                                  // camera gradient [6 NB] | diagonal [6 NB] | scalars [kXNum] | max |g| [nranks]
                                  // | FrameDistance cost

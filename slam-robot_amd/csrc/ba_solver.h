@@ -113,6 +113,7 @@ class BaSolver {
   int merge_ = getenv("SG_XCHG_MERGE") ? (std::string(getenv("SG_XCHG_MERGE")) == "force" ? 2 : atoi(getenv("SG_XCHG_MERGE")) != 0)
                                        : 1;
   size_t ntail_ = 0;   // doubles of the merged exchange's tail
+  bool pending_decision_ = false;   // speculative chain: the last enqueued step awaits its decision
   int32_t nallreduce_ = 0;   // landmark-shard all-reduces issued (sg_ba_info.num_allreduces)
   size_t npack_ = 0;                                      // band of S + rhs, doubles (all-reduce size)
   bool stamp_on_ = false;

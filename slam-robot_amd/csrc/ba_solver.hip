@@ -440,12 +440,34 @@ __global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_linearize(Dev d) {
 // block's list, the slices combined in slice order; the last workgroup reduces the chunk scalars.
 constexpr int kCamSlices = 32;
 constexpr int kRedThreads = 1024;   // >= kCamSlices * kCamV
-__global__ __launch_bounds__(kRedThreads) void k_cam_reduce(Dev d) {
+__device__ void upd_reduce_body(const Dev& d, int fuse);
+
+// mode 0: the current slot's partials (after a solve's first k_linearize, or after k_linearize in the two-pass
+//         chain), into xchg_cam / xcam_loc; a step that did not linearize (need_lin = 0) leaves them, and with
+//         landmark shards copies this rank's blocks into the all-reduce buffer again;
+// mode 1: speculative chain, right after k_update_lin: the candidate slot's partials into xchg_cand (the decision
+//         that follows copies them to the current blocks if it accepts the step), and block NB + 1 reduces the
+//         update scalars (k_upd_reduce without the decision).  Nothing here writes LmState, so every block reads
+//         the same slot.
+__global__ __launch_bounds__(kRedThreads) void k_cam_reduce(Dev d, int mode) {
   const LmState* st = d.st;
-  if (st->done || !st->need_lin) return;
+  if (mode == 1 && (int)blockIdx.x == d.NB + 1) {
+    upd_reduce_body(d, 0);
+    return;
+  }
+  if (st->done) return;
   const int tid = threadIdx.x;
   const int nv = d.NB * kCamV;
-  const int cur = st->cur;
+  const int nx = nv + kXNum + d.nranks;
+  if (mode == 0 && !st->need_lin) {
+    // no new linearization: the shards' camera-block all-reduce sums this rank's current blocks again
+    if (d.nranks > 1 && blockIdx.x == 0)
+      for (int i = tid; i < nx; i += blockDim.x) d.xchg_cam[i] = d.xcam_loc[i];
+    return;
+  }
+  const int cur = mode == 1 ? st->cur ^ 1 : st->cur;
+  double* dst = mode == 1 ? d.xchg_cand : d.xchg_cam;
+  double* dst2 = mode == 1 ? d.xchg_cand : d.xcam_loc;
   if ((int)blockIdx.x < d.NB) {
     const int b = blockIdx.x;
     __shared__ double part[kCamSlices][kCamV];
@@ -476,8 +498,8 @@ __global__ __launch_bounds__(kRedThreads) void k_cam_reduce(Dev d) {
       if (!d.spec) d.cam_wide[cur][i] = 0.0;
 #pragma unroll
       for (int k = 0; k < kCamSlices; ++k) s += part[k][tid];
-      d.xchg_cam[i] = s;   // summed over the shards (camera-block all-reduce) or left as this rank's
-      d.xcam_loc[i] = s;   // this rank's own (k_S_reduce's local assembly, k_cam_finalize mode 1)
+      dst[i] = s;    // summed over the shards (camera-block all-reduce) or left as this rank's
+      dst2[i] = s;   // this rank's own (k_S_reduce's local assembly, k_cam_finalize mode 1)
     }
     return;
   }
@@ -514,9 +536,9 @@ __global__ __launch_bounds__(kRedThreads) void k_cam_reduce(Dev d) {
   gm = block_max<kRedThreads>(gm, redm);
   if (tid == 0) {
 #pragma unroll
-    for (int j = 0; j < kXNum; ++j) d.xchg_cam[nv + j] = d.xcam_loc[nv + j] = v[j];
+    for (int j = 0; j < kXNum; ++j) dst[nv + j] = dst2[nv + j] = v[j];
     // max |g| travels in the same sum all-reduce: one slot per rank, zeros in the others' slots
-    for (int r = 0; r < d.nranks; ++r) d.xchg_cam[nv + kXNum + r] = d.xcam_loc[nv + kXNum + r] = (r == d.rank) ? gm : 0.0;
+    for (int r = 0; r < d.nranks; ++r) dst[nv + kXNum + r] = dst2[nv + kXNum + r] = (r == d.rank) ? gm : 0.0;
   }
 }
 
@@ -587,9 +609,14 @@ __device__ __forceinline__ void fin_count(LmState& s0) {
 //         into the exchange tail with the cost scalars; no bookkeeping;
 // mode 2: after the merged exchange (every rank, identically): the bookkeeping on the summed tail, the LM
 //         diagonal, and the damping D^2 / radius added to the summed S (k_S_reduce's local assembly leaves it out).
-__global__ __launch_bounds__(256) void k_cam_finalize(Dev d, int mode) {
+// decide: the speculative chain on one rank, or shards after the update-scalar all-reduce: thread 0 first takes
+// the pending step's decision (decide_step, as k_decide) and, when it accepts, the candidate's camera blocks and
+// scalars (k_cam_reduce mode 1, xchg_cand) become the current ones — so no separate decision launch.
+__device__ void decide_step(LmState& s, const double* u, const double* c);
+__global__ __launch_bounds__(256) void k_cam_finalize(Dev d, int mode, int decide) {
   LmState* st = d.st;
   __shared__ double red[4];
+  __shared__ int dsh[4];   // after the decision: cur, need_lin, done, accepted
   __shared__ double fdcost[256];
   __shared__ double fdJs[6 * kFinFdSh], fdrs[kFinFdSh];
   __shared__ double gsh[kFinNSh], dgsh[kFinNSh], scsh[kFinNSh];
@@ -606,15 +633,20 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d, int mode) {
   const double* U0 = mode == 1 ? d.xcam_loc : d.xchg_cam;
   // block pass operands of block tid (the common case NB <= 256) and the first FrameDistance pair: their
   // loads go out beside LmState's (see k_S_reduce) and stay in flight during the FrameDistance pass
-  double Ug[6], Ud[6];
+  double Ug[6], Ud[6], Ugc[6], Udc[6];
   int e0 = 0, e1 = 0;
   const int b0 = tid < d.NB ? tid : 0;
   if (mode != 2) {
     const double* U = U0 + (size_t)b0 * kCamV;
+    const double* Uc = d.xchg_cand + (size_t)b0 * kCamV;   // (read only when a decision accepts)
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
       Ug[a] = U[21 + a];
       Ud[a] = U[u6(a, a)];
+      if (decide) {
+        Ugc[a] = Uc[21 + a];
+        Udc[a] = Uc[u6(a, a)];
+      }
     }
     e0 = d.fd_boff[b0];
     e1 = d.fd_boff[b0 + 1];
@@ -626,9 +658,48 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d, int mode) {
   if (tid == 0) s0 = *st;
   const int fa0 = d.D > 0 ? d.fd_a[dd0] : 0, fb0 = d.D > 0 ? d.fd_b[dd0] : 0;
   // read once, before thread 0 updates them below (no other thread re-reads LmState flags afterwards)
-  const int cur = st->cur;
-  const bool lin = st->need_lin, first = st->first, jacobi = st->jacobi;
-  if (st->done) return;
+  const bool first = st->first, jacobi = st->jacobi;
+  int cur;
+  bool lin;
+  if (decide) {
+    if (tid == 0) {
+      int acc = 0;
+      if (!s0.done) {
+        const int c0 = s0.cur;
+        decide_step(s0, d.xchg_upd, d.xchg_chol);
+        acc = s0.cur != c0;
+      }
+      dsh[0] = s0.cur;
+      dsh[1] = s0.need_lin;
+      dsh[2] = s0.done;
+      dsh[3] = acc;
+    }
+    __syncthreads();
+    cur = dsh[0];
+    lin = dsh[1];
+    if (dsh[2]) {
+      if (tid == 0) *st = s0;
+      return;
+    }
+    if (dsh[3]) {   // accepted: the candidate's blocks and scalars are the current ones from here on
+      const int nx = nv + kXNum + d.nranks;
+      for (int i = tid; i < nx; i += blockDim.x) {
+        const double v = d.xchg_cand[i];
+        d.xchg_cam[i] = v;
+        d.xcam_loc[i] = v;
+      }
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+        Ug[a] = Ugc[a];
+        Ud[a] = Udc[a];
+      }
+      __syncthreads();
+    }
+  } else {
+    cur = st->cur;
+    lin = st->need_lin;
+    if (st->done) return;
+  }
   if (mode == 2) {
     if (lin) {
       // gradient max-norm over the free camera columns of the summed gradient, and the per-rank point maxima
@@ -758,7 +829,10 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d, int mode) {
     if (mode == 1) {
       // this rank's cost scalars and max |g| slots, and the FrameDistance cost (rank 0), into the tail
       if (tid < kXNum + d.nranks) txs[tid] = d.xcam_loc[nv + tid];
-      if (tid == 0) txs[kXNum + d.nranks] = fd_here ? fd_total : 0.0;
+      if (tid == 0) {
+        txs[kXNum + d.nranks] = fd_here ? fd_total : 0.0;
+        if (decide) *st = s0;   // the decision taken above (the bookkeeping follows the exchange, mode 2)
+      }
       return;
     }
     __syncthreads();
@@ -798,6 +872,7 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d, int mode) {
   if (mode == 1) {
     // not linearized (a rejected step): the tail is not read after the exchange; keep it finite
     for (int i = tid; i < 2 * nf + kXNum + d.nranks + 1; i += blockDim.x) d.xtail[i] = 0.0;
+    if (decide && tid == 0) *st = s0;
     return;
   }
   __syncthreads();
@@ -4208,7 +4283,9 @@ __global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_update_lin(Dev d) {
 __device__ void decide_step(LmState& s, const double* u, const double* c);
 
 // fuse: single rank, no all-reduce in between: thread 0 also runs k_decide's step (one launch less).
-__global__ __launch_bounds__(kRedThreads) void k_upd_reduce(Dev d, int fuse) {
+__global__ __launch_bounds__(kRedThreads) void k_upd_reduce(Dev d, int fuse) { upd_reduce_body(d, fuse); }
+
+__device__ void upd_reduce_body(const Dev& d, int fuse) {
   const LmState* st = d.st;
   const int done = st->done;   // tested after the scalar loads are out (see k_S_reduce)
   __shared__ double red[kRedThreads / 64 * kUNum];
@@ -4263,14 +4340,29 @@ __global__ __launch_bounds__(kRedThreads) void k_upd_reduce(Dev d, int fuse) {
 
 // ------------------------------------------------------------------------------------------------
 // k_decide: TrustRegionMinimizer + LevenbergMarquardtStrategy step bookkeeping (Ceres 1.8 semantics).
-__global__ void k_decide(Dev d) {
+// take (speculative chain): the accepted candidate's camera blocks and scalars (k_cam_reduce mode 1) become this
+// rank's current ones, and the all-reduce buffer holds this rank's current blocks again (the camera-block
+// all-reduce of landmark shards sums it in place).  256 threads.
+__global__ void k_decide(Dev d, int take) {
+  __shared__ int acc_sh;
   if (threadIdx.x == 0) {
     LmState s = *d.st;
     double u[kUNum], c[kCNum];
     for (int j = 0; j < kUNum; ++j) u[j] = d.xchg_upd[j];
     for (int j = 0; j < kCNum; ++j) c[j] = d.xchg_chol[j];
+    const int c0 = s.cur;
     decide_step(s, u, c);
     *d.st = s;
+    acc_sh = s.cur != c0;
+  }
+  if (!take) return;
+  __syncthreads();
+  const int nx = d.NB * kCamV + kXNum + d.nranks;
+  const bool acc = acc_sh != 0;
+  for (int i = threadIdx.x; i < nx; i += blockDim.x) {
+    const double v = acc ? d.xchg_cand[i] : d.xcam_loc[i];
+    d.xcam_loc[i] = v;
+    d.xchg_cam[i] = v;
   }
 }
 
@@ -5250,7 +5342,7 @@ void BaSolver::Load(const sg_problem& p) {
   lap("flush");
   cam_wide_.Resize(2 * (size_t)std::max(NB_, 1) * kCamV);
   S_wide_.Resize(nn * nn);
-  xchg_cam_.Resize(2 * ((size_t)NB_ * kCamV + kXNum + nranks()));   // summed | this rank's
+  xchg_cam_.Resize(3 * ((size_t)NB_ * kCamV + kXNum + nranks()));   // summed | this rank's | candidate
   S_.Resize(nn * nn + nn + 2);   // S, then the rhs partial xc (one all-reduce covers both), then {0, 1}
   rhs_.Resize(nn);
   xchg_upd_.Resize(kUNum);
@@ -5296,6 +5388,7 @@ void BaSolver::Load(const sg_problem& p) {
   }
   loaded_ = true;
   began_ = false;
+  pending_decision_ = false;
 }
 
 void BaSolver::Reserve(int F, int P, int M) {
@@ -5454,6 +5547,7 @@ void BaSolver::LoadValues(const sg_problem& p) {
   value_loads_++;
   loaded_ = true;
   began_ = false;
+  pending_decision_ = false;
 }
 
 Dev BaSolver::MakeDev() {
@@ -5535,6 +5629,7 @@ Dev BaSolver::MakeDev() {
   d.S_wide = S_wide_.ptr;
   d.xchg_cam = xchg_cam_.ptr;
   d.xcam_loc = xchg_cam_.ptr + (size_t)NB_ * kCamV + kXNum + nranks();
+  d.xchg_cand = xchg_cam_.ptr + 2 * ((size_t)NB_ * kCamV + kXNum + nranks());
   d.xtail = Spk_.ptr + npack_;
   d.rank = comm_ ? comm_->rank() : 0;
   d.nranks = nranks();
@@ -5681,6 +5776,7 @@ void BaSolver::Begin(const sg_solver_options& o) {
     hipLaunchKernelGGL(k_reset_buffers, dim3(1), dim3(256), 0, stream_, z);
   }
   need_seq_ = true;   // the first iteration fixes the camera scale: k_schur waits for it
+  pending_decision_ = false;
   for (auto& t : timers_) {
     t.total_ms = 0.0;
     t.count = 0;
@@ -5710,7 +5806,7 @@ void BaSolver::Iterate(int n) {
   // the kernels' arguments (device pointers, sizes, variant flags) are fixed between loads.  One rank, no
   // per-kernel timing, no stamps, no side stream.
   const bool graphable = graph_ok_ && !timing_ && !stamp_on_ && !(comm_ && comm_->nranks() > 1) && !pack_force_ &&
-                         nk_ == 0 && !overlap_ok_;
+                         nk_ == 0 && !overlap_ok_ && !spec_;
   if (graphable && n > 0 && need_seq_) {   // a solve's first iteration (it linearizes) outside the graph
     EnqueueIterations(1);
     --n;
@@ -5749,7 +5845,7 @@ void BaSolver::EnqueueIterations(int n) {
     }
     // k_schur beside the camera reduction (see side_ in ba_solver.h)
     const bool first_it = need_seq_;
-    const bool overlap = overlap_ok_ && !need_seq_ && nk_ == 0;
+    const bool overlap = overlap_ok_ && !need_seq_ && nk_ == 0 && !spec_;
     need_seq_ = false;
     if (overlap) {
       SG_HIP_CHECK(hipEventRecord(ev_lin_, stream_));
@@ -5768,10 +5864,28 @@ void BaSolver::EnqueueIterations(int n) {
     // one rank too (tests the path).
     const bool multi_x = (comm_ && comm_->nranks() > 1);
     const bool merged = !first_it && nk_ == 0 && (merge_ == 2 || (multi_x && merge_ == 1));
-    TimedLaunchBegin(kKCamReduce);
     const int nv = NB_ * kCamV;
-    hipLaunchKernelGGL(k_cam_reduce, dim3(NB_ + 1), dim3(kRedThreads), 0, stream_, d);
-    TimedLaunchEnd(kKCamReduce);
+    // Speculative chain: the previous iteration ended with the candidate's camera reduce and the update scalars
+    // (k_cam_reduce mode 1, + their all-reduce on shards); the pending decision is taken by k_cam_finalize
+    // itself (one rank, or merged shards), else by k_decide, which then also makes the accepted candidate's
+    // blocks current.  No pending decision (a batch's first iteration: EnqueueIterations settles it at the
+    // end of every batch): the current blocks are in place.
+    bool decide_in_fin = false;
+    if (spec_ && !first_it) {
+      if (pending_decision_) {
+        decide_in_fin = nk_ == 0 && (merged || !multi_x);
+        if (!decide_in_fin) {
+          TimedLaunchBegin(kKDecide);
+          hipLaunchKernelGGL(k_decide, dim3(1), dim3(256), 0, stream_, d, 1);
+          TimedLaunchEnd(kKDecide);
+        }
+        pending_decision_ = false;
+      }
+    } else {
+      TimedLaunchBegin(kKCamReduce);
+      hipLaunchKernelGGL(k_cam_reduce, dim3(NB_ + 1), dim3(kRedThreads), 0, stream_, d, 0);
+      TimedLaunchEnd(kKCamReduce);
+    }
     if (!merged) AllReduceSum(xchg_cam_.ptr, (size_t)nv + kXNum + nranks());
     if (nk_) {
       hipLaunchKernelGGL(k_intr_zero, dim3((n_ * nk_ + 255) / 256), dim3(256), 0, stream_, d);
@@ -5779,7 +5893,7 @@ void BaSolver::EnqueueIterations(int n) {
       hipLaunchKernelGGL(k_intr_fin, dim3(1), dim3(64), 0, stream_, d);
     }
     TimedLaunchBegin(kKCamFinal);
-    hipLaunchKernelGGL(k_cam_finalize, dim3(1), dim3(256), 0, stream_, d, merged ? 1 : 0);
+    hipLaunchKernelGGL(k_cam_finalize, dim3(1), dim3(256), 0, stream_, d, merged ? 1 : 0, decide_in_fin ? 1 : 0);
     TimedLaunchEnd(kKCamFinal);
     if (overlap) {
       SG_HIP_CHECK(hipStreamWaitEvent(stream_, ev_schur_, 0));
@@ -5812,7 +5926,7 @@ void BaSolver::EnqueueIterations(int n) {
       TimedLaunchEnd(kKXchg);
       if (merged) {
         TimedLaunchBegin(kKCamFinal);
-        hipLaunchKernelGGL(k_cam_finalize, dim3(1), dim3(256), 0, stream_, d, 2);
+        hipLaunchKernelGGL(k_cam_finalize, dim3(1), dim3(256), 0, stream_, d, 2, 0);
         TimedLaunchEnd(kKCamFinal);
       }
     }
@@ -5840,14 +5954,26 @@ void BaSolver::EnqueueIterations(int n) {
     TimedLaunchEnd(kKPointUpd);
     const bool multi = comm_ && comm_->nranks() > 1;
     TimedLaunchBegin(kKUpdRed);
-    hipLaunchKernelGGL(k_upd_reduce, dim3(1), dim3(kRedThreads), 0, stream_, d, multi ? 0 : 1);
+    if (spec_)   // the candidate's camera blocks and linearization scalars beside the update scalars, one launch
+      hipLaunchKernelGGL(k_cam_reduce, dim3(NB_ + 2), dim3(kRedThreads), 0, stream_, d, 1);
+    else
+      hipLaunchKernelGGL(k_upd_reduce, dim3(1), dim3(kRedThreads), 0, stream_, d, multi ? 0 : 1);
     TimedLaunchEnd(kKUpdRed);
-    if (multi) {
-      AllReduceSum(xchg_upd_.ptr, kUNum);
+    if (multi) AllReduceSum(xchg_upd_.ptr, kUNum);
+    if (spec_) {
+      pending_decision_ = true;
+    } else if (multi) {
       TimedLaunchBegin(kKDecide);
-      hipLaunchKernelGGL(k_decide, dim3(1), dim3(64), 0, stream_, d);
+      hipLaunchKernelGGL(k_decide, dim3(1), dim3(256), 0, stream_, d, 0);
       TimedLaunchEnd(kKDecide);
     }
+  }
+  // a batch leaves no decision pending: the host's state reads and downloads see the decided step
+  if (pending_decision_) {
+    TimedLaunchBegin(kKDecide);
+    hipLaunchKernelGGL(k_decide, dim3(1), dim3(256), 0, stream_, d, 1);
+    TimedLaunchEnd(kKDecide);
+    pending_decision_ = false;
   }
   SG_HIP_CHECK(hipGetLastError());
 }
