@@ -131,6 +131,9 @@ struct LmState {
   int32_t termination, ok, pushed, lm_iters;
   int32_t n_succ, n_unsucc, n_invalid, consecutive_invalid;
   int32_t reuse_diag, sync_timeouts;   // sync_timeouts: Cholesky hand-off time-outs seen (kCTimeout)
+  // speculative chain: the slot k_update_lin linearized the candidate into (written by k_update_lin only), and
+  // whether the last decision accepted a step whose candidate camera blocks (xchg_cand) are still to be taken
+  int32_t spec_slot, accepted;
   double radius, decrease_factor;
   double cost, fixed_cost, initial_cost, x_norm, abs_gtol, min_pushed_cost;
   double last_model, last_new_cost, last_rel_decrease, last_step_norm;

@@ -74,7 +74,7 @@ class BaSolver {
   hipGraphExec_t iter_exec_ = nullptr;
   void DropGraph();
   void EnqueueIterations(int n);
-  hipEvent_t dev_marks_[4] = {nullptr, nullptr, nullptr, nullptr};   // SG_HOST_TIMING: device times in Load
+  hipEvent_t dev_marks_[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};   // SG_HOST_TIMING: device times in Load
   void DevMark(hipStream_t s, int i);
   hipEvent_t ev_lin_ = nullptr, ev_schur_ = nullptr;
   bool overlap_ok_ = getenv("SG_SCHUR_OVERLAP") && atoi(getenv("SG_SCHUR_OVERLAP")) == 1;

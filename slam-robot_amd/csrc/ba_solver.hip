@@ -142,6 +142,30 @@ __device__ __forceinline__ void block_sum_multi(double (&v)[NV], double* red) {
   }
 }
 
+// The same sums, for thread 0 only (the large reductions of k_cam_reduce / k_upd_reduce): lane j < NV of wave 0
+// sums partial j over the waves in the same fixed order, and thread 0 gathers the totals by v_readlane — every
+// thread summing all NV x NT/64 partials held them all in registers at once and spilled (1024-thread, 128-VGPR
+// kernels).  Only thread 0's v is meaningful afterwards.
+template <int NT, int NV>
+__device__ __forceinline__ void block_sum_multi_t0(double (&v)[NV], double* red) {
+  static_assert(NV <= 64, "one lane per value");
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) v[j] = wave_sum_full(v[j]);
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int j = 0; j < NV; ++j) red[w * NV + j] = v[j];
+  __syncthreads();
+  if (w == 0) {
+    const int j = threadIdx.x < NV ? threadIdx.x : 0;
+    double t = 0.0;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) t += red[i * NV + j];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] = readlane_dd(t, k);
+  }
+}
+
 // packed upper-triangle index of a 6x6 block (a <= c)
 __device__ __forceinline__ int u6(int a, int c) { return a * (11 - a) / 2 + c; }
 // packed upper-triangle index of a 4x4 block (a <= c)
@@ -449,10 +473,12 @@ __device__ void upd_reduce_body(const Dev& d, int fuse);
 //         that follows copies them to the current blocks if it accepts the step), and block NB + 1 reduces the
 //         update scalars (k_upd_reduce without the decision).  Nothing here writes LmState, so every block reads
 //         the same slot.
+// mode 2: mode 1 with the decision in block NB + 1 (one rank): the step is decided here, so every block takes the
+//         candidate slot from LmState::spec_slot (written by k_update_lin, unchanged by the decision), not from cur.
 __global__ __launch_bounds__(kRedThreads) void k_cam_reduce(Dev d, int mode) {
   const LmState* st = d.st;
-  if (mode == 1 && (int)blockIdx.x == d.NB + 1) {
-    upd_reduce_body(d, 0);
+  if (mode >= 1 && (int)blockIdx.x == d.NB + 1) {
+    upd_reduce_body(d, mode == 2 ? 1 : 0);
     return;
   }
   if (st->done) return;
@@ -465,9 +491,9 @@ __global__ __launch_bounds__(kRedThreads) void k_cam_reduce(Dev d, int mode) {
       for (int i = tid; i < nx; i += blockDim.x) d.xchg_cam[i] = d.xcam_loc[i];
     return;
   }
-  const int cur = mode == 1 ? st->cur ^ 1 : st->cur;
-  double* dst = mode == 1 ? d.xchg_cand : d.xchg_cam;
-  double* dst2 = mode == 1 ? d.xchg_cand : d.xcam_loc;
+  const int cur = mode >= 1 ? st->spec_slot : st->cur;
+  double* dst = mode >= 1 ? d.xchg_cand : d.xchg_cam;
+  double* dst2 = mode >= 1 ? d.xchg_cand : d.xcam_loc;
   if ((int)blockIdx.x < d.NB) {
     const int b = blockIdx.x;
     __shared__ double part[kCamSlices][kCamV];
@@ -532,7 +558,7 @@ __global__ __launch_bounds__(kRedThreads) void k_cam_reduce(Dev d, int mode) {
         gm = fmax(gm, t[u][kXNum]);
       }
   }
-  block_sum_multi<kRedThreads, kXNum>(v, red);
+  block_sum_multi_t0<kRedThreads, kXNum>(v, red);
   gm = block_max<kRedThreads>(gm, redm);
   if (tid == 0) {
 #pragma unroll
@@ -609,19 +635,48 @@ __device__ __forceinline__ void fin_count(LmState& s0) {
 //         into the exchange tail with the cost scalars; no bookkeeping;
 // mode 2: after the merged exchange (every rank, identically): the bookkeeping on the summed tail, the LM
 //         diagonal, and the damping D^2 / radius added to the summed S (k_S_reduce's local assembly leaves it out).
-// decide: the speculative chain on one rank, or shards after the update-scalar all-reduce: thread 0 first takes
-// the pending step's decision (decide_step, as k_decide) and, when it accepts, the candidate's camera blocks and
-// scalars (k_cam_reduce mode 1, xchg_cand) become the current ones — so no separate decision launch.
+// decide 1: merged shards after the update-scalar all-reduce: thread 0 first takes the pending step's decision
+// (decide_step, as k_decide) and, when it accepts, the candidate's camera blocks and scalars (k_cam_reduce
+// mode 1, xchg_cand) become the current ones — so no separate decision launch;
+// decide 2: one rank: the decision was taken by k_cam_reduce mode 2; an accepted step's candidate blocks are
+// taken here (LmState::accepted).
 __device__ void decide_step(LmState& s, const double* u, const double* c);
-__global__ __launch_bounds__(256) void k_cam_finalize(Dev d, int mode, int decide) {
+// LDS of the finalize pass: its own in k_cam_finalize, carved from k_schur's operand buffer when a k_schur launch
+// runs it in one extra workgroup (k_schur's fin).
+struct FinLds {
+  double *red, *fdcost, *fdJs, *fdrs, *gsh, *dgsh, *scsh;
+  int *dsh, *done_sh;
+  static constexpr int kDoubles = 8 + 256 + 7 * kFinFdSh + 3 * kFinNSh + 4;
+  __device__ static FinLds carve(double* p) {
+    FinLds L;
+    L.red = p;
+    L.fdcost = p + 8;
+    L.fdJs = L.fdcost + 256;
+    L.fdrs = L.fdJs + 6 * kFinFdSh;
+    L.gsh = L.fdrs + kFinFdSh;
+    L.dgsh = L.gsh + kFinNSh;
+    L.scsh = L.dgsh + kFinNSh;
+    L.dsh = reinterpret_cast<int*>(L.scsh + kFinNSh);
+    L.done_sh = L.dsh + 4;
+    return L;
+  }
+};
+
+// The pass on the first 256 threads of the workgroup (the others only meet the barriers: k_schur's
+// workgroups are larger).
+__device__ __forceinline__ void cam_finalize_body(const Dev& d, int mode, int decide, const FinLds& L) {
   LmState* st = d.st;
-  __shared__ double red[4];
-  __shared__ int dsh[4];   // after the decision: cur, need_lin, done, accepted
-  __shared__ double fdcost[256];
-  __shared__ double fdJs[6 * kFinFdSh], fdrs[kFinFdSh];
-  __shared__ double gsh[kFinNSh], dgsh[kFinNSh], scsh[kFinNSh];
-  __shared__ int done_sh;
+  double* red = L.red;      // >= 8 (one slot per wave of a 512-thread workgroup)
+  int* dsh = L.dsh;         // after the decision: cur, need_lin, done, accepted
+  double* fdcost = L.fdcost;
+  double* fdJs = L.fdJs;
+  double* fdrs = L.fdrs;
+  double* gsh = L.gsh;
+  double* dgsh = L.dgsh;
+  double* scsh = L.scsh;
+  int& done_sh = *L.done_sh;
   const int tid = threadIdx.x;
+  const bool act = tid < 256;
   const int nv = d.NB * kCamV;
   const int nf = 6 * d.NB;
   const bool fd_lds = d.D <= kFinFdSh, n_lds = nf <= kFinNSh;
@@ -664,11 +719,14 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d, int mode, int decid
   if (decide) {
     if (tid == 0) {
       int acc = 0;
-      if (!s0.done) {
+      if (decide == 1 && !s0.done) {
         const int c0 = s0.cur;
         decide_step(s0, d.xchg_upd, d.xchg_chol);
         acc = s0.cur != c0;
+      } else if (decide == 2) {
+        acc = s0.accepted;
       }
+      s0.accepted = 0;
       dsh[0] = s0.cur;
       dsh[1] = s0.need_lin;
       dsh[2] = s0.done;
@@ -683,7 +741,7 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d, int mode, int decid
     }
     if (dsh[3]) {   // accepted: the candidate's blocks and scalars are the current ones from here on
       const int nx = nv + kXNum + d.nranks;
-      for (int i = tid; i < nx; i += blockDim.x) {
+      for (int i = tid; act && i < nx; i += 256) {
         const double v = d.xchg_cand[i];
         d.xchg_cam[i] = v;
         d.xcam_loc[i] = v;
@@ -704,7 +762,7 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d, int mode, int decid
     if (lin) {
       // gradient max-norm over the free camera columns of the summed gradient, and the per-rank point maxima
       double gm = 0.0;
-      for (int f = tid; f < d.F; f += blockDim.x) {
+      for (int f = tid; act && f < d.F; f += 256) {
         const int b = d.frame_block[f];
         if (b < 0) continue;
         if (d.rot_free[f])
@@ -729,7 +787,7 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d, int mode, int decid
     if (done_sh) return;
     const double radius = st->radius;
     const bool reuse = st->reuse_diag;
-    for (int i = tid; i < d.n; i += blockDim.x) {
+    for (int i = tid; act && i < d.n; i += 256) {
       double dg;
       if (!reuse) {
         const double s = d.scale_c[i];
@@ -749,7 +807,7 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d, int mode, int decid
   if (lin) {
     // FrameDistance residuals at x[cur]
     double myfd = 0.0;
-    for (int dd = tid; dd < d.D; dd += blockDim.x) {
+    for (int dd = tid; act && dd < d.D; dd += 256) {
       const int fa = dd == tid ? fa0 : d.fd_a[dd], fb = dd == tid ? fb0 : d.fd_b[dd];
       const double* ta = d.t[cur] + 3 * fa;
       const double* tb = d.t[cur] + 3 * fb;
@@ -789,7 +847,7 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d, int mode, int decid
     const double fd_total = (fdcost[0] + fdcost[1]) + (fdcost[2] + fdcost[3]);
     // per camera block: gradient, diag, FD diagonal block
     double gm = 0.0, xn2c = 0.0;
-    for (int b = tid; b < d.NB; b += blockDim.x) {
+    for (int b = tid; act && b < d.NB; b += 256) {
       if (b != tid) {   // NB > 256: operands not prefetched
         const double* U = U0 + (size_t)b * kCamV;
         for (int a = 0; a < 6; ++a) {
@@ -837,7 +895,7 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d, int mode, int decid
     }
     __syncthreads();
     // gradient max-norm over free camera columns; camera part of |x| at iteration 0
-    for (int f = tid; f < d.F; f += blockDim.x) {
+    for (int f = tid; act && f < d.F; f += 256) {
       const int b = d.frame_block[f];
       if (b < 0) continue;
       const double* cg = n_lds ? gsh : d.camg;
@@ -855,7 +913,7 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d, int mode, int decid
     gm = block_max<256>(gm, red);
     xn2c = block_sum<256>(xn2c, red);
     if (first) {
-      for (int i = tid; i < d.n; i += blockDim.x) {
+      for (int i = tid; act && i < d.n; i += 256) {
         const double cd = (n_lds && i < nf) ? dgsh[i] : d.camdiag[i];
         const double sc = jacobi ? 1.0 / (1.0 + sqrt(cd)) : 1.0;
         d.scale_c[i] = sc;
@@ -871,7 +929,7 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d, int mode, int decid
   }
   if (mode == 1) {
     // not linearized (a rejected step): the tail is not read after the exchange; keep it finite
-    for (int i = tid; i < 2 * nf + kXNum + d.nranks + 1; i += blockDim.x) d.xtail[i] = 0.0;
+    for (int i = tid; act && i < 2 * nf + kXNum + d.nranks + 1; i += 256) d.xtail[i] = 0.0;
     if (decide && tid == 0) *st = s0;
     return;
   }
@@ -884,12 +942,17 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d, int mode, int decid
   __syncthreads();
   if (done_sh) return;
   if (!st->reuse_diag)
-    for (int i = tid; i < d.n; i += blockDim.x) {
+    for (int i = tid; act && i < d.n; i += 256) {
       const bool sh = lin && n_lds && i < nf;   // written above in this launch
       const double s = (sh && first) ? scsh[i] : d.scale_c[i];
       const double cd = sh ? dgsh[i] : d.camdiag[i];
       d.diag_c[i] = fmin(fmax(s * s * cd, st->min_diag), st->max_diag);
     }
+}
+
+__global__ __launch_bounds__(256) void k_cam_finalize(Dev d, int mode, int decide) {
+  __shared__ double lds[FinLds::kDoubles];
+  cam_finalize_body(d, mode, decide, FinLds::carve(lds));
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1175,18 +1238,26 @@ __device__ __forceinline__ void schur_cells(const Dev& d, const double* J, const
 // Diagnostic stamps (SG_STAMP=1): workgroup 0, lane 0 of the first cell wave (slots 32-36), the point wave
 // (35, 37) and the first MFMA wave (40-45) accumulate s_memtime deltas per phase.
 #define SG_SSTAMP(slot)                                                                  \
-  if (d.stamps && blockIdx.x == 0 && lane == 0 && (wave == 0 || wave == kSchurCellWaves || wave == kSchurCellWaves + 1)) { \
+  if (d.stamps && seg == 0 && lane == 0 && (wave == 0 || wave == kSchurCellWaves || wave == kSchurCellWaves + 1)) { \
     const unsigned long long now_ = __builtin_amdgcn_s_memtime();                       \
     d.stamps[(slot)] += now_ - last_;                                                    \
     last_ = now_;                                                                        \
   }
-__global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d) {
+// fin (one rank, after a solve's first iteration): workgroup 0 runs k_cam_finalize's pass (mode 0, taking an
+// accepted step's candidate blocks) beside the segments — independent work (the segments read the decision's
+// radius and slot, taken by the previous launch; the pass writes what k_S_reduce reads), one launch less.
+__global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d, int fin) {
   const LmState* st = d.st;
-  if ((int)blockIdx.x >= d.nseg) return;
   __shared__ SchurLds sh;
+  if (fin && blockIdx.x == 0) {
+    cam_finalize_body(d, 0, 2, FinLds::carve(&sh.X[0][0]));
+    return;
+  }
+  const int seg = (int)blockIdx.x - fin;
+  if (seg >= d.nseg) return;
   unsigned long long last_ = __builtin_amdgcn_s_memtime();
   // the segment's descriptor load goes out beside LmState's (see k_S_reduce)
-  const SchurSeg sg = d.segs[blockIdx.x];
+  const SchurSeg sg = d.segs[seg];
   if (st->done) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nbt = sg.bt1 - sg.bt0;
@@ -1262,7 +1333,7 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d) {
     SG_SSTAMP(45)
   }
   linfail = block_sum<kSchurThreads>(linfail, sh.red);
-  if (tid == 0) d.seg_fail[blockIdx.x] = linfail;
+  if (tid == 0) d.seg_fail[seg] = linfail;
 }
 
 // A point spanning more blocks than a segment window (a whole-map solve's long track): one workgroup, the
@@ -4214,6 +4285,7 @@ __global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_update_lin(Dev d) {
   if (st->done) return;
   const int cur = st->cur, nxt = cur ^ 1;
   const LinChunk ch = d.lchunks[blockIdx.x];
+  if (blockIdx.x == 0 && threadIdx.x == 0) d.st->spec_slot = nxt;   // (k_cam_reduce mode 1 reads it)
   __shared__ double pacc[kLinPts * 14];         // candidate point blocks of the round: V (10) | g (4)
   __shared__ double camacc[kLinNbMax * kCamV];  // candidate camera blocks of the window
   __shared__ double lsum[2][kLinThreads];       // candidate failures: free, fixed observations
@@ -4291,9 +4363,10 @@ __device__ void upd_reduce_body(const Dev& d, int fuse) {
   __shared__ double red[kRedThreads / 64 * kUNum];
   const int tid = threadIdx.x;
   // the decision's inputs are loaded up front (one round trip overlapping the reduction, not a chain of
-  // dependent ones after it)
-  LmState s;
-  double cc[kCNum];
+  // dependent ones after it), into LDS: thread 0's register copy of LmState beside the reduction's loads in
+  // flight spilled (this body shares k_cam_reduce's 1024-thread, 128-VGPR budget)
+  __shared__ LmState s;
+  __shared__ double cc[kCNum];
   if (fuse && tid == 0) {
     s = *st;
     for (int j = 0; j < kCNum; ++j) cc[j] = d.xchg_chol[j];
@@ -4327,7 +4400,7 @@ __device__ void upd_reduce_body(const Dev& d, int fuse) {
   }
   for (int g = tid; g < d.nseg + d.nwide; g += kRedThreads) v[kULinFail] += d.seg_fail[g];
   if (done) return;
-  block_sum_multi<kRedThreads, kUNum>(v, red);
+  block_sum_multi_t0<kRedThreads, kUNum>(v, red);
   if (tid == 0) {
 #pragma unroll
     for (int j = 0; j < kUNum; ++j) d.xchg_upd[j] = v[j];
@@ -4352,8 +4425,9 @@ __global__ void k_decide(Dev d, int take) {
     for (int j = 0; j < kCNum; ++j) c[j] = d.xchg_chol[j];
     const int c0 = s.cur;
     decide_step(s, u, c);
-    *d.st = s;
     acc_sh = s.cur != c0;
+    if (take) s.accepted = 0;
+    *d.st = s;
   }
   if (!take) return;
   __syncthreads();
@@ -4414,6 +4488,7 @@ __device__ void decide_step(LmState& s, const double* u, const double* c) {
       s.decrease_factor = 2.0;
       s.reuse_diag = 0;
       s.cur ^= 1;
+      s.accepted = 1;
       s.x_norm = sqrt(u[kUCandX2] + c[kCCandX2]);
       s.cost = new_cost;
       s.need_lin = 1;   // the iteration is pushed after the gradient test in k_cam_finalize
@@ -4686,6 +4761,10 @@ void BaSolver::Load(const sg_problem& p) {
     lt0 = t;
   };
   SG_HIP_CHECK(hipSetDevice(dev_.device));
+  // a device mark at the load's start, with its host time: the GPU time from here to the last mark against the
+  // host's wall time tells a late device (its queue started late) from a late host (the waiting thread)
+  auto load_t0 = std::chrono::steady_clock::now();
+  if (host_timing) DevMark(stream_, 4);
   {
     // Everything that can reject this rank's problem runs before the first collective, and the verdict rides
     // in that collective (2: some rank's problem is invalid), so that all ranks fail together instead of
@@ -5370,8 +5449,12 @@ void BaSolver::Load(const sg_problem& p) {
     (void)hipEventElapsedTime(&a, dev_marks_[0], dev_marks_[1]);
     (void)hipEventElapsedTime(&b, dev_marks_[1], dev_marks_[2]);
     (void)hipEventElapsedTime(&c, dev_marks_[2], dev_marks_[3]);
-    char buf[128];
-    snprintf(buf, sizeof(buf), " [device: batch1..batch2 %.2f, scatter2 %.2f, reset %.2f]", a, b, c);
+    float e = 0;
+    (void)hipEventElapsedTime(&e, dev_marks_[4], dev_marks_[3]);
+    const double hw = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - load_t0).count();
+    char buf[192];
+    snprintf(buf, sizeof(buf), " [device: batch1..batch2 %.2f, scatter2 %.2f, reset %.2f; load start..reset: device "
+             "%.2f, host %.2f]", a, b, c, e, hw);
     lap_log += buf;
   }
   if (host_timing) {
@@ -5851,7 +5934,7 @@ void BaSolver::EnqueueIterations(int n) {
       SG_HIP_CHECK(hipEventRecord(ev_lin_, stream_));
       SG_HIP_CHECK(hipStreamWaitEvent(side_, ev_lin_, 0));
       TimedLaunchBegin(kKSchur, side_);
-      hipLaunchKernelGGL(k_schur, dim3(std::max(nseg_, 1)), dim3(kSchurThreads), 0, side_, d);
+      hipLaunchKernelGGL(k_schur, dim3(std::max(nseg_, 1)), dim3(kSchurThreads), 0, side_, d, 0);
       if (nwide_) hipLaunchKernelGGL(k_schur_wide, dim3(nwide_), dim3(kSchurThreads), 0, side_, d);
       TimedLaunchEnd(kKSchur, side_);
       SG_HIP_CHECK(hipEventRecord(ev_schur_, side_));
@@ -5870,8 +5953,13 @@ void BaSolver::EnqueueIterations(int n) {
     // itself (one rank, or merged shards), else by k_decide, which then also makes the accepted candidate's
     // blocks current.  No pending decision (a batch's first iteration: EnqueueIterations settles it at the
     // end of every batch): the current blocks are in place.
+    // One rank (no free intrinsics): the previous iteration's reduce took the decision (k_cam_reduce mode 2) and
+    // this iteration's finalize pass runs inside the k_schur launch.
+    const bool fin_in_schur = spec_ && !first_it && !multi_x && nk_ == 0 && !merged;
     bool decide_in_fin = false;
-    if (spec_ && !first_it) {
+    if (fin_in_schur) {
+      // (nothing pending: the candidate blocks of an accepted step are taken by the pass)
+    } else if (spec_ && !first_it) {
       if (pending_decision_) {
         decide_in_fin = nk_ == 0 && (merged || !multi_x);
         if (!decide_in_fin) {
@@ -5892,14 +5980,17 @@ void BaSolver::EnqueueIterations(int n) {
       hipLaunchKernelGGL(k_intr_lin, dim3((std::max(M_, 1) + 255) / 256), dim3(256), 0, stream_, d);
       hipLaunchKernelGGL(k_intr_fin, dim3(1), dim3(64), 0, stream_, d);
     }
-    TimedLaunchBegin(kKCamFinal);
-    hipLaunchKernelGGL(k_cam_finalize, dim3(1), dim3(256), 0, stream_, d, merged ? 1 : 0, decide_in_fin ? 1 : 0);
-    TimedLaunchEnd(kKCamFinal);
+    if (!fin_in_schur) {
+      TimedLaunchBegin(kKCamFinal);
+      hipLaunchKernelGGL(k_cam_finalize, dim3(1), dim3(256), 0, stream_, d, merged ? 1 : 0, decide_in_fin ? 1 : 0);
+      TimedLaunchEnd(kKCamFinal);
+    }
     if (overlap) {
       SG_HIP_CHECK(hipStreamWaitEvent(stream_, ev_schur_, 0));
     } else {
       TimedLaunchBegin(kKSchur);
-      hipLaunchKernelGGL(k_schur, dim3(std::max(nseg_, 1)), dim3(kSchurThreads), 0, stream_, d);
+      hipLaunchKernelGGL(k_schur, dim3(std::max(nseg_, 1) + (fin_in_schur ? 1 : 0)), dim3(kSchurThreads), 0, stream_, d,
+                         fin_in_schur ? 1 : 0);
       if (nwide_) hipLaunchKernelGGL(k_schur_wide, dim3(nwide_), dim3(kSchurThreads), 0, stream_, d);
       TimedLaunchEnd(kKSchur);
     }
@@ -5953,15 +6044,18 @@ void BaSolver::EnqueueIterations(int n) {
       hipLaunchKernelGGL(k_point_update, dim3(std::max(npu_, 1)), dim3(kLinThreads), 0, stream_, d);
     TimedLaunchEnd(kKPointUpd);
     const bool multi = comm_ && comm_->nranks() > 1;
+    // the candidate's camera blocks and linearization scalars beside the update scalars, one launch; on one rank
+    // (no free intrinsics, no forced merged chain) the decision too
+    const bool decide_in_reduce = !multi && nk_ == 0 && merge_ != 2;
     TimedLaunchBegin(kKUpdRed);
-    if (spec_)   // the candidate's camera blocks and linearization scalars beside the update scalars, one launch
-      hipLaunchKernelGGL(k_cam_reduce, dim3(NB_ + 2), dim3(kRedThreads), 0, stream_, d, 1);
+    if (spec_)
+      hipLaunchKernelGGL(k_cam_reduce, dim3(NB_ + 2), dim3(kRedThreads), 0, stream_, d, decide_in_reduce ? 2 : 1);
     else
       hipLaunchKernelGGL(k_upd_reduce, dim3(1), dim3(kRedThreads), 0, stream_, d, multi ? 0 : 1);
     TimedLaunchEnd(kKUpdRed);
     if (multi) AllReduceSum(xchg_upd_.ptr, kUNum);
     if (spec_) {
-      pending_decision_ = true;
+      pending_decision_ = !decide_in_reduce;
     } else if (multi) {
       TimedLaunchBegin(kKDecide);
       hipLaunchKernelGGL(k_decide, dim3(1), dim3(256), 0, stream_, d, 0);
