@@ -115,6 +115,8 @@ class BaSolver {
   size_t ntail_ = 0;   // doubles of the merged exchange's tail
   bool pending_decision_ = false;   // speculative chain: the last enqueued step awaits its decision
   int32_t nallreduce_ = 0;   // landmark-shard all-reduces issued (sg_ba_info.num_allreduces)
+  // tests: issue the communicator's collectives on one rank too (SG_COMM_FORCE=1: RCCL with one rank is a copy)
+  bool comm_force_ = getenv("SG_COMM_FORCE") && atoi(getenv("SG_COMM_FORCE")) == 1;
   size_t npack_ = 0;                                      // band of S + rhs, doubles (all-reduce size)
   bool stamp_on_ = false;
   int ncu_ = 256;                       // compute units (Schur segment count), queried once

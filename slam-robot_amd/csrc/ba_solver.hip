@@ -4734,7 +4734,7 @@ void BaSolver::CommInitHost(int nranks, int rank, int (*fn)(double*, long long, 
 int BaSolver::nranks() const { return comm_ ? comm_->nranks() : 1; }
 
 void BaSolver::AllReduceSum(double* buf, size_t n) {
-  if (comm_ && comm_->nranks() > 1) {
+  if (comm_ && (comm_->nranks() > 1 || comm_force_)) {
     comm_->AllReduceSum(buf, n, stream_);
     ++nallreduce_;
   }
@@ -4788,7 +4788,7 @@ void BaSolver::Load(const sg_problem& p) {
     }
     // incremental update: every rank must take the same path (the full path has a load-time all-reduce)
     double changed = vcode != SG_OK ? 2.0 : (loaded_ && !getenv("SG_NO_REUSE") && SameStructure(p)) ? 0.0 : 1.0;
-    if (comm_ && comm_->nranks() > 1) {
+    if (comm_ && (comm_->nranks() > 1 || comm_force_)) {
       DBuf<double> flag;
       flag.Upload(std::vector<double>{changed}, stream_);
       comm_->AllReduceMax(flag.ptr, 1, stream_);
@@ -5259,7 +5259,7 @@ void BaSolver::Load(const sg_problem& p) {
   // Landmark shards: S is summed over every rank's points, so each rank must factor it with the envelope of
   // the whole problem (the union of the shards' envelopes), not of its own points.  One max all-reduce of
   // -lo(J) at load time.
-  if (comm_ && comm_->nranks() > 1 && NB_ > 0) {
+  if (comm_ && (comm_->nranks() > 1 || comm_force_) && NB_ > 0) {
     std::vector<double> neg(NB_);
     for (int b = 0; b < NB_; ++b) neg[b] = -(double)lo_blk[b];
     DBuf<double> env;

@@ -687,3 +687,28 @@ def test_merged_exchange_chain_on_one_rank(gpu_lib, monkeypatch):
     assert abs(s0["final_cost"] - s1["final_cost"]) <= 1e-12 * s0["final_cost"]
     np.testing.assert_allclose(p1.q, p0.q, rtol=0, atol=1e-10)
     np.testing.assert_allclose(p1.t, p0.t, rtol=0, atol=1e-6)
+
+
+def test_rccl_communicator_on_one_rank(gpu_lib, monkeypatch):
+    """The product communicator (RcclComm: ncclCommInitRank on a unique id, ncclAllReduce on the solver's stream)
+    with one rank, its collectives forced (SG_COMM_FORCE=1) through the merged exchange chain (SG_XCHG_MERGE=force):
+    the load's max all-reduces, the camera-block and packed-band all-reduces, each an RCCL copy on one rank.  The
+    solve equals the same chain without a communicator bit for bit.  (RCCL needs one GPU per rank; the pool's
+    boxes have one, so more ranks run at the driver's 8-GPU bench only.)"""
+    m = make_config("C2")
+    pa = ba.problem_from_map_frames(m, 48, 50, 2.0)
+    o = default_solver_options(max_num_iterations=6)
+    s0, p0 = _solve_env(pa, {"SG_XCHG_MERGE": "force"}, monkeypatch, options=o)
+    monkeypatch.setenv("SG_XCHG_MERGE", "force")
+    monkeypatch.setenv("SG_COMM_FORCE", "1")
+    g = ba.BundleAdjuster()
+    g.comm_init(ba.BundleAdjuster.unique_id(), 1, 0)
+    p1 = pa.copy()
+    g.load(p1)
+    s1 = g.solve(o)
+    n_ar = g.info()["num_allreduces"]
+    g.close()
+    assert n_ar >= 7, n_ar
+    assert s0 == s1
+    np.testing.assert_array_equal(p0.q, p1.q)
+    np.testing.assert_array_equal(p0.X, p1.X)
