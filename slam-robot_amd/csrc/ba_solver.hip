@@ -4645,7 +4645,10 @@ BaSolver::BaSolver(const sg_device_options& dev) : dev_(dev) {
              "sg_device_options.precision: only 0 (fp64, the reference's arithmetic) is implemented");
   SG_HIP_CHECK(hipSetDevice(dev.device));
   SG_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-  SG_HIP_CHECK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+  // the side stream only in the Schur-overlap mode: every stream holds a hardware queue (GPU_MAX_HW_QUEUES = 4
+  // per process on the pool), and an idle queue that has to be scheduled again was the one measured cause of
+  // the replay's late load starts (tools/e2e_replay.py)
+  if (overlap_ok_) SG_HIP_CHECK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
   SG_HIP_CHECK(hipEventCreateWithFlags(&ev_lin_, hipEventDisableTiming));
   SG_HIP_CHECK(hipEventCreateWithFlags(&ev_schur_, hipEventDisableTiming));
   {

@@ -156,8 +156,10 @@ control = {"calls": len(ctrl), "passes": CONTROL_PASSES,
            "tiny_call_ms_median": float(np.median(tinys)), "tiny_call_ms_max": float(tinys.max()),
            "noop_over_5ms": [(round(float(g), 2), round(float(v), 2)) for g, v in zip(cgaps, noops) if v > 5],
            "tiny_over_5ms": [(round(float(g), 2), round(float(v), 2)) for g, v in zip(cgaps, tinys) if v > 5],
-           "loads_over_5ms": [(round(float(c["gap_ms"]), 2), round(float(c["load_ms"]), 2)) for c in ctrl
-                              if c["load_ms"] > 5]}
+           "loads": len(later), "noop_stalls": int((noops > 5).sum()), "tiny_call_stalls": int((tinys > 5).sum()),
+           "load_stalls": int(sum(r["load"] > 5 for r in later)),
+           "loads_over_5ms": [(round(float(r["gap_ms"]), 2), round(float(r["load"]), 2)) for r in later
+                              if r["load"] > 5]}
 summary["control"] = control
 print("control (same gaps, no load):", json.dumps(control))
 print("load counts (full, values):", slam.load_counts())
