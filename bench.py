@@ -521,7 +521,10 @@ def run_workload(cfg, args, n_gpus, rank, local, dist, steps, warmup, weak=False
 
 
 def bench_sweep(local, sweep_obs):
-    """Scaled sweep: the linearization kernel on a problem large enough to amortise launch latency."""
+    """Scaled sweep on a problem large enough to amortise launch latency: the linearization kernel alone
+    (k_linearize, which the speculative chain runs once per solve), and the per-iteration sweep of that chain
+    (k_update_lin: the point update, the candidate's linearization and its cost in one pass) timed inside K
+    always-linearize LM iterations (`update_lin`)."""
     from slamgpu import ba
     from slamgpu.capi import default_solver_options
     from slamgpu.scene import make_scene
@@ -540,16 +543,35 @@ def bench_sweep(local, sweep_obs):
     wb = bs.kernel_work()["linearize"][0]
     ach = wb / (kt[0] * 1e-3) / 1e9
     bs.close()
+    # the per-iteration sweep: K LM iterations on the same problem, k_update_lin's HIP-event average
+    bs = ba.BundleAdjuster(device=local)
+    bs.load(bp.copy())
+    bs.begin(default_solver_options(max_num_iterations=40, disable_termination=1, always_linearize=1))
+    bs.iterate(3)
+    bs.sync()
+    bs.set_timing(True)
+    bs.iterate(10)
+    bs.sync()
+    ku = bs.kernel_times()["point_update"]
+    wu = bs.kernel_work()["point_update"][0]
+    s1 = bs.summary()
+    bs.close()
+    assert s1["ok"] == 1 and s1["num_lm_iterations"] == 13, s1
+    achu = wu / (ku[0] * 1e-3) / 1e9
     return {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": ach / HBM_PEAK_GBS, "obs": bp.num_obs, "points": bp.num_points,
-            "ms_per_launch": kt[0], "bytes_per_launch": wb, **traffic_fields("k_linearize", "sweep", wb)}
+            "ms_per_launch": kt[0], "bytes_per_launch": wb, **traffic_fields("k_linearize", "sweep", wb),
+            "update_lin": {"kernel": "k_update_lin", "achieved": achu, "frac": achu / HBM_PEAK_GBS,
+                           "ms_per_launch": ku[0], "bytes_per_launch": wu, "launches": ku[1],
+                           **traffic_fields("k_update_lin", "sweep", wu)}}
 
 
 def bench_solve_all(local, steps=20, warmup=3):
     """Whole-map refinements of main.cpp's calibration step (SolveAllFrames(map, 2, false / true), main.cpp:282,
     327; slam.cpp:447-480) on the config-2 map: every frame free but the gauge, and with solve_cameras the 7
-    intrinsics of each camera couple every frame, so the reduced system is dense and takes the one-workgroup
-    global-memory Cholesky (k_cholesky_global) instead of the tiled band.  LM iterations per second over K
+    intrinsics of each camera couple every frame, so the reduced system is an arrowhead (the frame band bordered
+    by 14 dense columns) and takes the bordered band solve (k_chol_tiles on the frames, k_chol_border for the
+    intrinsics; SG_CHOL_BORDER=0: the one-workgroup k_cholesky_global).  LM iterations per second over K
     always-linearize iterations (termination off) and the per-kernel times."""
     from slamgpu import ba
     from slamgpu.capi import default_solver_options

@@ -240,7 +240,8 @@ typedef struct sg_ba_info {
   int32_t n;                                 /* reduced camera system dimension (6 blocks + free intrinsics) */
   int32_t band_tiles;                        /* widest row of the Cholesky envelope, in 16-wide tiles */
   int32_t cholesky_path;                     /* 0: tiled band (k_chol_tiles), 1: LDS window, 2: global memory
-                                                (panel rows staged in LDS), 3: global memory */
+                                                (panel rows staged in LDS), 3: global memory, 4: bordered band
+                                                (free intrinsics: frame band tiled, then the border) */
   int32_t num_pairs;                         /* Schur observation pairs (s <= t) of this rank's free points */
   int32_t rank, nranks;
   int32_t cholesky_split;                    /* tiled path: tile rows factored bottom-up by a second workgroup

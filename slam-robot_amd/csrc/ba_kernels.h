@@ -70,7 +70,10 @@ constexpr int kSchurCellWaves = 3;   // operand-tile waves (a batch has <= 64 kS
 constexpr int kSchurCWaves = SG_SCHUR_CW;   // MFMA waves (4: one per SIMD; 8: two); a point wave between the groups
 constexpr int kSchurWaves = kSchurCellWaves + 1 + kSchurCWaves;
 constexpr int kSchurThreads = 64 * kSchurWaves;
-constexpr int kSchurTW = 10;
+#ifndef SG_SCHUR_TW
+#define SG_SCHUR_TW 10   // window width in tiles (variant builds: tools/build_variant.sh)
+#endif
+constexpr int kSchurTW = SG_SCHUR_TW;
 constexpr int kSchurTiles = kSchurTW * (kSchurTW + 1) / 2;
 constexpr int kSchurAug = kSchurTiles + kSchurTW;   // window tiles + one rhs tile per tile row
 constexpr int kSchurTPW = (kSchurAug + kSchurCWaves - 1) / kSchurCWaves;   // accumulator tiles per wave
@@ -245,6 +248,10 @@ struct Dev {
   double* Jk;                    // [M][14] corrected, unscaled d(uv)/dk of each observation
   double* KU;                    // [n][nk] intrinsics columns of J^T J, unscaled (frame rows, then the k block)
   double* kst;                   // [ncam][56] CameraStabilization corrected residual (7) and Jacobian (7x7)
+  double* Yk;                    // [P][ncam][28] W_kp V~p^-1 of each free point (k_intr_schur -> k_intr_fk)
+  double* kpart;                 // [NB + 1][ncam][42] per-block J_k^T J_k / J_k^T r / diagonal partials
+  const int32_t* intr_boff;      // [NB + 2] per frame block (then the fixed frames' block NB): observations
+  const int32_t* intr_bidx;      //   of non-fixed observations, in observation order
   double stab_b, stab_inv_b;     // CauchyLoss(stab_range): b = stab_range^2
 };
 constexpr int kMaxIntrCams = 4;  // cameras whose intrinsics the device solver can free at once

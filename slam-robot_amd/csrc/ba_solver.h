@@ -84,6 +84,9 @@ class BaSolver {
   bool began_ = false;
   bool chol_window_ = true;
   bool chol_tiles_ = false;    // tiled register-resident band Cholesky (k_chol_tiles)
+  bool chol_border_ = false;   // free intrinsics: k_chol_tiles on the frame band, then k_chol_border
+  int border_flags_ = 0;       // its LDS placements (bit 0 q_K tiles, bit 1 candidate operands)
+  size_t border_lds_max_ = 0;  // its dynamic LDS limit
   size_t tile_lds_ = 0;        // its dynamic LDS
   DBuf<double> Wg_;            // its back-substitution tiles W_KJ = U_KK^-1 U_KJ (+ the bottom half's)
   int chol_nd_ = 0;            // dissected band: tile rows the second workgroup factors bottom-up (0: one WG)
@@ -176,6 +179,8 @@ class BaSolver {
   DBuf<int32_t> obs_pnt_, pairs_;   // Schur work lists
   DBuf<int32_t> obs_meta_;         // packed per-observation facts (kMeta*)
   DBuf<double> Jk_, KU_, kst_;     // free intrinsics (nk_ > 0)
+  DBuf<double> Yk_, kpart_;        //   W_kp V~p^-1 per point and camera; per-block camera sums
+  DBuf<int32_t> intr_boff_, intr_bidx_;   //   per-block observation lists
   int nk_ = 0;                     // 7 * cameras when the intrinsics are free
   double stab_b_ = 25.0;
   DBuf<SchurSeg> segs_;

@@ -23,6 +23,7 @@
 #include <chrono>
 #include <string>
 #include <thread>
+#include <exception>
 
 #include <algorithm>
 #include <cfloat>
@@ -1610,94 +1611,141 @@ __global__ __launch_bounds__(256) void k_intr_zero(Dev d) {
   }
 }
 
-// One thread per observation: J_k (the same corrected projection Jacobian as k_linearize) and its
-// J^T J / J^T r terms.
-// The per-camera sums (upper 7x7 of Jk^T Jk, gradient, diagonal: 42 values per camera, all observations of
-// the camera add into them) go through LDS per workgroup and then one global atomic per value and workgroup:
-// a global atomic per observation on 42 shared addresses serialised the launch (9.5 ms at config 2).  The
-// frame-intrinsics block KU_fk likewise accumulates in LDS over a window of kIntrWin frame blocks from the
-// workgroup's first point's first block (observations are point-major, points in device order by first
-// block); observations in blocks outside the window add globally.
+// One thread per observation: J_k (the same corrected projection Jacobian as k_linearize), stored for
+// k_intr_fk, which forms the frame-intrinsics block KU_fk and the per-camera sums (upper 7x7 of J_k^T J_k, the
+// gradient, the diagonal) per frame block from the observation lists, without atomics; k_intr_fin adds the
+// per-block partials in block order.  (Per-observation LDS / global atomics on a few hundred shared addresses
+// took 49 us at config 2.)
 constexpr int kIntrCamV = 42;
 constexpr int kIntrKMax = 7 * kMaxIntrCams;
-constexpr int kIntrWin = 32;
 __global__ __launch_bounds__(256) void k_intr_lin(Dev d) {
   const LmState* st = d.st;
   if (st->done || !st->need_lin) return;
-  __shared__ double kacc[kMaxIntrCams * kIntrCamV];
-  __shared__ double kfw[kIntrWin * 6 * kIntrKMax];
-  __shared__ int b_lo_sh;
-  const int tid = threadIdx.x;
-  for (int i = tid; i < kMaxIntrCams * kIntrCamV; i += blockDim.x) kacc[i] = 0.0;
-  for (int i = tid; i < kIntrWin * 6 * kIntrKMax; i += blockDim.x) kfw[i] = 0.0;
-  if (tid == 0) {
-    const int o0 = min((int)(blockIdx.x * blockDim.x), d.M - 1);
-    b_lo_sh = o0 >= 0 ? max(0, d.pinfo[d.obs_pnt[o0]].y >> 8) : 0;
-  }
-  __syncthreads();
-  const int b_lo = b_lo_sh;
-  const int o = blockIdx.x * blockDim.x + tid;
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= d.M) return;
   const int cur = st->cur;
-  const int nk = d.nk;
-  if (o < d.M) {
-    const int m = d.obs_meta[o], f = d.obs_frame[o], p = d.obs_pnt[o], cam = meta_cam(m);
-    double* Jko = d.Jk + 14 * (size_t)o;
-    const double4 Xv = reinterpret_cast<const double4*>(d.X[cur])[p];
-    const double X[4] = {Xv.x, Xv.y, Xv.z, Xv.w};
-    const double pt[2] = {d.obs_pt[2 * o], d.obs_pt[2 * o + 1]};
-    double rr[2], Jc[12], Jp[8], Jk[14], c;
-    if ((m & kMetaFixed) || !LinearizeObservation(d.q[cur] + 4 * f, d.t[cur] + 3 * f, d.k[cur] + 7 * cam, X, pt,
-                                                  d.b, d.inv_b, rr, Jc, Jp, &c, Jk)) {
-      for (int i = 0; i < 14; ++i) Jko[i] = 0.0;   // a failed projection fails the linearization (k_linearize)
-    } else {
-      for (int i = 0; i < 14; ++i) Jko[i] = Jk[i];
-      double* ka = kacc + cam * kIntrCamV;
-      int u = 0;
-      for (int a = 0; a < 7; ++a) {
-        for (int j = a; j < 7; ++j) atomicAdd(ka + u++, Jk[a] * Jk[j] + Jk[7 + a] * Jk[7 + j]);
-        atomicAdd(ka + 28 + a, Jk[a] * rr[0] + Jk[7 + a] * rr[1]);
-        atomicAdd(ka + 35 + a, Jk[a] * Jk[a] + Jk[7 + a] * Jk[7 + a]);
-      }
-      const int b = meta_block(m);
-      if (b >= 0) {
-        if (!(m & kMetaRot)) { Jc[0] = Jc[1] = Jc[2] = Jc[6] = Jc[7] = Jc[8] = 0.0; }
-        if (!(m & kMetaTrans)) { Jc[3] = Jc[4] = Jc[5] = Jc[9] = Jc[10] = Jc[11] = 0.0; }
-        const int wb = b - b_lo;
-        if (wb >= 0 && wb < kIntrWin) {
-          double* Kf = kfw + (6 * wb) * kIntrKMax + 7 * cam;
-          for (int a = 0; a < 6; ++a)
-            for (int j = 0; j < 7; ++j) atomicAdd(Kf + a * kIntrKMax + j, Jc[a] * Jk[j] + Jc[6 + a] * Jk[7 + j]);
-        } else {
-          double* Kf = d.KU + (size_t)(6 * b) * nk + 7 * cam;
-          for (int a = 0; a < 6; ++a)
-            for (int j = 0; j < 7; ++j) atomicAdd(Kf + (size_t)a * nk + j, Jc[a] * Jk[j] + Jc[6 + a] * Jk[7 + j]);
-        }
-      }
-    }
+  const int m = d.obs_meta[o], f = d.obs_frame[o], p = d.obs_pnt[o], cam = meta_cam(m);
+  double* Jko = d.Jk + 14 * (size_t)o;
+  const double4 Xv = reinterpret_cast<const double4*>(d.X[cur])[p];
+  const double X[4] = {Xv.x, Xv.y, Xv.z, Xv.w};
+  const double pt[2] = {d.obs_pt[2 * o], d.obs_pt[2 * o + 1]};
+  double rr[2], Jc[12], Jp[8], Jk[14], c;
+  const bool ok = !(m & kMetaFixed) && LinearizeObservation(d.q[cur] + 4 * f, d.t[cur] + 3 * f, d.k[cur] + 7 * cam,
+                                                            X, pt, d.b, d.inv_b, rr, Jc, Jp, &c, Jk);
+  // a failed projection fails the linearization (k_linearize) and contributes nothing
+#pragma unroll
+  for (int i = 0; i < 14; ++i) Jko[i] = ok ? Jk[i] : 0.0;
+}
+
+// Sum of kV values over the workgroup's waves (wave sums, then the waves in order): the result for value e is in
+// red[0][e] after the call.
+template <int kWaves, int kV>
+__device__ __forceinline__ void wg_sum_values(const double (&v)[kV], double (*red)[kV]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int e = 0; e < kV; ++e) {
+    const double t = wave_sum(v[e]);
+    if (lane == 0) red[wave][e] = t;
   }
   __syncthreads();
-  for (int i = tid; i < d.ncam * kIntrCamV; i += blockDim.x) {
-    const double v = kacc[i];
-    if (v == 0.0) continue;
-    const int cam = i / kIntrCamV, e = i - cam * kIntrCamV, kc = 7 * cam;
-    if (e < 28) {
-      int a = 0, u = e;
-      while (u >= 7 - a) {
-        u -= 7 - a;
-        ++a;
+  for (int e = threadIdx.x; e < kV; e += 64 * kWaves) {
+    double t = red[0][e];
+    for (int w = 1; w < kWaves; ++w) t += red[w][e];
+    red[0][e] = t;
+  }
+  __syncthreads();
+}
+
+// Per frame block b (blockIdx.x; b = NB: the observations of fixed frames) and camera c (blockIdx.y), over the
+// block's observation list:
+//   kMode 0 (after k_intr_lin): KU_fk rows of b, columns of c: sum J_c^T J_k over the block's observations of
+//     camera c (stored: one writer per entry), and the camera sums of those observations into kpart[b][c];
+//   kMode 1 (after k_intr_schur): S_fk rows of b, columns of c -= sum over the block's observations of free
+//     points of A_c^T (A_p Y_pc^T) (Y_pc = W_kp V~p^-1 of camera c, k_intr_schur).
+constexpr int kIntrFkThreads = 512;
+template <int kMode>
+__global__ __launch_bounds__(kIntrFkThreads) void k_intr_fk(Dev d) {
+  const LmState* st = d.st;
+  if (st->done) return;
+  if (kMode == 0 && !st->need_lin) return;
+  constexpr int kV = kMode == 0 ? 2 * kIntrCamV : kIntrCamV;
+  constexpr int kW = kIntrFkThreads / 64;
+  __shared__ double red[kW][kV];
+  const int b = blockIdx.x, c = blockIdx.y, tid = threadIdx.x, cur = st->cur, nk = d.nk, ncam = d.ncam;
+  const int i0 = d.intr_boff[b], i1 = d.intr_boff[b + 1];
+  double acc[kV];
+#pragma unroll
+  for (int e = 0; e < kV; ++e) acc[e] = 0.0;
+  const double* J = d.J[cur];
+  for (int i = i0 + tid; i < i1; i += kIntrFkThreads) {
+    const int o = d.intr_bidx[i];
+    const int m = d.obs_meta[o];
+    if constexpr (kMode == 0) {
+      if (meta_cam(m) != c) continue;
+      const double* Jko = d.Jk + 14 * (size_t)o;
+      double Jk[14], r[2], Jc[12];
+#pragma unroll
+      for (int e = 0; e < 14; ++e) Jk[e] = Jko[e];
+      const double2 rv = jload2(J, o, 0);
+      r[0] = rv.x;
+      r[1] = rv.y;
+#pragma unroll
+      for (int e = 0; e < 6; ++e) {
+        const double2 v = jload2(J, o, 1 + e);   // raw J_c (zero outside the frame's free parts)
+        Jc[2 * e] = v.x;
+        Jc[2 * e + 1] = v.y;
       }
-      atomicAdd(d.KU + (size_t)(d.kc0 + kc + a) * nk + kc + a + u, v);
-    } else if (e < 35) {
-      atomicAdd(d.camg + d.kc0 + kc + (e - 28), v);
+      if (b < d.NB) {
+#pragma unroll
+        for (int a = 0; a < 6; ++a)
+#pragma unroll
+          for (int j = 0; j < 7; ++j) acc[7 * a + j] += Jc[a] * Jk[j] + Jc[6 + a] * Jk[7 + j];
+      }
+      double* ka = acc + kIntrCamV;
+      int u = 0;
+#pragma unroll
+      for (int a = 0; a < 7; ++a) {
+#pragma unroll
+        for (int j = a; j < 7; ++j) ka[u++] += Jk[a] * Jk[j] + Jk[7 + a] * Jk[7 + j];
+        ka[28 + a] += Jk[a] * r[0] + Jk[7 + a] * r[1];
+        ka[35 + a] += Jk[a] * Jk[a] + Jk[7 + a] * Jk[7 + a];
+      }
     } else {
-      atomicAdd(d.camdiag + d.kc0 + kc + (e - 35), v);
+      if (!(m & kMetaPfree)) continue;
+      const int p = d.obs_pnt[o];
+      const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
+      const double sp[4] = {s4.x, s4.y, s4.z, s4.w};
+      double r[2], Jc[12], Jp[8];
+      load_scaled_J(d, J, o, b, sp, r, Jc, Jp);
+      const double* Y = d.Yk + ((size_t)p * ncam + c) * 28;
+      double Mx[14];   // A_p Y^T (2x7)
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+        for (int j = 0; j < 7; ++j) {
+          double v = 0.0;
+#pragma unroll
+          for (int a = 0; a < 4; ++a) v += Jp[4 * rr + a] * Y[4 * j + a];
+          Mx[7 * rr + j] = v;
+        }
+#pragma unroll
+      for (int a = 0; a < 6; ++a)
+#pragma unroll
+        for (int j = 0; j < 7; ++j) acc[7 * a + j] -= Jc[a] * Mx[j] + Jc[6 + a] * Mx[7 + j];
     }
   }
-  for (int i = tid; i < kIntrWin * 6 * nk; i += blockDim.x) {
-    const int row = i / nk, j = i - row * nk;   // row = 6 (b - b_lo) + a
-    const int b = b_lo + row / 6;
-    const double v = kfw[row * kIntrKMax + j];
-    if (b < d.NB && v != 0.0) atomicAdd(d.KU + (size_t)(6 * b + row % 6) * nk + j, v);
+  wg_sum_values<kW, kV>(acc, red);
+  if constexpr (kMode == 0) {
+    for (int e = tid; e < kV; e += kIntrFkThreads) {
+      if (e < kIntrCamV) {
+        if (b < d.NB) d.KU[(size_t)(6 * b + e / 7) * nk + 7 * c + e % 7] = red[0][e];
+      } else {
+        d.kpart[((size_t)b * ncam + c) * kIntrCamV + e - kIntrCamV] = red[0][e];
+      }
+    }
+  } else {
+    for (int e = tid; e < kV; e += kIntrFkThreads)
+      d.S[(size_t)(6 * b + e / 7) * d.n + d.kc0 + 7 * c + e % 7] += red[0][e];
   }
 }
 
@@ -1726,6 +1774,25 @@ __global__ __launch_bounds__(64) void k_intr_fin(Dev d) {
   LmState* st = d.st;
   if (st->done || !st->need_lin) return;
   const int lane = threadIdx.x, cur = st->cur, nk = d.nk;
+  // the per-block camera sums (k_intr_fk<0>), in block order
+  for (int e = lane; e < d.ncam * kIntrCamV; e += 64) {
+    const int cam = e / kIntrCamV, v = e - cam * kIntrCamV, kc = 7 * cam;
+    double t = 0.0;
+    for (int bb = 0; bb <= d.NB; ++bb) t += d.kpart[((size_t)bb * d.ncam + cam) * kIntrCamV + v];
+    if (v < 28) {
+      int a = 0, u = v;
+      while (u >= 7 - a) {
+        u -= 7 - a;
+        ++a;
+      }
+      d.KU[(size_t)(d.kc0 + kc + a) * nk + kc + a + u] += t;
+    } else if (v < 35) {
+      d.camg[d.kc0 + kc + (v - 28)] += t;
+    } else {
+      d.camdiag[d.kc0 + kc + (v - 35)] += t;
+    }
+  }
+  __syncthreads();
   double cost = 0.0, xn2 = 0.0;
   if (lane < d.ncam) {
     const double* k = d.k[cur] + 7 * lane;
@@ -1789,16 +1856,13 @@ __global__ __launch_bounds__(256) void k_intr_assemble(Dev d) {
 }
 
 // Thread per free point p: W_kp = A_k^T A_p over its observations of camera c (scaled), Y = W_kp V~p^-1, then
-// S_kk -= Y W_kp'^T, rhs_k -= W_kp t_p, and for each observation (frame block b) S_bk -= A_c^T (A_p Y^T).
-// The k-k block of S and the k rhs (shared by every point) accumulate in LDS per workgroup, then one global
-// atomic per entry and workgroup (a global atomic per point on ~120 shared addresses took 1.9 ms at config 2).
-// The frame-intrinsics coupling S_fk of the workgroup's points accumulates in LDS too, over a window of
-// kIntrWin frame blocks from the workgroup's first point's first block (points are in device order, by first
-// block, so a workgroup's points touch a narrow band of blocks); blocks outside the window add globally.
+// S_kk -= Y W_kp'^T and rhs_k -= W_kp t_p; Y goes to Yk for the frame-intrinsics terms S_bk -= A_c^T (A_p Y^T),
+// which k_intr_fk<1> sums per frame block over the block's observation list.  The k-k block of S and the k rhs
+// (shared by every point) accumulate in LDS per workgroup, then one global atomic per entry and workgroup (a
+// global atomic per point on ~120 shared addresses took 1.9 ms at config 2).  (The S_fk terms as LDS atomics per
+// observation here took 200 us at config 2.)
 struct IntrSchurLds {
   double skk[kIntrKMax * kIntrKMax], sxk[kIntrKMax];
-  double sfk[kIntrWin * 6 * kIntrKMax];
-  int b_lo;
 };
 __device__ __forceinline__ void intr_schur_point(const Dev& d, int p, bool act, IntrSchurLds& sh);
 __global__ __launch_bounds__(128) void k_intr_schur(Dev d) {
@@ -1807,12 +1871,7 @@ __global__ __launch_bounds__(128) void k_intr_schur(Dev d) {
   __shared__ IntrSchurLds sh;
   const int tid = threadIdx.x;
   for (int i = tid; i < kIntrKMax * kIntrKMax; i += blockDim.x) sh.skk[i] = 0.0;
-  for (int i = tid; i < kIntrWin * 6 * kIntrKMax; i += blockDim.x) sh.sfk[i] = 0.0;
   if (tid < kIntrKMax) sh.sxk[tid] = 0.0;
-  if (tid == 0) {
-    const int p0 = min((int)(blockIdx.x * blockDim.x), d.P - 1);
-    sh.b_lo = p0 >= 0 ? max(0, d.pinfo[p0].y >> 8) : 0;
-  }
   __syncthreads();
   const int p = blockIdx.x * blockDim.x + tid;
   intr_schur_point(d, min(p, d.P - 1), p < d.P && d.pfree[p], sh);   // every lane: wave sums inside
@@ -1824,12 +1883,6 @@ __global__ __launch_bounds__(128) void k_intr_schur(Dev d) {
     if (c >= r && v != 0.0) atomicAdd(d.S + (size_t)(d.kc0 + r) * n + d.kc0 + c, v);
   }
   if (tid < K && sh.sxk[tid] != 0.0) atomicAdd(d.xc + d.kc0 + tid, sh.sxk[tid]);
-  for (int i = tid; i < kIntrWin * 6 * K; i += blockDim.x) {
-    const int row = i / K, j = i - row * K;   // row = 6 (b - b_lo) + a
-    const int b = sh.b_lo + row / 6;
-    const double v = sh.sfk[row * kIntrKMax + j];
-    if (b < d.NB && v != 0.0) atomicAdd(d.S + (size_t)(6 * b + row % 6) * n + d.kc0 + j, v);
-  }
 }
 
 // Called by every lane (inactive ones with no observations, so W = 0): the S_kk and rhs terms, shared by all
@@ -1838,7 +1891,7 @@ __device__ __forceinline__ void intr_schur_point(const Dev& d, int p, bool act, 
   double* skk = sh.skk;
   double* sxk = sh.sxk;
   const bool lane0 = (threadIdx.x & 63) == 0;
-  const int o0 = act ? d.poff[p] : 0, o1 = act ? d.poff[p + 1] : 0, n = d.n;
+  const int o0 = act ? d.poff[p] : 0, o1 = act ? d.poff[p + 1] : 0;
   const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
   const double sp[4] = {s4.x, s4.y, s4.z, s4.w};
   double Vi[10];
@@ -1870,7 +1923,6 @@ __device__ __forceinline__ void intr_schur_point(const Dev& d, int p, bool act, 
   for (int c = 0; c < d.ncam; ++c) {
     double W[28], Y[28];
     const bool has = build_W(c, W);
-    const int kc = d.kc0 + 7 * c;
     for (int j = 0; j < 7; ++j) {
       double r = 0.0;
       for (int a = 0; a < 4; ++a) {
@@ -1898,29 +1950,10 @@ __device__ __forceinline__ void intr_schur_point(const Dev& d, int p, bool act, 
           if (lane0) atomicAdd(skk + (7 * c + j) * kIntrKMax + 7 * c2 + j2, vs);
         }
     }
-    // S_fk: every observation of the point in a free frame block (none without observations of camera c)
-    for (int o = has ? o0 : o1; o < o1; ++o) {
-      const int m = d.obs_meta[o], b = meta_block(m);
-      if ((m & kMetaFixed) || b < 0) continue;
-      double r[2], Jc[12], Jp[8];
-      load_scaled_J(d, d.J[d.st->cur], o, b, sp, r, Jc, Jp);
-      double Mx[14];   // A_p Y^T (2x7)
-      for (int rr = 0; rr < 2; ++rr)
-        for (int j = 0; j < 7; ++j) {
-          double v = 0.0;
-          for (int a = 0; a < 4; ++a) v += Jp[4 * rr + a] * Y[4 * j + a];
-          Mx[7 * rr + j] = v;
-        }
-      const int wb = b - sh.b_lo;
-      if (wb >= 0 && wb < kIntrWin) {
-        double* dst = sh.sfk + (6 * wb) * kIntrKMax + 7 * c;
-        for (int a = 0; a < 6; ++a)
-          for (int j = 0; j < 7; ++j) atomicAdd(dst + a * kIntrKMax + j, -(Jc[a] * Mx[j] + Jc[6 + a] * Mx[7 + j]));
-      } else {
-        for (int a = 0; a < 6; ++a)
-          for (int j = 0; j < 7; ++j)
-            atomicAdd(d.S + (size_t)(6 * b + a) * n + kc + j, -(Jc[a] * Mx[j] + Jc[6 + a] * Mx[7 + j]));
-      }
+    // Y_pc for the S_fk terms of the point's observations (k_intr_fk<1>)
+    if (act) {
+      double* Yo = d.Yk + ((size_t)p * d.ncam + c) * 28;
+      for (int i = 0; i < 28; ++i) Yo[i] = Y[i];
     }
   }
 }
@@ -2920,16 +2953,21 @@ __device__ __forceinline__ double row_sum16(double v) {
 // the bottom half of the dissected band (k_chol_tiles, blockIdx 1) factors the index-reversed matrix
 // P S P (index i -> 16 NT - 1 - i, still banded), whose upper tile (I, J) is the transposed lower tile of S,
 // and starts its separator tiles (rows and columns >= sep) and their rhs at zero: the top half holds S there.
+// nb: the factored system's order (the frame part, nb = kc0, when the free intrinsics border it: k_chol_border);
+// ld: S's pitch (its full order n; the rhs follows S at ld ld, the constants at ld ld + ld).
 struct TileSrc {
   int rev;   // 0: S as stored; 1: reversed
   int np;    // 16 NT (padded order)
   int sep;   // first separator tile row (reversed side only; the top half passes NT)
+  int nb;    // rows / columns factored
+  int ld;    // pitch of S
 };
 
-__device__ __forceinline__ f64x4 tile_load(const double* __restrict__ S, int n, int I, int J, int li, int lk,
+__device__ __forceinline__ f64x4 tile_load(const double* __restrict__ S, int I, int J, int li, int lk,
                                            const TileSrc& ts) {
   f64x4 t;
-  const int cz = n * n + n;
+  const int n = ts.nb, ld = ts.ld;
+  const int cz = ld * ld + ld;
   const bool zsep = I >= ts.sep && J >= ts.sep;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -2937,7 +2975,7 @@ __device__ __forceinline__ f64x4 tile_load(const double* __restrict__ S, int n, 
     // source row / column in S's own order (upper triangle: si <= sj for I <= J)
     const int si = ts.rev ? ts.np - 1 - gj : gi, sj = ts.rev ? ts.np - 1 - gi : gj;
     const bool in = I >= 0 && si < n && sj < n && !zsep;
-    t[q] = S[in ? si * n + sj : cz + ((gi == gj && !zsep) ? 1 : 0)];
+    t[q] = S[in ? si * ld + sj : cz + ((gi == gj && !zsep) ? 1 : 0)];
   }
   return t;
 }
@@ -3186,7 +3224,8 @@ __device__ __forceinline__ bool tile_diag(const f64x4& D, double ypart, TileShar
 
 // z'_K = Z_K^T z_K for the back substitution, from the posted Z_K and z_K (LDS ring slot K & 3): formed by
 // the owner one phase later (its late phase), off the pivot chain.
-__device__ __forceinline__ void tile_zp(const TileShared& sh, double* zp, int K, int lane) {
+// zg (bordered mode): Z_K row-major into slot 0 of W row K (W tiles start at slot 1), for k_chol_border.
+__device__ __forceinline__ void tile_zp(const TileShared& sh, double* zp, int K, int lane, double* zg = nullptr) {
   if (lane < 16) {
     const double* Zs = sh.Zs[K & 3];
     const double* zk = sh.zK[K & 3];
@@ -3195,11 +3234,18 @@ __device__ __forceinline__ void tile_zp(const TileShared& sh, double* zp, int K,
     for (int r = 0; r < kCholNb; ++r) s = fma(Zs[r * kTLd + lane], zk[r], s);
     zp[16 * K + lane] = s;
   }
+  if (zg) {
+    const double* Zs = sh.Zs[K & 3];
+    double* dst = zg + (size_t)K * kTB * 256;
+#pragma unroll
+    for (int e = lane; e < 256; e += 64) dst[e] = Zs[(e >> 4) * kTLd + (e & 15)];
+  }
 }
 
 // Dinv mode (flags bit 5): D_K^-1 = Z_K^T Z_K (one MFMA chain from the posted Z_K) and z'_K, posted for the
 // phase's other waves by the wave that factored D_K (in its late step), released by dflag = K.
-__device__ __forceinline__ void tile_dinv_post(TileShared& sh, double* zp, int K, int lane, int li, int lk) {
+__device__ __forceinline__ void tile_dinv_post(TileShared& sh, double* zp, int K, int lane, int li, int lk,
+                                               double* zg = nullptr) {
   const double* Zs = sh.Zs[K & 3];
   double zt[4];
   f64x4 zb;
@@ -3209,7 +3255,7 @@ __device__ __forceinline__ void tile_dinv_post(TileShared& sh, double* zp, int K
   const f64x4 Dv = mfma_f64_k16(zt, zb, zero);   // (Z^T Z)[lk + 4q][li]
 #pragma unroll
   for (int q = 0; q < 4; ++q) sh.Dv[(lk + 4 * q) * kTLd + li] = Dv[q];
-  tile_zp(sh, zp, K, lane);
+  tile_zp(sh, zp, K, lane, zg);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   if (lane == 0) __hip_atomic_store(&sh.dflag, K, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -3262,10 +3308,10 @@ __device__ __forceinline__ void tile_rotate(f64x4 (&acc)[kTB]) {
 __device__ __forceinline__ void tile_col_load(f64x4 (&acc)[kTB], double& ypart, const Dev& d, int J, int K,
                                               int li, int lk, const TileSrc& ts) {
 #pragma unroll
-  for (int u = 0; u < kTB; ++u) acc[u] = tile_load(d.S, d.n, J - ((J - (u + K - 1)) & 7), J, li, lk, ts);
-  const int gj = 16 * J + li, n = d.n;
+  for (int u = 0; u < kTB; ++u) acc[u] = tile_load(d.S, J - ((J - (u + K - 1)) & 7), J, li, lk, ts);
+  const int gj = 16 * J + li, ld = ts.ld;
   const int sj = ts.rev ? ts.np - 1 - gj : gj;
-  ypart = d.S[(lk == 0 && sj < n && J < ts.sep) ? n * n + sj : n * n + n];
+  ypart = d.S[(lk == 0 && sj < ts.nb && J < ts.sep) ? ld * ld + sj : ld * ld + ld];
 }
 
 // One phase (tile row K) of a wave.  `late`: this wave owned the diagonal of the previous phase and still
@@ -3283,7 +3329,7 @@ template <bool kStamp>
 __device__ __forceinline__ void tile_phase(f64x4 (&acc)[kTB], double& ypart, int& J, bool& late, bool& bad,
                                            bool& tmo, int la, TileShared& sh, const Dev& d,
                                            double* __restrict__ Wg, double* zp, const int* tend, int K, int NT,
-                                           int lane, int li, int lk, const TileSrc& ts,
+                                           int lane, int li, int lk, const TileSrc& ts, double* zg,
                                            unsigned long long (&tacc)[16], unsigned long long& tlast) {
   if (late) {
     // the previous phase's owner (column J = K): its row K-1 tile (slot 0) -> W, then column J + 8, which
@@ -3292,11 +3338,11 @@ __device__ __forceinline__ void tile_phase(f64x4 (&acc)[kTB], double& ypart, int
     f64x4 Wt = {0.0, 0.0, 0.0, 0.0};
     if (hasw) Wt = tile_w(acc[0], sh.Zs[(K - 1) & 3], li, lk);
     const int Jw = J;
-    if (la & 4) tile_dinv_post(sh, zp, K, lane, li, lk);   // D_K^-1 and z'_K for the phase's other waves first
+    if (la & 4) tile_dinv_post(sh, zp, K, lane, li, lk, zg);   // D_K^-1 and z'_K for the phase's other waves first
     J += kTB;
     tile_col_load(acc, ypart, d, J, K, li, lk, ts);
     if (hasw) tile_w_store(Wt, Wg, K - 1, Jw, lane);
-    if (!(la & 4)) tile_zp(sh, zp, K, lane);   // the diagonal this wave factored last phase
+    if (!(la & 4)) tile_zp(sh, zp, K, lane, zg);   // the diagonal this wave factored last phase
     late = false;
     SG_TSTAMP(13)
     return;
@@ -3717,7 +3763,10 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
   unsigned long long tlast = kStamp ? __builtin_amdgcn_s_memtime() : 0ull, tacc[16] = {};
   __shared__ TileShared sh;
   extern __shared__ double tdyn[];
-  const int n = d.n, tid = threadIdx.x, lane = tid & 63;
+  // flags bit 3: the frame part of a system bordered by free intrinsics (order kc0 in S of pitch n): factor it,
+  // keep each Z_K (slot 0 of its W row) and x_f0 = S_ff^-1 r_f for k_chol_border, which finishes the solve
+  const bool border = (flags & 8) != 0;
+  const int n = border ? d.kc0 : d.n, tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, lk = lane >> 4;
   const int NT = (n + 15) >> 4;
@@ -3728,7 +3777,8 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
   double* zpg = Wg + (size_t)2 * NT * kTB * 256;   // [16 nd] the bottom half's z'
   double* sepb = zpg + 16 * NT;                     // [49][256] separator contribution
   double* sepy = sepb + 49 * 256;                   // [7][16]   its rhs
-  const TileSrc ts{bottom ? 1 : 0, 16 * NT, bottom ? nd : (1 << 28)};
+  const TileSrc ts{bottom ? 1 : 0, 16 * NT, bottom ? nd : (1 << 28), n, d.n};
+  double* zg = border ? Wb : nullptr;
   double* xs = tdyn;              // [16 NT] back-substitution solution
   double* zp = tdyn + 16 * NT;    // [16 NT] Z_K^T z_K
   int* tend = reinterpret_cast<int*>(tdyn + 32 * NT);   // [NT] band end (tiles, exclusive) per tile row
@@ -3787,9 +3837,9 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
     double y0 = 0.0;
     if (J == 0) {
       // D_0 has no updates: load it and column 8 together, then factor D_0 while column 8 arrives
-      D0 = tile_load(d.S, d.n, 0, 0, li, lk, ts);
-      const int sj0 = ts.rev ? ts.np - 1 - li : li;
-      y0 = d.S[(lk == 0 && sj0 < n && 0 < ts.sep) ? n * n + sj0 : n * n + n];
+      D0 = tile_load(d.S, 0, 0, li, lk, ts);
+      const int sj0 = ts.rev ? ts.np - 1 - li : li, ld = ts.ld;
+      y0 = d.S[(lk == 0 && sj0 < n && 0 < ts.sep) ? ld * ld + sj0 : ld * ld + ld];
       J = kTB;
     }
     const int done = st->done;
@@ -3815,9 +3865,9 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
              : (la & 2) ? tile_diag<true>(D0, y0, sh, zp, 0, lane, li, lk)
                         : tile_diag<false>(D0, y0, sh, zp, 0, lane, li, lk);
       if (la & 4)
-        tile_dinv_post(sh, zp, 0, lane, li, lk);
+        tile_dinv_post(sh, zp, 0, lane, li, lk, zg);
       else
-        tile_zp(sh, zp, 0, lane);   // (the wave's own LDS writes: visible to it in order)
+        tile_zp(sh, zp, 0, lane, zg);   // (the wave's own LDS writes: visible to it in order)
     }
     else if (cand_lds)   // the seven waves that wait at the first barrier
       cand_prefetch(d, cl, st->cur, (col - 1) * 64 + lane, kTileThreads - 64);
@@ -3854,8 +3904,8 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
         tmo |= spin >= spin_max;
         sep_merge(acc, ypart, J, m, sepb, sepy, lane, li, lk);
       }
-      tile_phase<kStamp>(acc, ypart, J, late, bad, tmo, la, sh, d, Wb, zp, tend, K, NTf, lane, li, lk, ts, tacc,
-                         tlast);
+      tile_phase<kStamp>(acc, ypart, J, late, bad, tmo, la, sh, d, Wb, zp, tend, K, NTf, lane, li, lk, ts, zg,
+                         tacc, tlast);
       SG_TSTAMP(2)
       // the owner of the next diagonal (now late) is on the critical path until the barrier: it rotates after
       if (!late) tile_rotate(acc);
@@ -3943,6 +3993,13 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
     d.xc[i] = xs[i];
     y[i] = xs[i];
   }
+  if (border) {   // k_chol_border reads the factor's status and runs the candidate pass
+    if (tid == 0) {
+      d.xchg_chol[kCFail] = sh.fail ? 1.0 : 0.0;
+      d.xchg_chol[kCTimeout] = sh.tmo ? 1.0 : 0.0;
+    }
+    return;
+  }
   if (!cand_lds) __syncthreads();
   if (cand_lds)
     chol_candidates_lds<kTileThreads>(d, xs, sh.fail, cl, cur, sh.tmo);
@@ -3953,6 +4010,248 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
     for (int s_ = 0; s_ < 16; ++s_) d.stamps[16 * wave + s_] += tacc[s_];
 }
 #undef SG_TSTAMP
+
+// ------------------------------------------------------------------------------------------------
+// Bordered band solve: SolveAllFrames(..., true) (slam.cpp:447-480), free intrinsics.  S is an arrowhead: the
+// frame part S_ff (order nf = kc0) keeps its co-visibility band and only the nk <= 16 intrinsics columns S_fk
+// are dense.  k_chol_tiles factors S_ff = U^T U on its band (flags bit 3) and leaves, per tile row K, Z_K =
+// U_KK^-T (slot 0 of the W row), W_KJ = U_KK^-1 U_KJ and x_f0 = S_ff^-1 r_f in xc.  With U = Db (I + W) (Db the
+// diagonal tiles), this workgroup finishes by block elimination of the border:
+//   (1) forward chain over the tile rows (one wave, the intrinsics as one 16-wide tile column):
+//         v_K = S_KB - sum_{d=1..7} W_{K-d,K}^T v_{K-d},   w_K = Z_K v_K   (w = U^-T S_fk),
+//       C = S_kk - sum_K w_K^T w_K, and q_K = Z_K^T w_K kept for step (3); four MFMAs per tile product;
+//   (2) beside it, the other waves form r_k - S_kf x_f0; then x_k = C^-1 (r_k - S_kf x_f0) (one wave, column
+//       per lane);
+//   (3) t = S_ff^-1 S_fk x_k = U^-1 (w x_k) by the band back substitution (bs_chain over the same W tiles with
+//       z'_K = q_K x_k), and x_f = x_f0 - t;
+//   (4) the candidate pass (chol_candidates) on x, as k_chol_tiles would have run it.
+// The same elimination as k_cholesky_global's arrowhead factorisation, reordered: equal up to rounding.
+constexpr int kBordThreads = 256;
+// Dynamic LDS (doubles): x [16 NT], z' [16 NT], row flags [NT ints], then (flags bit 0) the q_K tiles [256 NT] and
+// (bit 1) the candidate pass's operands (CandLds, staged by the waves that wait for the chain).
+static inline size_t border_lds_doubles(int NT, int flags, int F, int D, int n) {
+  size_t o = 32 * (size_t)NT + (NT + 1) / 2;
+  if (flags & 1) o += 256 * (size_t)NT;
+  if (flags & 2) o += (CandLds::bytes(F, D, n) + 7) / 8;
+  return o;
+}
+__global__ __launch_bounds__(kBordThreads) void k_chol_border(Dev d, double* __restrict__ Wg, int flags) {
+  const LmState* st = d.st;
+  if (st->done) return;
+  extern __shared__ double bdyn[];
+  const int n = d.n, nf = d.kc0, nk = n - nf, NT = (nf + 15) >> 4;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, li = lane & 15, lk = lane >> 4;
+  const bool cand_lds = (flags & 2) != 0;
+  double* xs = bdyn;                                   // [16 NT] t, then x_f
+  double* zq = bdyn + 16 * NT;                         // [16 NT] q_K x_k
+  int* rdone = reinterpret_cast<int*>(bdyn + 32 * NT);   // [NT] bs_chain2 row flags
+  size_t off = 32 * (size_t)NT + (NT + 1) / 2;
+  // q_K tiles (acc layout): LDS, or the dissected bottom's W space
+  double* Q = (flags & 1) ? bdyn + off : Wg + (size_t)NT * kTB * 256;
+  if (flags & 1) off += 256 * (size_t)NT;
+  CandLds cl;
+  cl.carve(bdyn + off, d.F, d.D, n);
+  const double* S = d.S;
+  const double* xc = d.xc;                             // x_f0 (frame rows), r_k (border rows)
+  __shared__ double Cs[16][17];
+  __shared__ double rk[16], xk[16], rpart[kBordThreads / 64 - 1][16];
+  __shared__ int bad_sh;
+  // SG_STAMP=1: thread 0's s_memtime after each step, the deltas accumulated over launches in d.stamps[40 + k]
+  // at the end (no global access between the stamps)
+  unsigned long long tst[6];
+  tst[0] = __builtin_amdgcn_s_memtime();
+  auto bstamp = [&](int k) { tst[k + 1] = __builtin_amdgcn_s_memtime(); };
+  const int fail0 = d.xchg_chol[kCFail] != 0.0, tmo0 = d.xchg_chol[kCTimeout] != 0.0;
+  for (int k = tid; k < NT; k += kBordThreads) rdone[k] = 0;
+  if (tid == 0) bad_sh = fail0;
+  if (wave == 0) {
+    // (1) the forward chain; v_{K-1..K-7} in registers
+    f64x4 vr[kTB - 1];
+    const f64x4 zero = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int dd = 0; dd < kTB - 1; ++dd) vr[dd] = zero;
+    f64x4 C;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = lk + 4 * q, c = li;
+      const int a = min(r, c), b = max(r, c);   // S_kk upper triangle
+      C[q] = (r < nk && c < nk) ? S[(size_t)(nf + a) * n + nf + b] : (r == c ? 1.0 : 0.0);
+    }
+    // row K's operands (S_KB, W_{K-d,K}, Z_K) do not depend on the chain: loaded one row ahead
+    struct RowOps {
+      double sb[4], w[kTB - 1][4], za[4], zb[4];
+    };
+    auto row_load = [&](RowOps& o, int K) {
+      const int Kc = min(K, NT - 1);
+      // unconditional loads (a load under a condition compiles to a branch that waits for it): the index is
+      // selected (S's zero constant past the system), and rows before 0 read some finite W tile that multiplies
+      // the zero v_{K-d}
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = 16 * Kc + lk + 4 * q;
+        o.sb[q] = S[(r < nf && li < nk) ? (size_t)r * n + nf + li : (size_t)n * n + n];
+      }
+#pragma unroll
+      for (int dd = 1; dd < kTB; ++dd) {
+        const double* wt = Wg + ((size_t)max(Kc - dd, 0) * kTB + dd) * 256 + lane;
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) o.w[dd - 1][s4] = -wt[s4 * 64];
+      }
+      const double* Z = Wg + (size_t)Kc * kTB * 256;   // row-major Z_K
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        o.za[s4] = Z[li * 16 + 4 * s4 + lk];     // Z^T in acc layout: Z v
+        o.zb[s4] = Z[(4 * s4 + lk) * 16 + li];   // Z in acc layout: Z^T w
+      }
+    };
+    RowOps ops[2];
+    row_load(ops[0], 0);
+    auto row = [&](RowOps& o, int K) {
+      // the far terms (two accumulators, independent of v_{K-1}), then v_{K-1}'s product
+      f64x4 va, vb = zero;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) va[q] = o.sb[q];
+#pragma unroll
+      for (int dd = kTB - 1; dd >= 2; --dd) {
+        if (dd & 1) va = mfma_f64_k16(o.w[dd - 1], vr[dd - 1], va);
+        else vb = mfma_f64_k16(o.w[dd - 1], vr[dd - 1], vb);
+      }
+      vb = mfma_f64_k16(o.w[0], vr[0], vb);
+      f64x4 v;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = va[q] + vb[q];
+      const f64x4 w = mfma_f64_k16(o.za, v, zero);
+      double wn[4];
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) wn[s4] = -w[s4];
+      C = mfma_f64_k16(wn, w, C);
+      const f64x4 qv = mfma_f64_k16(o.zb, w, zero);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Q[(size_t)K * 256 + q * 64 + lane] = qv[q];
+#pragma unroll
+      for (int dd = kTB - 2; dd >= 1; --dd) vr[dd] = vr[dd - 1];
+      vr[0] = v;
+    };
+#pragma nounroll
+    for (int K = 0; K < NT; K += 2) {
+      row_load(ops[1], K + 1);
+      row(ops[0], K);
+      if (K + 1 < NT) {
+        row_load(ops[0], K + 2);
+        row(ops[1], K + 1);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) Cs[lk + 4 * q][li] = C[q];
+  } else {
+    // (2) S_kf x_f0 beside the chain: the other waves take the frame rows (a row's 14 border entries are
+    // contiguous), per-wave sums per intrinsic, combined in wave order below
+    constexpr int kOt = kBordThreads - 64;
+    double part[kCholNb];
+#pragma unroll
+    for (int c = 0; c < kCholNb; ++c) part[c] = 0.0;
+    for (int i = tid - 64; i < nf; i += kOt) {
+      const double xi = xc[i];
+      const double* row = S + (size_t)i * n + nf;
+#pragma unroll
+      for (int c = 0; c < kCholNb; ++c) part[c] = fma(row[c], xi, part[c]);   // (c >= nk: unused, inside S)
+    }
+#pragma unroll
+    for (int c = 0; c < kCholNb; ++c) {
+      const double v = wave_sum(part[c]);
+      if (lane == 0) rpart[wave - 1][c] = v;
+    }
+    if (cand_lds) cand_prefetch(d, cl, st->cur, tid - 64, kOt);
+  }
+  if (d.stamps && tid == 0) bstamp(0);
+  __syncthreads();
+  if (tid < nk) rk[tid] = xc[nf + tid] - ((rpart[0][tid] + rpart[1][tid]) + rpart[2][tid]);
+  __syncthreads();
+  if (wave == 0) {
+    // x_k = C^-1 rk: C = U_c^T U_c column per lane, then the two triangular solves
+    double col[kCholNb];
+#pragma unroll
+    for (int r = 0; r < kCholNb; ++r) col[r] = (lane < nk && r <= lane) ? Cs[r][lane] : 0.0;
+    bool bad = false;
+    chol_diag16(col, nk, lane, bad);
+    if (lane < nk) {
+#pragma unroll
+      for (int r = 0; r < kCholNb; ++r)
+        if (r <= lane) Cs[r][lane] = col[r];
+    }
+    // 1 / U_jj for every pivot first (independent divisions), then the two solves on multiplies
+    double inv[kCholNb];
+#pragma unroll
+    for (int j = 0; j < kCholNb; ++j) inv[j] = j < nk ? 1.0 / readlane_d(col[j], j) : 0.0;
+    double s = lane < nk ? rk[lane] : 0.0;
+#pragma unroll
+    for (int j = 0; j < kCholNb; ++j) {
+      if (j < nk) {
+        const double zj = readlane_d(s, j) * inv[j];
+        if (lane == j) s = zj;
+        else if (lane > j) s = fma(-col[j], zj, s);
+      }
+    }
+#pragma unroll
+    for (int j = kCholNb - 1; j >= 0; --j) {
+      if (j < nk) {
+        const double xj = readlane_d(s, j) * inv[j];
+        if (lane == j) s = xj;
+        else if (lane < j) s = fma(-Cs[lane][j], xj, s);
+      }
+    }
+    if (lane < 16) xk[lane] = lane < nk ? s : 0.0;
+    if (lane == 0 && bad) bad_sh = 1;
+  }
+  if (d.stamps && tid == 0) bstamp(1);
+  __syncthreads();
+  // (3) z'_K = q_K x_k, then t = U^-1 (w x_k)
+  for (int i = tid; i < 16 * NT; i += kBordThreads) {
+    const int K = i >> 4, r = i & 15;
+    const double* qk = Q + (size_t)K * 256 + (r >> 2) * 64 + (r & 3) * 16;
+    double acc = 0.0;
+#pragma unroll
+    for (int c = 0; c < kCholNb; ++c) acc = fma(qk[c], xk[c], acc);   // (columns >= nk: zero in q and x_k)
+    zq[i] = acc;
+  }
+  if (d.stamps && tid == 0) bstamp(2);
+  __syncthreads();
+  bool tmo = tmo0;
+  {
+    double xw[kTB - 1];
+#pragma unroll
+    for (int dd = 0; dd < kTB - 1; ++dd) xw[dd] = 0.0;
+    constexpr int kBs2Rows = 12;
+    if (NT >= kBs2Rows) {
+      if (wave < 2) bs_chain2<false>(Wg, zq, xs, rdone, NT - 1, 0, xw, NT, wave, lane, li, lk, tmo);
+    } else if (wave == 0) {
+      bs_chain<false>(Wg, zq, xs, NT - 1, 0, xw, NT, lane, li, lk);
+    }
+  }
+  __shared__ int tmo_sh;
+  if (tid == 0) tmo_sh = 0;
+  if (d.stamps && tid == 0) bstamp(3);
+  __syncthreads();
+  if (tmo && lane == 0) tmo_sh = 1;
+  // (4) x = (x_f0 - t, x_k): xc, the solution copy in work, and the candidate pass
+  double* y = d.work;
+  for (int i = tid; i < n; i += kBordThreads) {
+    const double x = i < nf ? xc[i] - xs[i] : xk[i - nf];
+    if (i < nf) xs[i] = x;
+    d.xc[i] = x;
+    y[i] = x;
+  }
+  __syncthreads();
+  if (cand_lds)
+    chol_candidates_lds<kBordThreads>(d, xs, bad_sh, cl, st->cur, tmo_sh);
+  else
+    chol_candidates<kBordThreads>(d, xs, bad_sh, tmo_sh);
+  if (d.stamps && tid == 0) {
+    bstamp(4);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) d.stamps[40 + k] += tst[k + 1] - tst[k];
+  }
+}
 
 // ------------------------------------------------------------------------------------------------
 // k_point_update: back-substitution x_p = V~^-1 (g~_p - A_p^T A_c x_c), model cost change
@@ -4629,12 +4928,20 @@ void BaSolver::LaunchCholTiles(bool stamp, int la, dim3 grid, const Dev& d, int 
   const int idx = chol_tiles_index(la);   // validated in the constructor (CheckCholVariant)
   const void* f = stamp ? kCholTilesStamped[(la & 16) ? 2 : (la & 8) ? 1 : 0] : kCholTilesKernels[1 + idx];
   Dev dd = d;
-  const int32_t* pj = (const int32_t*)work_i_.ptr;
+  // bordered: the frame band ends follow the arrowhead's panel ends in work_i_
+  const int32_t* pj = (const int32_t*)work_i_.ptr + (chol_border_ ? (n_ + kCholNb - 1) / kCholNb : 0);
   double* wg = Wg_.ptr;
   int32_t* tf = tflag_.ptr;
   int nd = chol_nd_;
+  if (chol_border_) flags |= 8;
   void* args[] = {&dd, &pj, &wg, &tf, &nd, &flags};
   SG_HIP_CHECK(hipLaunchKernel(f, grid, dim3(kTileThreads), args, tile_lds_, stream_));
+  if (chol_border_) {
+    const int ntf = (6 * NB_ + kCholNb - 1) / kCholNb;
+    hipLaunchKernelGGL(k_chol_border, dim3(1), dim3(kBordThreads),
+                       border_lds_doubles(ntf, border_flags_, F_, D_, n_) * sizeof(double), stream_, d, Wg_.ptr,
+                       border_flags_);
+  }
 }
 
 BaSolver::BaSolver(const sg_device_options& dev) : dev_(dev) {
@@ -4691,6 +4998,13 @@ BaSolver::BaSolver(const sg_device_options& dev) : dev_(dev) {
     gchol_lds_max_ = (size_t)160 * 1024 - ga.sharedSizeBytes;
     for (const void* f : {(const void*)k_cholesky_global<true>, (const void*)k_cholesky_global<false>})
       SG_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)gchol_lds_max_));
+    hipFuncAttributes ba;
+    SG_HIP_CHECK(hipFuncGetAttributes(&ba, (const void*)k_chol_border));
+    border_lds_max_ = (size_t)160 * 1024 - ba.sharedSizeBytes;
+    SG_REQUIRE(border_lds_doubles(kTileMaxNT, 0, 0, 0, 0) * sizeof(double) <= border_lds_max_, SG_EINVAL,
+               "k_chol_border: LDS for kTileMaxNT rows");
+    SG_HIP_CHECK(hipFuncSetAttribute((const void*)k_chol_border, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)border_lds_max_));
   }
   st_.Resize(1);
   timers_.resize(kKNum);
@@ -4957,6 +5271,170 @@ void BaSolver::Load(const sg_problem& p) {
     SG_HIP_CHECK(hipGetLastError());
   }
   lap("upload-1");
+  // Schur work lists (see SchurSeg): the cells of every free point (one per block of its span, with the
+  // point's observations in that block), segments of consecutive points whose columns fit kSchurTW tiles of
+  // S, their batches, and each wide point's observation pairs (s <= t, both on free frames).
+  // They run on a second host thread while this one builds the sweep lists: both read the same inputs and their
+  // outputs are disjoint (members: npairs_, schur_mfma_, nseg_, nwide_ there; nlin_, npu_ here).
+  std::vector<int32_t> pinfo(2 * (size_t)std::max(P_, 1), 0), pmx(4 * (size_t)std::max(P_, 1), 0), cells, cell_obs;
+  std::vector<SchurSeg> segs;
+  std::vector<SchurBatch> sbatch;
+  std::vector<WideSeg> wsegs;
+  std::vector<int32_t> pairs_flat;   // int2 per pair (wide points)
+  int s_off = 0;
+  auto build_schur_lists = [&] {
+    std::vector<int32_t> obs_blk(M_);
+    for (int o = 0; o < M_; ++o) obs_blk[o] = frame_block[obs_frame[o]];
+    // span in blocks of a free point's Schur terms (0: none)
+    auto sspan = [&](int i) {
+      const int pt = point_perm_[i];
+      return (pfree[i] && pfirst[pt] < NB_) ? plast[pt] - pfirst[pt] + 1 : 0;
+    };
+    std::vector<int32_t> simple_obs(std::max(P_, 1), -1);   // observation of the first block if one per block
+    int ncell = 0;
+    npairs_ = 0;
+    schur_mfma_ = 0.0;
+    {
+      std::vector<std::pair<int, int>> bo;
+      cells.reserve(4 * (size_t)M_ + 4);
+      cell_obs.reserve((size_t)M_ / 4 + 1);
+      for (int i = 0; i < P_; ++i) {
+        size_t kb = 0;
+        for (int o = poff[i]; o < poff[i + 1]; ++o) kb += obs_blk[o] >= 0;
+        if (pfree[i]) npairs_ += kb * (kb + 1) / 2;
+        const int sp = sspan(i);
+        if (sp == 0 || sp > kSegNbMax) continue;
+        const int pf = pfirst[point_perm_[i]];
+        pinfo[2 * i] = (int)(cells.size() / 4);
+        pinfo[2 * i + 1] = (pf << 8) | sp;
+        bo.clear();
+        for (int o = poff[i]; o < poff[i + 1]; ++o)
+          if (obs_blk[o] >= 0) bo.emplace_back(obs_blk[o], o);
+        if (!std::is_sorted(bo.begin(), bo.end())) std::sort(bo.begin(), bo.end());   // sorted at load already
+        {
+          bool one = (int)bo.size() == sp;   // observations sorted by block at load: consecutive
+          for (int q = 0; one && q < sp; ++q) one = bo[q].first == pf + q && bo[q].second == bo[0].second + q;
+          if (one) simple_obs[i] = bo[0].second;
+        }
+        size_t k = 0;
+        for (int b = pf; b < pf + sp; ++b) {
+          // {first observation or -1, point, (block << 16) | further observations, their offset in cell_obs}
+          int o0 = -1;
+          if (k < bo.size() && bo[k].first == b) o0 = bo[k++].second;
+          const int k1 = (int)cell_obs.size();
+          while (k < bo.size() && bo[k].first == b) cell_obs.push_back(bo[k++].second);
+          cells.insert(cells.end(), {o0, i, (int)(((unsigned)b << 16) | (unsigned)(cell_obs.size() - k1)), k1});
+        }
+      }
+      ncell = (int)cells.size() / 4;
+      if (cells.empty()) cells.assign(4, 0);
+      if (cell_obs.empty()) cell_obs.push_back(0);
+    }
+    {
+      // points per segment: one segment per CU (the workgroup's LDS holds one per CU; fewer, longer segments
+      // write fewer partial tiles and keep the producer/consumer pipeline full; SG_SCHUR_SEGS: tuning)
+      const int ncu = ncu_;
+      // (with k_schur beside the camera reduction, one CU per XCD stays free for k_cam_reduce / k_cam_finalize:
+      // a k_schur workgroup's 140 KB of LDS leaves no room for them on its CU)
+      const int target = getenv("SG_SCHUR_SEGS") ? std::max(1, atoi(getenv("SG_SCHUR_SEGS")))
+                                                 : (overlap_ok_ ? std::max(1, ncu - 8) : ncu);
+      const int maxpts = std::max(16, (P_ + target - 1) / target);
+      int cnext = 0;
+      for (int i = 0; i < P_;) {
+        if (sspan(i) > kSegNbMax) {
+          WideSeg w{};
+          w.p = i;
+          w.pair_lo = (int)pairs_flat.size() / 2;
+          for (int os = poff[i]; os < poff[i + 1]; ++os) {
+            if (obs_blk[os] < 0) continue;
+            for (int ot = os; ot < poff[i + 1]; ++ot) {
+              if (obs_blk[ot] < 0) continue;
+              pairs_flat.push_back(((os - poff[i]) << 16) | (ot - poff[i]));
+              pairs_flat.push_back((obs_blk[os] << 16) | obs_blk[ot]);
+            }
+          }
+          w.pair_hi = (int)pairs_flat.size() / 2;
+          wsegs.push_back(w);
+          ++i;
+          continue;
+        }
+        SchurSeg sg{};
+        sg.p0 = i;
+        int clo = INT32_MAX, chi = -1, blo = INT32_MAX, bhi = -1;   // columns [clo, chi), blocks [blo, bhi]
+        int j = i;
+        while (j < P_ && j - i < maxpts) {
+          const int sp = sspan(j);
+          if (sp > kSegNbMax) break;
+          if (sp > 0) {
+            const int pf = pfirst[point_perm_[j]];
+            const int l2 = std::min(clo, 6 * pf), h2 = std::max(chi, 6 * (pf + sp));
+            if ((h2 + 15) / 16 - l2 / 16 > kSchurTW) break;
+            clo = l2;
+            chi = h2;
+            blo = std::min(blo, pf);
+            bhi = std::max(bhi, pf + sp - 1);
+          }
+          ++j;
+        }
+        sg.p1 = j;
+        if (chi >= 0) {
+          sg.t0 = clo / 16;
+          sg.ntw = (chi + 15) / 16 - sg.t0;
+          sg.b_lo = blo;
+          sg.nb = bhi - blo + 1;
+        }
+        sg.s_off = s_off;
+        s_off += sg.ntw * (sg.ntw + 1) / 2 * 256 + 16 * sg.ntw;
+        // last window tile of each point's columns (-1: no Schur terms)
+        auto pjhi = [&](int k) {
+          const int sp = sspan(k);
+          return sp == 0 ? -1 : (6 * (pfirst[point_perm_[k]] + sp) - 1 - 16 * sg.t0) / 16;
+        };
+        sg.bt0 = (int)sbatch.size();
+        for (int k = i; k < j;) {
+          SchurBatch B{};
+          B.p0 = k;
+          B.c0 = cnext;
+          int nc = 0, nx = 0;
+          while (k < j && k - B.p0 < kSchurBatchPts && nx + 64 * (pjhi(k) + 1) <= kSchurXCap &&
+                 nc + sspan(k) <= 64 * kSchurCellWaves) {
+            pmx[4 * k] = nx;
+            pmx[4 * k + 1] = pjhi(k);
+            pmx[4 * k + 2] = simple_obs[k];
+            pmx[4 * k + 3] = nc;
+            nx += 64 * (pjhi(k) + 1);
+            schur_mfma_ += schur_aug_base(pjhi(k) + 1);
+            nc += sspan(k++);
+          }
+          B.p1 = k;
+          B.c1 = B.c0 + nc;
+          cnext += nc;
+          sbatch.push_back(B);
+        }
+        sg.bt1 = (int)sbatch.size();
+        segs.push_back(sg);
+        i = j;
+      }
+      SG_REQUIRE(cnext == ncell, SG_EINVAL, "Schur cells out of step with the batches");
+    }
+    nseg_ = (int)segs.size();
+    nwide_ = (int)wsegs.size();
+    if (pairs_flat.empty()) pairs_flat.assign(2, 0);
+  };
+  std::exception_ptr schur_err;
+  std::thread schur_thr([&] {
+    try {
+      build_schur_lists();
+    } catch (...) {
+      schur_err = std::current_exception();
+    }
+  });
+  struct Joiner {
+    std::thread& t;
+    ~Joiner() {
+      if (t.joinable()) t.join();
+    }
+  } schur_join{schur_thr};
   // k_linearize decomposition (see LinChunk): rounds of whole points (<= kLinObs observations), up to
   // maxr rounds per chunk sharing one camera window; fewer rounds per chunk on small problems so that the
   // grid still fills the chip.
@@ -5049,152 +5527,8 @@ void BaSolver::Load(const sg_problem& p) {
   npu_ = (int)pu_units.size();
   if (pu_units.empty()) pu_units.push_back(0);
   lap("lin-lists");
-  // Schur work lists (see SchurSeg): the cells of every free point (one per block of its span, with the
-  // point's observations in that block), segments of consecutive points whose columns fit kSchurTW tiles of
-  // S, their batches, and each wide point's observation pairs (s <= t, both on free frames).
-  std::vector<int32_t> obs_blk(M_);
-  for (int o = 0; o < M_; ++o) obs_blk[o] = frame_block[obs_frame[o]];
-  // span in blocks of a free point's Schur terms (0: none)
-  auto sspan = [&](int i) {
-    const int pt = point_perm_[i];
-    return (pfree[i] && pfirst[pt] < NB_) ? plast[pt] - pfirst[pt] + 1 : 0;
-  };
-  std::vector<int32_t> pinfo(2 * (size_t)std::max(P_, 1), 0), pmx(4 * (size_t)std::max(P_, 1), 0), cells, cell_obs;
-  std::vector<int32_t> simple_obs(std::max(P_, 1), -1);   // observation of the first block if one per block
-  int ncell = 0;
-  std::vector<SchurSeg> segs;
-  std::vector<SchurBatch> sbatch;
-  std::vector<WideSeg> wsegs;
-  std::vector<int32_t> pairs_flat;   // int2 per pair (wide points)
-  npairs_ = 0;
-  schur_mfma_ = 0.0;
-  {
-    std::vector<std::pair<int, int>> bo;
-    cells.reserve(4 * (size_t)M_ + 4);
-    cell_obs.reserve((size_t)M_ / 4 + 1);
-    for (int i = 0; i < P_; ++i) {
-      size_t kb = 0;
-      for (int o = poff[i]; o < poff[i + 1]; ++o) kb += obs_blk[o] >= 0;
-      if (pfree[i]) npairs_ += kb * (kb + 1) / 2;
-      const int sp = sspan(i);
-      if (sp == 0 || sp > kSegNbMax) continue;
-      const int pf = pfirst[point_perm_[i]];
-      pinfo[2 * i] = (int)(cells.size() / 4);
-      pinfo[2 * i + 1] = (pf << 8) | sp;
-      bo.clear();
-      for (int o = poff[i]; o < poff[i + 1]; ++o)
-        if (obs_blk[o] >= 0) bo.emplace_back(obs_blk[o], o);
-      if (!std::is_sorted(bo.begin(), bo.end())) std::sort(bo.begin(), bo.end());   // sorted at load already
-      {
-        bool one = (int)bo.size() == sp;   // observations sorted by block at load: consecutive
-        for (int q = 0; one && q < sp; ++q) one = bo[q].first == pf + q && bo[q].second == bo[0].second + q;
-        if (one) simple_obs[i] = bo[0].second;
-      }
-      size_t k = 0;
-      for (int b = pf; b < pf + sp; ++b) {
-        // {first observation or -1, point, (block << 16) | further observations, their offset in cell_obs}
-        int o0 = -1;
-        if (k < bo.size() && bo[k].first == b) o0 = bo[k++].second;
-        const int k1 = (int)cell_obs.size();
-        while (k < bo.size() && bo[k].first == b) cell_obs.push_back(bo[k++].second);
-        cells.insert(cells.end(), {o0, i, (int)(((unsigned)b << 16) | (unsigned)(cell_obs.size() - k1)), k1});
-      }
-    }
-    ncell = (int)cells.size() / 4;
-    if (cells.empty()) cells.assign(4, 0);
-    if (cell_obs.empty()) cell_obs.push_back(0);
-  }
-  int s_off = 0;
-  {
-    // points per segment: one segment per CU (the workgroup's LDS holds one per CU; fewer, longer segments
-    // write fewer partial tiles and keep the producer/consumer pipeline full; SG_SCHUR_SEGS: tuning)
-    const int ncu = ncu_;
-    // (with k_schur beside the camera reduction, one CU per XCD stays free for k_cam_reduce / k_cam_finalize:
-    // a k_schur workgroup's 140 KB of LDS leaves no room for them on its CU)
-    const int target = getenv("SG_SCHUR_SEGS") ? std::max(1, atoi(getenv("SG_SCHUR_SEGS")))
-                                               : (overlap_ok_ ? std::max(1, ncu - 8) : ncu);
-    const int maxpts = std::max(16, (P_ + target - 1) / target);
-    int cnext = 0;
-    for (int i = 0; i < P_;) {
-      if (sspan(i) > kSegNbMax) {
-        WideSeg w{};
-        w.p = i;
-        w.pair_lo = (int)pairs_flat.size() / 2;
-        for (int os = poff[i]; os < poff[i + 1]; ++os) {
-          if (obs_blk[os] < 0) continue;
-          for (int ot = os; ot < poff[i + 1]; ++ot) {
-            if (obs_blk[ot] < 0) continue;
-            pairs_flat.push_back(((os - poff[i]) << 16) | (ot - poff[i]));
-            pairs_flat.push_back((obs_blk[os] << 16) | obs_blk[ot]);
-          }
-        }
-        w.pair_hi = (int)pairs_flat.size() / 2;
-        wsegs.push_back(w);
-        ++i;
-        continue;
-      }
-      SchurSeg sg{};
-      sg.p0 = i;
-      int clo = INT32_MAX, chi = -1, blo = INT32_MAX, bhi = -1;   // columns [clo, chi), blocks [blo, bhi]
-      int j = i;
-      while (j < P_ && j - i < maxpts) {
-        const int sp = sspan(j);
-        if (sp > kSegNbMax) break;
-        if (sp > 0) {
-          const int pf = pfirst[point_perm_[j]];
-          const int l2 = std::min(clo, 6 * pf), h2 = std::max(chi, 6 * (pf + sp));
-          if ((h2 + 15) / 16 - l2 / 16 > kSchurTW) break;
-          clo = l2;
-          chi = h2;
-          blo = std::min(blo, pf);
-          bhi = std::max(bhi, pf + sp - 1);
-        }
-        ++j;
-      }
-      sg.p1 = j;
-      if (chi >= 0) {
-        sg.t0 = clo / 16;
-        sg.ntw = (chi + 15) / 16 - sg.t0;
-        sg.b_lo = blo;
-        sg.nb = bhi - blo + 1;
-      }
-      sg.s_off = s_off;
-      s_off += sg.ntw * (sg.ntw + 1) / 2 * 256 + 16 * sg.ntw;
-      // last window tile of each point's columns (-1: no Schur terms)
-      auto pjhi = [&](int k) {
-        const int sp = sspan(k);
-        return sp == 0 ? -1 : (6 * (pfirst[point_perm_[k]] + sp) - 1 - 16 * sg.t0) / 16;
-      };
-      sg.bt0 = (int)sbatch.size();
-      for (int k = i; k < j;) {
-        SchurBatch B{};
-        B.p0 = k;
-        B.c0 = cnext;
-        int nc = 0, nx = 0;
-        while (k < j && k - B.p0 < kSchurBatchPts && nx + 64 * (pjhi(k) + 1) <= kSchurXCap &&
-               nc + sspan(k) <= 64 * kSchurCellWaves) {
-          pmx[4 * k] = nx;
-          pmx[4 * k + 1] = pjhi(k);
-          pmx[4 * k + 2] = simple_obs[k];
-          pmx[4 * k + 3] = nc;
-          nx += 64 * (pjhi(k) + 1);
-          schur_mfma_ += schur_aug_base(pjhi(k) + 1);
-          nc += sspan(k++);
-        }
-        B.p1 = k;
-        B.c1 = B.c0 + nc;
-        cnext += nc;
-        sbatch.push_back(B);
-      }
-      sg.bt1 = (int)sbatch.size();
-      segs.push_back(sg);
-      i = j;
-    }
-    SG_REQUIRE(cnext == ncell, SG_EINVAL, "Schur cells out of step with the batches");
-  }
-  nseg_ = (int)segs.size();
-  nwide_ = (int)wsegs.size();
-  if (pairs_flat.empty()) pairs_flat.assign(2, 0);
+  schur_thr.join();
+  if (schur_err) std::rethrow_exception(schur_err);
   lap("segments");
   // deterministic reduction lists: for every camera block, the slab offsets of the chunk partials that cover
   // it (fixed chunk order), and of the segments' rhs partials
@@ -5313,10 +5647,30 @@ void BaSolver::Load(const sg_problem& p) {
   chol_tiles_ = n_ > 0 && nk_ == 0 && npanel <= kTileMaxNT && !getenv("SG_CHOL_WINDOW");
   for (int pk = 0; pk < npanel; ++pk)
     if ((panel_jmax[pk] + kCholNb - 1) / kCholNb - pk > kTB) chol_tiles_ = false;
+  // free intrinsics (one 16-wide border tile): the frame band on k_chol_tiles, the border by k_chol_border
+  // (SG_CHOL_BORDER=0: the arrowhead k_cholesky_global)
+  chol_border_ = false;
+  if (nk_ > 0 && NB_ > 0 && n_ - 6 * NB_ <= kCholNb && !getenv("SG_CHOL_WINDOW") &&
+      !(getenv("SG_CHOL_BORDER") && atoi(getenv("SG_CHOL_BORDER")) == 0)) {
+    const int ntf = (6 * NB_ + kCholNb - 1) / kCholNb;
+    chol_border_ = ntf <= kTileMaxNT;
+    for (int pk = 0; pk < ntf; ++pk)
+      if ((panel_bend[pk] + kCholNb - 1) / kCholNb - pk > kTB) chol_border_ = false;
+    if (chol_border_) {
+      chol_tiles_ = true;
+      // q_K tiles and the candidate operands in LDS where they fit (else global q_K / chol_candidates)
+      border_flags_ = 0;
+      for (int f : {1, 2, 3})   // the last that fits: both, else the candidate operands, else the q_K tiles
+        if (border_lds_doubles(ntf, f, F_, D_, n_) * sizeof(double) <= border_lds_max_ &&
+            (!(f & 2) || (F_ <= kCandMax && D_ <= kCandMax)))
+          border_flags_ = f;
+    }
+  }
   // dissected band: a second workgroup factors the bottom nd tile rows (reversed) while the first factors
   // the top, both meeting at a 7-tile separator (k_chol_tiles); worth it from about 12 tile rows
   chol_nd_ = 0;
-  if (chol_tiles_ && npanel >= kSplitMinNT && !(getenv("SG_CHOL_SPLIT") && atoi(getenv("SG_CHOL_SPLIT")) == 0))
+  if (chol_tiles_ && !chol_border_ && npanel >= kSplitMinNT &&
+      !(getenv("SG_CHOL_SPLIT") && atoi(getenv("SG_CHOL_SPLIT")) == 0))
     chol_nd_ = (npanel - 9) / 2;   // the bottom (nd rows + hand-off) done before the top reaches row m - 1
   if (chol_nd_ > 0 && getenv("SG_CHOL_ND")) chol_nd_ = std::max(1, std::min(atoi(getenv("SG_CHOL_ND")), (npanel - 9) / 2 + 1));
   if (chol_tiles_) {
@@ -5327,11 +5681,13 @@ void BaSolver::Load(const sg_problem& p) {
     stager_->Add(Wg_, wz);
     stager_->Add(tflag_, std::vector<int32_t>(2, 0));
     tile_lds_ = (size_t)npanel * 32 * sizeof(double) + (size_t)(3 * npanel + 1) / 2 * sizeof(double);
-    chol_cand_lds_ = F_ <= kCandMax && D_ <= kCandMax && tile_lds_ + CandLds::bytes(F_, D_, n_) <= 100 * 1024 &&
+    chol_cand_lds_ = !chol_border_ && F_ <= kCandMax && D_ <= kCandMax &&
+                     tile_lds_ + CandLds::bytes(F_, D_, n_) <= 100 * 1024 &&
                      tile_lds_ + CandLds::bytes(F_, D_, n_) <= tile_lds_set_;
     if (chol_cand_lds_) tile_lds_ += CandLds::bytes(F_, D_, n_);
     if (tile_lds_ > tile_lds_set_) {   // beyond the LDS granted at construction: the one-workgroup kernels
       chol_tiles_ = false;
+      chol_border_ = false;
       chol_nd_ = 0;
     }
   }
@@ -5418,6 +5774,25 @@ void BaSolver::Load(const sg_problem& p) {
   S_slab_.Resize(std::max(s_off, 1));
   chunk_scal_.Resize((size_t)std::max(npu_, 1) * kNScal);
   stg.Add(pu_units_, pu_units);
+  if (nk_) {
+    // free intrinsics: each frame block's non-fixed observations (block NB: the fixed frames'), for k_intr_fk
+    std::vector<int32_t> boff(NB_ + 2, 0), bidx;
+    for (int o = 0; o < M_; ++o)
+      if (!(obs_meta[o] & kMetaFixed)) {
+        const int b = meta_block(obs_meta[o]);
+        boff[(b >= 0 ? b : NB_) + 1] += 1;
+      }
+    for (int b = 0; b <= NB_; ++b) boff[b + 1] += boff[b];
+    bidx.resize(std::max(boff[NB_ + 1], 1), 0);
+    std::vector<int32_t> fill(boff.begin(), boff.end() - 1);
+    for (int o = 0; o < M_; ++o)
+      if (!(obs_meta[o] & kMetaFixed)) {
+        const int b = meta_block(obs_meta[o]);
+        bidx[fill[b >= 0 ? b : NB_]++] = o;
+      }
+    stg.Add(intr_boff_, boff);
+    stg.Add(intr_bidx_, bidx);
+  }
   if (host_timing) DevMark(s, 1);
   stg.Flush(s);
   if (host_timing) DevMark(s, 2);
@@ -5438,6 +5813,8 @@ void BaSolver::Load(const sg_problem& p) {
     Jk_.Resize(14 * (size_t)std::max(M_, 1));
     KU_.Resize(nn * nk_);
     kst_.Resize(56 * (size_t)ncam_);
+    Yk_.Resize(28 * (size_t)std::max(P_, 1) * ncam_);
+    kpart_.Resize((size_t)(NB_ + 1) * ncam_ * 42);
   }
   stamp_on_ = getenv("SG_STAMP") && getenv("SG_STAMP")[0] == '1';
   if (stamp_on_) stamps_.Resize(64 + 2 * 128 * 16);
@@ -5647,6 +6024,10 @@ Dev BaSolver::MakeDev() {
   d.Jk = Jk_.ptr;
   d.KU = KU_.ptr;
   d.kst = kst_.ptr;
+  d.Yk = Yk_.ptr;
+  d.kpart = kpart_.ptr;
+  d.intr_boff = intr_boff_.ptr;
+  d.intr_bidx = intr_bidx_.ptr;
   d.stab_b = stab_b_;
   d.stab_inv_b = 1.0 / stab_b_;
   d.q[0] = q_.ptr;
@@ -5981,6 +6362,7 @@ void BaSolver::EnqueueIterations(int n) {
     if (nk_) {
       hipLaunchKernelGGL(k_intr_zero, dim3((n_ * nk_ + 255) / 256), dim3(256), 0, stream_, d);
       hipLaunchKernelGGL(k_intr_lin, dim3((std::max(M_, 1) + 255) / 256), dim3(256), 0, stream_, d);
+      hipLaunchKernelGGL(k_intr_fk<0>, dim3(NB_ + 1, ncam_), dim3(kIntrFkThreads), 0, stream_, d);
       hipLaunchKernelGGL(k_intr_fin, dim3(1), dim3(64), 0, stream_, d);
     }
     if (!fin_in_schur) {
@@ -6005,6 +6387,7 @@ void BaSolver::EnqueueIterations(int n) {
     if (nk_) {
       hipLaunchKernelGGL(k_intr_assemble, dim3((n_ * nk_ + 255) / 256), dim3(256), 0, stream_, d);
       hipLaunchKernelGGL(k_intr_schur, dim3((std::max(P_, 1) + 127) / 128), dim3(128), 0, stream_, d);
+      if (NB_ > 0) hipLaunchKernelGGL(k_intr_fk<1>, dim3(NB_, ncam_), dim3(kIntrFkThreads), 0, stream_, d);
     }
     if (multi_x || pack_force_ || merged) {
       // the band of S and the rhs partial are summed over landmark shards (packed: the band only), with the
@@ -6262,7 +6645,7 @@ void BaSolver::Info(sg_ba_info* o) const {
   o->num_blocks = NB_;
   o->n = n_;
   o->band_tiles = band_tiles_;
-  o->cholesky_path = chol_tiles_ ? 0 : (chol_window_ ? 1 : (chol_gstage_ ? 2 : 3));
+  o->cholesky_path = chol_border_ ? 4 : chol_tiles_ ? 0 : (chol_window_ ? 1 : (chol_gstage_ ? 2 : 3));
   o->cholesky_split = chol_tiles_ ? chol_nd_ : 0;
   o->num_pairs = (int32_t)std::min<size_t>(npairs_, INT32_MAX);
   o->rank = comm_ ? comm_->rank() : 0;

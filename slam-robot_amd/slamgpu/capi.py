@@ -84,7 +84,8 @@ class SgBaInfo(C.Structure):
                                          "num_allreduces")]
     CHOLESKY_PATHS = {0: "tiled band (k_chol_tiles)", 1: "LDS window (k_cholesky_window)",
                       2: "global memory (k_cholesky_global, LDS-staged panel rows)",
-                      3: "global memory (k_cholesky_global, unstaged)"}
+                      3: "global memory (k_cholesky_global, unstaged)",
+                      4: "bordered band (k_chol_tiles on the frames, k_chol_border for the intrinsics)"}
 
     def as_dict(self):
         d = {n: getattr(self, n) for n, _ in self._fields_}

@@ -543,16 +543,20 @@ def test_solver_variants_match_default(gpu_lib, monkeypatch, env):
     np.testing.assert_allclose(p1.t, p0.t, rtol=0, atol=1e-6)
 
 
-@pytest.mark.parametrize("stage", ["1", "0"], ids=["staged", "unstaged"])
-def test_free_intrinsics_c2_global_cholesky_matches_oracle(gpu_lib, oracle_lib, monkeypatch, stage):
+@pytest.mark.parametrize("path", ["border", "staged", "unstaged"])
+def test_free_intrinsics_c2_global_cholesky_matches_oracle(gpu_lib, oracle_lib, monkeypatch, path):
     """SolveAllFrames(C2 map, 2.0, true) (slam.cpp:447-480) at the size where the free-intrinsics path runs its
-    global-memory pieces: n = 314 > kCholWS, so S (dense through the 14 intrinsics columns) is factored by
-    k_cholesky_global (arrowhead trailing update, MFMA tiles; with and without the LDS-staged panel rows,
-    SG_CHOL_GSTAGE=0), and 48 free frame blocks > kIntrWin = 32, so k_intr_lin / k_intr_schur take their
-    out-of-window global-atomic branches.  Three LM iterations against the oracle's dense solve: the same
+    global-memory pieces: n = 314 > kCholWS, S is an arrowhead (the frame band, dense through the 14 intrinsics
+    columns), and 48 free frame blocks > kIntrWin = 32, so k_intr_lin / k_intr_schur take their out-of-window
+    global-atomic branches.  The default factors it as a bordered band (k_chol_tiles on the 19 frame tile rows,
+    k_chol_border for the intrinsics: forward chain, 14 x 14 Schur complement, band back substitution);
+    SG_CHOL_BORDER=0 takes k_cholesky_global (arrowhead trailing update, MFMA tiles; with and without the
+    LDS-staged panel rows, SG_CHOL_GSTAGE=0).  Three LM iterations against the oracle's dense solve: the same
     steps, cost to 1e-8 relative, intrinsics to 1e-7, translations to 1e-5 mm."""
     import os
-    monkeypatch.setenv("SG_CHOL_GSTAGE", stage)
+    if path != "border":
+        monkeypatch.setenv("SG_CHOL_BORDER", "0")
+        monkeypatch.setenv("SG_CHOL_GSTAGE", "1" if path == "staged" else "0")
     m = make_config("C2")
     for c in range(len(m.k) // 7):
         k = m.k[7 * c:7 * c + 7]
@@ -565,7 +569,7 @@ def test_free_intrinsics_c2_global_cholesky_matches_oracle(gpu_lib, oracle_lib, 
     g.load(pg)
     info = g.info()
     assert info["n"] > 128 and info["num_blocks"] > 32
-    assert info["cholesky_path"] == (2 if stage == "1" else 3), info
+    assert info["cholesky_path"] == {"border": 4, "staged": 2, "unstaged": 3}[path], info
     o = default_solver_options(max_num_iterations=3)
     sg = g.solve(o)
     so = oracle_lib.solve(po, o, nthreads=min(16, os.cpu_count() or 1))
