@@ -249,7 +249,7 @@ struct Dev {
   double* KU;                    // [n][nk] intrinsics columns of J^T J, unscaled (frame rows, then the k block)
   double* kst;                   // [ncam][56] CameraStabilization corrected residual (7) and Jacobian (7x7)
   double* Yk;                    // [P][ncam][28] W_kp V~p^-1 of each free point (k_intr_schur -> k_intr_fk)
-  double* kpart;                 // [NB + 1][ncam][42] per-block J_k^T J_k / J_k^T r / diagonal partials
+  double* kpart;                 // [(NB + 1) nsl][ncam][42] per-(block, slice) J_k^T J_k / J_k^T r / diagonal partials
   const int32_t* intr_boff;      // [NB + 2] per frame block (then the fixed frames' block NB): observations
   const int32_t* intr_bidx;      //   of non-fixed observations, in observation order
   double stab_b, stab_inv_b;     // CauchyLoss(stab_range): b = stab_range^2

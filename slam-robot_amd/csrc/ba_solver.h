@@ -181,6 +181,7 @@ class BaSolver {
   DBuf<double> Jk_, KU_, kst_;     // free intrinsics (nk_ > 0)
   DBuf<double> Yk_, kpart_;        //   W_kp V~p^-1 per point and camera; per-block camera sums
   DBuf<int32_t> intr_boff_, intr_bidx_;   //   per-block observation lists
+  int intr_nsl_ = 1;                      //   k_intr_fk workgroups per block list
   int nk_ = 0;                     // 7 * cameras when the intrinsics are free
   double stab_b_ = 25.0;
   DBuf<SchurSeg> segs_;

@@ -23,7 +23,6 @@
 #include <chrono>
 #include <string>
 #include <thread>
-#include <exception>
 
 #include <algorithm>
 #include <cfloat>
@@ -81,6 +80,14 @@ __device__ __forceinline__ double wave_sum_full(double v) {
   v += dpp_d<0x140>(v);   // row_mirror: every lane holds its 16-lane row sum
   return (readlane_dd(v, 0) + readlane_dd(v, 16)) + (readlane_dd(v, 32) + readlane_dd(v, 48));
 }
+// The same butterfly for the maximum (fmax is exact, so any order gives the same bits).  All 64 lanes active.
+__device__ __forceinline__ double wave_max_full(double v) {
+  v = fmax(v, dpp_d<0xB1>(v));
+  v = fmax(v, dpp_d<0x4E>(v));
+  v = fmax(v, dpp_d<0x141>(v));
+  v = fmax(v, dpp_d<0x140>(v));
+  return fmax(fmax(readlane_dd(v, 0), readlane_dd(v, 16)), fmax(readlane_dd(v, 32), readlane_dd(v, 48)));
+}
 // LDS-only workgroup barrier: waits for this wave's LDS traffic, not for outstanding global loads or
 // stores (those may stay in flight across it).
 __device__ __forceinline__ void lds_barrier() {
@@ -102,7 +109,7 @@ __device__ __forceinline__ double wave_max(double v) {
 // Block reduction in a fixed order (deterministic).  red: LDS scratch of >= nwaves doubles.
 template <int NT>
 __device__ __forceinline__ double block_sum(double v, double* red) {
-  v = wave_sum(v);
+  v = wave_sum_full(v);   // (every thread of the block calls it: all lanes active)
   __syncthreads();
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
@@ -113,7 +120,7 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
 }
 template <int NT>
 __device__ __forceinline__ double block_max(double v, double* red) {
-  v = wave_max(v);
+  v = wave_max_full(v);
   __syncthreads();
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
@@ -446,7 +453,7 @@ __global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_linearize(Dev d) {
   const double fixed = wave_sum_full(lsum[1][lane]);
   const double ffail = wave_sum_full(lsum[2][lane]);
   const double xn2 = wave_sum_full(lsum[3][lane]);
-  gmax = wave_max(gmax);
+  gmax = wave_max_full(gmax);
   if (lane == 0) {
     double* sc = d.lin_scal[cur] + blockIdx.x;   // structure of arrays: slot j at [j * nlin + chunk]
     const size_t ns = d.nlin;
@@ -1600,11 +1607,14 @@ __global__ __launch_bounds__(256) void k_S_pack(double* S, int n, const int32_t*
 //   k_intr_step (after the solve): candidate intrinsics k+ = k - S x_k, step norms, stabilization
 //     model term and candidate cost.  The observation model terms take A_k x_k in k_point_update.
 
+constexpr int kIntrCamV = 42;   // per camera: upper 7x7 of J_k^T J_k (28), J_k^T r (7), diagonal (7)
+constexpr int kIntrKMax = 7 * kMaxIntrCams;
 __global__ __launch_bounds__(256) void k_intr_zero(Dev d) {
   const LmState* st = d.st;
   if (st->done || !st->need_lin) return;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < d.n * d.nk) d.KU[i] = 0.0;
+  if (i < (d.NB + 1) * d.ncam * kIntrCamV) d.kpart[i] = 0.0;
   if (i < d.nk) {
     d.camg[d.kc0 + i] = 0.0;
     d.camdiag[d.kc0 + i] = 0.0;
@@ -1616,8 +1626,6 @@ __global__ __launch_bounds__(256) void k_intr_zero(Dev d) {
 // gradient, the diagonal) per frame block from the observation lists, without atomics; k_intr_fin adds the
 // per-block partials in block order.  (Per-observation LDS / global atomics on a few hundred shared addresses
 // took 49 us at config 2.)
-constexpr int kIntrCamV = 42;
-constexpr int kIntrKMax = 7 * kMaxIntrCams;
 __global__ __launch_bounds__(256) void k_intr_lin(Dev d) {
   const LmState* st = d.st;
   if (st->done || !st->need_lin) return;
@@ -1644,7 +1652,7 @@ __device__ __forceinline__ void wg_sum_values(const double (&v)[kV], double (*re
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
   for (int e = 0; e < kV; ++e) {
-    const double t = wave_sum(v[e]);
+    const double t = wave_sum_full(v[e]);   // DPP (every lane active here)
     if (lane == 0) red[wave][e] = t;
   }
   __syncthreads();
@@ -1662,17 +1670,20 @@ __device__ __forceinline__ void wg_sum_values(const double (&v)[kV], double (*re
 //     camera c (stored: one writer per entry), and the camera sums of those observations into kpart[b][c];
 //   kMode 1 (after k_intr_schur): S_fk rows of b, columns of c -= sum over the block's observations of free
 //     points of A_c^T (A_p Y_pc^T) (Y_pc = W_kp V~p^-1 of camera c, k_intr_schur).
-constexpr int kIntrFkThreads = 512;
+constexpr int kIntrFkThreads = 256;
 template <int kMode>
-__global__ __launch_bounds__(kIntrFkThreads) void k_intr_fk(Dev d) {
+__global__ __launch_bounds__(kIntrFkThreads) void k_intr_fk(Dev d, int nsl) {
   const LmState* st = d.st;
   if (st->done) return;
   if (kMode == 0 && !st->need_lin) return;
   constexpr int kV = kMode == 0 ? 2 * kIntrCamV : kIntrCamV;
   constexpr int kW = kIntrFkThreads / 64;
   __shared__ double red[kW][kV];
-  const int b = blockIdx.x, c = blockIdx.y, tid = threadIdx.x, cur = st->cur, nk = d.nk, ncam = d.ncam;
-  const int i0 = d.intr_boff[b], i1 = d.intr_boff[b + 1];
+  // workgroup (b, slice sl) of blockIdx.x takes the sl-th part of block b's list
+  const int b = blockIdx.x / nsl, sl = blockIdx.x - b * nsl, c = blockIdx.y, tid = threadIdx.x, cur = st->cur;
+  const int nk = d.nk, ncam = d.ncam;
+  const int l0 = d.intr_boff[b], len = d.intr_boff[b + 1] - l0;
+  const int i0 = l0 + (int)((long long)len * sl / nsl), i1 = l0 + (int)((long long)len * (sl + 1) / nsl);
   double acc[kV];
 #pragma unroll
   for (int e = 0; e < kV; ++e) acc[e] = 0.0;
@@ -1735,17 +1746,18 @@ __global__ __launch_bounds__(kIntrFkThreads) void k_intr_fk(Dev d) {
     }
   }
   wg_sum_values<kW, kV>(acc, red);
+  // the slices of a block add into KU_fk / S_fk (nsl atomics per entry); the camera sums go to their partial slot
   if constexpr (kMode == 0) {
     for (int e = tid; e < kV; e += kIntrFkThreads) {
       if (e < kIntrCamV) {
-        if (b < d.NB) d.KU[(size_t)(6 * b + e / 7) * nk + 7 * c + e % 7] = red[0][e];
+        if (b < d.NB) atomicAdd(d.KU + (size_t)(6 * b + e / 7) * nk + 7 * c + e % 7, red[0][e]);
       } else {
-        d.kpart[((size_t)b * ncam + c) * kIntrCamV + e - kIntrCamV] = red[0][e];
+        atomicAdd(d.kpart + ((size_t)b * ncam + c) * kIntrCamV + e - kIntrCamV, red[0][e]);   // (nsl slices)
       }
     }
   } else {
     for (int e = tid; e < kV; e += kIntrFkThreads)
-      d.S[(size_t)(6 * b + e / 7) * d.n + d.kc0 + 7 * c + e % 7] += red[0][e];
+      atomicAdd(d.S + (size_t)(6 * b + e / 7) * d.n + d.kc0 + 7 * c + e % 7, red[0][e]);
   }
 }
 
@@ -1770,31 +1782,54 @@ __device__ __forceinline__ void stab_residual(const double* k, double* res, doub
 
 // One wave: stabilization terms of every camera (lane = camera), then the cost, |g|_inf of the k columns
 // and |k|^2 into the exchange slots k_cam_finalize reads.
-__global__ __launch_bounds__(64) void k_intr_fin(Dev d) {
+constexpr int kIntrFinThreads = 256;
+__global__ __launch_bounds__(kIntrFinThreads) void k_intr_fin(Dev d, int nsl) {
   LmState* st = d.st;
   if (st->done || !st->need_lin) return;
-  const int lane = threadIdx.x, cur = st->cur, nk = d.nk;
-  // the per-block camera sums (k_intr_fk<0>), in block order
-  for (int e = lane; e < d.ncam * kIntrCamV; e += 64) {
-    const int cam = e / kIntrCamV, v = e - cam * kIntrCamV, kc = 7 * cam;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, cur = st->cur, nk = d.nk;
+  // the per-block camera sums of k_intr_fk<0> (NB + 1 partials per value): h threads per value, each summing
+  // every h-th block, then the h parts in order
+  __shared__ double part[kIntrFinThreads];
+  const int nv = d.ncam * kIntrCamV, h = max(1, kIntrFinThreads / nv), np = d.NB + 1;
+  {
+    const int v = tid / h, hh = tid - v * h;
     double t = 0.0;
-    for (int bb = 0; bb <= d.NB; ++bb) t += d.kpart[((size_t)bb * d.ncam + cam) * kIntrCamV + v];
-    if (v < 28) {
-      int a = 0, u = v;
+    if (v < nv) {
+      const int cam = v / kIntrCamV, e = v - cam * kIntrCamV;
+      for (int q0 = hh; q0 < np; q0 += 8 * h) {
+        double u[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int q = q0 + k * h;
+          u[k] = q < np ? d.kpart[((size_t)q * d.ncam + cam) * kIntrCamV + e] : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) t += u[k];
+      }
+    }
+    part[tid] = t;
+  }
+  __syncthreads();
+  for (int v = tid; v < nv; v += kIntrFinThreads) {
+    const int cam = v / kIntrCamV, e = v - cam * kIntrCamV, kc = 7 * cam;
+    double t = 0.0;
+    for (int hh = 0; hh < h; ++hh) t += part[v * h + hh];
+    if (e < 28) {
+      int a = 0, u = e;
       while (u >= 7 - a) {
         u -= 7 - a;
         ++a;
       }
       d.KU[(size_t)(d.kc0 + kc + a) * nk + kc + a + u] += t;
-    } else if (v < 35) {
-      d.camg[d.kc0 + kc + (v - 28)] += t;
+    } else if (e < 35) {
+      d.camg[d.kc0 + kc + (e - 28)] += t;
     } else {
-      d.camdiag[d.kc0 + kc + (v - 35)] += t;
+      d.camdiag[d.kc0 + kc + (e - 35)] += t;
     }
   }
   __syncthreads();
   double cost = 0.0, xn2 = 0.0;
-  if (lane < d.ncam) {
+  if (tid < d.ncam) {   // (wave 0 from here)
     const double* k = d.k[cur] + 7 * lane;
     double res[7], J[49];
     stab_residual(k, res, J);
@@ -1804,28 +1839,41 @@ __global__ __launch_bounds__(64) void k_intr_fin(Dev d) {
     Cauchy(sq, d.stab_b, d.stab_inv_b, &rho0, &rho1);
     cost = 0.5 * rho0;
     const double sr = sqrt(rho1);
+    // the corrected residual and Jacobian in registers (k_intr_step reads the stored copy)
+    double kr[7], kj[49];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) kr[i] = sr * res[i];
+#pragma unroll
+    for (int i = 0; i < 49; ++i) kj[i] = sr * J[i];
     double* ks = d.kst + 56 * lane;
-    for (int i = 0; i < 7; ++i) ks[i] = sr * res[i];
-    for (int i = 0; i < 49; ++i) ks[7 + i] = sr * J[i];
+#pragma unroll
+    for (int i = 0; i < 7; ++i) ks[i] = kr[i];
+#pragma unroll
+    for (int i = 0; i < 49; ++i) ks[7 + i] = kj[i];
     const int kc = 7 * lane;
     double* Kk = d.KU + (size_t)(d.kc0 + kc) * nk;
+#pragma unroll
     for (int a = 0; a < 7; ++a) {
       double g = 0.0, dg = 0.0;
+#pragma unroll
       for (int i = 0; i < 7; ++i) {
-        g += ks[7 + 7 * i + a] * ks[i];
-        dg += ks[7 + 7 * i + a] * ks[7 + 7 * i + a];
+        g += kj[7 * i + a] * kr[i];
+        dg += kj[7 * i + a] * kj[7 * i + a];
       }
       d.camg[d.kc0 + kc + a] += g;
       d.camdiag[d.kc0 + kc + a] += dg;
+#pragma unroll
       for (int j = a; j < 7; ++j) {
         double v = 0.0;
-        for (int i = 0; i < 7; ++i) v += ks[7 + 7 * i + a] * ks[7 + 7 * i + j];
+#pragma unroll
+        for (int i = 0; i < 7; ++i) v += kj[7 * i + a] * kj[7 * i + j];
         Kk[(size_t)a * nk + kc + j] += v;
       }
     }
     for (int i = 0; i < 7; ++i) xn2 += k[i] * k[i];
   }
   __syncthreads();
+  if (wave != 0) return;
   double gm = 0.0;
   for (int i = lane; i < nk; i += 64) gm = fmax(gm, fabs(d.camg[d.kc0 + i]));
   gm = wave_max(gm);
@@ -1898,8 +1946,10 @@ __device__ __forceinline__ void intr_schur_point(const Dev& d, int p, bool act, 
   for (int i = 0; i < 10; ++i) Vi[i] = d.Vinv[10 * (size_t)p + i];
   const double4 t4 = reinterpret_cast<const double4*>(d.tp)[p];
   const double tpv[4] = {t4.x, t4.y, t4.z, t4.w};
-  // W of camera c (7x4, row-major), accumulated over the point's observations of that camera
-  auto build_W = [&](int c, double* W) -> bool {
+  // W of camera c (7x4, row-major), accumulated over the point's observations of that camera (one walk per
+  // camera; loops unrolled so W, Y stay in registers)
+  auto build_W = [&](int c, double (&W)[28]) -> bool {
+#pragma unroll
     for (int i = 0; i < 28; ++i) W[i] = 0.0;
     bool any = false;
     for (int o = o0; o < o1; ++o) {
@@ -1908,13 +1958,16 @@ __device__ __forceinline__ void intr_schur_point(const Dev& d, int p, bool act, 
       any = true;
       const double* Jk = d.Jk + 14 * (size_t)o;
       double Jr[8];   // corrected Jp (2x4)
+#pragma unroll
       for (int i = 0; i < 4; ++i) {
         const double2 v = jload2(d.J[d.st->cur], o, 7 + i);
         Jr[2 * i] = v.x;
         Jr[2 * i + 1] = v.y;
       }
+#pragma unroll
       for (int j = 0; j < 7; ++j) {
         const double k0 = Jk[j] * d.scale_c[d.kc0 + 7 * c + j], k1 = Jk[7 + j] * d.scale_c[d.kc0 + 7 * c + j];
+#pragma unroll
         for (int a = 0; a < 4; ++a) W[4 * j + a] += (k0 * Jr[a] + k1 * Jr[4 + a]) * sp[a];
       }
     }
@@ -1923,10 +1976,13 @@ __device__ __forceinline__ void intr_schur_point(const Dev& d, int p, bool act, 
   for (int c = 0; c < d.ncam; ++c) {
     double W[28], Y[28];
     const bool has = build_W(c, W);
+#pragma unroll
     for (int j = 0; j < 7; ++j) {
       double r = 0.0;
+#pragma unroll
       for (int a = 0; a < 4; ++a) {
         double y = 0.0;
+#pragma unroll
         for (int e = 0; e < 4; ++e) y += W[4 * j + e] * sym4(Vi, e, a);
         Y[4 * j + a] = has ? y : 0.0;   // (a lane without observations of c adds exact zeros)
         r += W[4 * j + a] * tpv[a];
@@ -1934,25 +1990,38 @@ __device__ __forceinline__ void intr_schur_point(const Dev& d, int p, bool act, 
       const double rs = wave_sum_full(has ? -r : 0.0);
       if (lane0) atomicAdd(sxk + 7 * c + j, rs);
     }
-    // S_kk blocks (c, c2 >= c), upper triangle
-    for (int c2 = c; c2 < d.ncam; ++c2) {
-      double W2[28];
-      if (c2 == c) {
-        for (int i = 0; i < 28; ++i) W2[i] = W[i];
-      } else {
-        build_W(c2, W2);
+    // S_kk block (c, c), upper triangle
+#pragma unroll
+    for (int j = 0; j < 7; ++j)
+#pragma unroll
+      for (int j2 = j; j2 < 7; ++j2) {
+        double v = 0.0;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) v += Y[4 * j + a] * W[4 * j2 + a];
+        const double vs = wave_sum_full(-v);
+        if (lane0) atomicAdd(skk + (7 * c + j) * kIntrKMax + 7 * c + j2, vs);
       }
+    // blocks (c', c) of the earlier cameras: Y_c' (this lane's own store below, read back) W_c^T
+    for (int c1 = 0; c1 < c; ++c1) {
+      double Y1[28];
+      const double* Yi = d.Yk + ((size_t)p * d.ncam + c1) * 28;
+#pragma unroll
+      for (int i = 0; i < 28; ++i) Y1[i] = act ? Yi[i] : 0.0;
+#pragma unroll
       for (int j = 0; j < 7; ++j)
-        for (int j2 = (c2 == c ? j : 0); j2 < 7; ++j2) {
+#pragma unroll
+        for (int j2 = 0; j2 < 7; ++j2) {
           double v = 0.0;
-          for (int a = 0; a < 4; ++a) v += Y[4 * j + a] * W2[4 * j2 + a];
+#pragma unroll
+          for (int a = 0; a < 4; ++a) v += Y1[4 * j + a] * W[4 * j2 + a];
           const double vs = wave_sum_full(-v);
-          if (lane0) atomicAdd(skk + (7 * c + j) * kIntrKMax + 7 * c2 + j2, vs);
+          if (lane0) atomicAdd(skk + (7 * c1 + j) * kIntrKMax + 7 * c + j2, vs);
         }
     }
-    // Y_pc for the S_fk terms of the point's observations (k_intr_fk<1>)
+    // Y_pc for the S_fk terms of the point's observations (k_intr_fk<1>) and the later cameras' blocks
     if (act) {
       double* Yo = d.Yk + ((size_t)p * d.ncam + c) * 28;
+#pragma unroll
       for (int i = 0; i < 28; ++i) Yo[i] = Y[i];
     }
   }
@@ -4158,7 +4227,7 @@ __global__ __launch_bounds__(kBordThreads) void k_chol_border(Dev d, double* __r
     }
 #pragma unroll
     for (int c = 0; c < kCholNb; ++c) {
-      const double v = wave_sum(part[c]);
+      const double v = wave_sum_full(part[c]);
       if (lane == 0) rpart[wave - 1][c] = v;
     }
     if (cand_lds) cand_prefetch(d, cl, st->cur, tid - 64, kOt);
@@ -4638,7 +4707,7 @@ __global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_update_lin(Dev d) {
   cost = wave_sum_full(cost);
   const double fail = wave_sum_full(lsum[0][lane]);
   const double ffail = wave_sum_full(lsum[1][lane]);
-  gmax = wave_max(gmax);
+  gmax = wave_max_full(gmax);
   if (lane == 0) {
     double* sc = d.lin_scal[nxt] + blockIdx.x;   // k_linearize's scalars of the candidate (never iteration 0)
     const size_t ns = d.nlin;
@@ -5274,167 +5343,12 @@ void BaSolver::Load(const sg_problem& p) {
   // Schur work lists (see SchurSeg): the cells of every free point (one per block of its span, with the
   // point's observations in that block), segments of consecutive points whose columns fit kSchurTW tiles of
   // S, their batches, and each wide point's observation pairs (s <= t, both on free frames).
-  // They run on a second host thread while this one builds the sweep lists: both read the same inputs and their
-  // outputs are disjoint (members: npairs_, schur_mfma_, nseg_, nwide_ there; nlin_, npu_ here).
   std::vector<int32_t> pinfo(2 * (size_t)std::max(P_, 1), 0), pmx(4 * (size_t)std::max(P_, 1), 0), cells, cell_obs;
   std::vector<SchurSeg> segs;
   std::vector<SchurBatch> sbatch;
   std::vector<WideSeg> wsegs;
   std::vector<int32_t> pairs_flat;   // int2 per pair (wide points)
   int s_off = 0;
-  auto build_schur_lists = [&] {
-    std::vector<int32_t> obs_blk(M_);
-    for (int o = 0; o < M_; ++o) obs_blk[o] = frame_block[obs_frame[o]];
-    // span in blocks of a free point's Schur terms (0: none)
-    auto sspan = [&](int i) {
-      const int pt = point_perm_[i];
-      return (pfree[i] && pfirst[pt] < NB_) ? plast[pt] - pfirst[pt] + 1 : 0;
-    };
-    std::vector<int32_t> simple_obs(std::max(P_, 1), -1);   // observation of the first block if one per block
-    int ncell = 0;
-    npairs_ = 0;
-    schur_mfma_ = 0.0;
-    {
-      std::vector<std::pair<int, int>> bo;
-      cells.reserve(4 * (size_t)M_ + 4);
-      cell_obs.reserve((size_t)M_ / 4 + 1);
-      for (int i = 0; i < P_; ++i) {
-        size_t kb = 0;
-        for (int o = poff[i]; o < poff[i + 1]; ++o) kb += obs_blk[o] >= 0;
-        if (pfree[i]) npairs_ += kb * (kb + 1) / 2;
-        const int sp = sspan(i);
-        if (sp == 0 || sp > kSegNbMax) continue;
-        const int pf = pfirst[point_perm_[i]];
-        pinfo[2 * i] = (int)(cells.size() / 4);
-        pinfo[2 * i + 1] = (pf << 8) | sp;
-        bo.clear();
-        for (int o = poff[i]; o < poff[i + 1]; ++o)
-          if (obs_blk[o] >= 0) bo.emplace_back(obs_blk[o], o);
-        if (!std::is_sorted(bo.begin(), bo.end())) std::sort(bo.begin(), bo.end());   // sorted at load already
-        {
-          bool one = (int)bo.size() == sp;   // observations sorted by block at load: consecutive
-          for (int q = 0; one && q < sp; ++q) one = bo[q].first == pf + q && bo[q].second == bo[0].second + q;
-          if (one) simple_obs[i] = bo[0].second;
-        }
-        size_t k = 0;
-        for (int b = pf; b < pf + sp; ++b) {
-          // {first observation or -1, point, (block << 16) | further observations, their offset in cell_obs}
-          int o0 = -1;
-          if (k < bo.size() && bo[k].first == b) o0 = bo[k++].second;
-          const int k1 = (int)cell_obs.size();
-          while (k < bo.size() && bo[k].first == b) cell_obs.push_back(bo[k++].second);
-          cells.insert(cells.end(), {o0, i, (int)(((unsigned)b << 16) | (unsigned)(cell_obs.size() - k1)), k1});
-        }
-      }
-      ncell = (int)cells.size() / 4;
-      if (cells.empty()) cells.assign(4, 0);
-      if (cell_obs.empty()) cell_obs.push_back(0);
-    }
-    {
-      // points per segment: one segment per CU (the workgroup's LDS holds one per CU; fewer, longer segments
-      // write fewer partial tiles and keep the producer/consumer pipeline full; SG_SCHUR_SEGS: tuning)
-      const int ncu = ncu_;
-      // (with k_schur beside the camera reduction, one CU per XCD stays free for k_cam_reduce / k_cam_finalize:
-      // a k_schur workgroup's 140 KB of LDS leaves no room for them on its CU)
-      const int target = getenv("SG_SCHUR_SEGS") ? std::max(1, atoi(getenv("SG_SCHUR_SEGS")))
-                                                 : (overlap_ok_ ? std::max(1, ncu - 8) : ncu);
-      const int maxpts = std::max(16, (P_ + target - 1) / target);
-      int cnext = 0;
-      for (int i = 0; i < P_;) {
-        if (sspan(i) > kSegNbMax) {
-          WideSeg w{};
-          w.p = i;
-          w.pair_lo = (int)pairs_flat.size() / 2;
-          for (int os = poff[i]; os < poff[i + 1]; ++os) {
-            if (obs_blk[os] < 0) continue;
-            for (int ot = os; ot < poff[i + 1]; ++ot) {
-              if (obs_blk[ot] < 0) continue;
-              pairs_flat.push_back(((os - poff[i]) << 16) | (ot - poff[i]));
-              pairs_flat.push_back((obs_blk[os] << 16) | obs_blk[ot]);
-            }
-          }
-          w.pair_hi = (int)pairs_flat.size() / 2;
-          wsegs.push_back(w);
-          ++i;
-          continue;
-        }
-        SchurSeg sg{};
-        sg.p0 = i;
-        int clo = INT32_MAX, chi = -1, blo = INT32_MAX, bhi = -1;   // columns [clo, chi), blocks [blo, bhi]
-        int j = i;
-        while (j < P_ && j - i < maxpts) {
-          const int sp = sspan(j);
-          if (sp > kSegNbMax) break;
-          if (sp > 0) {
-            const int pf = pfirst[point_perm_[j]];
-            const int l2 = std::min(clo, 6 * pf), h2 = std::max(chi, 6 * (pf + sp));
-            if ((h2 + 15) / 16 - l2 / 16 > kSchurTW) break;
-            clo = l2;
-            chi = h2;
-            blo = std::min(blo, pf);
-            bhi = std::max(bhi, pf + sp - 1);
-          }
-          ++j;
-        }
-        sg.p1 = j;
-        if (chi >= 0) {
-          sg.t0 = clo / 16;
-          sg.ntw = (chi + 15) / 16 - sg.t0;
-          sg.b_lo = blo;
-          sg.nb = bhi - blo + 1;
-        }
-        sg.s_off = s_off;
-        s_off += sg.ntw * (sg.ntw + 1) / 2 * 256 + 16 * sg.ntw;
-        // last window tile of each point's columns (-1: no Schur terms)
-        auto pjhi = [&](int k) {
-          const int sp = sspan(k);
-          return sp == 0 ? -1 : (6 * (pfirst[point_perm_[k]] + sp) - 1 - 16 * sg.t0) / 16;
-        };
-        sg.bt0 = (int)sbatch.size();
-        for (int k = i; k < j;) {
-          SchurBatch B{};
-          B.p0 = k;
-          B.c0 = cnext;
-          int nc = 0, nx = 0;
-          while (k < j && k - B.p0 < kSchurBatchPts && nx + 64 * (pjhi(k) + 1) <= kSchurXCap &&
-                 nc + sspan(k) <= 64 * kSchurCellWaves) {
-            pmx[4 * k] = nx;
-            pmx[4 * k + 1] = pjhi(k);
-            pmx[4 * k + 2] = simple_obs[k];
-            pmx[4 * k + 3] = nc;
-            nx += 64 * (pjhi(k) + 1);
-            schur_mfma_ += schur_aug_base(pjhi(k) + 1);
-            nc += sspan(k++);
-          }
-          B.p1 = k;
-          B.c1 = B.c0 + nc;
-          cnext += nc;
-          sbatch.push_back(B);
-        }
-        sg.bt1 = (int)sbatch.size();
-        segs.push_back(sg);
-        i = j;
-      }
-      SG_REQUIRE(cnext == ncell, SG_EINVAL, "Schur cells out of step with the batches");
-    }
-    nseg_ = (int)segs.size();
-    nwide_ = (int)wsegs.size();
-    if (pairs_flat.empty()) pairs_flat.assign(2, 0);
-  };
-  std::exception_ptr schur_err;
-  std::thread schur_thr([&] {
-    try {
-      build_schur_lists();
-    } catch (...) {
-      schur_err = std::current_exception();
-    }
-  });
-  struct Joiner {
-    std::thread& t;
-    ~Joiner() {
-      if (t.joinable()) t.join();
-    }
-  } schur_join{schur_thr};
   // k_linearize decomposition (see LinChunk): rounds of whole points (<= kLinObs observations), up to
   // maxr rounds per chunk sharing one camera window; fewer rounds per chunk on small problems so that the
   // grid still fills the chip.
@@ -5527,8 +5441,143 @@ void BaSolver::Load(const sg_problem& p) {
   npu_ = (int)pu_units.size();
   if (pu_units.empty()) pu_units.push_back(0);
   lap("lin-lists");
-  schur_thr.join();
-  if (schur_err) std::rethrow_exception(schur_err);
+  std::vector<int32_t> obs_blk(M_);
+  for (int o = 0; o < M_; ++o) obs_blk[o] = frame_block[obs_frame[o]];
+  // span in blocks of a free point's Schur terms (0: none)
+  auto sspan = [&](int i) {
+    const int pt = point_perm_[i];
+    return (pfree[i] && pfirst[pt] < NB_) ? plast[pt] - pfirst[pt] + 1 : 0;
+  };
+  std::vector<int32_t> simple_obs(std::max(P_, 1), -1);   // observation of the first block if one per block
+  int ncell = 0;
+  npairs_ = 0;
+  schur_mfma_ = 0.0;
+  {
+    std::vector<std::pair<int, int>> bo;
+    cells.reserve(4 * (size_t)M_ + 4);
+    cell_obs.reserve((size_t)M_ / 4 + 1);
+    for (int i = 0; i < P_; ++i) {
+      size_t kb = 0;
+      for (int o = poff[i]; o < poff[i + 1]; ++o) kb += obs_blk[o] >= 0;
+      if (pfree[i]) npairs_ += kb * (kb + 1) / 2;
+      const int sp = sspan(i);
+      if (sp == 0 || sp > kSegNbMax) continue;
+      const int pf = pfirst[point_perm_[i]];
+      pinfo[2 * i] = (int)(cells.size() / 4);
+      pinfo[2 * i + 1] = (pf << 8) | sp;
+      bo.clear();
+      for (int o = poff[i]; o < poff[i + 1]; ++o)
+        if (obs_blk[o] >= 0) bo.emplace_back(obs_blk[o], o);
+      if (!std::is_sorted(bo.begin(), bo.end())) std::sort(bo.begin(), bo.end());   // sorted at load already
+      {
+        bool one = (int)bo.size() == sp;   // observations sorted by block at load: consecutive
+        for (int q = 0; one && q < sp; ++q) one = bo[q].first == pf + q && bo[q].second == bo[0].second + q;
+        if (one) simple_obs[i] = bo[0].second;
+      }
+      size_t k = 0;
+      for (int b = pf; b < pf + sp; ++b) {
+        // {first observation or -1, point, (block << 16) | further observations, their offset in cell_obs}
+        int o0 = -1;
+        if (k < bo.size() && bo[k].first == b) o0 = bo[k++].second;
+        const int k1 = (int)cell_obs.size();
+        while (k < bo.size() && bo[k].first == b) cell_obs.push_back(bo[k++].second);
+        cells.insert(cells.end(), {o0, i, (int)(((unsigned)b << 16) | (unsigned)(cell_obs.size() - k1)), k1});
+      }
+    }
+    ncell = (int)cells.size() / 4;
+    if (cells.empty()) cells.assign(4, 0);
+    if (cell_obs.empty()) cell_obs.push_back(0);
+  }
+  {
+    // points per segment: one segment per CU (the workgroup's LDS holds one per CU; fewer, longer segments
+    // write fewer partial tiles and keep the producer/consumer pipeline full; SG_SCHUR_SEGS: tuning)
+    const int ncu = ncu_;
+    // (with k_schur beside the camera reduction, one CU per XCD stays free for k_cam_reduce / k_cam_finalize:
+    // a k_schur workgroup's 140 KB of LDS leaves no room for them on its CU)
+    const int target = getenv("SG_SCHUR_SEGS") ? std::max(1, atoi(getenv("SG_SCHUR_SEGS")))
+                                               : (overlap_ok_ ? std::max(1, ncu - 8) : ncu);
+    const int maxpts = std::max(16, (P_ + target - 1) / target);
+    int cnext = 0;
+    for (int i = 0; i < P_;) {
+      if (sspan(i) > kSegNbMax) {
+        WideSeg w{};
+        w.p = i;
+        w.pair_lo = (int)pairs_flat.size() / 2;
+        for (int os = poff[i]; os < poff[i + 1]; ++os) {
+          if (obs_blk[os] < 0) continue;
+          for (int ot = os; ot < poff[i + 1]; ++ot) {
+            if (obs_blk[ot] < 0) continue;
+            pairs_flat.push_back(((os - poff[i]) << 16) | (ot - poff[i]));
+            pairs_flat.push_back((obs_blk[os] << 16) | obs_blk[ot]);
+          }
+        }
+        w.pair_hi = (int)pairs_flat.size() / 2;
+        wsegs.push_back(w);
+        ++i;
+        continue;
+      }
+      SchurSeg sg{};
+      sg.p0 = i;
+      int clo = INT32_MAX, chi = -1, blo = INT32_MAX, bhi = -1;   // columns [clo, chi), blocks [blo, bhi]
+      int j = i;
+      while (j < P_ && j - i < maxpts) {
+        const int sp = sspan(j);
+        if (sp > kSegNbMax) break;
+        if (sp > 0) {
+          const int pf = pfirst[point_perm_[j]];
+          const int l2 = std::min(clo, 6 * pf), h2 = std::max(chi, 6 * (pf + sp));
+          if ((h2 + 15) / 16 - l2 / 16 > kSchurTW) break;
+          clo = l2;
+          chi = h2;
+          blo = std::min(blo, pf);
+          bhi = std::max(bhi, pf + sp - 1);
+        }
+        ++j;
+      }
+      sg.p1 = j;
+      if (chi >= 0) {
+        sg.t0 = clo / 16;
+        sg.ntw = (chi + 15) / 16 - sg.t0;
+        sg.b_lo = blo;
+        sg.nb = bhi - blo + 1;
+      }
+      sg.s_off = s_off;
+      s_off += sg.ntw * (sg.ntw + 1) / 2 * 256 + 16 * sg.ntw;
+      // last window tile of each point's columns (-1: no Schur terms)
+      auto pjhi = [&](int k) {
+        const int sp = sspan(k);
+        return sp == 0 ? -1 : (6 * (pfirst[point_perm_[k]] + sp) - 1 - 16 * sg.t0) / 16;
+      };
+      sg.bt0 = (int)sbatch.size();
+      for (int k = i; k < j;) {
+        SchurBatch B{};
+        B.p0 = k;
+        B.c0 = cnext;
+        int nc = 0, nx = 0;
+        while (k < j && k - B.p0 < kSchurBatchPts && nx + 64 * (pjhi(k) + 1) <= kSchurXCap &&
+               nc + sspan(k) <= 64 * kSchurCellWaves) {
+          pmx[4 * k] = nx;
+          pmx[4 * k + 1] = pjhi(k);
+          pmx[4 * k + 2] = simple_obs[k];
+          pmx[4 * k + 3] = nc;
+          nx += 64 * (pjhi(k) + 1);
+          schur_mfma_ += schur_aug_base(pjhi(k) + 1);
+          nc += sspan(k++);
+        }
+        B.p1 = k;
+        B.c1 = B.c0 + nc;
+        cnext += nc;
+        sbatch.push_back(B);
+      }
+      sg.bt1 = (int)sbatch.size();
+      segs.push_back(sg);
+      i = j;
+    }
+    SG_REQUIRE(cnext == ncell, SG_EINVAL, "Schur cells out of step with the batches");
+  }
+  nseg_ = (int)segs.size();
+  nwide_ = (int)wsegs.size();
+  if (pairs_flat.empty()) pairs_flat.assign(2, 0);
   lap("segments");
   // deterministic reduction lists: for every camera block, the slab offsets of the chunk partials that cover
   // it (fixed chunk order), and of the segments' rhs partials
@@ -5792,6 +5841,10 @@ void BaSolver::Load(const sg_problem& p) {
       }
     stg.Add(intr_boff_, boff);
     stg.Add(intr_bidx_, bidx);
+    // slices per block list: about one observation per thread of a k_intr_fk workgroup
+    int lmax = 1;
+    for (int b = 0; b <= NB_; ++b) lmax = std::max(lmax, boff[b + 1] - boff[b]);
+    intr_nsl_ = std::max(1, std::min(32, (lmax + kIntrFkThreads - 1) / kIntrFkThreads));
   }
   if (host_timing) DevMark(s, 1);
   stg.Flush(s);
@@ -6360,10 +6413,12 @@ void BaSolver::EnqueueIterations(int n) {
     }
     if (!merged) AllReduceSum(xchg_cam_.ptr, (size_t)nv + kXNum + nranks());
     if (nk_) {
-      hipLaunchKernelGGL(k_intr_zero, dim3((n_ * nk_ + 255) / 256), dim3(256), 0, stream_, d);
+      hipLaunchKernelGGL(k_intr_zero, dim3((std::max(n_ * nk_, (NB_ + 1) * ncam_ * 42) + 255) / 256), dim3(256), 0,
+                         stream_, d);
       hipLaunchKernelGGL(k_intr_lin, dim3((std::max(M_, 1) + 255) / 256), dim3(256), 0, stream_, d);
-      hipLaunchKernelGGL(k_intr_fk<0>, dim3(NB_ + 1, ncam_), dim3(kIntrFkThreads), 0, stream_, d);
-      hipLaunchKernelGGL(k_intr_fin, dim3(1), dim3(64), 0, stream_, d);
+      hipLaunchKernelGGL(k_intr_fk<0>, dim3((NB_ + 1) * intr_nsl_, ncam_), dim3(kIntrFkThreads), 0, stream_, d,
+                         intr_nsl_);
+      hipLaunchKernelGGL(k_intr_fin, dim3(1), dim3(kIntrFinThreads), 0, stream_, d, intr_nsl_);
     }
     if (!fin_in_schur) {
       TimedLaunchBegin(kKCamFinal);
@@ -6387,7 +6442,8 @@ void BaSolver::EnqueueIterations(int n) {
     if (nk_) {
       hipLaunchKernelGGL(k_intr_assemble, dim3((n_ * nk_ + 255) / 256), dim3(256), 0, stream_, d);
       hipLaunchKernelGGL(k_intr_schur, dim3((std::max(P_, 1) + 127) / 128), dim3(128), 0, stream_, d);
-      if (NB_ > 0) hipLaunchKernelGGL(k_intr_fk<1>, dim3(NB_, ncam_), dim3(kIntrFkThreads), 0, stream_, d);
+      if (NB_ > 0)
+        hipLaunchKernelGGL(k_intr_fk<1>, dim3(NB_ * intr_nsl_, ncam_), dim3(kIntrFkThreads), 0, stream_, d, intr_nsl_);
     }
     if (multi_x || pack_force_ || merged) {
       // the band of S and the rhs partial are summed over landmark shards (packed: the band only), with the
