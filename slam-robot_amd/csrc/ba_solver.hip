@@ -906,11 +906,12 @@ __device__ __forceinline__ void cam_finalize_body(const Dev& d, int mode, int de
     for (int f = tid; act && f < d.F; f += 256) {
       const int b = d.frame_block[f];
       if (b < 0) continue;
-      const double* cg = n_lds ? gsh : d.camg;
+      // (the value is selected, not the pointer: an LDS-or-global pointer compiles to flat accesses)
+      auto cg = [&](int i) { return n_lds ? gsh[i] : d.camg[i]; };
       if (d.rot_free[f])
-        for (int a = 0; a < 3; ++a) gm = fmax(gm, fabs(cg[6 * b + a]));
+        for (int a = 0; a < 3; ++a) gm = fmax(gm, fabs(cg(6 * b + a)));
       if (d.trans_free[f])
-        for (int a = 3; a < 6; ++a) gm = fmax(gm, fabs(cg[6 * b + a]));
+        for (int a = 3; a < 6; ++a) gm = fmax(gm, fabs(cg(6 * b + a)));
       if (first) {
         if (d.rot_free[f])
           for (int a = 0; a < 4; ++a) xn2c += d.q[cur][4 * f + a] * d.q[cur][4 * f + a];
@@ -4104,6 +4105,7 @@ static inline size_t border_lds_doubles(int NT, int flags, int F, int D, int n) 
   if (flags & 2) o += (CandLds::bytes(F, D, n) + 7) / 8;
   return o;
 }
+template <bool kQlds>   // (flags bit 0 as a template parameter: a run-time choice of LDS or global compiles to flat accesses)
 __global__ __launch_bounds__(kBordThreads) void k_chol_border(Dev d, double* __restrict__ Wg, int flags) {
   const LmState* st = d.st;
   if (st->done) return;
@@ -4115,9 +4117,12 @@ __global__ __launch_bounds__(kBordThreads) void k_chol_border(Dev d, double* __r
   double* zq = bdyn + 16 * NT;                         // [16 NT] q_K x_k
   int* rdone = reinterpret_cast<int*>(bdyn + 32 * NT);   // [NT] bs_chain2 row flags
   size_t off = 32 * (size_t)NT + (NT + 1) / 2;
-  // q_K tiles (acc layout): LDS, or the dissected bottom's W space
-  double* Q = (flags & 1) ? bdyn + off : Wg + (size_t)NT * kTB * 256;
-  if (flags & 1) off += 256 * (size_t)NT;
+  // q_K tiles (acc layout): LDS, or the dissected bottom's W space.  Two pointers and a uniform branch at each
+  // use, never one pointer that may be either (that compiles to flat accesses, which wait on both counters)
+  constexpr bool qlds = kQlds;
+  double* Ql = bdyn + off;
+  double* Qg = Wg + (size_t)NT * kTB * 256;
+  if (qlds) off += 256 * (size_t)NT;
   CandLds cl;
   cl.carve(bdyn + off, d.F, d.D, n);
   const double* S = d.S;
@@ -4196,7 +4201,10 @@ __global__ __launch_bounds__(kBordThreads) void k_chol_border(Dev d, double* __r
       C = mfma_f64_k16(wn, w, C);
       const f64x4 qv = mfma_f64_k16(o.zb, w, zero);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) Q[(size_t)K * 256 + q * 64 + lane] = qv[q];
+      for (int q = 0; q < 4; ++q) {
+        if constexpr (qlds) Ql[(size_t)K * 256 + q * 64 + lane] = qv[q];
+        else Qg[(size_t)K * 256 + q * 64 + lane] = qv[q];
+      }
 #pragma unroll
       for (int dd = kTB - 2; dd >= 1; --dd) vr[dd] = vr[dd - 1];
       vr[0] = v;
@@ -4277,10 +4285,15 @@ __global__ __launch_bounds__(kBordThreads) void k_chol_border(Dev d, double* __r
   // (3) z'_K = q_K x_k, then t = U^-1 (w x_k)
   for (int i = tid; i < 16 * NT; i += kBordThreads) {
     const int K = i >> 4, r = i & 15;
-    const double* qk = Q + (size_t)K * 256 + (r >> 2) * 64 + (r & 3) * 16;
+    const size_t qo = (size_t)K * 256 + (r >> 2) * 64 + (r & 3) * 16;
     double acc = 0.0;
+    if constexpr (qlds) {
 #pragma unroll
-    for (int c = 0; c < kCholNb; ++c) acc = fma(qk[c], xk[c], acc);   // (columns >= nk: zero in q and x_k)
+      for (int c = 0; c < kCholNb; ++c) acc = fma(Ql[qo + c], xk[c], acc);   // (columns >= nk: zero in q and x_k)
+    } else {
+#pragma unroll
+      for (int c = 0; c < kCholNb; ++c) acc = fma(Qg[qo + c], xk[c], acc);
+    }
     zq[i] = acc;
   }
   if (d.stamps && tid == 0) bstamp(2);
@@ -5007,7 +5020,7 @@ void BaSolver::LaunchCholTiles(bool stamp, int la, dim3 grid, const Dev& d, int 
   SG_HIP_CHECK(hipLaunchKernel(f, grid, dim3(kTileThreads), args, tile_lds_, stream_));
   if (chol_border_) {
     const int ntf = (6 * NB_ + kCholNb - 1) / kCholNb;
-    hipLaunchKernelGGL(k_chol_border, dim3(1), dim3(kBordThreads),
+    hipLaunchKernelGGL((border_flags_ & 1) ? k_chol_border<true> : k_chol_border<false>, dim3(1), dim3(kBordThreads),
                        border_lds_doubles(ntf, border_flags_, F_, D_, n_) * sizeof(double), stream_, d, Wg_.ptr,
                        border_flags_);
   }
@@ -5067,13 +5080,16 @@ BaSolver::BaSolver(const sg_device_options& dev) : dev_(dev) {
     gchol_lds_max_ = (size_t)160 * 1024 - ga.sharedSizeBytes;
     for (const void* f : {(const void*)k_cholesky_global<true>, (const void*)k_cholesky_global<false>})
       SG_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)gchol_lds_max_));
-    hipFuncAttributes ba;
-    SG_HIP_CHECK(hipFuncGetAttributes(&ba, (const void*)k_chol_border));
-    border_lds_max_ = (size_t)160 * 1024 - ba.sharedSizeBytes;
+    border_lds_max_ = (size_t)160 * 1024;
+    for (const void* f : {(const void*)k_chol_border<true>, (const void*)k_chol_border<false>}) {
+      hipFuncAttributes ba;
+      SG_HIP_CHECK(hipFuncGetAttributes(&ba, f));
+      border_lds_max_ = std::min(border_lds_max_, (size_t)160 * 1024 - ba.sharedSizeBytes);
+    }
     SG_REQUIRE(border_lds_doubles(kTileMaxNT, 0, 0, 0, 0) * sizeof(double) <= border_lds_max_, SG_EINVAL,
                "k_chol_border: LDS for kTileMaxNT rows");
-    SG_HIP_CHECK(hipFuncSetAttribute((const void*)k_chol_border, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)border_lds_max_));
+    for (const void* f : {(const void*)k_chol_border<true>, (const void*)k_chol_border<false>})
+      SG_HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)border_lds_max_));
   }
   st_.Resize(1);
   timers_.resize(kKNum);
