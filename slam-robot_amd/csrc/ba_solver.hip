@@ -5907,8 +5907,9 @@ void BaSolver::Load(const sg_problem& p) {
     lap_log += buf;
   }
   if (host_timing) {
-    char buf[64];
-    snprintf(buf, sizeof(buf), " (staged %.2f MB)", stg.staged_bytes() / 1e6);
+    char buf[96];
+    snprintf(buf, sizeof(buf), " (staged %.2f MB; device allocations so far %ld)", stg.staged_bytes() / 1e6,
+             g_dbuf_allocs.load());
     lap_log += buf;
   }
   SaveStructure(p);

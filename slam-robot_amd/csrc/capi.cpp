@@ -251,6 +251,7 @@ static void RunProblem(sg_slam* s, sg_problem* p, sg_map* map, const sg_solver_o
     s->res_p = std::max(s->res_p, 2 * p->num_points + 64);
     s->res_m = std::max(s->res_m, 2 * p->num_obs + 512);
     s->solver->Reserve(s->res_f, s->res_p, s->res_m);
+    if (timing) fprintf(stderr, "[sg] reserve frames %d points %d observations %d\n", s->res_f, s->res_p, s->res_m);
   }
   s->solver->Load(*p);
   const auto t1 = now();

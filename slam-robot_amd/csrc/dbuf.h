@@ -5,11 +5,15 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <vector>
 
 #include "common.h"
 
 namespace sg {
+
+// device allocations made by every DBuf of the process (SG_HOST_TIMING: reported per load)
+inline std::atomic<long> g_dbuf_allocs{0};
 
 template <typename T>
 struct DBuf {
@@ -31,6 +35,7 @@ struct DBuf {
     ptr = nullptr;
     cap = 0;
     SG_HIP_CHECK(hipMalloc(&ptr, std::max<size_t>(ncap, 1) * sizeof(T)));
+    g_dbuf_allocs.fetch_add(1, std::memory_order_relaxed);
     cap = ncap;
     return true;
   }

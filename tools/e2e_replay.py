@@ -130,6 +130,8 @@ print("criteria:", json.dumps(crit))
 # download).  If these also take 10-28 ms after the gaps where loads did, the stall is the idle GPU's start
 # latency, independent of the load path.
 xz = torch.zeros(1, device="cuda")
+xz.add_(1.0)   # the first launch of the add kernel loads its code object (~60 ms): not part of the control
+torch.cuda.synchronize()
 tiny = make_scene(num_frames=2, num_points=1, seed=1, run_max=2)
 ctrl = []
 CONTROL_PASSES = int(os.environ.get("REPLAY_CONTROL_PASSES", "4"))   # rare stalls need many samples
