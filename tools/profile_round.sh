@@ -3,7 +3,7 @@
 # for each workload (C2, C5, the scaled sweep, the front end) one kernel-trace --stats run and two separate
 # --pmc passes (FETCH_SIZE, WRITE_SIZE) of `bench.py --only <workload>` with the driver's arguments
 # (--steps 20 --warmup 5), so every file holds that workload's own launches only:
-#   profiles/<tag>_kernel_stats_<workload>.csv   rocprofv3 kernel statistics
+#   profiles/<tag>_kernel_stats_<workload>.csv   rocprofv3 kernel statistics (the workload alone: no modelled shards)
 #   profiles/<tag>_pmc_traffic_<workload>.json   HBM bytes per launch (tools/pmc_traffic.py)
 # bench.py's traffic fields read the newest *_pmc_traffic_<workload>.json.  Usage: profile_round.sh <tag> [workloads]
 # On a gpurun box only gpurun_out/ comes back: the summaries are written to gpurun_out/prof_<tag>/profiles/ as
@@ -19,7 +19,7 @@ KRE="k_chol_tiles|k_cholesky_window|k_linearize|k_cam_reduce|k_cam_finalize|k_sc
 for W in $WLS; do
   echo "== $W kernel trace"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt_$W" -o run --output-format csv \
-    -- python3 "$R/bench.py" --only "$W" --steps 20 --warmup 5 > "$OUT/kt_$W.json" 2> "$OUT/kt_$W.log" \
+    -- python3 "$R/bench.py" --only "$W" --steps 20 --warmup 5 --model-scaling 0 --weak 0 > "$OUT/kt_$W.json" 2> "$OUT/kt_$W.log" \
     || { echo "kernel trace $W failed"; tail -5 "$OUT/kt_$W.log"; exit 1; }
   f=$(ls "$OUT"/kt_$W/run_kernel_stats.csv "$OUT"/kt_$W/*/run_kernel_stats.csv "$OUT"/kt_$W/*/*/run_kernel_stats.csv 2>/dev/null | head -1)
   mkdir -p "$OUT/profiles"
@@ -29,7 +29,7 @@ for W in $WLS; do
     i=$((i+1))
     echo "== $W pmc $c"
     timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex "$KRE" -d "$OUT/pmc_$W/p$i" -o run \
-      --output-format csv -- python3 "$R/bench.py" --only "$W" --steps 20 --warmup 5 \
+      --output-format csv -- python3 "$R/bench.py" --only "$W" --steps 20 --warmup 5 --model-scaling 0 --weak 0 \
       > "$OUT/pmc_${W}_p$i.json" 2> "$OUT/pmc_${W}_p$i.log" \
       || { echo "pmc $c $W failed"; tail -5 "$OUT/pmc_${W}_p$i.log"; exit 1; }
   done
