@@ -112,7 +112,12 @@ def pmc_traffic(kernel, workload):
     return g["traffic_bytes"], os.path.basename(files[-1])
 
 
+TRAFFIC_APPLIES = True   # False for N > 1: the committed PMC files profile the one-GPU workload, not a shard
+
+
 def traffic_fields(kernel, workload, algorithmic_bytes=None):
+    if not TRAFFIC_APPLIES:
+        return {"traffic": None, "traffic_file": None}
     t, src = pmc_traffic(kernel, workload)
     d = {"traffic": t, "traffic_file": src}
     if t is not None and algorithmic_bytes:
@@ -468,7 +473,9 @@ def kernel_report(res, steps, n_text, workload):
     chain, where k_linearize runs only in a solve's first iteration; k_linearize otherwise."""
     kt, work = res["kt"], res["work"]
     per_iter_ms = {k: v[0] * v[1] / max(steps, 1) for k, v in kt.items()}
-    dominant = max(per_iter_ms, key=per_iter_ms.get)
+    # the dominant kernel (the exchange timer of a multi-rank chain — pack, all-reduce, unpack — is not a kernel
+    # and has no algorithmic work figure)
+    dominant = max((k for k in per_iter_ms if k in work and k != "exchange"), key=per_iter_ms.get)
     dom_ms = kt[dominant][0]
     dom_bytes, dom_flops = work[dominant]
     if dom_flops > 0 and dominant == "cholesky":
@@ -697,6 +704,8 @@ def main():
         dist.init_process_group("nccl" if args.comm == "rccl" else "gloo", rank=rank, world_size=ws)
     n_gpus = ws
     c5 = args.config == "C5"
+    global TRAFFIC_APPLIES
+    TRAFFIC_APPLIES = n_gpus == 1
 
     full, prob, desc, res, info, start, bal = run_workload(args.config, args, n_gpus, rank, local, dist,
                                                            args.steps, args.warmup)
