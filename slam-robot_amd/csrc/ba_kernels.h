@@ -78,7 +78,10 @@ constexpr int kSchurTiles = kSchurTW * (kSchurTW + 1) / 2;
 constexpr int kSchurAug = kSchurTiles + kSchurTW;   // window tiles + one rhs tile per tile row
 constexpr int kSchurTPW = (kSchurAug + kSchurCWaves - 1) / kSchurCWaves;   // accumulator tiles per wave
 constexpr int kSchurXCap = 112 * 64;   // operand tiles (64 doubles each) per batch buffer
-constexpr int kSchurBatchPts = 32;   // <= 64: a batch's point table is one point per lane
+#ifndef SG_SCHUR_BATCH
+#define SG_SCHUR_BATCH 32
+#endif
+constexpr int kSchurBatchPts = SG_SCHUR_BATCH;   // <= 64: a batch's point table is one point per lane
 constexpr int kSchurBatchCells = kSchurBatchPts * 24;   // cells of a batch (spans <= kSegNbMax)
 static_assert(6 * kSegNbMax + 14 <= 16 * kSchurTW, "a widest point must fit the tile window");
 struct SchurSeg {

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <chrono>
 #include <memory>
 #include <string>
 #include <vector>
@@ -75,6 +76,11 @@ class BaSolver {
   void DropGraph();
   void EnqueueIterations(int n);
   hipEvent_t dev_marks_[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};   // SG_HOST_TIMING: device times in Load
+  hipEvent_t ev_idle_ = nullptr;                                            //   the stream last seen idle (MarkIdle)
+  hipEvent_t ev_idle_prev_ = nullptr;                                       //   the previous call's, at a load
+  std::chrono::steady_clock::time_point idle_host_;
+  bool idle_valid_ = false;
+  void MarkIdle(hipStream_t s);
   void DevMark(hipStream_t s, int i);
   hipEvent_t ev_lin_ = nullptr, ev_schur_ = nullptr;
   bool overlap_ok_ = getenv("SG_SCHUR_OVERLAP") && atoi(getenv("SG_SCHUR_OVERLAP")) == 1;

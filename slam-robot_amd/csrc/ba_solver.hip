@@ -5101,6 +5101,8 @@ BaSolver::~BaSolver() {
   for (auto& t : timers_)
     for (auto e : t.ev) (void)hipEventDestroy(e);
   if (ev_wait_) (void)hipEventDestroy(ev_wait_);
+  if (ev_idle_) (void)hipEventDestroy(ev_idle_);
+  if (ev_idle_prev_) (void)hipEventDestroy(ev_idle_prev_);
   if (ev_lin_) (void)hipEventDestroy(ev_lin_);
   if (ev_schur_) (void)hipEventDestroy(ev_schur_);
   if (side_) (void)hipStreamDestroy(side_);
@@ -5166,6 +5168,10 @@ void BaSolver::Load(const sg_problem& p) {
   // a device mark at the load's start, with its host time: the GPU time from here to the last mark against the
   // host's wall time tells a late device (its queue started late) from a late host (the waiting thread)
   auto load_t0 = std::chrono::steady_clock::now();
+  const bool idle_valid_prev = idle_valid_;
+  const double idle_gap_host =
+      idle_valid_ ? std::chrono::duration<double, std::milli>(load_t0 - idle_host_).count() : 0.0;
+  std::swap(ev_idle_, ev_idle_prev_);   // (this load's own waits re-mark ev_idle_)
   if (host_timing) DevMark(stream_, 4);
   {
     // Everything that can reject this rank's problem runs before the first collective, and the verdict rides
@@ -5901,10 +5907,16 @@ void BaSolver::Load(const sg_problem& p) {
     float e = 0;
     (void)hipEventElapsedTime(&e, dev_marks_[4], dev_marks_[3]);
     const double hw = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - load_t0).count();
-    char buf[192];
+    char buf[320];
     snprintf(buf, sizeof(buf), " [device: batch1..batch2 %.2f, scatter2 %.2f, reset %.2f; load start..reset: device "
              "%.2f, host %.2f]", a, b, c, e, hw);
     lap_log += buf;
+    if (idle_valid_prev) {
+      float g = 0;
+      const hipError_t ge = hipEventElapsedTime(&g, ev_idle_prev_, dev_marks_[4]);
+      snprintf(buf, sizeof(buf), " [last idle..load start: device %.2f (%d), host %.2f]", g, (int)ge, idle_gap_host);
+      lap_log += buf;
+    }
   }
   if (host_timing) {
     char buf[96];
@@ -6241,12 +6253,28 @@ void BaSolver::WaitStream(hipStream_t s) {
   const auto t0 = std::chrono::steady_clock::now();
   while (true) {
     const hipError_t e = hipEventQuery(ev_wait_);
-    if (e == hipSuccess) return;
+    if (e == hipSuccess) {
+      MarkIdle(s);
+      return;
+    }
     if (e != hipErrorNotReady) SG_HIP_CHECK(e);
     if (std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() > limit) break;
     if (shared) std::this_thread::yield();
   }
   SG_HIP_CHECK(hipEventSynchronize(ev_wait_));
+  MarkIdle(s);
+}
+
+// SG_HOST_TIMING: a device marker and the host clock at the moment the stream was last seen idle, so a load can
+// compare the device's and the host's time from there to its first command (a late queue start shows as a
+// device gap longer than the host's).
+void BaSolver::MarkIdle(hipStream_t s) {
+  static const bool host_timing = getenv("SG_HOST_TIMING") != nullptr;
+  if (!host_timing) return;
+  if (!ev_idle_) SG_HIP_CHECK(hipEventCreate(&ev_idle_));
+  SG_HIP_CHECK(hipEventRecord(ev_idle_, s));
+  idle_host_ = std::chrono::steady_clock::now();
+  idle_valid_ = true;
 }
 
 void BaSolver::DevMark(hipStream_t s, int i) {

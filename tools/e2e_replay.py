@@ -148,9 +148,9 @@ for r in [r for _ in range(CONTROL_PASSES) for r in later]:
     small = 1e3 * (time.perf_counter() - t0)
     ctrl.append({"frame": r["frame"], "gap_ms": r["gap_ms"], "load_ms": r["load"], "noop_ms": noop,
                  "tiny_call_ms": small})
-noops = np.array([c["noop_ms"] for c in ctrl])
-tinys = np.array([c["tiny_call_ms"] for c in ctrl])
-cgaps = np.array([c["gap_ms"] for c in ctrl])
+noops = np.array([c["noop_ms"] for c in ctrl] or [0.0])
+tinys = np.array([c["tiny_call_ms"] for c in ctrl] or [0.0])
+cgaps = np.array([c["gap_ms"] for c in ctrl] or [0.0])
 control = {"calls": len(ctrl), "passes": CONTROL_PASSES,
            "noop_stall_rate": float((noops > 5).mean()), "tiny_call_stall_rate": float((tinys > 5).mean()),
            "load_stall_rate": float(np.mean([r["load"] > 5 for r in later])),
