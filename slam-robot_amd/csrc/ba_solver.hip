@@ -4127,87 +4127,106 @@ __global__ __launch_bounds__(kBordThreads) void k_chol_border(Dev d, double* __r
   cl.carve(bdyn + off, d.F, d.D, n);
   const double* S = d.S;
   const double* xc = d.xc;                             // x_f0 (frame rows), r_k (border rows)
-  __shared__ double Cs[16][17];
-  __shared__ double rk[16], xk[16], rpart[kBordThreads / 64 - 1][16];
+  __shared__ double Cs[16][kTLd];
+  __shared__ double rk[16], xk[16], rpart[kBordThreads / 64][16];
+  __shared__ double Ids[16 * kTLd], prw[2 * kCholNb];   // tile_factor's identity tile and pivot-row scratch
+  for (int i = tid; i < 16 * kTLd; i += kBordThreads) Ids[i] = (i / kTLd == i % kTLd) ? 1.0 : 0.0;
   __shared__ int bad_sh;
   // SG_STAMP=1: thread 0's s_memtime after each step, the deltas accumulated over launches in d.stamps[40 + k]
   // at the end (no global access between the stamps)
-  unsigned long long tst[6];
-  tst[0] = __builtin_amdgcn_s_memtime();
-  auto bstamp = [&](int k) { tst[k + 1] = __builtin_amdgcn_s_memtime(); };
+  unsigned long long tst[10];
+  // (asm volatile with a memory clobber: the builtin may be scheduled across the code it should bracket)
+  auto now_t = []() {
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+    return t;
+  };
+  tst[0] = now_t();
+  auto bstamp = [&](int k) { tst[k + 1] = now_t(); };
+  for (int k = 1; k < 10; ++k) tst[k] = tst[0];
   const int fail0 = d.xchg_chol[kCFail] != 0.0, tmo0 = d.xchg_chol[kCTimeout] != 0.0;
   for (int k = tid; k < NT; k += kBordThreads) rdone[k] = 0;
   if (tid == 0) bad_sh = fail0;
+  // (1) the forward chain on four waves, handing tiles over through LDS rings behind monotonic flags:
+  //   wave 0 (the chain): v_K = S_KB + F_K - W_{K-2,K}^T v_{K-2} - W_{K-1,K}^T v_{K-1}, w_K = Z_K v_K; posts
+  //     v_K, w_K (vpost = K);
+  //   waves 1, 2: the far terms F_K = -sum W_{K-d,K}^T v_{K-d}, d in {3, 4, 5} / {6, 7}, up to three rows ahead
+  //     of the chain (they need v up to K-3), posted per row (fpost[h] = K);
+  //   wave 3: C -= w_K^T w_K and q_K = Z_K^T w_K from the posted w_K (wdone = K).
+  // So the chain's own matrix-core work per row is 12 MFMAs (was 40 on one SIMD).  Ring safety: v slot K & 7 is
+  // rewritten at row K + 8 after F_{K+7} was consumed; F slot K & 3 at row K + 4 after the chain used F_K; w
+  // slot K & 3 at row K + 4 after wave 3 took w_K.  Bounded waits (a time-out is reported as kCTimeout).
+  __shared__ double vring[8][256], wring[4][256], fring[2][4][256];
+  __shared__ int vpost, fpost[2], wdone;
+  if (tid == 0) {
+    vpost = -1;
+    fpost[0] = fpost[1] = -1;
+    wdone = -1;
+  }
+  __syncthreads();
+  bool tmo_chain = false;
+  // The rings and flags are LDS, whose accesses from one wave execute in order: data then flag on the writer,
+  // flag then data on the reader need only compiler barriers — no fence, which would also wait for this wave's
+  // outstanding global loads (the next row's prefetch) on every post.
+  auto wait_ge = [&](int* flag, int v) {
+    int spin = 0;
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < v && ++spin < kLaSpinMax)
+      __builtin_amdgcn_s_sleep(0);
+    tmo_chain |= spin >= kLaSpinMax;
+    asm volatile("" ::: "memory");
+  };
+  auto post = [&](int* flag, int v) {
+    asm volatile("" ::: "memory");
+    if (lane == 0) __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
+  const f64x4 zero = {0.0, 0.0, 0.0, 0.0};
   if (wave == 0) {
-    // (1) the forward chain; v_{K-1..K-7} in registers
-    f64x4 vr[kTB - 1];
-    const f64x4 zero = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int dd = 0; dd < kTB - 1; ++dd) vr[dd] = zero;
-    f64x4 C;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int r = lk + 4 * q, c = li;
-      const int a = min(r, c), b = max(r, c);   // S_kk upper triangle
-      C[q] = (r < nk && c < nk) ? S[(size_t)(nf + a) * n + nf + b] : (r == c ? 1.0 : 0.0);
-    }
-    // row K's operands (S_KB, W_{K-d,K}, Z_K) do not depend on the chain: loaded one row ahead
+    // row K's operands (S_KB, W_{K-1,K}, Z_K) loaded one row ahead; unconditional loads (an index selected, not a
+    // value: S's zero constant past the system; row -1's W tile multiplies the zero v_{-1})
     struct RowOps {
-      double sb[4], w[kTB - 1][4], za[4], zb[4];
+      double sb[4], w1[4], w2[4], za[4];
     };
     auto row_load = [&](RowOps& o, int K) {
       const int Kc = min(K, NT - 1);
-      // unconditional loads (a load under a condition compiles to a branch that waits for it): the index is
-      // selected (S's zero constant past the system), and rows before 0 read some finite W tile that multiplies
-      // the zero v_{K-d}
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int r = 16 * Kc + lk + 4 * q;
         o.sb[q] = S[(r < nf && li < nk) ? (size_t)r * n + nf + li : (size_t)n * n + n];
       }
+      const double* wt = Wg + ((size_t)max(Kc - 1, 0) * kTB + 1) * 256 + lane;
+      const double* wt2 = Wg + ((size_t)max(Kc - 2, 0) * kTB + 2) * 256 + lane;
 #pragma unroll
-      for (int dd = 1; dd < kTB; ++dd) {
-        const double* wt = Wg + ((size_t)max(Kc - dd, 0) * kTB + dd) * 256 + lane;
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) o.w[dd - 1][s4] = -wt[s4 * 64];
+      for (int s4 = 0; s4 < 4; ++s4) {
+        o.w1[s4] = -wt[s4 * 64];
+        o.w2[s4] = -wt2[s4 * 64];
       }
       const double* Z = Wg + (size_t)Kc * kTB * 256;   // row-major Z_K
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        o.za[s4] = Z[li * 16 + 4 * s4 + lk];     // Z^T in acc layout: Z v
-        o.zb[s4] = Z[(4 * s4 + lk) * 16 + li];   // Z in acc layout: Z^T w
-      }
+      for (int s4 = 0; s4 < 4; ++s4) o.za[s4] = Z[li * 16 + 4 * s4 + lk];   // Z^T in acc layout: Z v
     };
+    f64x4 vprev = zero, vprev2 = zero;
     RowOps ops[2];
     row_load(ops[0], 0);
     auto row = [&](RowOps& o, int K) {
-      // the far terms (two accumulators, independent of v_{K-1}), then v_{K-1}'s product
-      f64x4 va, vb = zero;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) va[q] = o.sb[q];
-#pragma unroll
-      for (int dd = kTB - 1; dd >= 2; --dd) {
-        if (dd & 1) va = mfma_f64_k16(o.w[dd - 1], vr[dd - 1], va);
-        else vb = mfma_f64_k16(o.w[dd - 1], vr[dd - 1], vb);
-      }
-      vb = mfma_f64_k16(o.w[0], vr[0], vb);
       f64x4 v;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = va[q] + vb[q];
-      const f64x4 w = mfma_f64_k16(o.za, v, zero);
-      double wn[4];
+      for (int q = 0; q < 4; ++q) v[q] = o.sb[q];
+      v = mfma_f64_k16(o.w2, vprev2, v);   // d = 2, then d = 1 (the helpers hold d >= 3: three rows of slack)
+      v = mfma_f64_k16(o.w1, vprev, v);
+      wait_ge(&fpost[0], K);
+      wait_ge(&fpost[1], K);
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) wn[s4] = -w[s4];
-      C = mfma_f64_k16(wn, w, C);
-      const f64x4 qv = mfma_f64_k16(o.zb, w, zero);
+      for (int q = 0; q < 4; ++q) v[q] += fring[0][K & 3][q * 64 + lane] + fring[1][K & 3][q * 64 + lane];
+      const f64x4 w = mfma_f64_k16(o.za, v, zero);
+      if (K >= 4) wait_ge(&wdone, K - 4);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        if constexpr (qlds) Ql[(size_t)K * 256 + q * 64 + lane] = qv[q];
-        else Qg[(size_t)K * 256 + q * 64 + lane] = qv[q];
+        vring[K & 7][q * 64 + lane] = v[q];
+        wring[K & 3][q * 64 + lane] = w[q];
       }
-#pragma unroll
-      for (int dd = kTB - 2; dd >= 1; --dd) vr[dd] = vr[dd - 1];
-      vr[0] = v;
+      post(&vpost, K);
+      vprev2 = vprev;
+      vprev = v;
     };
 #pragma nounroll
     for (int K = 0; K < NT; K += 2) {
@@ -4218,16 +4237,96 @@ __global__ __launch_bounds__(kBordThreads) void k_chol_border(Dev d, double* __r
         row(ops[1], K + 1);
       }
     }
+  } else if (wave <= 2) {
+    // far terms, d in {3, 4, 5} (wave 1) or {6, 7} (wave 2); W tiles one row ahead
+    const int h = wave - 1, d0 = 3 + 3 * h;
+    double wn[2][3][4];
+    auto wload = [&](double (&o)[3][4], int K) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) Cs[lk + 4 * q][li] = C[q];
+      for (int j = 0; j < 3; ++j) {
+        const int dj = min(d0 + j, kTB - 1);   // (wave 2's third slot is past the band: loaded, never used)
+        const double* wt = Wg + ((size_t)max(K - dj, 0) * kTB + dj) * 256 + lane;
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) o[j][s4] = -wt[s4 * 64];
+      }
+    };
+    // (buffers by compile-time index: the loop is unrolled by two, a run-time index would put them in scratch)
+    auto hrow = [&](double (&wc)[3][4], double (&wnx)[3][4], int K) {
+      if (K + 1 < NT) wload(wnx, K + 1);
+      // v up to K - d0 posted, and F slot K & 3 free (the chain has used F_{K-4})
+      wait_ge(&vpost, max(K - d0, K - 4));
+      f64x4 f = zero;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        const int Kv = K - (d0 + j);
+        if (Kv >= 0 && d0 + j < kTB) {
+          f64x4 vt;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) vt[q] = vring[Kv & 7][q * 64 + lane];
+          f = mfma_f64_k16(wc[j], vt, f);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) fring[h][K & 3][q * 64 + lane] = f[q];
+      post(&fpost[h], K);
+    };
+    wload(wn[0], 0);
+#pragma nounroll
+    for (int K = 0; K < NT; K += 2) {
+      hrow(wn[0], wn[1], K);
+      if (K + 1 < NT) hrow(wn[1], wn[0], K + 1);
+    }
   } else {
-    // (2) S_kf x_f0 beside the chain: the other waves take the frame rows (a row's 14 border entries are
-    // contiguous), per-wave sums per intrinsic, combined in wave order below
-    constexpr int kOt = kBordThreads - 64;
+    // C and the q_K tiles from the posted w_K
+    f64x4 C;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = lk + 4 * q, c = li;
+      const int a = min(r, c), b = max(r, c);   // S_kk upper triangle
+      C[q] = (r < nk && c < nk) ? S[(size_t)(nf + a) * n + nf + b] : (r == c ? 1.0 : 0.0);
+    }
+    double zb[2][4];
+    auto zload = [&](double (&o)[4], int K) {
+      const double* Z = Wg + (size_t)min(K, NT - 1) * kTB * 256;
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) o[s4] = Z[(4 * s4 + lk) * 16 + li];   // Z in acc layout: Z^T w
+    };
+    auto crow = [&](double (&zc)[4], double (&znx)[4], int K) {
+      zload(znx, K + 1);
+      wait_ge(&vpost, K);
+      f64x4 w;
+      double wn4[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        w[q] = wring[K & 3][q * 64 + lane];
+        wn4[q] = -w[q];
+      }
+      post(&wdone, K);
+      C = mfma_f64_k16(wn4, w, C);
+      const f64x4 qv = mfma_f64_k16(zc, w, zero);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if constexpr (qlds) Ql[(size_t)K * 256 + q * 64 + lane] = qv[q];
+        else Qg[(size_t)K * 256 + q * 64 + lane] = qv[q];
+      }
+    };
+    zload(zb[0], 0);
+#pragma nounroll
+    for (int K = 0; K < NT; K += 2) {
+      crow(zb[0], zb[1], K);
+      if (K + 1 < NT) crow(zb[1], zb[0], K + 1);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) Cs[lk + 4 * q][li] = (lk + 4 * q <= li) ? C[q] : 0.0;   // upper (tile_factor)
+  }
+  __syncthreads();
+  // (2) S_kf x_f0 on every wave: a thread per frame row (a row's 14 border entries are contiguous), per-wave sums
+  // per intrinsic, combined in wave order below
+  {
     double part[kCholNb];
 #pragma unroll
     for (int c = 0; c < kCholNb; ++c) part[c] = 0.0;
-    for (int i = tid - 64; i < nf; i += kOt) {
+    for (int i = tid; i < nf; i += kBordThreads) {
       const double xi = xc[i];
       const double* row = S + (size_t)i * n + nf;
 #pragma unroll
@@ -4236,52 +4335,35 @@ __global__ __launch_bounds__(kBordThreads) void k_chol_border(Dev d, double* __r
 #pragma unroll
     for (int c = 0; c < kCholNb; ++c) {
       const double v = wave_sum_full(part[c]);
-      if (lane == 0) rpart[wave - 1][c] = v;
+      if (lane == 0) rpart[wave][c] = v;
     }
-    if (cand_lds) cand_prefetch(d, cl, st->cur, tid - 64, kOt);
   }
   if (d.stamps && tid == 0) bstamp(0);
   __syncthreads();
-  if (tid < nk) rk[tid] = xc[nf + tid] - ((rpart[0][tid] + rpart[1][tid]) + rpart[2][tid]);
+  if (d.stamps && tid == 0) bstamp(5);
+  if (tid < kCholNb)
+    rk[tid] = tid < nk ? xc[nf + tid] - (((rpart[0][tid] + rpart[1][tid]) + rpart[2][tid]) + rpart[3][tid]) : 0.0;
   __syncthreads();
+  if (d.stamps && tid == 0) bstamp(6);
   if (wave == 0) {
-    // x_k = C^-1 rk: C = U_c^T U_c column per lane, then the two triangular solves
-    double col[kCholNb];
+    // x_k = C^-1 rk by the tiled Cholesky's 16x16 factorisation (tile_factor: the identity and rk as augmented
+    // columns give Z = U_c^-T and z = Z rk), then x_k = Z^T z (lanes 16..31 hold Z's columns)
+    double ca[kCholNb];
+    const bool bad = tile_factor(&Cs[0][0], rk, Ids, prw, ca);
+    double zr[kCholNb];
 #pragma unroll
-    for (int r = 0; r < kCholNb; ++r) col[r] = (lane < nk && r <= lane) ? Cs[r][lane] : 0.0;
-    bool bad = false;
-    chol_diag16(col, nk, lane, bad);
-    if (lane < nk) {
+    for (int r = 0; r < kCholNb; ++r) zr[r] = readlane_d(ca[r], 32);
+    if (lane >= 16 && lane < 32) {
+      double x = 0.0;
 #pragma unroll
-      for (int r = 0; r < kCholNb; ++r)
-        if (r <= lane) Cs[r][lane] = col[r];
+      for (int r = 0; r < kCholNb; ++r) x = fma(ca[r], zr[r], x);
+      xk[lane - 16] = lane - 16 < nk ? x : 0.0;
     }
-    // 1 / U_jj for every pivot first (independent divisions), then the two solves on multiplies
-    double inv[kCholNb];
-#pragma unroll
-    for (int j = 0; j < kCholNb; ++j) inv[j] = j < nk ? 1.0 / readlane_d(col[j], j) : 0.0;
-    double s = lane < nk ? rk[lane] : 0.0;
-#pragma unroll
-    for (int j = 0; j < kCholNb; ++j) {
-      if (j < nk) {
-        const double zj = readlane_d(s, j) * inv[j];
-        if (lane == j) s = zj;
-        else if (lane > j) s = fma(-col[j], zj, s);
-      }
-    }
-#pragma unroll
-    for (int j = kCholNb - 1; j >= 0; --j) {
-      if (j < nk) {
-        const double xj = readlane_d(s, j) * inv[j];
-        if (lane == j) s = xj;
-        else if (lane < j) s = fma(-Cs[lane][j], xj, s);
-      }
-    }
-    if (lane < 16) xk[lane] = lane < nk ? s : 0.0;
     if (lane == 0 && bad) bad_sh = 1;
   }
   if (d.stamps && tid == 0) bstamp(1);
   __syncthreads();
+  if (d.stamps && tid == 0) bstamp(7);
   // (3) z'_K = q_K x_k, then t = U^-1 (w x_k)
   for (int i = tid; i < 16 * NT; i += kBordThreads) {
     const int K = i >> 4, r = i & 15;
@@ -4298,17 +4380,20 @@ __global__ __launch_bounds__(kBordThreads) void k_chol_border(Dev d, double* __r
   }
   if (d.stamps && tid == 0) bstamp(2);
   __syncthreads();
-  bool tmo = tmo0;
+  if (d.stamps && tid == 0) bstamp(8);
+  bool tmo = tmo0 || tmo_chain;
   {
     double xw[kTB - 1];
 #pragma unroll
     for (int dd = 0; dd < kTB - 1; ++dd) xw[dd] = 0.0;
     constexpr int kBs2Rows = 12;
+    const int nbs = NT >= kBs2Rows ? 2 : 1;   // waves on the back substitution; the others stage the candidates
     if (NT >= kBs2Rows) {
       if (wave < 2) bs_chain2<false>(Wg, zq, xs, rdone, NT - 1, 0, xw, NT, wave, lane, li, lk, tmo);
     } else if (wave == 0) {
       bs_chain<false>(Wg, zq, xs, NT - 1, 0, xw, NT, lane, li, lk);
     }
+    if (wave >= nbs && cand_lds) cand_prefetch(d, cl, st->cur, tid - 64 * nbs, kBordThreads - 64 * nbs);
   }
   __shared__ int tmo_sh;
   if (tid == 0) tmo_sh = 0;
@@ -4330,8 +4415,10 @@ __global__ __launch_bounds__(kBordThreads) void k_chol_border(Dev d, double* __r
     chol_candidates<kBordThreads>(d, xs, bad_sh, tmo_sh);
   if (d.stamps && tid == 0) {
     bstamp(4);
+    // stamps[48 + k]: time from the start to stamp k (0 chain, 5 after B1, 6 after B2, 1 C solve, 7 after B3,
+    // 2 z', 8 after B4, 3 back substitution, 4 end), accumulated over launches
 #pragma unroll
-    for (int k = 0; k < 5; ++k) d.stamps[40 + k] += tst[k + 1] - tst[k];
+    for (int k = 1; k < 10; ++k) d.stamps[48 + k - 1] += tst[k] - tst[0];   // (slots 32-45: k_schur's)
   }
 }
 

@@ -18,13 +18,14 @@ g.iterate(steps)
 g.sync()
 s = g.summary()
 print(g.info()["cholesky"], s["num_lm_iterations"], s["ok"], flush=True)
-if os.environ.get("SG_STAMP") == "1":   # k_chol_border's per-step s_memtime sums (d.stamps[40..44])
+if os.environ.get("SG_STAMP") == "1":   # k_chol_border's per-step s_memtime sums (d.stamps[48..56])
     import ctypes as C
     import numpy as np
     buf = np.zeros(64, np.uint64)
     g.lib.sg_ba_debug_stamps.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
     g.lib.sg_ba_debug_stamps(g.h, buf.ctypes.data, 64)
-    names = ["chain+Skf", "C solve", "z'", "back-sub", "candidates"]
-    print("k_chol_border per launch (s_memtime ticks):",
-          {k: round(float(buf[40 + i]) / steps, 1) for i, k in enumerate(names)}, flush=True)
+    names = ["chain", "C solve", "z'", "back-sub", "end", "after B1", "after B2", "after B3", "after B4"]
+    t = {k: round(float(buf[48 + i]) / steps) for i, k in enumerate(names)}
+    order = ["chain", "after B1", "after B2", "C solve", "after B3", "z'", "after B4", "back-sub", "end"]
+    print("k_chol_border, ticks from its start (per launch):", [(k, t[k]) for k in order], flush=True)
 g.close()
