@@ -1681,6 +1681,15 @@ __global__ __launch_bounds__(kIntrFkThreads) void k_intr_fk(Dev d, int nsl) {
   constexpr int kW = kIntrFkThreads / 64;
   __shared__ double red[kW][kV];
   // workgroup (b, slice sl) of blockIdx.x takes the sl-th part of block b's list
+  // SG_STAMP=1: one mid-grid workgroup's thread 0 times its steps (d.stamps[58 + 3 kMode ..]; 48-56: k_chol_border)
+  const bool stw = d.stamps && blockIdx.x == gridDim.x / 2 && blockIdx.y == 0 && threadIdx.x == 0;
+  unsigned long long t0s = 0;
+  auto nowt = []() {
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+    return t;
+  };
+  if (stw) t0s = nowt();
   const int b = blockIdx.x / nsl, sl = blockIdx.x - b * nsl, c = blockIdx.y, tid = threadIdx.x, cur = st->cur;
   const int nk = d.nk, ncam = d.ncam;
   const int l0 = d.intr_boff[b], len = d.intr_boff[b + 1] - l0;
@@ -1746,7 +1755,10 @@ __global__ __launch_bounds__(kIntrFkThreads) void k_intr_fk(Dev d, int nsl) {
         for (int j = 0; j < 7; ++j) acc[7 * a + j] -= Jc[a] * Mx[j] + Jc[6 + a] * Mx[7 + j];
     }
   }
+  unsigned long long t1s = 0, t2s = 0;
+  if (stw) t1s = nowt();
   wg_sum_values<kW, kV>(acc, red);
+  if (stw) t2s = nowt();
   // the slices of a block add into KU_fk / S_fk (nsl atomics per entry); the camera sums go to their partial slot
   if constexpr (kMode == 0) {
     for (int e = tid; e < kV; e += kIntrFkThreads) {
@@ -1759,6 +1771,12 @@ __global__ __launch_bounds__(kIntrFkThreads) void k_intr_fk(Dev d, int nsl) {
   } else {
     for (int e = tid; e < kV; e += kIntrFkThreads)
       atomicAdd(d.S + (size_t)(6 * b + e / 7) * d.n + d.kc0 + 7 * c + e % 7, red[0][e]);
+  }
+  if (stw) {
+    const unsigned long long t3s = nowt();
+    d.stamps[58 + 3 * kMode] += t1s - t0s;
+    d.stamps[59 + 3 * kMode] += t2s - t1s;
+    d.stamps[60 + 3 * kMode] += t3s - t2s;
   }
 }
 

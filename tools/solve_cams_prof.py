@@ -28,4 +28,6 @@ if os.environ.get("SG_STAMP") == "1":   # k_chol_border's per-step s_memtime sum
     t = {k: round(float(buf[48 + i]) / steps) for i, k in enumerate(names)}
     order = ["chain", "after B1", "after B2", "C solve", "after B3", "z'", "after B4", "back-sub", "end"]
     print("k_chol_border, ticks from its start (per launch):", [(k, t[k]) for k in order], flush=True)
+    print("k_intr_fk<0>, <1> mid-grid workgroup (loop, sums, tail ticks):",
+          [round(float(buf[58 + i]) / steps) for i in range(6)], flush=True)
 g.close()
