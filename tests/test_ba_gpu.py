@@ -440,6 +440,49 @@ def test_free_intrinsics_solve_matches_oracle(gpu_lib, oracle_lib):
     np.testing.assert_allclose(pg.k, po.k, rtol=1e-5, atol=1e-6)
 
 
+def test_free_intrinsics_one_camera_matches_oracle(gpu_lib, oracle_lib):
+    """One camera (nk = 7): the bordered band solve's 16-wide border tile is half padding (identity on the
+    padded diagonal, zero coupling); two LM iterations against the oracle as in the two-camera test."""
+    m = _intrinsics_scene(seed=5)
+    m.frame_camera[:] = 0
+    m.k = m.k[:7].copy()
+    pa = ba.problem_from_map_all(m, 2.0, solve_cameras=True)
+    o = default_solver_options(max_num_iterations=2, function_tolerance=1e-9)
+    g = ba.BundleAdjuster()
+    g.load(pa.copy())
+    info = g.info()
+    g.close()
+    assert info["cholesky_path"] == 4 and info["n"] == info["num_blocks"] * 6 + 7, info
+    pg, sg, po, so = _solve_both(oracle_lib, pa, o)
+    assert sg["ok"] == so["ok"] == 1
+    assert abs(sg["initial_cost"] - so["initial_cost"]) <= 1e-10 * so["initial_cost"]
+    assert sg["num_successful_steps"] == so["num_successful_steps"]
+    assert abs(sg["final_cost"] - so["final_cost"]) <= 1e-8 * so["final_cost"]
+    np.testing.assert_allclose(pg.k, po.k, rtol=1e-7, atol=1e-9)
+    np.testing.assert_allclose(pg.t, po.t, atol=1e-5)
+
+
+def test_free_intrinsics_three_cameras_take_the_arrowhead_path(gpu_lib, oracle_lib):
+    """Three cameras (nk = 21 > 16): the border does not fit one tile, so the load takes the arrowhead
+    k_cholesky_global; two LM iterations against the oracle."""
+    m = _intrinsics_scene(seed=6)
+    m.frame_camera[:] = np.arange(len(m.frame_camera), dtype=np.int32) % 3
+    m.k = np.concatenate([m.k, m.k[:7]])
+    pa = ba.problem_from_map_all(m, 2.0, solve_cameras=True)
+    o = default_solver_options(max_num_iterations=2, function_tolerance=1e-9)
+    g = ba.BundleAdjuster()
+    g.load(pa.copy())
+    info = g.info()
+    g.close()
+    assert info["cholesky_path"] in (1, 2, 3) and info["n"] == info["num_blocks"] * 6 + 21, info
+    pg, sg, po, so = _solve_both(oracle_lib, pa, o)
+    assert sg["ok"] == so["ok"] == 1
+    assert abs(sg["initial_cost"] - so["initial_cost"]) <= 1e-10 * so["initial_cost"]
+    assert sg["num_successful_steps"] == so["num_successful_steps"]
+    assert abs(sg["final_cost"] - so["final_cost"]) <= 1e-8 * so["final_cost"]
+    np.testing.assert_allclose(pg.k, po.k, rtol=1e-7, atol=1e-9)
+
+
 def test_slam_solve_all_frames_with_cameras(gpu_lib, oracle_lib):
     """Slam::SolveAllFrames(map, 2.0, true) through the facade writes the solved intrinsics back to the map."""
     m = _intrinsics_scene(seed=4)
