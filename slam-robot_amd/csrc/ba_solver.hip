@@ -509,7 +509,10 @@ __global__ __launch_bounds__(kRedThreads) void k_cam_reduce(Dev d, int mode) {
     if (sl < kCamSlices) {
       const int j0 = d.cam_loff[b], j1 = d.cam_loff[b + 1];
       double acc = 0.0;
-      constexpr int kU = 16;   // offsets, then partials, kU at a time in flight (one round of each at C2)
+#ifndef SG_CAM_RED_U
+#define SG_CAM_RED_U 16
+#endif
+      constexpr int kU = SG_CAM_RED_U;   // offsets, then partials, kU at a time in flight (one round of each at C2)
       for (int jb = j0 + sl; jb < j1; jb += kU * kCamSlices) {
         int ix[kU];
         double v[kU];
@@ -543,7 +546,10 @@ __global__ __launch_bounds__(kRedThreads) void k_cam_reduce(Dev d, int mode) {
   __shared__ double redm[kRedThreads / 64];
   double v[kXNum] = {0, 0, 0, 0, 0};
   double gm = 0.0;
-  constexpr int kScalU = 2;   // chunks' loads in flight per thread (8 measured slower)
+#ifndef SG_SCAL_RED_U
+#define SG_SCAL_RED_U 2
+#endif
+  constexpr int kScalU = SG_SCAL_RED_U;   // chunks' loads in flight per thread (8 measured slower)
   for (int c0 = tid; c0 < d.nlin; c0 += kScalU * kRedThreads) {
     double t[kScalU][kXNum + 1];
 #pragma unroll
@@ -1671,7 +1677,10 @@ __device__ __forceinline__ void wg_sum_values(const double (&v)[kV], double (*re
 //     camera c (stored: one writer per entry), and the camera sums of those observations into kpart[b][c];
 //   kMode 1 (after k_intr_schur): S_fk rows of b, columns of c -= sum over the block's observations of free
 //     points of A_c^T (A_p Y_pc^T) (Y_pc = W_kp V~p^-1 of camera c, k_intr_schur).
-constexpr int kIntrFkThreads = 256;
+#ifndef SG_INTR_FK_THREADS
+#define SG_INTR_FK_THREADS 256
+#endif
+constexpr int kIntrFkThreads = SG_INTR_FK_THREADS;   // (the slices per block list stay ~256 observations)
 template <int kMode>
 __global__ __launch_bounds__(kIntrFkThreads) void k_intr_fk(Dev d, int nsl) {
   const LmState* st = d.st;
@@ -5971,7 +5980,7 @@ void BaSolver::Load(const sg_problem& p) {
     // slices per block list: about one observation per thread of a k_intr_fk workgroup
     int lmax = 1;
     for (int b = 0; b <= NB_; ++b) lmax = std::max(lmax, boff[b + 1] - boff[b]);
-    intr_nsl_ = std::max(1, std::min(32, (lmax + kIntrFkThreads - 1) / kIntrFkThreads));
+    intr_nsl_ = std::max(1, std::min(32, (lmax + 255) / 256));
   }
   if (host_timing) DevMark(s, 1);
   stg.Flush(s);
