@@ -3368,6 +3368,7 @@ __device__ __forceinline__ void tile_dinv_post(TileShared& sh, double* zp, int K
 // Per-phase absolute times (SG_STAMP=1 builds; tools/phase_trace.py): d.stamps[64 + (wg 128 + K) 16 + slot],
 // slots 0-7 the waves' barrier arrivals, 8-12 the owner's chain (start, after (0), TRSM, D update, factor).
 constexpr int kTraceK = 128;
+constexpr int kUlStamp = 64 + 2 * kTraceK * 16;   // k_update_lin's stamps (after the phase trace)
 #define SG_PTRACE(K, slot)                                                                  \
   if (kStamp && lane == 0 && (K) < kTraceK)                                                \
     d.stamps[64 + ((size_t)blockIdx.x * kTraceK + (K)) * 16 + (slot)] = __builtin_amdgcn_s_memtime();
@@ -4795,19 +4796,36 @@ __global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_update_lin(Dev d) {
   lds_fence_wave();
   double cost = 0.0, gmax = 0.0;
   double model = 0.0, candcost = 0.0, candfail = 0.0, step2 = 0.0, candx2 = 0.0;
+  // SG_STAMP=1: lane 0 of the mid-grid and the last workgroup time their steps (d.stamps[kUlStamp + 8 w + k])
+  const int stw = !d.stamps || lane != 0 ? -1
+                  : blockIdx.x == gridDim.x / 2 ? 0 : blockIdx.x == gridDim.x - 1 ? 1 : -1;
+  unsigned long long tl = 0;
+  auto ul_stamp = [&](int k) {
+    if (stw < 0) return;
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+    if (k >= 0) d.stamps[kUlStamp + 8 * stw + k] += t - tl;
+    tl = t;
+  };
+  ul_stamp(-1);
   if (!ch.wide) {
     for (int r = ch.r0; r < ch.r1; ++r) {
       const LinRound R = d.lrounds[r];
       PuObs ob;
       pu_pass1(d, cur, R, lane, ua, ob);
       lds_fence_wave();
+      ul_stamp(0);
       pu_pass2(d, R.p0, R.p1, lane, cur, nxt, ua, xps, Xns, step2, candx2);
       lds_fence_wave();
+      ul_stamp(1);
       ul_obs(d, R, ch, lane, nxt, ob, xps, Xns, pacc, camacc, lsum, model, cost, candcost, candfail);
       lds_fence_wave();
+      ul_stamp(2);
       ul_points(d, R.p0, R.p1, lane, nxt, pacc, gmax);
       lds_fence_wave();
+      ul_stamp(3);
       ul_unit_scalars(d, ch.u0 + (r - ch.r0), lane, model, candcost, candfail, step2, candx2);
+      ul_stamp(4);
     }
   } else {
     // one point over several rounds: its back substitution needs every piece's A_p^T u first
@@ -4845,6 +4863,8 @@ __global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_update_lin(Dev d) {
     sc[kXnorm2 * ns] = 0.0;
     sc[kGmax * ns] = gmax;
   }
+  ul_stamp(5);
+  if (stw >= 0) d.stamps[kUlStamp + 8 * stw + 6] += 1;   // launches stamped
 }
 
 __device__ void decide_step(LmState& s, const double* u, const double* c);
@@ -6006,7 +6026,7 @@ void BaSolver::Load(const sg_problem& p) {
     kpart_.Resize((size_t)(NB_ + 1) * ncam_ * 42);
   }
   stamp_on_ = getenv("SG_STAMP") && getenv("SG_STAMP")[0] == '1';
-  if (stamp_on_) stamps_.Resize(64 + 2 * 128 * 16);
+  if (stamp_on_) stamps_.Resize(kUlStamp + 16);
   lap("resize");
   ResetState(s);
   if (host_timing) DevMark(s, 3);
