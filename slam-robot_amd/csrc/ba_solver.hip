@@ -4776,6 +4776,7 @@ __device__ __forceinline__ void ul_unit_scalars(const Dev& d, int unit, int lane
   model = candcost = candfail = step2 = candx2 = 0.0;
 }
 
+template <bool kStamp>
 __global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_update_lin(Dev d) {
   const LmState* st = d.st;
   if (st->done) return;
@@ -4796,8 +4797,9 @@ __global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_update_lin(Dev d) {
   lds_fence_wave();
   double cost = 0.0, gmax = 0.0;
   double model = 0.0, candcost = 0.0, candfail = 0.0, step2 = 0.0, candx2 = 0.0;
-  // SG_STAMP=1: lane 0 of the mid-grid and the last workgroup time their steps (d.stamps[kUlStamp + 8 w + k])
-  const int stw = !d.stamps || lane != 0 ? -1
+  // SG_STAMP=1 (the kStamp build): lane 0 of the mid-grid and the last workgroup time their steps
+  // (d.stamps[kUlStamp + 8 w + k])
+  const int stw = !kStamp || !d.stamps || lane != 0 ? -1
                   : blockIdx.x == gridDim.x / 2 ? 0 : blockIdx.x == gridDim.x - 1 ? 1 : -1;
   unsigned long long tl = 0;
   auto ul_stamp = [&](int k) {
@@ -6659,10 +6661,14 @@ void BaSolver::EnqueueIterations(int n) {
     TimedLaunchEnd(kKChol);
     if (nk_) hipLaunchKernelGGL(k_intr_step, dim3(1), dim3(64), 0, stream_, d);
     TimedLaunchBegin(kKPointUpd);
-    if (spec_)
-      hipLaunchKernelGGL(k_update_lin, dim3(std::max(nlin_, 1)), dim3(kLinThreads), 0, stream_, d);
-    else
+    if (spec_) {
+      if (stamp_on_)
+        hipLaunchKernelGGL(k_update_lin<true>, dim3(std::max(nlin_, 1)), dim3(kLinThreads), 0, stream_, d);
+      else
+        hipLaunchKernelGGL(k_update_lin<false>, dim3(std::max(nlin_, 1)), dim3(kLinThreads), 0, stream_, d);
+    } else {
       hipLaunchKernelGGL(k_point_update, dim3(std::max(npu_, 1)), dim3(kLinThreads), 0, stream_, d);
+    }
     TimedLaunchEnd(kKPointUpd);
     const bool multi = comm_ && comm_->nranks() > 1;
     // the candidate's camera blocks and linearization scalars beside the update scalars, one launch; on one rank
