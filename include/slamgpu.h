@@ -248,6 +248,8 @@ typedef struct sg_ba_info {
                                                 (dissected band; 0: one workgroup) */
   int32_t num_allreduces;                    /* landmark-shard sum all-reduces this handle has issued in LM
                                                 iterations (0 on one rank) */
+  int32_t lin_waves;                         /* waves per Jacobian-sweep chunk (1, or 2 when the doubled grid
+                                                fits the device at once) */
 } sg_ba_info;
 int sg_ba_info_get(const sg_ba* h, sg_ba_info* out);
 

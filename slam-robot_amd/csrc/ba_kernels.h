@@ -106,8 +106,10 @@ struct WideSeg {
 // camera blocks fit one window of <= kLinNbMax blocks, split into rounds of <= kLinObs observations and
 // <= kLinPts points that hold whole points (one observation per lane).  A point with more observations, or
 // spanning more blocks, is a "wide" chunk of its own: rounds are pieces of it and its camera terms go to
-// global atomics.
-constexpr int kLinThreads = 64;
+// global atomics.  A chunk's workgroup has one or two waves (BaSolver::lin_waves_, fixed at load: two when the
+// grid would leave SIMDs idle): wave w takes rounds r0 + w, r0 + w + 2, ... into LDS accumulators of its own,
+// summed in wave order at the end (a wide chunk runs on wave 0).
+constexpr int kLinThreads = 64;   // lanes of one wave (one observation per lane)
 constexpr int kLinObs = 64;
 constexpr int kLinPts = 16;
 constexpr int kLinNbMax = 24;

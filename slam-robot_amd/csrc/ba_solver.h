@@ -196,6 +196,9 @@ class BaSolver {
   DBuf<uint16_t> llist_d_;
   DBuf<double> lin_scal_;
   int nlin_ = 0;
+  int lin_waves_ = 1;   // waves per k_linearize / k_update_lin chunk (2 when 2 nlin_ waves fit the chip at once)
+  void LaunchLinearize(const Dev& d);
+  void LaunchUpdateLin(const Dev& d);
   int npu_ = 0;
   DBuf<double> seg_fail_;
   int nseg_ = 0, nwide_ = 0, nstile_ = 0;

@@ -297,18 +297,49 @@ __device__ __forceinline__ void lds_fence_wave() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
-__global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_linearize(Dev d) {
+// The chunk's camera partial (the waves' window accumulators summed in wave order) into its cam_slab slot, and
+// wave 1's six chunk scalars into wave 0's (sums in wave order, gmax a maximum).  Every thread of the
+// workgroup calls it (a workgroup barrier).
+template <int kW>
+__device__ __forceinline__ void lin_combine_waves(double* slab, double (*camacc_w)[kLinNbMax * kCamV], int ncv,
+                                                  double* wscal, int wv, int lane, double& s0, double& s1,
+                                                  double& s2, double& s3, double& s4, double& gmax) {
+  if (kW == 1) {
+    for (int i = lane; i < ncv; i += kLinThreads) slab[i] = camacc_w[0][i];
+    return;
+  }
+  if (wv == 1 && lane == 0) {
+    wscal[0] = s0; wscal[1] = s1; wscal[2] = s2; wscal[3] = s3; wscal[4] = s4; wscal[5] = gmax;
+  }
+  lds_barrier();
+  for (int i = threadIdx.x; i < ncv; i += kLinThreads * kW) slab[i] = camacc_w[0][i] + camacc_w[kW - 1][i];
+  if (wv == 0) {
+    s0 += wscal[0]; s1 += wscal[1]; s2 += wscal[2]; s3 += wscal[3]; s4 += wscal[4];
+    gmax = fmax(gmax, wscal[5]);
+  }
+}
+
+template <int kW>
+__global__ __launch_bounds__(kLinThreads * kW) SG_LIN_ATTR void k_linearize(Dev d) {
   const LmState* st = d.st;
   if (st->done || !st->need_lin) return;
   const int cur = st->cur;
   const bool first = st->first != 0;
   const LinChunk ch = d.lchunks[blockIdx.x];
-  __shared__ double pacc[kLinPts * 14];         // point blocks of the round: V (10) | g (4)
-  __shared__ double camacc[kLinNbMax * kCamV];  // camera blocks of the window: upper Jc^T Jc (21) | Jc^T r (6)
+  // per wave (wave w takes every kW-th round of the chunk, see LinChunk):
+  __shared__ double pacc_w[kW][kLinPts * 14];         // point blocks of the round: V (10) | g (4)
+  __shared__ double camacc_w[kW][kLinNbMax * kCamV];  // camera blocks of the window: upper Jc^T Jc | Jc^T r
   // the rarely-touched per-lane sums (failures, the fixed cost and |X|^2 of iteration 0) live in LDS, one slot
   // per lane, so they hold no registers across the projection (k_linearize's VGPR budget sets its occupancy)
-  __shared__ double lsum[4][kLinThreads];       // fail, fixed, ffail, xn2
-  const int lane = threadIdx.x;
+  __shared__ double lsum_w[kW][4][kLinThreads];       // fail, fixed, ffail, xn2
+  __shared__ double wscal[8];                         // wave 1's chunk scalars
+  const int lane = threadIdx.x & (kLinThreads - 1), wv = threadIdx.x / kLinThreads;
+  double* pacc = pacc_w[wv];
+  double* camacc = camacc_w[wv];
+  double(*lsum)[kLinThreads] = lsum_w[wv];
+  // a wide chunk (one point in pieces) runs on wave 0 only
+  const int rstep = ch.wide ? 1 : kW, rbeg = ch.r0 + (ch.wide ? 0 : wv);
+  const bool active = !ch.wide || wv == 0;
   const double4* X4 = reinterpret_cast<const double4*>(d.X[cur]);
   const int ncv = ch.nb * kCamV;
   for (int i = lane; i < ncv; i += kLinThreads) camacc[i] = 0.0;
@@ -317,8 +348,12 @@ __global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_linearize(Dev d) {
   for (int k = 0; k < 4; ++k) lsum[k][lane] = 0.0;
   double cost = 0.0, gmax = 0.0;
   // per-observation inputs, software-pipelined one round ahead
-  LinRound R = d.lrounds[ch.r0];
-  int nobs = R.o1 - R.o0;
+  LinRound R{};
+  int nobs = 0;
+  if (active && rbeg < ch.r1) {
+    R = d.lrounds[rbeg];
+    nobs = R.o1 - R.o0;
+  }
   double2 n_uv = make_double2(0.0, 0.0);
   int n_f = 0, n_p = 0, n_m = 0;
   if (lane < nobs) {
@@ -329,14 +364,14 @@ __global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_linearize(Dev d) {
     n_m = d.obs_meta[o];
   }
   lds_fence_wave();
-  for (int r = ch.r0; r < ch.r1; ++r) {
+  for (int r = rbeg; active && r < ch.r1; r += rstep) {
     const double2 uv = n_uv;
     const int f = n_f, p = n_p, m = n_m;
     const bool fx = (m & kMetaFixed) != 0;
     const LinRound Rc = R;
     const int nc = nobs;
-    if (r + 1 < ch.r1) {
-      R = d.lrounds[r + 1];
+    if (r + rstep < ch.r1) {
+      R = d.lrounds[r + rstep];
       nobs = R.o1 - R.o0;
       if (lane < nobs) {
         const int o = R.o0 + lane;
@@ -447,14 +482,15 @@ __global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_linearize(Dev d) {
     }
   }
   lds_fence_wave();
-  for (int i = lane; i < ncv; i += kLinThreads) d.cam_slab[cur][ch.cam_off + i] = camacc[i];
   cost = wave_sum_full(cost);
-  const double fail = wave_sum_full(lsum[0][lane]);
-  const double fixed = wave_sum_full(lsum[1][lane]);
-  const double ffail = wave_sum_full(lsum[2][lane]);
-  const double xn2 = wave_sum_full(lsum[3][lane]);
+  double fail = wave_sum_full(lsum[0][lane]);
+  double fixed = wave_sum_full(lsum[1][lane]);
+  double ffail = wave_sum_full(lsum[2][lane]);
+  double xn2 = wave_sum_full(lsum[3][lane]);
   gmax = wave_max_full(gmax);
-  if (lane == 0) {
+  lin_combine_waves<kW>(d.cam_slab[cur] + ch.cam_off, camacc_w, ncv, wscal, wv, lane, cost, fail, fixed, ffail,
+                        xn2, gmax);
+  if (wv == 0 && lane == 0) {
     double* sc = d.lin_scal[cur] + blockIdx.x;   // structure of arrays: slot j at [j * nlin + chunk]
     const size_t ns = d.nlin;
     sc[kCost * ns] = cost;
@@ -4776,18 +4812,26 @@ __device__ __forceinline__ void ul_unit_scalars(const Dev& d, int unit, int lane
   model = candcost = candfail = step2 = candx2 = 0.0;
 }
 
-template <bool kStamp>
-__global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_update_lin(Dev d) {
+template <bool kStamp, int kW>
+__global__ __launch_bounds__(kLinThreads * kW) SG_LIN_ATTR void k_update_lin(Dev d) {
   const LmState* st = d.st;
   if (st->done) return;
   const int cur = st->cur, nxt = cur ^ 1;
   const LinChunk ch = d.lchunks[blockIdx.x];
   if (blockIdx.x == 0 && threadIdx.x == 0) d.st->spec_slot = nxt;   // (k_cam_reduce mode 1 reads it)
-  __shared__ double pacc[kLinPts * 14];         // candidate point blocks of the round: V (10) | g (4)
-  __shared__ double camacc[kLinNbMax * kCamV];  // candidate camera blocks of the window
-  __shared__ double lsum[2][kLinThreads];       // candidate failures: free, fixed observations
-  __shared__ double ua[kLinPts * 4], xps[kLinPts * 4], Xns[kLinPts * 4];   // A_p^T A_c x_c, x_p, X+ per point
-  const int lane = threadIdx.x;
+  // per wave (k_linearize's split of the chunk's rounds over its waves):
+  __shared__ double pacc_w[kW][kLinPts * 14];         // candidate point blocks of the round: V (10) | g (4)
+  __shared__ double camacc_w[kW][kLinNbMax * kCamV];  // candidate camera blocks of the window
+  __shared__ double lsum_w[kW][2][kLinThreads];       // candidate failures: free, fixed observations
+  __shared__ double ua_w[kW][kLinPts * 4], xps_w[kW][kLinPts * 4], Xns_w[kW][kLinPts * 4];
+  __shared__ double wscal[8];                         // wave 1's chunk scalars
+  const int lane = threadIdx.x & (kLinThreads - 1), wv = threadIdx.x / kLinThreads;
+  double* pacc = pacc_w[wv];
+  double* camacc = camacc_w[wv];
+  double(*lsum)[kLinThreads] = lsum_w[wv];
+  double* ua = ua_w[wv];     // A_p^T A_c x_c per point
+  double* xps = xps_w[wv];   // x_p
+  double* Xns = Xns_w[wv];   // X+
   const int ncv = ch.nb * kCamV;
   for (int i = lane; i < ncv; i += kLinThreads) camacc[i] = 0.0;
   for (int i = lane; i < kLinPts * 14; i += kLinThreads) pacc[i] = 0.0;
@@ -4799,7 +4843,7 @@ __global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_update_lin(Dev d) {
   double model = 0.0, candcost = 0.0, candfail = 0.0, step2 = 0.0, candx2 = 0.0;
   // SG_STAMP=1 (the kStamp build): lane 0 of the mid-grid and the last workgroup time their steps
   // (d.stamps[kUlStamp + 8 w + k])
-  const int stw = !kStamp || !d.stamps || lane != 0 ? -1
+  const int stw = !kStamp || !d.stamps || threadIdx.x != 0 ? -1
                   : blockIdx.x == gridDim.x / 2 ? 0 : blockIdx.x == gridDim.x - 1 ? 1 : -1;
   unsigned long long tl = 0;
   auto ul_stamp = [&](int k) {
@@ -4811,7 +4855,7 @@ __global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_update_lin(Dev d) {
   };
   ul_stamp(-1);
   if (!ch.wide) {
-    for (int r = ch.r0; r < ch.r1; ++r) {
+    for (int r = ch.r0 + wv; r < ch.r1; r += kW) {
       const LinRound R = d.lrounds[r];
       PuObs ob;
       pu_pass1(d, cur, R, lane, ua, ob);
@@ -4829,7 +4873,7 @@ __global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_update_lin(Dev d) {
       ul_unit_scalars(d, ch.u0 + (r - ch.r0), lane, model, candcost, candfail, step2, candx2);
       ul_stamp(4);
     }
-  } else {
+  } else if (wv == 0) {
     // one point over several rounds: its back substitution needs every piece's A_p^T u first
     for (int r = ch.r0; r < ch.r1; ++r) {
       PuObs ob;
@@ -4850,12 +4894,15 @@ __global__ __launch_bounds__(kLinThreads) SG_LIN_ATTR void k_update_lin(Dev d) {
     ul_unit_scalars(d, ch.u0, lane, model, candcost, candfail, step2, candx2);
   }
   lds_fence_wave();
-  for (int i = lane; i < ncv; i += kLinThreads) d.cam_slab[nxt][ch.cam_off + i] = camacc[i];
   cost = wave_sum_full(cost);
-  const double fail = wave_sum_full(lsum[0][lane]);
-  const double ffail = wave_sum_full(lsum[1][lane]);
+  double fail = wave_sum_full(lsum[0][lane]);
+  double ffail = wave_sum_full(lsum[1][lane]);
   gmax = wave_max_full(gmax);
-  if (lane == 0) {
+  // the same combine as k_linearize's (its fixed and |X|^2 sums are zero here)
+  double fixed = 0.0, xn2 = 0.0;
+  lin_combine_waves<kW>(d.cam_slab[nxt] + ch.cam_off, camacc_w, ncv, wscal, wv, lane, cost, fail, fixed, ffail,
+                        xn2, gmax);
+  if (wv == 0 && lane == 0) {
     double* sc = d.lin_scal[nxt] + blockIdx.x;   // k_linearize's scalars of the candidate (never iteration 0)
     const size_t ns = d.nlin;
     sc[kCost * ns] = cost;
@@ -5588,6 +5635,11 @@ void BaSolver::Load(const sg_problem& p) {
     }
   }
   nlin_ = (int)lchunks.size();
+  // two waves per chunk (its rounds split between them) while the doubled grid still fits the chip at three
+  // waves per SIMD (k_linearize's occupancy): config 2's ~1.5 k chunks; one wave per chunk when there are more
+  // chunks than that (config 5, the scaled sweep), where the second wave only adds the combine
+  lin_waves_ = 2 * (long long)nlin_ <= 12LL * ncu_ ? 2 : 1;
+  if (const char* e = getenv("SG_LIN_WAVES")) lin_waves_ = atoi(e) == 2 ? 2 : 1;   // A/B and tests
   std::vector<int32_t> pu_units;   // k_point_update work units: a round index, or -(chunk + 1) for wide chunks
   for (int c = 0; c < nlin_; ++c) {
     lchunks[c].u0 = (int)pu_units.size();   // k_update_lin writes the units' scalars
@@ -6541,7 +6593,7 @@ void BaSolver::EnqueueIterations(int n) {
     // the accepted point in the slot k_update_lin filled (k_linearize would exit at once: no launch)
     if (!spec_ || need_seq_) {
       TimedLaunchBegin(kKLin);
-      hipLaunchKernelGGL(k_linearize, dim3(std::max(nlin_, 1)), dim3(kLinThreads), 0, stream_, d);
+      LaunchLinearize(d);
       TimedLaunchEnd(kKLin);
     }
     // k_schur beside the camera reduction (see side_ in ba_solver.h)
@@ -6662,10 +6714,7 @@ void BaSolver::EnqueueIterations(int n) {
     if (nk_) hipLaunchKernelGGL(k_intr_step, dim3(1), dim3(64), 0, stream_, d);
     TimedLaunchBegin(kKPointUpd);
     if (spec_) {
-      if (stamp_on_)
-        hipLaunchKernelGGL(k_update_lin<true>, dim3(std::max(nlin_, 1)), dim3(kLinThreads), 0, stream_, d);
-      else
-        hipLaunchKernelGGL(k_update_lin<false>, dim3(std::max(nlin_, 1)), dim3(kLinThreads), 0, stream_, d);
+      LaunchUpdateLin(d);
     } else {
       hipLaunchKernelGGL(k_point_update, dim3(std::max(npu_, 1)), dim3(kLinThreads), 0, stream_, d);
     }
@@ -6713,10 +6762,33 @@ void BaSolver::Sweep(int n) {
   for (int it = 0; it < n; ++it) {
     hipLaunchKernelGGL(k_force_linearize, dim3(1), dim3(64), 0, stream_, st_.ptr);
     TimedLaunchBegin(kKLin);
-    hipLaunchKernelGGL(k_linearize, dim3(std::max(nlin_, 1)), dim3(kLinThreads), 0, stream_, d);
+    LaunchLinearize(d);
     TimedLaunchEnd(kKLin);
   }
   SG_HIP_CHECK(hipGetLastError());
+}
+
+void BaSolver::LaunchLinearize(const Dev& d) {
+  const dim3 grid(std::max(nlin_, 1));
+  if (lin_waves_ == 2)
+    hipLaunchKernelGGL(k_linearize<2>, grid, dim3(2 * kLinThreads), 0, stream_, d);
+  else
+    hipLaunchKernelGGL(k_linearize<1>, grid, dim3(kLinThreads), 0, stream_, d);
+}
+
+void BaSolver::LaunchUpdateLin(const Dev& d) {
+  const dim3 grid(std::max(nlin_, 1));
+  if (lin_waves_ == 2) {
+    if (stamp_on_)
+      hipLaunchKernelGGL((k_update_lin<true, 2>), grid, dim3(2 * kLinThreads), 0, stream_, d);
+    else
+      hipLaunchKernelGGL((k_update_lin<false, 2>), grid, dim3(2 * kLinThreads), 0, stream_, d);
+  } else {
+    if (stamp_on_)
+      hipLaunchKernelGGL((k_update_lin<true, 1>), grid, dim3(kLinThreads), 0, stream_, d);
+    else
+      hipLaunchKernelGGL((k_update_lin<false, 1>), grid, dim3(kLinThreads), 0, stream_, d);
+  }
 }
 
 std::vector<unsigned long long> BaSolver::Stamps() {
@@ -6892,6 +6964,7 @@ void BaSolver::Info(sg_ba_info* o) const {
   o->rank = comm_ ? comm_->rank() : 0;
   o->nranks = comm_ ? comm_->nranks() : 1;
   o->num_allreduces = nallreduce_;
+  o->lin_waves = lin_waves_;
 }
 
 double BaSolver::ReprojectMap(sg_map* m) {

@@ -684,6 +684,28 @@ def test_speculative_linearization_matches_two_pass_chain(gpu_lib, monkeypatch, 
         np.testing.assert_allclose(p1.t, p0.t, rtol=0, atol=1e-5)
 
 
+@pytest.mark.parametrize("spec", ["1", "0"])
+def test_two_wave_chunks_match_one_wave(gpu_lib, monkeypatch, spec):
+    """k_linearize / k_update_lin with a chunk's rounds split over two waves (the default at C2: 2 nlin waves
+    fit the chip) against one wave per chunk (SG_LIN_WAVES=1, config 5's choice).  The two waves' camera
+    partials and chunk scalars are summed once more at the end, so the sums differ by rounding: the same steps,
+    cost 1e-12 relative, poses 1e-10 / 1e-6 mm; the speculative and two-pass chains agree on each split."""
+    m = make_config("C2")
+    pa = ba.problem_from_map_frames(m, 48, 50, 2.0)
+    g = ba.BundleAdjuster()
+    g.load(pa.copy())
+    assert g.info()["lin_waves"] == 2
+    g.close()
+    s1, p1 = _solve_env(pa, {"SG_LIN_WAVES": "1", "SG_SPEC": spec}, monkeypatch)
+    s2, p2 = _solve_env(pa, {"SG_LIN_WAVES": "2", "SG_SPEC": spec}, monkeypatch)
+    assert s1["ok"] == s2["ok"] == 1 and s2["sync_timeouts"] == 0
+    for k in ("num_iterations", "num_successful_steps", "num_unsuccessful_steps", "termination"):
+        assert s1[k] == s2[k], k
+    assert abs(s1["final_cost"] - s2["final_cost"]) <= 1e-12 * s1["final_cost"]
+    np.testing.assert_allclose(p2.q, p1.q, rtol=0, atol=1e-10)
+    np.testing.assert_allclose(p2.t, p1.t, rtol=0, atol=1e-6)
+
+
 def test_speculative_solve_is_bitwise_reproducible_with_rejections(gpu_lib, monkeypatch):
     """The speculative chain in the benchmark regime past convergence (rejected and invalid steps: the current
     slot is re-reduced, the candidate slot overwritten) is deterministic: two fresh handles agree bit for bit."""
