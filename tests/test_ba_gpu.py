@@ -208,6 +208,7 @@ def test_c5_first_iterations_match_oracle(gpu_lib, oracle_lib):
     info = g.info()
     assert info["n"] == 6 * 198 and info["band_tiles"] <= 8
     assert info["cholesky"].startswith("tiled band")
+    assert info["lin_waves"] == 1   # ~10 k Jacobian-sweep chunks fill the chip with one wave each
     sg = g.solve(o)
     so = oracle_lib.solve(po, o, nthreads=min(16, os.cpu_count() or 1))
     assert sg["ok"] == so["ok"] == 1 and sg["sync_timeouts"] == 0
