@@ -4,11 +4,85 @@
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -Islam-robot_amd/csrc -Iinclude tools/schur_bench.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 #include "schur_tiles.h"
 using namespace sg;
+// Variants of the consumer loop (argv[1]): 0 the library's schur_wave_batch; 1 three operand buffers (point
+// t + 2's reads before point t's MFMAs); 2 no operand reads in the loop (point 0's operands for every point:
+// the MFMA issue and slot branches alone); 3 as 2 with every point over the whole window (kSchurTPW MFMAs per
+// wave and point: the cost per MFMA of the slot chain without its early exit).
+template <int W>
+__device__ __forceinline__ void wave_batch3(f64x4 (&acc)[kSchurTPW], const double* Xb, const double* wsh,
+                                            const int4* pinf, int npts, int lane) {
+  constexpr unsigned kNeed = schur_need(W);
+  const int4 pv = pinf[min(lane, npts - 1)];
+  double XA[kSchurTW], XB[kSchurTW], XC[kSchurTW];
+#pragma unroll
+  for (int j = 0; j < kSchurTW; ++j) XA[j] = XB[j] = XC[j] = 0.0;
+  double wa, wb, wc;
+  int ha, hb, hc;
+  schur_fetch<kNeed>(Xb, wsh, pv, 0, npts, lane, XA, wa, ha);
+  schur_fetch<kNeed>(Xb, wsh, pv, 1, npts, lane, XB, wb, hb);
+  for (int t = 0; t < npts; t += 3) {
+    schur_fetch<kNeed>(Xb, wsh, pv, t + 2, npts, lane, XC, wc, hc);
+    schur_mfma<W>(acc, XA, wa, ha);
+    schur_fetch<kNeed>(Xb, wsh, pv, t + 3, npts, lane, XA, wa, ha);
+    schur_mfma<W>(acc, XB, wb, hb);
+    schur_fetch<kNeed>(Xb, wsh, pv, t + 4, npts, lane, XB, wb, hb);
+    schur_mfma<W>(acc, XC, wc, hc);
+  }
+}
+template <int W>
+__device__ __forceinline__ void wave_batch_nofetch(f64x4 (&acc)[kSchurTPW], const double* Xb, const double* wsh,
+                                                   const int4* pinf, int npts, int lane, bool full) {
+  constexpr unsigned kNeed = schur_need(W);
+  const int4 pv = pinf[min(lane, npts - 1)];
+  double XA[kSchurTW];
+#pragma unroll
+  for (int j = 0; j < kSchurTW; ++j) XA[j] = 0.0;
+  double wa;
+  int ha;
+  schur_fetch<kNeed>(Xb, wsh, pv, 0, npts, lane, XA, wa, ha);
+  for (int t = 0; t < npts; ++t) {
+    const int h = full ? kSchurTW - 1 : __builtin_amdgcn_readlane(pv.w, t);
+    schur_mfma<W>(acc, XA, wa, h);
+  }
+}
+// mode 4: every slot of the window per point with no branches between the MFMAs (straight-line chain)
+template <int W, int S>
+__device__ __forceinline__ void slots_straight(f64x4 (&acc)[kSchurTPW], const double (&X)[kSchurTW], double wop) {
+  if constexpr (S < kSchurTPW && W + kSchurCWaves * S < kSchurAug) {
+    constexpr int u = W + kSchurCWaves * S;
+    constexpr int c = schur_aug_c(u), r = schur_aug_r(u);
+    if constexpr (r <= c) mfma_acc(acc[S], X[r], X[c]);
+    else mfma_acc(acc[S], X[c], wop);
+    slots_straight<W, S + 1>(acc, X, wop);
+  }
+}
+template <int W>
+__device__ __forceinline__ void wave_batch_straight(f64x4 (&acc)[kSchurTPW], const double* Xb, const double* wsh,
+                                                    const int4* pinf, int npts, int lane) {
+  constexpr unsigned kNeed = schur_need(W);
+  const int4 pv = pinf[min(lane, npts - 1)];
+  double XA[kSchurTW];
+#pragma unroll
+  for (int j = 0; j < kSchurTW; ++j) XA[j] = 0.0;
+  double wa;
+  int ha;
+  schur_fetch<kNeed>(Xb, wsh, pv, 0, npts, lane, XA, wa, ha);
+  for (int t = 0; t < npts; ++t) slots_straight<W, 0>(acc, XA, wa);
+}
+template <int W>
+__device__ __forceinline__ void run_variant(int mode, f64x4 (&acc)[kSchurTPW], const double* Xb, const double* wsh,
+                                            const int4* pinf, int npts, int lane) {
+  if (mode == 1) wave_batch3<W>(acc, Xb, wsh, pinf, npts, lane);
+  else if (mode == 4) wave_batch_straight<W>(acc, Xb, wsh, pinf, npts, lane);
+  else if (mode == 2 || mode == 3) wave_batch_nofetch<W>(acc, Xb, wsh, pinf, npts, lane, mode == 3);
+  else schur_wave_batch<W>(acc, Xb, wsh, pinf, npts, lane);
+}
 __global__ __launch_bounds__(256) void k_bench(const double* Xg, const int4* pg, int npts, int ntw, int reps,
-                                               double* out, unsigned long long* cyc) {
+                                               double* out, unsigned long long* cyc, int mode) {
   __shared__ double Xb[kSchurXCap + 64 * kSchurTW];
   __shared__ double wsh[4 * kSchurBatchPts];
   __shared__ int4 pinf[kSchurBatchPts];
@@ -22,10 +96,10 @@ __global__ __launch_bounds__(256) void k_bench(const double* Xg, const int4* pg,
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
   for (int r = 0; r < reps; ++r) {
     switch (cw) {
-      case 0: schur_wave_batch<0>(acc, Xb, wsh, pinf, npts, lane); break;
-      case 1: schur_wave_batch<1>(acc, Xb, wsh, pinf, npts, lane); break;
-      case 2: schur_wave_batch<2>(acc, Xb, wsh, pinf, npts, lane); break;
-      default: schur_wave_batch<3>(acc, Xb, wsh, pinf, npts, lane); break;
+      case 0: run_variant<0>(mode, acc, Xb, wsh, pinf, npts, lane); break;
+      case 1: run_variant<1>(mode, acc, Xb, wsh, pinf, npts, lane); break;
+      case 2: run_variant<2>(mode, acc, Xb, wsh, pinf, npts, lane); break;
+      default: run_variant<3>(mode, acc, Xb, wsh, pinf, npts, lane); break;
     }
   }
   mfma_drain();
@@ -35,7 +109,8 @@ __global__ __launch_bounds__(256) void k_bench(const double* Xg, const int4* pg,
   out[tid] = s;
   if (lane == 0) cyc[cw] = t1 - t0;
 }
-int main() {
+int main(int argc, char** argv) {
+  const int mode = argc > 1 ? atoi(argv[1]) : 0;
   std::vector<double> X(kSchurXCap);
   for (size_t i = 0; i < X.size(); ++i) X[i] = 1e-3 * (double)((i * 2654435761u) % 1000);
   std::vector<int4> P;
@@ -55,9 +130,9 @@ int main() {
   (void)hipMalloc(&out, 256 * 8); (void)hipMalloc(&cyc, 64);
   (void)hipMemcpy(Xg, X.data(), X.size() * 8, hipMemcpyHostToDevice);
   (void)hipMemcpy(pg, P.data(), P.size() * 16, hipMemcpyHostToDevice);
-  printf("%d points, %d tile + %d rhs MFMAs per pass (%.1f per wave-point)\n", npts, mf, mr, (mf + mr) / 4.0 / npts);
-  hipLaunchKernelGGL(k_bench, dim3(1), dim3(256), 0, 0, Xg, pg, npts, ntw, reps, out, cyc);
-  hipLaunchKernelGGL(k_bench, dim3(1), dim3(256), 0, 0, Xg, pg, npts, ntw, reps, out, cyc);
+  printf("mode %d: %d points, %d tile + %d rhs MFMAs per pass (%.1f per wave-point)\n", mode, npts, mf, mr, (mf + mr) / 4.0 / npts);
+  hipLaunchKernelGGL(k_bench, dim3(1), dim3(256), 0, 0, Xg, pg, npts, ntw, reps, out, cyc, mode);
+  hipLaunchKernelGGL(k_bench, dim3(1), dim3(256), 0, 0, Xg, pg, npts, ntw, reps, out, cyc, mode);
   (void)hipDeviceSynchronize();
   unsigned long long c[8];
   (void)hipMemcpy(c, cyc, 64, hipMemcpyDeviceToHost);
