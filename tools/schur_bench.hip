@@ -73,10 +73,48 @@ __device__ __forceinline__ void wave_batch_straight(f64x4 (&acc)[kSchurTPW], con
   schur_fetch<kNeed>(Xb, wsh, pv, 0, npts, lane, XA, wa, ha);
   for (int t = 0; t < npts; ++t) slots_straight<W, 0>(acc, XA, wa);
 }
+// mode 5: one dispatch per point (a switch on the wave's slot count) into a straight-line chain of that length
+template <int W, int S, int N>
+__device__ __forceinline__ void chain_n(f64x4 (&acc)[kSchurTPW], const double (&X)[kSchurTW], double wop) {
+  if constexpr (S < N && S < kSchurTPW && W + kSchurCWaves * S < kSchurAug) {
+    constexpr int u = W + kSchurCWaves * S;
+    constexpr int c = schur_aug_c(u), r = schur_aug_r(u);
+    if constexpr (r <= c) mfma_acc(acc[S], X[r], X[c]);
+    else mfma_acc(acc[S], X[c], wop);
+    chain_n<W, S + 1, N>(acc, X, wop);
+  }
+}
+template <int W, int N>
+__device__ __forceinline__ void chain_switch(f64x4 (&acc)[kSchurTPW], const double (&X)[kSchurTW], double wop, int ns) {
+  if constexpr (N <= kSchurTPW) {
+    if (ns == N) { chain_n<W, 0, N>(acc, X, wop); return; }
+    chain_switch<W, N + 1>(acc, X, wop, ns);
+  }
+}
+template <int W>
+__device__ __forceinline__ void wave_batch_dispatch(f64x4 (&acc)[kSchurTPW], const double* Xb, const double* wsh,
+                                                    const int4* pinf, int npts, int lane) {
+  constexpr unsigned kNeed = schur_need(W);
+  const int4 pv = pinf[min(lane, npts - 1)];
+  double XA[kSchurTW], XB[kSchurTW];
+#pragma unroll
+  for (int j = 0; j < kSchurTW; ++j) XA[j] = XB[j] = 0.0;
+  double wa, wb;
+  int ha, hb;
+  auto nsl = [](int jhi) { return (schur_aug_base(jhi + 1) - W + kSchurCWaves - 1) / kSchurCWaves; };
+  schur_fetch<kNeed>(Xb, wsh, pv, 0, npts, lane, XA, wa, ha);
+  for (int t = 0; t < npts; t += 2) {
+    schur_fetch<kNeed>(Xb, wsh, pv, t + 1, npts, lane, XB, wb, hb);
+    chain_switch<W, 1>(acc, XA, wa, nsl(ha));
+    schur_fetch<kNeed>(Xb, wsh, pv, t + 2, npts, lane, XA, wa, ha);
+    chain_switch<W, 1>(acc, XB, wb, nsl(hb));
+  }
+}
 template <int W>
 __device__ __forceinline__ void run_variant(int mode, f64x4 (&acc)[kSchurTPW], const double* Xb, const double* wsh,
                                             const int4* pinf, int npts, int lane) {
   if (mode == 1) wave_batch3<W>(acc, Xb, wsh, pinf, npts, lane);
+  else if (mode == 5) wave_batch_dispatch<W>(acc, Xb, wsh, pinf, npts, lane);
   else if (mode == 4) wave_batch_straight<W>(acc, Xb, wsh, pinf, npts, lane);
   else if (mode == 2 || mode == 3) wave_batch_nofetch<W>(acc, Xb, wsh, pinf, npts, lane, mode == 3);
   else schur_wave_batch<W>(acc, Xb, wsh, pinf, npts, lane);
