@@ -129,6 +129,15 @@ struct LinChunk {
   int32_t u0;         // its first k_point_update work unit (one per round; one for a wide chunk)
 };
 
+// Concurrency contract.  Two launches store the whole LmState from one thread while other workgroups of the
+// SAME launch read it: k_cam_reduce mode 2 (workgroup NB+1 takes the decision while workgroups 0..NB read
+// `done` and `spec_slot`) and k_schur with fin (workgroup 0 runs the finalize pass while the segments read `cur`,
+// `done`, `reuse_diag` and `radius`).  Within those launches the writer may change only `done` (a reader that
+// sees the old value does the work the next launch would discard anyway), `accepted`, the counters and the cost
+// bookkeeping; `cur`, `spec_slot`, `reuse_diag` and `radius` are changed only by launches in which nothing else
+// reads them (the decision of k_cam_reduce mode 2 flips `cur` / sets `radius` for the NEXT launch, and its
+// readers in that launch read `done` / `spec_slot` only).  An edit that breaks this must hand the readers their
+// fields through a separate word written by an earlier launch.
 struct LmState {
   // options (copied from sg_solver_options)
   int32_t max_iter, max_invalid, disable_term, jacobi;
@@ -223,7 +232,6 @@ struct Dev {
   double* work;                  // [n] solver scratch
   const int32_t* fd_pair;        // [NB][NB] (I<J): FrameDistance residual coupling blocks I and J, or -1
   int32_t assemble;              // this rank adds blockdiag(U) + FD + damping to S (rank 0 of a shard group)
-  int32_t dbg;                   // development switches (SG_DBG), 0 in production
   const int32_t* obs_pnt;        // [M] point (device order) of each observation
   const int32_t* obs_meta;       // [M] packed block / camera / freedom flags (kMeta*)
   const LinChunk* lchunks;       // [nlin] k_linearize workgroups

@@ -1,0 +1,668 @@
+// ba_schur.hip — point elimination and reduced-camera-system assembly (the SchurEliminator of Ceres 1.8's
+// SPARSE_SCHUR behind slam.cpp:489, restated on the matrix cores): k_schur (whitened point Jacobians, one
+// v_mfma_f64_16x16x4f64 per point and tile of S), k_schur_wide, the fixed-order reduce k_S_reduce, the landmark
+// shards' band packing k_S_pack, and the camera finalize pass k_cam_finalize (FrameDistance, slam.cpp:86-105).
+#include "ba_lm.h"
+
+namespace sg {
+
+__global__ __launch_bounds__(256) void k_cam_finalize(Dev d, int mode, int decide) {
+  __shared__ double lds[FinLds::kDoubles];
+  cam_finalize_body(d, mode, decide, FinLds::carve(lds));
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_schur: the point elimination S -= W V~^-1 W^T and rhs -= W V~^-1 g~, as batched rank-4 updates on the
+// matrix cores.
+//
+// For a free point p with damped, scaled block V~ = L L^T, whiten its camera Jacobians per block b of its
+// span:  E_{p,b} = L^-1 sum_{o of p in b} J~p,o^T J~c,o  (4 x 6; zero for a block it does not observe).
+// Then its Schur term over every block pair of its span is E_p^T E_p with E_p = [E_{p,b}]_b (4 x 6 span), and
+// its rhs term is E_p^T w_p with w_p = L^-1 g~ — one v_mfma_f64_16x16x4f64 per 16x16 tile of S the point
+// touches (K = 4: one point per MFMA).  Two observations of p in one block simply sum into one E_{p,b}.
+//
+// One workgroup (4 waves) per segment: consecutive points (device order: by first block) whose columns fit
+// a window of kSchurTW tiles of S.  The window's upper tiles stay in MFMA accumulators for the whole
+// segment — wave w owns tiles u = w + 4 s (column-major upper order) — so every tile of a segment is
+// written once, summed in point order (bitwise reproducible).  The segment streams through LDS in batches:
+//   1. thread per point: V~, L^-1, V~^-1 and t = V~^-1 g~ (for k_point_update), w = L^-1 g~;
+//   2. thread per cell (point, block of its span): E_{p,b} and its rhs term E_{p,b}^T w_p;
+//   3. every wave walks the batch's points: operands X_j[lane i + 16 k] = E_p[k][16 j + i] read straight
+//      from the cells, one MFMA per owned tile inside the point's span; the rhs threads (6 per block of the
+//      segment) add the cells' rhs terms.
+// Points spanning more than kSegNbMax blocks take k_schur_wide (observation pairs, global atomics).
+
+__device__ __forceinline__ void load_Jc_scaled(const Dev& d, const double* J, int o, int b, double* Jc) {
+  const double* sc = d.scale_c + 6 * b;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const double2 v = jload2(J, o, 1 + i);   // (pair 0: r)
+    Jc[2 * i] = v.x * sc[(2 * i) % 6];
+    Jc[2 * i + 1] = v.y * sc[(2 * i + 1) % 6];
+  }
+}
+__device__ __forceinline__ void load_Jp_scaled(const double* J, int o, const double4& s4, double* Jp) {
+  const double sp[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const double2 v = jload2(J, o, 7 + i);   // (pairs 0-6: r, Jc)
+    Jp[2 * i] = v.x * sp[(2 * i) % 4];
+    Jp[2 * i + 1] = v.y * sp[(2 * i + 1) % 4];
+  }
+}
+
+// Damped, scaled point block of point p: V~ = S V S + D^2 / radius (D^2 = clamped diag(S V S), refreshed
+// unless the step reuses it), its inverse and L^-1 (V~ = L L^T), t = V~^-1 g~, w = L^-1 g~; Vinv, tp and
+// diag_p go to global memory for k_point_update.  Returns false when V~ is not positive definite (Vi, Li NaN).
+__device__ __forceinline__ bool point_block(const Dev& d, const LmState* st, int p, double* Vi, double* Li,
+                                            double* w) {
+  const double* Vp = d.V[st->cur] + 10 * (size_t)p;
+  double V[10];
+#pragma unroll
+  for (int i = 0; i < 10; ++i) V[i] = Vp[i];
+  const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
+  const double sp[4] = {s4.x, s4.y, s4.z, s4.w};
+  const double4 g4 = reinterpret_cast<const double4*>(d.g[st->cur])[p];
+  const double gs[4] = {g4.x * sp[0], g4.y * sp[1], g4.z * sp[2], g4.w * sp[3]};
+  double dp[4];
+  if (!st->reuse_diag) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a) dp[a] = fmin(fmax(sp[a] * sp[a] * V[u4(a, a)], st->min_diag), st->max_diag);
+    reinterpret_cast<double4*>(d.diag_p)[p] = make_double4(dp[0], dp[1], dp[2], dp[3]);
+  } else {
+    const double4 d4 = reinterpret_cast<const double4*>(d.diag_p)[p];
+    dp[0] = d4.x; dp[1] = d4.y; dp[2] = d4.z; dp[3] = d4.w;
+  }
+  const double radius = st->radius;
+  double Vt[10];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (c >= a) Vt[u4(a, c)] = sp[a] * V[u4(a, c)] * sp[c] + (a == c ? dp[a] / radius : 0.0);
+  const bool ok = inv4_spd(Vt, Vi, Li);
+  if (!ok) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) Vi[i] = Li[i] = NAN;
+  }
+  double tp[4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    double s = 0.0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) s += sym4(Vi, a, c) * gs[c];
+    tp[a] = s;
+  }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    double s = 0.0;
+#pragma unroll
+    for (int c = 0; c <= a; ++c) s += Li[l4(a, c)] * gs[c];
+    w[a] = s;
+  }
+  double* Vo = d.Vinv + 10 * (size_t)p;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) Vo[i] = Vi[i];
+  reinterpret_cast<double4*>(d.tp)[p] = make_double4(tp[0], tp[1], tp[2], tp[3]);
+  return ok;
+}
+
+// The segment's batches run as a software pipeline over three wave groups, one LDS barrier per step:
+//   cell waves (kSchurCellWaves), step s: the operand tiles of batch s (buffer s % 2);
+//   the point wave, step s: the point blocks of batch s + 1 (point slot (s + 1) % 3);
+//   MFMA waves (kSchurCWaves), step s: batch s - 1 (buffer (s - 1) % 2, point slot (s - 1) % 3).
+// The groups run separate loops with the same barrier count, so the accumulators are not live elsewhere.
+struct SchurLds {
+  double X[2][kSchurXCap + 64 * kSchurTW];   // operand tiles of the batch's points; padding for over-reads
+  double L[3][kSchurBatchPts * 10];          // L^-1 of the batch's points
+  double w[3][kSchurBatchPts * 4];           // w = L^-1 g~
+  int4 pinf[3][kSchurBatchPts];              // first block, span, operand offset, last window tile (jhi)
+  int2 pob[3][kSchurBatchPts];               // observation of its first block (-1: cell records), first cell
+  uint8_t cmap[3][kSchurBatchCells];         // batch-local cell -> point
+  double red[kSchurThreads / 64];
+};
+
+// Point wave, thread t < npts of batch B: its point block, table entries and cell map.
+__device__ __forceinline__ double schur_points(const Dev& d, const LmState* st, const SchurBatch& B, int t,
+                                               double* Lsh, double* wsh, int4* pinf, int2* pob, uint8_t* cmap) {
+  if (t >= B.p1 - B.p0) return 0.0;
+  const int p = B.p0 + t;
+  const int2 pi = d.pinfo[p];
+  const int4 pm = d.pmx[p];   // operand offset, jhi, observation of the first block (-1), first cell
+  int span = pi.y & 0xff, jhi = pm.y;
+  double fail = 0.0;
+  if (d.pfree[p]) {
+    double Vi[10], Li[10], w[4];
+    if (!point_block(d, st, p, Vi, Li, w)) fail = 1.0;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) Lsh[10 * t + i] = Li[i];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) wsh[4 * t + a] = w[a];
+  } else {
+    span = 0;
+    jhi = -1;
+  }
+  pinf[t] = make_int4(pi.y >> 8, span, pm.x, jhi);
+  pob[t] = make_int2(pm.z, pm.w);
+  for (int k = 0; k < span; ++k) cmap[pm.w + k] = (uint8_t)t;
+  return fail;
+}
+
+// Cell waves: thread per cell (point p, block b) of batch B.  E_{p,b} = sum_o G_o J~c,o with
+// G_o = L^-1 J~p,o^T (4 x 2), written straight into the point's operand tiles: window column c = 6 b + a - c0w
+// goes to tile c >> 4, lane (c & 15) + 16 k.  A point observed once in every block of its span (obs sorted by
+// block at load) finds its observation at a fixed offset; others read the cell records.  The first and last
+// cell of a point also zero the columns of its tiles 0 .. jhi outside its span.
+// Each thread takes two cells per round and issues the loads of both (the common single-observation cells:
+// J pairs and scales) before either's arithmetic, so two cells' memory latencies overlap (the same
+// arithmetic in the same order as one cell at a time: the same bits).
+struct CellOps {
+  double2 jp[4], jc[6];
+  double4 s4;
+  double sc[6];
+};
+__device__ __forceinline__ void cell_load(const Dev& d, const double* J, int o, int b, int p, CellOps& c) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) c.jp[i] = jload2(J, o, 7 + i);   // (pairs 0-6: r, Jc)
+#pragma unroll
+  for (int i = 0; i < 6; ++i) c.jc[i] = jload2(J, o, 1 + i);   // (pair 0: r)
+  c.s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) c.sc[i] = d.scale_c[6 * b + i];
+}
+// E_{p,b} += (or =) the observation's G J~c from preloaded operands (load_Jp_scaled / load_Jc_scaled's
+// arithmetic)
+template <typename At>
+__device__ __forceinline__ void cell_apply(const CellOps& c, const double* L, int col0, bool first, At at) {
+  double G[4][2];
+  {
+    const double sp[4] = {c.s4.x, c.s4.y, c.s4.z, c.s4.w};
+    double Jp[8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      Jp[2 * i] = c.jp[i].x * sp[(2 * i) % 4];
+      Jp[2 * i + 1] = c.jp[i].y * sp[(2 * i + 1) % 4];
+    }
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      double g0 = 0.0, g1 = 0.0;
+#pragma unroll
+      for (int m = 0; m <= kk; ++m) {
+        g0 += L[l4(kk, m)] * Jp[m];
+        g1 += L[l4(kk, m)] * Jp[4 + m];
+      }
+      G[kk][0] = g0;
+      G[kk][1] = g1;
+    }
+  }
+  double Jc[12];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    Jc[2 * i] = c.jc[i].x * c.sc[(2 * i) % 6];
+    Jc[2 * i + 1] = c.jc[i].y * c.sc[(2 * i + 1) % 6];
+  }
+  if (first) {
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+      for (int a = 0; a < 6; ++a) at(col0 + a, kk) = G[kk][0] * Jc[a] + G[kk][1] * Jc[6 + a];
+  } else {
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+      for (int a = 0; a < 6; ++a) at(col0 + a, kk) += G[kk][0] * Jc[a] + G[kk][1] * Jc[6 + a];
+  }
+}
+__device__ __forceinline__ void schur_cells(const Dev& d, const double* J, const SchurBatch& B, int tid, int c0w,
+                                            const double* Lsh,
+                                            const int4* pinf, const int2* pob, const uint8_t* cmap, double* Xb) {
+  const int ncell = B.c1 - B.c0;
+  constexpr int kStride = 64 * kSchurCellWaves;
+  // cells per thread and round: 2 with four MFMA waves (their loads overlap); 1 with eight, whose register budget
+  // (three waves per SIMD) does not hold two cells' operands
+  constexpr int kCpt = kSchurCWaves > 4 ? 1 : 2;
+  for (int lc0 = tid; lc0 < ncell; lc0 += kCpt * kStride) {
+    // both cells' table entries and, for single-observation cells, their operand loads first
+    int tc[kCpt], bc[kCpt], oc[kCpt];
+    bool simple[kCpt];
+    CellOps ops[kCpt];
+#pragma unroll
+    for (int h = 0; h < kCpt; ++h) {
+      const int lc = lc0 + h * kStride;
+      simple[h] = false;
+      oc[h] = -1;
+      tc[h] = 0;
+      bc[h] = 0;
+      if (lc < ncell) {
+        const int t = cmap[lc];
+        const int4 pi = pinf[t];
+        const int2 po = pob[t];
+        tc[h] = t;
+        bc[h] = pi.x + (lc - po.y);
+        if (po.x >= 0) {
+          simple[h] = true;
+          oc[h] = po.x + (bc[h] - pi.x);
+          cell_load(d, J, oc[h], bc[h], B.p0 + t, ops[h]);
+        }
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < kCpt; ++h) {
+      const int lc = lc0 + h * kStride;
+      if (lc >= ncell) break;
+      const int t = tc[h];
+      const int4 pi = pinf[t];
+      const int b = bc[h];
+      const double* L = Lsh + 10 * t;
+      double* xp = Xb + pi.z;
+      const int col0 = 6 * b - c0w;
+      auto at = [&](int col, int k) -> double& { return xp[64 * (col >> 4) + 16 * k + (col & 15)]; };
+      if (b == pi.x)   // left margin: the columns of tiles 0 .. jhi before the span (the consumer reads them all)
+        for (int col = 0; col < col0; ++col)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) at(col, k) = 0.0;
+      if (b == pi.x + pi.y - 1)   // right margin: after the span, to the end of tile jhi
+        for (int col = col0 + 6; col < 16 * (pi.w + 1); ++col)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) at(col, k) = 0.0;
+      if (simple[h]) {
+        cell_apply(ops[h], L, col0, true, at);
+        continue;
+      }
+      const int4 ci = d.cells[B.c0 + lc];   // first observation (-1: none), point, (block << 16) | further, offset
+      const int o0 = ci.x;
+      const int k1 = ci.w;
+      const int k2 = ci.w + (ci.z & 0xffff);
+      if (o0 < 0) {
+#pragma unroll
+        for (int a = 0; a < 6; ++a)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) at(col0 + a, k) = 0.0;
+        continue;
+      }
+#pragma unroll 1
+      for (int k = k1 - 1; k < k2; ++k) {
+        const int o = k < k1 ? o0 : d.cell_obs[k];
+        CellOps c;
+        cell_load(d, J, o, b, B.p0 + t, c);
+        cell_apply(c, L, col0, k < k1, at);
+      }
+    }
+  }
+}
+
+// Diagnostic stamps (SG_STAMP=1): workgroup 0, lane 0 of the first cell wave (slots 32-36), the point wave
+// (35, 37) and the first MFMA wave (40-45) accumulate s_memtime deltas per phase.
+#define SG_SSTAMP(slot)                                                                  \
+  if (d.stamps && seg == 0 && lane == 0 && (wave == 0 || wave == kSchurCellWaves || wave == kSchurCellWaves + 1)) { \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime();                       \
+    d.stamps[(slot)] += now_ - last_;                                                    \
+    last_ = now_;                                                                        \
+  }
+// fin (one rank, after a solve's first iteration): workgroup 0 runs k_cam_finalize's pass (mode 0, taking an
+// accepted step's candidate blocks) beside the segments — independent work (the segments read the decision's
+// radius and slot, taken by the previous launch; the pass writes what k_S_reduce reads), one launch less.
+__global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d, int fin) {
+  const LmState* st = d.st;
+  __shared__ SchurLds sh;
+  static_assert(FinLds::kDoubles <= sizeof(sh.X) / sizeof(double), "the finalize pass's LDS fits the operand buffer");
+  if (fin && blockIdx.x == 0) {
+    cam_finalize_body(d, 0, 2, FinLds::carve(&sh.X[0][0]));
+    return;
+  }
+  const int seg = (int)blockIdx.x - fin;
+  if (seg >= d.nseg) return;
+  unsigned long long last_ = __builtin_amdgcn_s_memtime();
+  // the segment's descriptor load goes out beside LmState's (see k_S_reduce)
+  const SchurSeg sg = d.segs[seg];
+  if (st->done) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nbt = sg.bt1 - sg.bt0;
+  const int c0w = 16 * sg.t0;
+  double* slab = d.S_slab + sg.s_off;
+  double linfail = 0.0;
+  if (wave < kSchurCellWaves) {
+    SG_SSTAMP(32)
+    __syncthreads();
+    SG_SSTAMP(33)
+    for (int s = 0; s <= nbt; ++s) {
+      if (s < nbt)
+        schur_cells(d, d.J[st->cur], d.sbatch[sg.bt0 + s], tid, c0w, sh.L[s % 3], sh.pinf[s % 3], sh.pob[s % 3], sh.cmap[s % 3],
+                    sh.X[s & 1]);
+      SG_SSTAMP(34)
+      __syncthreads();
+      SG_SSTAMP(36)
+    }
+  } else if (wave == kSchurCellWaves) {
+    // the point wave
+    if (nbt > 0) linfail += schur_points(d, st, d.sbatch[sg.bt0], lane, sh.L[0], sh.w[0], sh.pinf[0], sh.pob[0], sh.cmap[0]);
+    __syncthreads();
+    for (int s = 0; s <= nbt; ++s) {
+      if (s + 1 < nbt) {
+        const int q = (s + 1) % 3;
+        linfail += schur_points(d, st, d.sbatch[sg.bt0 + s + 1], lane, sh.L[q], sh.w[q], sh.pinf[q], sh.pob[q],
+                                sh.cmap[q]);
+      }
+      SG_SSTAMP(35)
+      __syncthreads();
+      SG_SSTAMP(37)
+    }
+  } else {
+    // MFMA waves: wave cw owns the augmented window slots u = cw + kSchurCWaves s
+    const int cw = wave - kSchurCellWaves - 1;
+    f64x4 acc[kSchurTPW];
+#pragma unroll
+    for (int s = 0; s < kSchurTPW; ++s) acc[s] = f64x4{0.0, 0.0, 0.0, 0.0};
+    SG_SSTAMP(40)
+    __syncthreads();
+    SG_SSTAMP(41)
+    for (int s = 0; s <= nbt; ++s) {
+      if (s >= 1) {
+        const SchurBatch B = d.sbatch[sg.bt0 + s - 1];
+        const int npts = B.p1 - B.p0;
+        const double* Xb = sh.X[(s - 1) & 1];
+        const double* wsh = sh.w[(s - 1) % 3];
+        const int4* pinf = sh.pinf[(s - 1) % 3];
+        switch (cw) {
+#define SG_SCHUR_CASE(W) \
+          case W: schur_wave_batch<W>(acc, Xb, wsh, pinf, npts, lane); break;
+          SG_SCHUR_CASE(0) SG_SCHUR_CASE(1) SG_SCHUR_CASE(2) SG_SCHUR_CASE(3)
+#if SG_SCHUR_CW > 4
+          SG_SCHUR_CASE(4) SG_SCHUR_CASE(5) SG_SCHUR_CASE(6) SG_SCHUR_CASE(7)
+#endif
+#undef SG_SCHUR_CASE
+        }
+        SG_SSTAMP(42)
+      }
+      __syncthreads();
+      SG_SSTAMP(44)
+    }
+    mfma_drain();
+    switch (cw) {
+#define SG_SCHUR_CASE(W) \
+      case W: schur_store<W>(acc, slab, sg.ntw, lane); break;
+      SG_SCHUR_CASE(0) SG_SCHUR_CASE(1) SG_SCHUR_CASE(2) SG_SCHUR_CASE(3)
+#if SG_SCHUR_CW > 4
+      SG_SCHUR_CASE(4) SG_SCHUR_CASE(5) SG_SCHUR_CASE(6) SG_SCHUR_CASE(7)
+#endif
+#undef SG_SCHUR_CASE
+    }
+    SG_SSTAMP(45)
+  }
+  linfail = block_sum<kSchurThreads>(linfail, sh.red);
+  if (tid == 0) d.seg_fail[seg] = linfail;
+}
+
+// A point spanning more blocks than a segment window (a whole-map solve's long track): one workgroup, the
+// observation pairs (s <= t) of the point, each 6x6 block -A_c,s^T (P_s A_p,t^T) A_c,t into S_wide and the
+// rhs terms into rhs with global atomics (k_S_reduce adds both).
+__device__ __forceinline__ void schur_pair_add(double* dst, int ld, const double* Jcs, const double* Ps,
+                                               const double* Jpt, const double* Jct, bool same_obs,
+                                               bool same_blk, bool s_first) {
+  double M[2][2];
+#pragma unroll
+  for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      M[rr][u] = Ps[4 * rr] * Jpt[4 * u] + Ps[4 * rr + 1] * Jpt[4 * u + 1] + Ps[4 * rr + 2] * Jpt[4 * u + 2] +
+                 Ps[4 * rr + 3] * Jpt[4 * u + 3];
+  double N[6][2];
+#pragma unroll
+  for (int a = 0; a < 6; ++a)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) N[a][u] = Jcs[a] * M[0][u] + Jcs[6 + a] * M[1][u];
+#pragma unroll
+  for (int a = 0; a < 6; ++a)
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+      const double Tac = N[a][0] * Jct[c] + N[a][1] * Jct[6 + c];
+      const double Tca = N[c][0] * Jct[a] + N[c][1] * Jct[6 + a];
+      double v;
+      if (same_obs) v = Tac;
+      else if (same_blk) v = Tac + Tca;
+      else if (s_first) v = Tac;
+      else v = Tca;
+      atomicAdd(dst + a * ld + c, -v);
+    }
+}
+
+__global__ __launch_bounds__(kSchurThreads) void k_schur_wide(Dev d) {
+  const LmState* st = d.st;
+  if (st->done || (int)blockIdx.x >= d.nwide) return;
+  __shared__ double vinv[10], tpv[4];
+  const WideSeg ws = d.wsegs[blockIdx.x];
+  const int p = ws.p, tid = threadIdx.x;
+  if (!d.pfree[p]) return;
+  if (tid == 0) {
+    double Vi[10], Li[10], w[4];
+    d.seg_fail[d.nseg + blockIdx.x] = point_block(d, st, p, Vi, Li, w) ? 0.0 : 1.0;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) vinv[i] = Vi[i];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) tpv[a] = d.tp[4 * (size_t)p + a];
+  }
+  __syncthreads();
+  const int obs_lo = d.poff[p], obs_hi = d.poff[p + 1];
+  const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
+  const double* Jw = d.J[st->cur];
+  for (int o = obs_lo + tid; o < obs_hi; o += kSchurThreads) {
+    const int b = d.frame_block[d.obs_frame[o]];
+    if (b < 0) continue;
+    double Jp[8], Jc[12];
+    load_Jp_scaled(Jw, o, s4, Jp);
+    load_Jc_scaled(d, Jw, o, b, Jc);
+    const double e0 = Jp[0] * tpv[0] + Jp[1] * tpv[1] + Jp[2] * tpv[2] + Jp[3] * tpv[3];
+    const double e1 = Jp[4] * tpv[0] + Jp[5] * tpv[1] + Jp[6] * tpv[2] + Jp[7] * tpv[3];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) atomicAdd(d.rhs + 6 * b + a, -(Jc[a] * e0 + Jc[6 + a] * e1));
+  }
+  for (int k = ws.pair_lo + tid; k < ws.pair_hi; k += kSchurThreads) {
+    const int2 pr = d.pairs[k];
+    const int os = obs_lo + (pr.x >> 16), ot = obs_lo + (pr.x & 0xffff);
+    const int bs = pr.y >> 16, bt = pr.y & 0xffff;
+    double Jcs[12], Jct[12], Jpt[8], Jps[8], Ps[8];
+    load_Jc_scaled(d, Jw, os, bs, Jcs);
+    load_Jc_scaled(d, Jw, ot, bt, Jct);
+    load_Jp_scaled(Jw, ot, s4, Jpt);
+    load_Jp_scaled(Jw, os, s4, Jps);
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        double a = 0.0;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) a += Jps[4 * rr + m] * sym4(vinv, m, c);
+        Ps[4 * rr + c] = a;
+      }
+    const int I = bs < bt ? bs : bt, Jb = bs < bt ? bt : bs;
+    schur_pair_add(d.S_wide + (size_t)(6 * I) * d.n + 6 * Jb, d.n, Jcs, Ps, Jpt, Jct, os == ot, bs == bt, bs < bt);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// The camera-camera terms of the damped reduced system that do not come from the Schur complement:
+// blockdiag(U) (observation Jacobians) + FrameDistance diagonal and cross blocks + D^2 = diag/radius,
+// all Jacobi-scaled, for element (6I+a, 6J+c), J >= I.
+//
+// k_S_reduce: one workgroup per 16x16 tile (R <= C) of the band of S (the frame columns), then one per rhs
+// block.  A tile's partials (one per segment whose window covers it, in segment order) are split over the four
+// waves (partial k to wave k mod 4, every lane summing 4 elements, 8 partials in flight), the four wave sums
+// combined in wave order (deterministic); then each thread finishes one element: the wide-point accumulator
+// and, on the assembling rank, the camera-only terms.  S leaves here damped; elements below the diagonal of a
+// diagonal tile are written as 0 (no factorisation reads them).  Tiles outside the band are never written
+// (zero since the load).
+// amode: 0 this rank adds no camera-only terms (landmark shards: ranks > 0 in a solve's first iteration);
+// 1 blockdiag(U) of the summed camera blocks + FrameDistance + damping (one rank; rank 0 of shards in the
+// first iteration); 2 this rank's own camera blocks, the FrameDistance terms on rank 0, no damping (landmark
+// shards after the first iteration: summed with S in one exchange, k_cam_finalize mode 2 adds the damping).
+__global__ __launch_bounds__(256) void k_S_reduce(Dev d, int amode) {
+  // LmState is read beside the first work-list loads, not ahead of them: the done test comes after the
+  // partial walk (a finished solve's trailing launches walk once more; every other launch saves a round trip)
+  const LmState* st = d.st;
+  const int done = st->done;
+  const double radius = st->radius;
+  const int tid = threadIdx.x, lane = tid & 63, part = tid >> 6;
+  const int wv = blockIdx.x;
+  if (wv >= d.nstile + d.NB) return;
+  const int nf = 6 * d.NB;   // frame columns
+  if (wv < d.nstile) {
+    const int rc = d.stile[wv];
+    const int R = rc >> 16, C = rc & 0xffff;
+    const int i = 16 * R + (tid >> 4), j = 16 * C + (tid & 15);
+    const bool live = i < nf && j < nf;
+    const bool up = live && i <= j;
+    const size_t gi = (size_t)(live ? i : 0) * d.n + (live ? j : 0);
+    // epilogue operands first, so their round trips overlap the partial walk
+    const double e_acc = (up && d.nwide) ? d.S_wide[gi] : 0.0;
+    const int I = i / 6, a = i - 6 * (i / 6), Jb = j / 6, c = j - 6 * (j / 6);
+    double e_si = 0.0, e_sj = 0.0, e_u = 0.0, e_fd = 0.0, e_dg = 0.0, e_x = 0.0;
+    const bool fd_here = amode == 1 || (amode == 2 && d.rank == 0);
+    if (amode != 0 && up) {
+      e_si = d.scale_c[i];
+      e_sj = d.scale_c[j];
+      if (I == Jb) {
+        e_u = (amode == 2 ? d.xcam_loc : d.xchg_cam)[(size_t)I * kCamV + u6(a, c)];
+        e_fd = (fd_here && a >= 3 && c >= 3) ? d.fd_D[9 * I + 3 * (a - 3) + (c - 3)] : 0.0;
+        e_dg = (amode == 1 && a == c) ? d.diag_c[i] : 0.0;
+      } else if (fd_here && a >= 3 && c >= 3) {
+        const int dd = d.fd_pair[I * d.NB + Jb];
+        if (dd >= 0) {
+          const double* Xd = d.fd_X + 9 * dd;   // J_a J_b^T, rows: frame a's translation
+          e_x = d.frame_block[d.fd_a[dd]] == I ? Xd[3 * (a - 3) + (c - 3)] : Xd[3 * (c - 3) + (a - 3)];
+        }
+      }
+    }
+    const int j0 = d.s_loff[wv], j1 = d.s_loff[wv + 1];
+    __shared__ double wsum[4][256];
+    double s[4] = {0.0, 0.0, 0.0, 0.0};
+    constexpr int kSR = 8;
+    for (int base = j0 + part; base < j1; base += 4 * 64) {
+      const int cnt = min(64, (j1 - base + 3) / 4);
+      const int myoff = d.s_lidx[lane < cnt ? base + 4 * lane : j0];
+      for (int k = 0; k < cnt; k += kSR) {
+        double v[kSR][4];
+#pragma unroll
+        for (int u = 0; u < kSR; ++u) {
+          const double* src = d.S_slab + __builtin_amdgcn_readlane(myoff, min(k + u, 63)) + lane;
+#pragma unroll
+          for (int m = 0; m < 4; ++m) v[u][m] = src[64 * m];
+        }
+#pragma unroll
+        for (int u = 0; u < kSR; ++u)
+          if (k + u < cnt)
+#pragma unroll
+            for (int m = 0; m < 4; ++m) s[m] += v[u][m];
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) wsum[part][lane + 64 * m] = s[m];
+    __syncthreads();
+    if (done || !live) return;
+    if (!up) {
+      d.S[gi] = 0.0;
+      if (d.nwide) d.S_wide[gi] = 0.0;   // schur_pair_add also adds a diagonal block's lower half: keep it clean
+      return;
+    }
+    double t = ((wsum[0][tid] + wsum[1][tid]) + wsum[2][tid]) + wsum[3][tid];
+    t += e_acc;
+    if (d.nwide) d.S_wide[gi] = 0.0;
+    if (amode != 0) {   // assembly_term, from the prefetched operands
+      double v;
+      if (I == Jb) {
+        v = (e_u + e_fd) * (e_si * e_sj);
+        if (a == c) v += e_dg / radius;
+      } else {
+        v = e_x * e_si * e_sj;
+      }
+      t += v;
+    }
+    d.S[gi] = t;
+    return;
+  }
+  // rhs block I: one wave per 64-entry chunk of its partial list (in list order), lanes 0..5
+  const int I = wv - d.nstile;
+  // speculative linearization: clear block I of the candidate slot's wide-chunk camera accumulator before
+  // k_update_lin adds to it (k_cam_reduce keeps the current slot's)
+  if (d.spec && part == 1 && lane < kCamV) d.cam_wide[st->cur ^ 1][(size_t)I * kCamV + lane] = 0.0;
+  const int j0 = d.r_loff[I], j1 = d.r_loff[I + 1];
+  const int el = lane < 6 ? lane : 0;
+  const int ei = 6 * I + el;
+  const double e_acc = d.rhs[ei];
+  const double e_si = amode != 0 ? d.scale_c[ei] : 0.0, e_g = amode != 0 ? d.camg[ei] : 0.0;
+  __shared__ double rsum[4][6];
+  constexpr int kSR = 32;
+  double s = 0.0;
+  int myoff = d.r_lidx[(j0 + 64 * part + lane < j1) ? j0 + 64 * part + lane : 0];
+  for (int base = j0 + 64 * part; base < j1; base += 256) {
+    const int cnt = min(64, j1 - base);
+    const int nxt = d.r_lidx[(base + 256 + lane < j1) ? base + 256 + lane : 0];
+    for (int k = 0; k < cnt; k += kSR) {
+      double v[kSR];
+#pragma unroll
+      for (int u = 0; u < kSR; ++u) v[u] = d.S_slab[__builtin_amdgcn_readlane(myoff, min(k + u, 63)) + el];
+#pragma unroll
+      for (int u = 0; u < kSR; ++u)
+        if (k + u < cnt) s += v[u];
+    }
+    myoff = nxt;
+  }
+  if (lane < 6) rsum[part][lane] = s;
+  __syncthreads();
+  if (done || part != 0 || lane >= 6) return;
+  s = ((rsum[0][lane] + rsum[1][lane]) + rsum[2][lane]) + rsum[3][lane];
+  s += e_acc;
+  if (amode != 0) s += e_si * e_g;   // y = rhs_sub + S g_c
+  d.xc[ei] = s;       // local rhs partial (all-reduced with S); the wide accumulator is reset
+  d.rhs[ei] = 0.0;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Landmark shards: the part of S the Cholesky reads (per 16-row panel, columns kb .. band end, row-major)
+// and the rhs, packed into one contiguous buffer for the all-reduce and unpacked after it.  Outside the
+// band every rank's S holds exact zeros (k_S_reduce writes every block pair), so only the band travels.
+// Block (pk, y) of the grid copies panel pk (pk == npanel: the rhs).
+__global__ __launch_bounds__(256) void k_S_pack(double* S, int n, const int32_t* panel_jend, const int32_t* off,
+                                                int npanel, double* buf, int unpack) {
+  const int pk = blockIdx.x;
+  const int stride = 256 * gridDim.y;
+  if (pk == npanel) {
+    double* xc = S + (size_t)n * n;
+    for (int i = blockIdx.y * 256 + threadIdx.x; i < n; i += stride) {
+      if (unpack) xc[i] = buf[off[npanel] + i];
+      else buf[off[npanel] + i] = xc[i];
+    }
+    return;
+  }
+  const int kb = pk * kCholNb, w = min(kCholNb, n - kb), width = panel_jend[pk] - kb;
+  const int cnt = w * width;
+  for (int e = blockIdx.y * 256 + threadIdx.x; e < cnt; e += stride) {
+    const int r = e / width, c = e - r * width;
+    const size_t gi = (size_t)(kb + r) * n + kb + c;
+    if (unpack) S[gi] = buf[off[pk] + e];
+    else buf[off[pk] + e] = S[gi];
+  }
+}
+
+
+// ------------------------------------------------------------------------------------------------
+// host launchers (ba_launch.h)
+
+void LaunchCamFinalizeK(hipStream_t s, const Dev& d, int mode, int decide) {
+  hipLaunchKernelGGL(k_cam_finalize, dim3(1), dim3(256), 0, s, d, mode, decide);
+}
+
+void LaunchSchurK(int nseg, int nwide, int fin, hipStream_t s, const Dev& d) {
+  hipLaunchKernelGGL(k_schur, dim3(nseg + (fin ? 1 : 0)), dim3(kSchurThreads), 0, s, d, fin);
+  if (nwide) hipLaunchKernelGGL(k_schur_wide, dim3(nwide), dim3(kSchurThreads), 0, s, d);
+}
+
+void LaunchSReduceK(int grid, hipStream_t s, const Dev& d, int amode) {
+  hipLaunchKernelGGL(k_S_reduce, dim3(grid), dim3(256), 0, s, d, amode);
+}
+
+void LaunchSPackK(dim3 grid, hipStream_t s, double* S, int n, const int32_t* panel_jend, const int32_t* off,
+                  int npanel, double* Spk, int dir) {
+  hipLaunchKernelGGL(k_S_pack, grid, dim3(256), 0, s, S, n, panel_jend, off, npanel, Spk, dir);
+}
+
+}  // namespace sg

@@ -13,6 +13,7 @@
 #include "ba_kernels.h"
 #include "common.h"
 #include "dbuf.h"
+#include "hostio.h"
 #include "hostmirror.h"
 
 namespace sg {
@@ -58,22 +59,10 @@ class BaSolver {
  private:
   sg_device_options dev_;
   hipStream_t stream_ = nullptr;
-  // Schur elimination beside the camera reduction: after the first linearisation of a solve (the Jacobi scale
-  // of the camera columns is fixed from then on, slam.cpp's Ceres LM: jacobi_scaling), k_schur depends only on
-  // k_linearize, so it can run on side_ while k_cam_reduce, the camera all-reduce and k_cam_finalize run on
-  // stream_; k_S_reduce waits for both.  Measured slower on one GPU (C2 6042 -> 5690 it/s, C5 equal:
-  // tools/overlap_ab.sh, profiles/r3_v6_schur_overlap_ab.log): a k_schur workgroup's 140 KB of LDS leaves no
-  // room for the camera kernels on its CU, and the cross-stream event waits cost more than the overlap hides.
-  // Opt-in (SG_SCHUR_OVERLAP=1) for multi-GPU runs, where it hides the camera all-reduce behind k_schur.
-  hipStream_t side_ = nullptr;
   HostMirror mb_;   // mapped mailbox: [0, 1 KB) the LM state read back, then the solution download
   void ReadState(LmState* h);   // LmState via mb_ (a kernel writes it: no copy engine), stream synchronised
   void WaitStream(hipStream_t s);   // spin-wait for the stream's work (see ba_solver.hip)
   hipEvent_t ev_wait_ = nullptr;
-  // graph mode (SG_GRAPH=1): the captured LM iteration (ba_solver.hip, Iterate)
-  bool graph_ok_ = getenv("SG_GRAPH") && atoi(getenv("SG_GRAPH")) == 1;
-  hipGraphExec_t iter_exec_ = nullptr;
-  void DropGraph();
   void EnqueueIterations(int n);
   hipEvent_t dev_marks_[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};   // SG_HOST_TIMING: device times in Load
   hipEvent_t ev_idle_ = nullptr;                                            //   the stream last seen idle (MarkIdle)
@@ -82,8 +71,6 @@ class BaSolver {
   bool idle_valid_ = false;
   void MarkIdle(hipStream_t s);
   void DevMark(hipStream_t s, int i);
-  hipEvent_t ev_lin_ = nullptr, ev_schur_ = nullptr;
-  bool overlap_ok_ = getenv("SG_SCHUR_OVERLAP") && atoi(getenv("SG_SCHUR_OVERLAP")) == 1;
   bool need_seq_ = true;   // the next iteration is the first of a solve (it computes the camera scale)
   std::unique_ptr<Comm> comm_;
   bool loaded_ = false;
@@ -97,21 +84,9 @@ class BaSolver {
   DBuf<double> Wg_;            // its back-substitution tiles W_KJ = U_KK^-1 U_KJ (+ the bottom half's)
   int chol_nd_ = 0;            // dissected band: tile rows the second workgroup factors bottom-up (0: one WG)
   DBuf<int32_t> tflag_;        // dissected band hand-off counters {bottom done, top done}
-  int chol_simdmap_ = !(getenv("SG_CHOL_SIMDMAP") && atoi(getenv("SG_CHOL_SIMDMAP")) == 0);
   bool chol_cand_lds_ = false;   // candidate-pass operands staged in the Cholesky's LDS (small problems)
   // tests only: force the dissected Cholesky's separator wait to time out (k_chol_tiles flags bit 2)
   bool chol_force_tmo_ = getenv("SG_CHOL_FORCE_TIMEOUT") && atoi(getenv("SG_CHOL_FORCE_TIMEOUT")) != 0;
-  // owner look-ahead of the tiled Cholesky (k_chol_tiles kLa bit 0; default on: C2 69.9 -> 67.8 us, C5 188.9 ->
-  // 183.8 us, r3_v2 chol_ab); SG_CHOL_LOOKAHEAD=0 turns it off
-  bool chol_lookahead_ = !(getenv("SG_CHOL_LOOKAHEAD") && atoi(getenv("SG_CHOL_LOOKAHEAD")) == 0);
-  // diagonal-tile factorisation: 0 two pivots per LDS broadcast, 1 v_readlane pivot rows, 2 in registers with
-  // MFMA panel updates (tile_factor_mfma); SG_CHOL_FACTOR
-  int chol_factor_ = getenv("SG_CHOL_FACTOR") ? atoi(getenv("SG_CHOL_FACTOR")) : 0;
-  // Dinv mode of the tiled Cholesky (k_chol_tiles flags bit 5): SG_CHOL_DINV=1
-  bool chol_dinv_ = getenv("SG_CHOL_DINV") && atoi(getenv("SG_CHOL_DINV")) == 1;
-  // dataflow phase sync of the tiled Cholesky (k_chol_tiles kLa bit 4: per-row counters instead of a barrier
-  // per tile row; needs the look-ahead): SG_CHOL_DATAFLOW=1
-  bool chol_dataflow_ = getenv("SG_CHOL_DATAFLOW") && atoi(getenv("SG_CHOL_DATAFLOW")) == 1;
   bool pack_force_ = getenv("SG_PACK_S") != nullptr;   // pack/unpack S on one rank too (tests the path)
   // speculative linearization (k_update_lin: the candidate pass linearizes at the candidate; k_linearize runs
   // only in a solve's first iteration); SG_SPEC=0: k_point_update + k_linearize every iteration
@@ -208,6 +183,7 @@ class BaSolver {
   DBuf<int32_t> pinfo_, pmx_, cells_, cell_obs_, stile_;
   DBuf<double> rdg_;       // 1/U_jj of the factor
   DBuf<double> mk_, mq_, mt_, mX_, mobs_pt_, mobs_err_, mred_;
+  HostIo io_;   // ReprojectMap's uploads and downloads (hostio.h)
   double range_b_ = 4.0, fd_target_ = 150.0, fd_b2_ = 225.0;
   // timing
   bool timing_ = false;
@@ -219,8 +195,7 @@ class BaSolver {
   };
   std::vector<KTimer> timers_;
   void TimedLaunchBegin(int id);
-  void LaunchCholTiles(bool stamp, int la, dim3 grid, const Dev& d, int flags);
-  int CholTilesLa() const;
+  void LaunchCholTiles(bool stamp, dim3 grid, const Dev& d, int flags);
   void TimedLaunchEnd(int id);
   void TimedLaunchBegin(int id, hipStream_t s);
   void TimedLaunchEnd(int id, hipStream_t s);

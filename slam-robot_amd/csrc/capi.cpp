@@ -334,7 +334,7 @@ int sg_slam_reproject_map(sg_slam* s, sg_map* map, double* mean) {
 }
 
 static sg::MapOps& MapOpsOf(sg_slam* s) {
-  if (!s->mapops) s->mapops.reset(new sg::MapOps(s->dev));
+  if (!s->mapops) s->mapops.reset(new sg::MapOps(s->dev, s->solver->stream()));   // one stream per Slam object
   return *s->mapops;
 }
 

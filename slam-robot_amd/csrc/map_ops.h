@@ -6,12 +6,15 @@
 
 #include "common.h"
 #include "dbuf.h"
+#include "hostio.h"
 
 namespace sg {
 
 class MapOps {
  public:
-  explicit MapOps(const sg_device_options& dev);
+  // stream: the HIP stream to run on (the Slam facade passes its solver's, so the object uses one hardware
+  // queue); nullptr: a stream of its own
+  explicit MapOps(const sg_device_options& dev, hipStream_t stream = nullptr);
   ~MapOps();
   // LocalMap::Clean (localmap.cpp:283-398): returns the reference's bool (0 when observations were disabled).
   int Clean(sg_map* m, double error_threshold);
@@ -26,6 +29,8 @@ class MapOps {
   void Download(sg_map* m, bool X, bool unc);
   sg_device_options dev_;
   hipStream_t stream_ = nullptr;
+  bool own_stream_ = false;
+  HostIo io_;   // uploads / downloads without a copy engine (hostio.h)
   int P_ = 0, M_ = 0;
   int32_t counters_h_[2] = {1, 0};
   DBuf<double> k_, q_, t_, X_, unc_, obs_pt_, obs_err_;

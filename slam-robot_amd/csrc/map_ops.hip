@@ -352,16 +352,21 @@ __global__ __launch_bounds__(kThreads) void k_normalize(NormArgs a, double* q, d
 
 }  // namespace
 
-MapOps::MapOps(const sg_device_options& dev) : dev_(dev) {
+MapOps::MapOps(const sg_device_options& dev, hipStream_t stream) : dev_(dev) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) throw Error(SG_ENODEV, "no HIP device available");
   SG_REQUIRE(dev.device >= 0 && dev.device < ndev, SG_ENODEV, "device ordinal out of range");
   SG_HIP_CHECK(hipSetDevice(dev.device));
-  SG_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  if (stream) {
+    stream_ = stream;
+  } else {
+    SG_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    own_stream_ = true;
+  }
 }
 
 MapOps::~MapOps() {
-  if (stream_) (void)hipStreamDestroy(stream_);
+  if (own_stream_ && stream_) (void)hipStreamDestroy(stream_);
 }
 
 // Upload a LocalMap and list each point's observations in TrackedPoint::observations() order (two stable
@@ -390,38 +395,36 @@ void MapOps::Upload(const sg_map* m) {
   }
   hipStream_t s = stream_;
   SG_HIP_CHECK(hipSetDevice(dev_.device));
-  k_.Upload(std::vector<double>(m->k, m->k + 7 * (size_t)m->num_cameras), s);
-  q_.Upload(std::vector<double>(m->q, m->q + 4 * (size_t)F), s);
-  t_.Upload(std::vector<double>(m->t, m->t + 3 * (size_t)F), s);
-  fcam_.Upload(std::vector<int32_t>(m->frame_camera, m->frame_camera + F), s);
-  X_.Upload(std::vector<double>(m->X, m->X + 4 * (size_t)P), s);
-  flags_.Upload(std::vector<int32_t>(m->point_flags, m->point_flags + P), s);
-  unc_.Upload(std::vector<double>(m->point_uncertainty, m->point_uncertainty + P), s);
-  obs_pt_.Upload(std::vector<double>(m->obs_pt, m->obs_pt + 2 * (size_t)M), s);
-  obs_err_.Upload(std::vector<double>(m->obs_error, m->obs_error + 2 * (size_t)M), s);
-  obs_frame_.Upload(std::vector<int32_t>(m->obs_frame, m->obs_frame + M), s);
-  obs_dis_.Upload(std::vector<int32_t>(m->obs_disabled, m->obs_disabled + M), s);
-  poff_.Upload(poff, s);
-  pobs_.Upload(pobs.empty() ? std::vector<int32_t>{0} : pobs, s);
-  cand_.Resize(std::max(M, 1));
-  cand_.Zero(s);
-  changed_.Resize(std::max(P, 1));
-  changed_.Zero(s);
-  scal_.Resize(2);
-  scal_.Zero(s);
-  counters_.Upload(std::vector<int32_t>{1, 0}, s);
+  io_.Begin();
+  io_.Up(k_, m->k, 7 * (size_t)m->num_cameras);
+  io_.Up(q_, m->q, 4 * (size_t)F);
+  io_.Up(t_, m->t, 3 * (size_t)F);
+  io_.Up(fcam_, m->frame_camera, (size_t)F);
+  io_.Up(X_, m->X, 4 * (size_t)P);
+  io_.Up(flags_, m->point_flags, (size_t)P);
+  io_.Up(unc_, m->point_uncertainty, (size_t)P);
+  io_.Up(obs_pt_, m->obs_pt, 2 * (size_t)M);
+  io_.Up(obs_err_, m->obs_error, 2 * (size_t)M);
+  io_.Up(obs_frame_, m->obs_frame, (size_t)M);
+  io_.Up(obs_dis_, m->obs_disabled, (size_t)M);
+  io_.Up(poff_, poff);
+  io_.Up(pobs_, pobs);
+  io_.UpZero(cand_, (size_t)M);
+  io_.UpZero(changed_, (size_t)P);
+  io_.UpZero(scal_, 2);
+  io_.Up(counters_, std::vector<int32_t>{1, 0});
+  io_.FlushUp(s);
   P_ = P;
   M_ = M;
 }
 
 void MapOps::Download(sg_map* m, bool X, bool unc) {
-  hipStream_t s = stream_;
-  if (X && P_) SG_HIP_CHECK(hipMemcpyAsync(m->X, X_.ptr, 32 * (size_t)P_, hipMemcpyDeviceToHost, s));
-  if (unc && P_) SG_HIP_CHECK(hipMemcpyAsync(m->point_uncertainty, unc_.ptr, 8 * (size_t)P_, hipMemcpyDeviceToHost, s));
-  if (P_) SG_HIP_CHECK(hipMemcpyAsync(m->point_flags, flags_.ptr, 4 * (size_t)P_, hipMemcpyDeviceToHost, s));
-  if (M_) SG_HIP_CHECK(hipMemcpyAsync(m->obs_disabled, obs_dis_.ptr, 4 * (size_t)M_, hipMemcpyDeviceToHost, s));
-  SG_HIP_CHECK(hipMemcpyAsync(counters_h_, counters_.ptr, 8, hipMemcpyDeviceToHost, s));
-  SG_HIP_CHECK(hipStreamSynchronize(s));
+  if (X) io_.Down(m->X, X_.ptr, 32 * (size_t)P_);
+  if (unc) io_.Down(m->point_uncertainty, unc_.ptr, 8 * (size_t)P_);
+  io_.Down(m->point_flags, flags_.ptr, 4 * (size_t)P_);
+  io_.Down(m->obs_disabled, obs_dis_.ptr, 4 * (size_t)M_);
+  io_.Down(counters_h_, counters_.ptr, 8);
+  io_.FinishDown(stream_);
 }
 
 static MapDev MakeMapDev(DBuf<double>& k, DBuf<double>& q, DBuf<double>& t, DBuf<int32_t>& fcam, DBuf<double>& X,
@@ -471,19 +474,21 @@ void MapOps::Normalize(sg_map* m) {
   const int F = m->num_frames, P = m->num_points;
   hipStream_t s = stream_;
   SG_HIP_CHECK(hipSetDevice(dev_.device));
-  q_.Upload(std::vector<double>(m->q, m->q + 4 * (size_t)F), s);
-  t_.Upload(std::vector<double>(m->t, m->t + 3 * (size_t)F), s);
-  X_.Upload(std::vector<double>(m->X, m->X + 4 * (size_t)P), s);
+  io_.Begin();
+  io_.Up(q_, m->q, 4 * (size_t)F);
+  io_.Up(t_, m->t, 3 * (size_t)F);
+  io_.Up(X_, m->X, 4 * (size_t)P);
+  io_.FlushUp(s);
   NormArgs a{};
   for (int c = 0; c < 4; ++c) a.q0[c] = m->q[c];
   for (int c = 0; c < 3; ++c) a.t0[c] = m->t[c];
   hipLaunchKernelGGL(k_normalize, dim3((F + P + kThreads - 1) / kThreads), dim3(kThreads), 0, s, a, q_.ptr, t_.ptr,
                      X_.ptr, F, P);
   SG_HIP_CHECK(hipGetLastError());
-  SG_HIP_CHECK(hipMemcpyAsync(m->q, q_.ptr, 32 * (size_t)F, hipMemcpyDeviceToHost, s));
-  SG_HIP_CHECK(hipMemcpyAsync(m->t, t_.ptr, 24 * (size_t)F, hipMemcpyDeviceToHost, s));
-  if (P) SG_HIP_CHECK(hipMemcpyAsync(m->X, X_.ptr, 32 * (size_t)P, hipMemcpyDeviceToHost, s));
-  SG_HIP_CHECK(hipStreamSynchronize(s));
+  io_.Down(m->q, q_.ptr, 32 * (size_t)F);
+  io_.Down(m->t, t_.ptr, 24 * (size_t)F);
+  io_.Down(m->X, X_.ptr, 32 * (size_t)P);
+  io_.FinishDown(s);
 }
 
 int MapOps::ApplyEpipolarConstraint(sg_map* m) {

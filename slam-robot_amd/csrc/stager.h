@@ -31,7 +31,7 @@ struct StagePiece {
 // staging buffer, at the same offsets, and the pinned buffer is only rewritten after Clear() (next load) has
 // waited for the last batch's copy.
 // One workgroup column per piece (blockIdx.y); 16-byte copies for the aligned body, bytes for the tail.
-__global__ __launch_bounds__(256) void k_stage_scatter(const StagePiece* __restrict__ pieces,
+static __global__ __launch_bounds__(256) void k_stage_scatter(const StagePiece* __restrict__ pieces,
                                                        const unsigned char* __restrict__ stage) {
   const StagePiece pc = pieces[blockIdx.y];
   const unsigned char* src = stage + pc.off;

@@ -127,19 +127,27 @@ def test_host_communicator_failure_is_reported(gpu_lib):
     g.close()
 
 
-def test_bench_two_ranks_host_transport():
-    """bench.py's N > 1 path as the driver launches it (torch.distributed.run, one process per rank, barriers,
-    max-over-ranks timing, rank-0 JSON), rehearsed on one GPU through the host transport (--comm host): the line
-    is the strong-scaling figure of the metric's own config-2 problem, sharded over the two ranks, and the bench
-    survives a chain whose exchange timer is the largest per-iteration entry (it did not: KeyError 'exchange')."""
+@pytest.mark.parametrize("launch", ["torchrun", "self"])
+def test_bench_two_ranks_host_transport(launch):
+    """bench.py's N > 1 path, rehearsed on one GPU through the host transport (--comm host): one process per rank,
+    barriers, max-over-ranks timing, rank-0 JSON.  `torchrun` is the driver's form (torch.distributed.run around
+    bench.py); `self` is a plain `bench.py --gpus 2`, which must start its two rank processes itself instead of
+    running one rank and printing n_gpus 1.  The line is the strong-scaling figure of the
+    metric's own config-2 problem, sharded over the two ranks, and the bench survives a chain whose exchange timer
+    is the largest per-iteration entry (it did not: KeyError 'exchange')."""
     import json
     import subprocess
-    port = _free_port()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--steps", "5", "--warmup", "2", "--comm", "host", "--other", "0", "--cpu-runs", "0",
-           "--cpu-seconds", "0", "--frontend", "0", "--solve-all", "0", "--model-scaling", "0", "--weak", "0"]
+    args = [os.path.join(ROOT, "bench.py"),
+            "--gpus", "2", "--steps", "5", "--warmup", "2", "--comm", "host", "--other", "0", "--cpu-runs", "0",
+            "--cpu-seconds", "0", "--frontend", "0", "--solve-all", "0", "--model-scaling", "0", "--weak", "0"]
+    if launch == "torchrun":
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + args
+    else:
+        cmd = [sys.executable] + args
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])

@@ -1,7 +1,7 @@
 #!/bin/bash
-# One GPU session of round 4: GPU tests, smoke, the driver's bench line, the main.cpp replay (host phases of
+# One GPU session of round 5: GPU tests, smoke, the driver's bench line, the main.cpp replay (host phases of
 # every SolveFrames load), then the per-workload rocprofv3 evidence (tools/profile_round.sh).  Every GPU step
-# has its own time limit and the chain stops at the first failure.  Usage: r3_round.sh <tag> [skip-profile]
+# has its own time limit and the chain stops at the first failure.  Usage: r5_round.sh <tag> [skip-profile]
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"
 cd "$R"
@@ -30,17 +30,6 @@ if o: print("C5 %.1f it/s kernels %s model %s" % (o["value"], o["kernel_ms_per_i
 for k, v in (d.get("solve_all_frames") or {}).items():
     print("solve_all %s: %.1f it/s (%.3f ms), n %d, %s" % (k, v["iters_per_s"], v["ms_per_iter"], v["n"], v["cholesky"]))
 PY
-if [ -n "$R3_DIAG" ]; then
-  timeout -k 10 300 python tools/chol_ab.py 40 > gpurun_out/chol_ab_$TAG.log 2>&1 || { echo "chol_ab failed"; tail -20 gpurun_out/chol_ab_$TAG.log; exit 1; }
-  cat gpurun_out/chol_ab_$TAG.log
-  timeout -k 10 120 python tools/phase_trace.py C2 > gpurun_out/phase_trace_C2_$TAG.log 2>&1 || { echo "trace C2 failed"; tail -5 gpurun_out/phase_trace_C2_$TAG.log; exit 1; }
-  tail -25 gpurun_out/phase_trace_C2_$TAG.log
-  timeout -k 10 180 python tools/phase_trace.py C5 > gpurun_out/phase_trace_C5_$TAG.log 2>&1 || { echo "trace C5 failed"; tail -5 gpurun_out/phase_trace_C5_$TAG.log; exit 1; }
-  timeout -k 10 120 python tools/tile_stamps.py C2 > gpurun_out/tile_stamps_C2_$TAG.log 2>&1 || { echo "tile stamps failed"; tail -5 gpurun_out/tile_stamps_C2_$TAG.log; exit 1; }
-  cat gpurun_out/tile_stamps_C2_$TAG.log
-  timeout -k 10 120 python tools/tracker_stamps.py 7 > gpurun_out/tracker_stamps_$TAG.log 2>&1 || { echo "tracker stamps failed"; tail -5 gpurun_out/tracker_stamps_$TAG.log; exit 1; }
-  cat gpurun_out/tracker_stamps_$TAG.log
-fi
 timeout -k 10 300 python tools/parity_pins.py > gpurun_out/parity_pins_$TAG.json 2> gpurun_out/parity_pins_$TAG.err \
   || { echo "parity pins failed"; tail -5 gpurun_out/parity_pins_$TAG.err; exit 1; }
 SG_HOST_TIMING=1 timeout -k 10 300 python tools/e2e_replay.py gpurun_out/e2e_replay_$TAG.json > gpurun_out/e2e_$TAG.log 2> gpurun_out/e2e_phases_$TAG.log \
