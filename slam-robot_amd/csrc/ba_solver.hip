@@ -434,7 +434,8 @@ void BaSolver::Load(const sg_problem& p) {
   nlin_ = (int)lchunks.size();
   // two waves per chunk (its rounds split between them) while the doubled grid still fits the chip at three
   // waves per SIMD (k_linearize's occupancy): config 2's ~1.5 k chunks; one wave per chunk when there are more
-  // chunks than that (config 5, the scaled sweep), where the second wave only adds the combine
+  // chunks than that (config 5, the scaled sweep), where the second wave only adds the combine.  (A producer /
+  // consumer split of a chunk's rounds over two waves was measured slower at config 5: DESIGN.md 8.)
   lin_waves_ = 2 * (long long)nlin_ <= 12LL * ncu_ ? 2 : 1;
   if (const char* e = getenv("SG_LIN_WAVES")) lin_waves_ = atoi(e) == 2 ? 2 : 1;   // A/B and tests
   std::vector<int32_t> pu_units;   // k_point_update work units: a round index, or -(chunk + 1) for wide chunks

@@ -110,10 +110,64 @@ __device__ __forceinline__ void wave_batch_dispatch(f64x4 (&acc)[kSchurTPW], con
     chain_switch<W, 1>(acc, XB, wb, nsl(hb));
   }
 }
+// mode 6 / 7: one dispatch per BATCH (the wave's largest slot count over the batch's points) into a loop whose
+// body is a straight-line chain of that length for every point; the slots past a point's own prefix multiply
+// operand columns zeroed at the fetch (mode 6; mode 7 leaves them unmasked: timing only).  With points ordered by
+// (first block, last block) a batch's points share their last tile, so little is padded.
+template <bool kMask, unsigned kNeed>
+__device__ __forceinline__ void fetch_masked(const double* Xb, const double* wsh, const int4& pv, int t, int npts,
+                                             int lane, double (&X)[kSchurTW], double& wop) {
+  const int tt = min(t, npts - 1);
+  const int jhi = t < npts ? __builtin_amdgcn_readlane(pv.w, tt) : -1;
+  const double* xp = Xb + __builtin_amdgcn_readlane(pv.z, tt) + lane;
+#pragma unroll
+  for (int j = 0; j < kSchurTW; ++j)
+    if ((kNeed >> j) & 1u) {
+      const double v = xp[64 * j];
+      X[j] = (!kMask || j <= jhi) ? v : 0.0;
+    }
+  const double wv = wsh[4 * tt + (lane >> 4)];
+  wop = ((lane & 15) == 0 && t < npts) ? wv : 0.0;
+}
+template <int W, int N, bool kMask>
+__device__ __forceinline__ void batch_chain(f64x4 (&acc)[kSchurTPW], const double* Xb, const double* wsh,
+                                            const int4& pv, int npts, int lane) {
+  constexpr unsigned kNeed = schur_need(W);
+  double XA[kSchurTW], XB[kSchurTW];
+#pragma unroll
+  for (int j = 0; j < kSchurTW; ++j) XA[j] = XB[j] = 0.0;
+  double wa, wb;
+  fetch_masked<kMask, kNeed>(Xb, wsh, pv, 0, npts, lane, XA, wa);
+  for (int t = 0; t < npts; t += 2) {
+    fetch_masked<kMask, kNeed>(Xb, wsh, pv, t + 1, npts, lane, XB, wb);
+    chain_n<W, 0, N>(acc, XA, wa);
+    fetch_masked<kMask, kNeed>(Xb, wsh, pv, t + 2, npts, lane, XA, wa);
+    chain_n<W, 0, N>(acc, XB, wb);
+  }
+}
+template <int W, int N, bool kMask>
+__device__ __forceinline__ void batch_switch(f64x4 (&acc)[kSchurTPW], const double* Xb, const double* wsh,
+                                             const int4& pv, int npts, int lane, int ns) {
+  if constexpr (N <= kSchurTPW) {
+    if (ns == N) { batch_chain<W, N, kMask>(acc, Xb, wsh, pv, npts, lane); return; }
+    batch_switch<W, N + 1, kMask>(acc, Xb, wsh, pv, npts, lane, ns);
+  }
+}
+template <int W, bool kMask>
+__device__ __forceinline__ void wave_batch_runs(f64x4 (&acc)[kSchurTPW], const double* Xb, const double* wsh,
+                                                const int4* pinf, int npts, int lane) {
+  const int4 pv = pinf[min(lane, npts - 1)];
+  const int jmax = __builtin_amdgcn_readfirstlane(
+      __reduce_max_sync(~0ull, lane < npts ? pv.w : 0));
+  const int ns = (schur_aug_base(jmax + 1) - W + kSchurCWaves - 1) / kSchurCWaves;
+  batch_switch<W, 1, kMask>(acc, Xb, wsh, pv, npts, lane, ns);
+}
 template <int W>
 __device__ __forceinline__ void run_variant(int mode, f64x4 (&acc)[kSchurTPW], const double* Xb, const double* wsh,
                                             const int4* pinf, int npts, int lane) {
   if (mode == 1) wave_batch3<W>(acc, Xb, wsh, pinf, npts, lane);
+  else if (mode == 6) wave_batch_runs<W, true>(acc, Xb, wsh, pinf, npts, lane);
+  else if (mode == 7) wave_batch_runs<W, false>(acc, Xb, wsh, pinf, npts, lane);
   else if (mode == 5) wave_batch_dispatch<W>(acc, Xb, wsh, pinf, npts, lane);
   else if (mode == 4) wave_batch_straight<W>(acc, Xb, wsh, pinf, npts, lane);
   else if (mode == 2 || mode == 3) wave_batch_nofetch<W>(acc, Xb, wsh, pinf, npts, lane, mode == 3);
@@ -149,13 +203,14 @@ __global__ __launch_bounds__(256) void k_bench(const double* Xg, const int4* pg,
 }
 int main(int argc, char** argv) {
   const int mode = argc > 1 ? atoi(argv[1]) : 0;
+  const int homog = argc > 2 ? atoi(argv[2]) : -1;   // >= 0: every point ends in this window tile
   std::vector<double> X(kSchurXCap);
   for (size_t i = 0; i < X.size(); ++i) X[i] = 1e-3 * (double)((i * 2654435761u) % 1000);
   std::vector<int4> P;
   int xoff = 0, mf = 0, mr = 0;
   for (int t = 0; t < 21; ++t) {
     const int pf = t % 2, span = 6 + (t * 7) % 13;
-    const int jhi = (6 * (pf + span) - 1) / 16;
+    const int jhi = homog >= 0 ? homog : (6 * (pf + span) - 1) / 16;
     if (xoff + 64 * (jhi + 1) > kSchurXCap) break;
     P.push_back(make_int4(0, 0, xoff, jhi));
     xoff += 64 * (jhi + 1);
@@ -168,7 +223,7 @@ int main(int argc, char** argv) {
   (void)hipMalloc(&out, 256 * 8); (void)hipMalloc(&cyc, 64);
   (void)hipMemcpy(Xg, X.data(), X.size() * 8, hipMemcpyHostToDevice);
   (void)hipMemcpy(pg, P.data(), P.size() * 16, hipMemcpyHostToDevice);
-  printf("mode %d: %d points, %d tile + %d rhs MFMAs per pass (%.1f per wave-point)\n", mode, npts, mf, mr, (mf + mr) / 4.0 / npts);
+  printf("mode %d (homog %d): %d points, %d tile + %d rhs MFMAs per pass (%.1f per wave-point)\n", mode, homog, npts, mf, mr, (mf + mr) / 4.0 / npts);
   hipLaunchKernelGGL(k_bench, dim3(1), dim3(256), 0, 0, Xg, pg, npts, ntw, reps, out, cyc, mode);
   hipLaunchKernelGGL(k_bench, dim3(1), dim3(256), 0, 0, Xg, pg, npts, ntw, reps, out, cyc, mode);
   (void)hipDeviceSynchronize();
