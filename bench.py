@@ -631,15 +631,16 @@ REPLICATED = ("cam_finalize", "cholesky", "decide")   # every landmark shard run
 
 
 def model_scaling(local, full, full_kernel_ms, ns=(2, 4, 8), steps=20, warmup=3, allreduce_us=20.0, band_gbs=50.0,
-                  decide_us=4.0):
+                  decide_us=0.0):
     """Modelled strong scaling of a BA workload over N landmark shards, from measured kernel times.  Every shard of
     the N-way split (sg_problem_shard) is loaded alone on this GPU and timed with the multi-rank chain forced
     (SG_XCHG_MERGE=force: each rank assembles its own camera blocks into its partial S, the band of S travels
     packed with the camera gradient / diagonal / cost scalars in its tail, and the bookkeeping and damping follow
     the exchange; the pack and unpack kernels are timed as 'exchange').  A shard's iteration = its shardable
     kernels (linearize, camera reduce, Schur, S reduce, point update + next linearization, update reduce, pack /
-    unpack) + the replicated ones measured on the whole problem in the same chain (camera finalize, Cholesky)
-    + the separate decision launch of a multi-rank chain (`decide_us`) + two all-reduces per iteration (the
+    unpack) + the replicated ones measured on the whole problem in the same chain (camera finalize, Cholesky, the
+    decision launch k_decide, timed in the forced merged chain) + `decide_us` of any further unmeasured launch +
+    two all-reduces per iteration (the
     packed band with its tail, the step scalars) priced at `allreduce_us` each plus the band at `band_gbs`
     (assumptions, not measurements: RCCL over xGMI is not measurable on this 1-GPU box).  The slowest shard sets
     the pace."""

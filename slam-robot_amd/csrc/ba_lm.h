@@ -395,6 +395,42 @@ __device__ __forceinline__ void cam_finalize_body(const Dev& d, int mode, int de
     }
 }
 
+// The bookkeeping of k_cam_finalize mode 2 alone (merged landmark-shard chain, after the band exchange): the
+// gradient max-norm of the summed camera gradient and the ranks' point maxima, Ceres's iteration push, the
+// iteration count.  256 threads; red >= 4 doubles of LDS.  The damping of S's diagonal that mode 2 also does is
+// applied by the unpack that runs beside it (k_S_unpack_fin).
+__device__ __forceinline__ void fin_merged_bookkeeping(const Dev& d, double* red) {
+  LmState* st = d.st;
+  const int tid = threadIdx.x;
+  const int nf = 6 * d.NB;
+  const double* tg = d.xtail;
+  const double* txs = d.xtail + 2 * nf;
+  LmState s0;
+  if (tid == 0) s0 = *st;
+  const bool lin = st->need_lin;
+  if (st->done) return;
+  if (lin) {
+    double gm = 0.0;
+    for (int f = tid; f < d.F; f += 256) {
+      const int b = d.frame_block[f];
+      if (b < 0) continue;
+      if (d.rot_free[f])
+        for (int a = 0; a < 3; ++a) gm = fmax(gm, fabs(tg[6 * b + a]));
+      if (d.trans_free[f])
+        for (int a = 3; a < 6; ++a) gm = fmax(gm, fabs(tg[6 * b + a]));
+    }
+    gm = block_max<256>(gm, red);
+    if (tid == 0) {
+      double gmax = gm;
+      for (int r = 0; r < d.nranks; ++r) gmax = fmax(gmax, txs[kXNum + r]);
+      fin_push(s0, false, txs[kXCost] + txs[kXNum + d.nranks], gmax, txs, 0.0);
+    }
+  }
+  if (tid == 0) {
+    fin_count(s0);
+    *st = s0;
+  }
+}
 
 static __device__ void decide_step(LmState& s, const double* u, const double* c) {
   if (s.done) return;

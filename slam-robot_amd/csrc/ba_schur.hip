@@ -307,10 +307,13 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d, int fin) {
   __shared__ SchurLds sh;
   static_assert(FinLds::kDoubles <= sizeof(sh.X) / sizeof(double), "the finalize pass's LDS fits the operand buffer");
   if (fin && blockIdx.x == 0) {
-    cam_finalize_body(d, 0, 2, FinLds::carve(&sh.X[0][0]));
+    // fin 1 (one rank): the full pass, taking an accepted step's candidate blocks (decide 2); fin 2 (merged
+    // landmark shards): this rank's camera gradient / diagonal and FrameDistance terms into the exchange tail
+    // (mode 1; the decision was taken by k_decide before this launch)
+    cam_finalize_body(d, fin == 2 ? 1 : 0, fin == 2 ? 0 : 2, FinLds::carve(&sh.X[0][0]));
     return;
   }
-  const int seg = (int)blockIdx.x - fin;
+  const int seg = (int)blockIdx.x - (fin ? 1 : 0);
   if (seg >= d.nseg) return;
   unsigned long long last_ = __builtin_amdgcn_s_memtime();
   // the segment's descriptor load goes out beside LmState's (see k_S_reduce)
@@ -643,6 +646,51 @@ __global__ __launch_bounds__(256) void k_S_pack(double* S, int n, const int32_t*
   }
 }
 
+// Merged landmark-shard chain: the unpack of the summed band (k_S_pack's unpack) with k_cam_finalize mode 2 in
+// the same launch — the LM diagonal (D^2 from the summed camera diagonal of the exchange tail, clamped, or the
+// kept one when the step reuses it) divided by the radius added to each diagonal element as it is unpacked, and
+// the minimizer bookkeeping on the summed tail in one extra workgroup (fin_merged_bookkeeping).  The bookkeeping
+// changes no field the unpack reads (radius, reuse_diag, the diagonal clamps: LmState's concurrency contract).
+__global__ __launch_bounds__(256) void k_S_unpack_fin(Dev d, const int32_t* panel_jend, const int32_t* off,
+                                                      int npanel, const double* buf) {
+  const int pk = blockIdx.x;
+  if (pk == npanel + 1) {
+    __shared__ double red[4];
+    if (blockIdx.y == 0) fin_merged_bookkeeping(d, red);
+    return;
+  }
+  const int n = d.n;
+  const int stride = 256 * gridDim.y;
+  if (pk == npanel) {
+    double* xc = d.S + (size_t)n * n;
+    for (int i = blockIdx.y * 256 + threadIdx.x; i < n; i += stride) xc[i] = buf[off[npanel] + i];
+    return;
+  }
+  const LmState* st = d.st;
+  const double radius = st->radius, min_diag = st->min_diag, max_diag = st->max_diag;
+  const bool reuse = st->reuse_diag != 0;
+  const double* tdg = d.xtail + 6 * d.NB;
+  const int kb = pk * kCholNb, w = min(kCholNb, n - kb), width = panel_jend[pk] - kb;
+  const int cnt = w * width;
+  for (int e = blockIdx.y * 256 + threadIdx.x; e < cnt; e += stride) {
+    const int r = e / width, c = e - r * width;
+    const size_t gi = (size_t)(kb + r) * n + kb + c;
+    double v = buf[off[pk] + e];
+    if (r == c) {
+      const int i = kb + r;
+      double dg;
+      if (!reuse) {
+        const double s = d.scale_c[i];
+        dg = fmin(fmax(s * s * tdg[i], min_diag), max_diag);
+        d.diag_c[i] = dg;
+      } else {
+        dg = d.diag_c[i];
+      }
+      v += dg / radius;
+    }
+    d.S[gi] = v;
+  }
+}
 
 // ------------------------------------------------------------------------------------------------
 // host launchers (ba_launch.h)
@@ -654,6 +702,11 @@ void LaunchCamFinalizeK(hipStream_t s, const Dev& d, int mode, int decide) {
 void LaunchSchurK(int nseg, int nwide, int fin, hipStream_t s, const Dev& d) {
   hipLaunchKernelGGL(k_schur, dim3(nseg + (fin ? 1 : 0)), dim3(kSchurThreads), 0, s, d, fin);
   if (nwide) hipLaunchKernelGGL(k_schur_wide, dim3(nwide), dim3(kSchurThreads), 0, s, d);
+}
+
+void LaunchSUnpackFinK(dim3 grid, hipStream_t s, const Dev& d, const int32_t* panel_jend, const int32_t* off,
+                       int npanel, const double* Spk) {
+  hipLaunchKernelGGL(k_S_unpack_fin, dim3(grid.x + 1, grid.y), dim3(256), 0, s, d, panel_jend, off, npanel, Spk);
 }
 
 void LaunchSReduceK(int grid, hipStream_t s, const Dev& d, int amode) {

@@ -1378,13 +1378,18 @@ void BaSolver::EnqueueIterations(int n) {
     // end of every batch): the current blocks are in place.
     // One rank (no free intrinsics): the previous iteration's reduce took the decision (k_cam_reduce mode 2) and
     // this iteration's finalize pass runs inside the k_schur launch.
+    // Merged landmark shards (speculative chain): the pending decision as its own small launch (k_decide, which
+    // also makes an accepted candidate's blocks current), the finalize pass's mode 1 inside the k_schur launch,
+    // and its mode 2 inside the unpack after the band exchange (k_S_unpack_fin): two single-workgroup launches of
+    // the replicated chain less per iteration.
     const bool fin_in_schur = spec_ && !first_it && !multi_x && nk_ == 0 && !merged;
+    const bool fin1_in_schur = spec_ && merged;
     bool decide_in_fin = false;
     if (fin_in_schur) {
       // (nothing pending: the candidate blocks of an accepted step are taken by the pass)
     } else if (spec_ && !first_it) {
       if (pending_decision_) {
-        decide_in_fin = nk_ == 0 && (merged || !multi_x);
+        decide_in_fin = nk_ == 0 && !fin1_in_schur && (merged || !multi_x);
         if (!decide_in_fin) {
           TimedLaunchBegin(kKDecide);
           LaunchDecideK(stream_, d, 1);
@@ -1401,13 +1406,13 @@ void BaSolver::EnqueueIterations(int n) {
     if (nk_) {
       LaunchIntrLinearizeK(stream_, d, n_, nk_, NB_, ncam_, M_, intr_nsl_);
     }
-    if (!fin_in_schur) {
+    if (!fin_in_schur && !fin1_in_schur) {
       TimedLaunchBegin(kKCamFinal);
       LaunchCamFinalizeK(stream_, d, merged ? 1 : 0, decide_in_fin ? 1 : 0);
       TimedLaunchEnd(kKCamFinal);
     }
     TimedLaunchBegin(kKSchur);
-    LaunchSchurK(std::max(nseg_, 1), nwide_, fin_in_schur ? 1 : 0, stream_, d);
+    LaunchSchurK(std::max(nseg_, 1), nwide_, fin_in_schur ? 1 : (fin1_in_schur ? 2 : 0), stream_, d);
     TimedLaunchEnd(kKSchur);
     TimedLaunchBegin(kKSReduce);
     const int nwv = nstile_ + NB_;
@@ -1425,10 +1430,14 @@ void BaSolver::EnqueueIterations(int n) {
       LaunchSPackK(pg, stream_, S_.ptr, n_, (const int32_t*)work_i_.ptr, (const int32_t*)pack_off_.ptr, npanel,
                    Spk_.ptr, 0);
       AllReduceSum(Spk_.ptr, npack_ + (merged ? ntail_ : 0));
-      LaunchSPackK(pg, stream_, S_.ptr, n_, (const int32_t*)work_i_.ptr, (const int32_t*)pack_off_.ptr, npanel,
-                   Spk_.ptr, 1);
+      if (fin1_in_schur)
+        LaunchSUnpackFinK(pg, stream_, d, (const int32_t*)work_i_.ptr, (const int32_t*)pack_off_.ptr, npanel,
+                          Spk_.ptr);
+      else
+        LaunchSPackK(pg, stream_, S_.ptr, n_, (const int32_t*)work_i_.ptr, (const int32_t*)pack_off_.ptr, npanel,
+                     Spk_.ptr, 1);
       TimedLaunchEnd(kKXchg);
-      if (merged) {
+      if (merged && !fin1_in_schur) {
         TimedLaunchBegin(kKCamFinal);
         LaunchCamFinalizeK(stream_, d, 2, 0);
         TimedLaunchEnd(kKCamFinal);
