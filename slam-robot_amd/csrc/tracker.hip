@@ -238,28 +238,37 @@ __device__ __forceinline__ bool stage_covers(const Stage& st, float x, float y, 
   return st.on && x >= st.c0 + lo && x <= st.c0 + hi && y >= st.r0 + lo && y <= st.r0 + hi;
 }
 
-// (Re)stage the tile around (x, y); levels smaller than the tile are never staged.
-__device__ __forceinline__ void stage_load(const LevelDev& L, float x, float y, int lane, float* tile, Stage& st) {
+// (Re)stage the tile around (x, y); levels smaller than the tile are never staged.  Split in two so a caller
+// can put the tile's loads in flight beside other loads (stage_issue), then write the tile (stage_commit).
+constexpr int kStV = (kStT * kStT + 63) / 64;   // tile values per lane
+__device__ __forceinline__ bool stage_issue(const LevelDev& L, float x, float y, int lane, float (&v)[kStV],
+                                            Stage& st) {
   if (L.w < kStT || L.h < kStT) {
     st.on = false;
-    return;
+    return false;
   }
   st.c0 = min(max((int)x - kStT / 2, 0), L.w - kStT);
   st.r0 = min(max((int)y - kStT / 2, 0), L.h - kStT);
   const __attribute__((address_space(1))) float* gi = (const __attribute__((address_space(1))) float*)L.img;
-  float v[(kStT * kStT + 63) / 64];
 #pragma unroll
-  for (int u = 0; u < (kStT * kStT + 63) / 64; ++u) {
+  for (int u = 0; u < kStV; ++u) {
     const int idx = min(lane + 64 * u, kStT * kStT - 1);
     v[u] = gi[(size_t)(st.r0 + idx / kStT) * L.w + st.c0 + idx % kStT];
   }
+  return true;
+}
+__device__ __forceinline__ void stage_commit(const float (&v)[kStV], int lane, float* tile, Stage& st) {
 #pragma unroll
-  for (int u = 0; u < (kStT * kStT + 63) / 64; ++u) {
+  for (int u = 0; u < kStV; ++u) {
     const int idx = lane + 64 * u;
     if (idx < kStT * kStT) tile[idx] = v[u];
   }
   __builtin_amdgcn_wave_barrier();
   st.on = true;
+}
+__device__ __forceinline__ void stage_load(const LevelDev& L, float x, float y, int lane, float* tile, Stage& st) {
+  float v[kStV];
+  if (stage_issue(L, x, y, lane, v, st)) stage_commit(v, lane, tile, st);
 }
 
 template <int kCtrl>
@@ -390,12 +399,27 @@ __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev&
     pq[r] = wave_tree_sum(pq[r]);
   }
   c.ts->mark(2);
+  // each probe's lighting fit (ScorePatchMatch, hessian.h:131-133: mean, second moment, alpha, beta) on its own
+  // lane (probe = lane, 0..5; the same float operations, so the same bits) and broadcast by readlane: one chain
+  // of three divisions and a square root in the instruction stream instead of six
+  float alphas[6], betas[6];
+  {
+    const int r = min(c.lane, 5);
+    const float psl = r == 0 ? ps[0] : r == 1 ? ps[1] : r == 2 ? ps[2] : r == 3 ? ps[3] : r == 4 ? ps[4] : ps[5];
+    const float pql = r == 0 ? pq[0] : r == 1 ? pq[1] : r == 2 ? pq[2] : r == 3 ? pq[3] : r == 4 ? pq[4] : pq[5];
+    const float mean = psl / c.len, sumsq = pql / c.len;
+    const float alpha = sqrtf(tp.sumsq / sumsq);
+    const float beta = tp.mean - alpha * mean;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      alphas[q] = readlane_f(alpha, q);
+      betas[q] = readlane_f(beta, q);
+    }
+  }
   float sc[6];
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
-    const float mean = ps[r] / c.len, sumsq = pq[r] / c.len;
-    const float alpha = sqrtf(tp.sumsq / sumsq);
-    const float beta = tp.mean - alpha * mean;
+    const float alpha = alphas[r], beta = betas[r];
     float acc = 0.f;
 #pragma unroll
     for (int k = 0; k < NK; ++k) {
@@ -414,12 +438,29 @@ __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev&
 #pragma unroll
   for (int r = 0; r < 6; ++r) sc[r] = wave_tree_sum(sc[r]);
   const double sad0 = sc[0], sadn1x = sc[1], sadn1y = sc[2], sadp1x = sc[3], sadp1y = sc[4], sadxy = sc[5];
-  *mdx = (float)(0.5 * (sadp1x - sadn1x) / hh);
-  *mdy = (float)(0.5 * (sadp1y - sadn1y) / hh);
-  *mdxx = (float)(((sadp1x - sad0) / hh - (sad0 - sadn1x) / hh) / hh);
-  *mdyy = (float)(((sadp1y - sad0) / hh - (sad0 - sadn1y) / hh) / hh);
-  *mdxy = (float)(((sadxy - sadp1y) / hh - (sadp1x - sad0) / hh) / hh);
-  *mdyx = (float)(((sadxy - sadp1x) / hh - (sadp1y - sad0) / hh) / hh);
+  // The six difference quotients of hessian.h:160-171, one per lane (lane e computes quotient e with the
+  // reference's fp64 operations in the reference's order, so the bits are the same) and gathered by readlane:
+  // three fp64 divisions in the wave's instruction stream instead of fourteen (a correctly rounded fp64
+  // division is about eleven dependent instructions).
+  //   e 0: mdx = 0.5 (p1x - n1x) / h        e 2: mdxx = ((p1x - s0) / h - (s0 - n1x) / h) / h
+  //   e 1: mdy = 0.5 (p1y - n1y) / h        e 3: mdyy = ((p1y - s0) / h - (s0 - n1y) / h) / h
+  //                                         e 4: mdxy = ((sxy - p1y) / h - (p1x - s0) / h) / h
+  //                                         e 5: mdyx = ((sxy - p1x) / h - (p1y - s0) / h) / h
+  const int e = c.lane;
+  const double qa = e == 0 ? sadp1x : e == 1 ? sadp1y : e == 2 ? sadp1x : e == 3 ? sadp1y : sadxy;
+  const double qb = e == 0 ? sadn1x : e == 1 ? sadn1y : e == 2 || e == 3 ? sad0 : e == 4 ? sadp1y : sadp1x;
+  const double qc = e == 2 || e == 3 ? sad0 : e == 4 ? sadp1x : sadp1y;
+  const double qd = e == 2 ? sadn1x : e == 3 ? sadn1y : sad0;
+  const double num = e < 2 ? 0.5 * (qa - qb) : (qa - qb);
+  const double q1 = num / hh;
+  const double q2 = (qc - qd) / hh;
+  const float res = (float)(e < 2 ? q1 : (q1 - q2) / hh);
+  *mdx = readlane_f(res, 0);
+  *mdy = readlane_f(res, 1);
+  *mdxx = readlane_f(res, 2);
+  *mdyy = readlane_f(res, 3);
+  *mdxy = readlane_f(res, 4);
+  *mdyx = readlane_f(res, 5);
   c.ts->mark(4);
 }
 
@@ -440,12 +481,18 @@ __device__ __forceinline__ int track_pass(const TrackCtx& c, const LevelDev* __r
     const LevelDev Ls = src[i], Ld = dst[i];
     Tmpl tp;
     c.ts->mark(7);
+    // the destination tile around the level's start estimate and the template patch: both sets of loads in
+    // flight together (one memory round trip per level instead of two); the tile is the one the first Newton
+    // iteration would stage (same values: the probes sample identical floats from it or from global memory)
+    Stage st;
+    float sv[kStV];
+    const bool pre = stage_issue(Ld, x, y, c.lane, sv, st);
     get_patch_ctx<NK>(c, Ls, tx, ty, tp);
+    if (pre) stage_commit(sv, c.lane, tile, st);
     c.ts->mark(6);
     const float margin = 0.01f;
     int it = 0;
     bool oob = false;
-    Stage st;
     for (; it < c.max_it; ++it) {
       if (x < margin || y < margin || (x + margin) > Ld.w || (y + margin) > Ld.h) {
         oob = true;

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Per-workload rocprofv3 evidence for bench.py's roofline fields (MI355X_MICROARCH.md HBM/rocprofv3 recipe):
 # for each workload (C2, C5, the scaled sweep, the front end) one kernel-trace --stats run and two separate
-# --pmc passes (FETCH_SIZE, WRITE_SIZE) of `bench.py --only <workload>` with the driver's arguments
+# --pmc passes (FETCH_SIZE, WRITE_SIZE), and for C2 / C5 a third (the matrix-core counters, tools/pmc_mfma.py) of `bench.py --only <workload>` with the driver's arguments
 # (--steps 20 --warmup 5), so every file holds that workload's own launches only:
 #   profiles/<tag>_kernel_stats_<workload>.csv   rocprofv3 kernel statistics (the workload alone: no modelled shards)
 #   profiles/<tag>_pmc_traffic_<workload>.json   HBM bytes per launch (tools/pmc_traffic.py)
@@ -36,4 +36,14 @@ for W in $WLS; do
   python3 "$R/tools/pmc_traffic.py" "$OUT/pmc_$W" "$R/profiles/${TAG}_pmc_traffic_${W}.json" \
     "bench.py --only $W --steps 20 --warmup 5" || exit 1
   cp "$R/profiles/${TAG}_pmc_traffic_${W}.json" "$OUT/profiles/"
+  if [ "$W" = C2 ] || [ "$W" = C5 ]; then
+    echo "== $W pmc mfma"
+    timeout -s KILL 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE \
+      --kernel-include-regex "k_schur|k_chol_tiles" -d "$OUT/mfma_$W" -o run --output-format csv \
+      -- python3 "$R/bench.py" --only "$W" --steps 20 --warmup 5 --model-scaling 0 --weak 0 \
+      > "$OUT/mfma_$W.json" 2> "$OUT/mfma_$W.log" || { echo "pmc mfma $W failed"; tail -5 "$OUT/mfma_$W.log"; exit 1; }
+    python3 "$R/tools/pmc_mfma.py" "$OUT/mfma_$W" "$R/profiles/${TAG}_pmc_mfma_${W}.json" \
+      "bench.py --only $W --steps 20 --warmup 5" || exit 1
+    cp "$R/profiles/${TAG}_pmc_mfma_${W}.json" "$OUT/profiles/"
+  fi
 done
