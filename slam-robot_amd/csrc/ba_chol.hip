@@ -1169,9 +1169,16 @@ __device__ __forceinline__ void tile_phase(f64x4 (&acc)[kTB], double& ypart, int
     return;
   }
   if (J == K + 1) SG_PTRACE(K, 8)
+#ifdef SG_X_IDLE   // timing-only A/B (tools/r5_chol_ab.sh): the waves off the owner's chain do nothing
+  if (J != K + 1) return;
+#endif
   // (0) trailing update by row K-1 (the owner's diagonal tile, dd = 2, already took it last phase; with the
   // look-ahead its row-K tile, dd = 1, too)
+#ifdef SG_X_NOTRAIL   // timing-only A/B: no trailing updates off the owner's chain
+  if (K >= 1 && J < tend[K - 1] && J == K + 1) {
+#else
   if (K >= 1 && J < tend[K - 1]) {
+#endif
     const double* Ub = sh.Ur[(K - 1) & 1][0];
     const bool own_la = J == K + 1 && la_done(tend, K - 1);
 #pragma unroll

@@ -129,35 +129,31 @@ struct Geo {
   float a11, a12, a21, a22, b1, b2;
 };
 
+// make_geo's two halves: the column geometry depends on px alone, the row geometry on py alone (the Newton
+// probes share them three ways, brute_hessian).
+struct GeoX {
+  int zx, pw, col0, rx, rw;
+  float a;
+};
+struct GeoY {
+  int zy, ph, base_row, ry, rh;
+  float b;
+};
 // kShift: HessianTracker::GetPatch's zero-filled left / top edge (hessian.h:63-75); without it the plain
 // getRectSubPix of klt.h / brute.h GetPatch.
 template <bool kShift = true>
-__device__ __forceinline__ void make_geo(float px, float py, int W, int w, int h, Geo& g) {
+__device__ __forceinline__ void make_geo_x(float px, int W, int w, GeoX& g) {
   g.zx = 0;
-  g.zy = 0;
   g.pw = W;
-  g.ph = W;
   if (kShift && px < 0.5 * W) {
     const int d = (int)((0.5 * W - px) + 0.9999);
     px = (float)(px + 0.5 * d);
     g.zx = d;
     g.pw = W - d;
   }
-  if (kShift && py < 0.5 * W) {
-    const int d = (int)(0.5 * W - py);
-    py = (float)(py + 0.5 * d);
-    g.zy = d;
-    g.ph = W - d;
-  }
-  float cx = px - (g.pw - 1) * 0.5f, cy = py - (g.ph - 1) * 0.5f;
-  const int ipx = (int)floorf(cx), ipy = (int)floorf(cy);
-  const float a = cx - ipx, b = cy - ipy;
-  g.a11 = (1.f - a) * (1.f - b);
-  g.a12 = a * (1.f - b);
-  g.a21 = (1.f - a) * b;
-  g.a22 = a * b;
-  g.b1 = 1.f - b;
-  g.b2 = b;
+  const float cx = px - (g.pw - 1) * 0.5f;
+  const int ipx = (int)floorf(cx);
+  g.a = cx - ipx;
   int base_col;
   if (ipx >= 0) { base_col = ipx; g.rx = 0; }
   else { base_col = 0; g.rx = min(-ipx, g.pw); }
@@ -166,6 +162,21 @@ __device__ __forceinline__ void make_geo(float px, float py, int W, int w, int h
     g.rw = w - ipx - 1;
     if (g.rw < 0) { base_col += g.rw; g.rw = 0; }
   }
+  g.col0 = base_col - g.rx;
+}
+template <bool kShift = true>
+__device__ __forceinline__ void make_geo_y(float py, int W, int h, GeoY& g) {
+  g.zy = 0;
+  g.ph = W;
+  if (kShift && py < 0.5 * W) {
+    const int d = (int)(0.5 * W - py);
+    py = (float)(py + 0.5 * d);
+    g.zy = d;
+    g.ph = W - d;
+  }
+  const float cy = py - (g.ph - 1) * 0.5f;
+  const int ipy = (int)floorf(cy);
+  g.b = cy - ipy;
   if (ipy >= 0) { g.base_row = ipy; g.ry = 0; }
   else { g.base_row = 0; g.ry = -ipy; }
   if (ipy < h - g.ph) g.rh = g.ph;
@@ -173,32 +184,78 @@ __device__ __forceinline__ void make_geo(float px, float py, int W, int w, int h
     g.rh = h - ipy - 1;
     if (g.rh < 0) { g.base_row += g.rh; g.rh = 0; }
   }
-  g.col0 = base_col - g.rx;
+}
+__device__ __forceinline__ void geo_join(const GeoX& x, const GeoY& y, Geo& g) {
+  g.zx = x.zx;
+  g.pw = x.pw;
+  g.col0 = x.col0;
+  g.rx = x.rx;
+  g.rw = x.rw;
+  g.zy = y.zy;
+  g.ph = y.ph;
+  g.base_row = y.base_row;
+  g.ry = y.ry;
+  g.rh = y.rh;
+  const float a = x.a, b = y.b;
+  g.a11 = (1.f - a) * (1.f - b);
+  g.a12 = a * (1.f - b);
+  g.a21 = (1.f - a) * b;
+  g.a22 = a * b;
+  g.b1 = 1.f - b;
+  g.b2 = b;
+}
+__device__ __forceinline__ bool geo_x_same(const GeoX& p, const GeoX& q) {
+  return p.zx == q.zx && p.pw == q.pw && p.col0 == q.col0 && p.rx == q.rx && p.rw == q.rw;
+}
+__device__ __forceinline__ bool geo_y_same(const GeoY& p, const GeoY& q) {
+  return p.zy == q.zy && p.ph == q.ph && p.base_row == q.base_row && p.ry == q.ry && p.rh == q.rh;
+}
+template <bool kShift = true>
+__device__ __forceinline__ void make_geo(float px, float py, int W, int w, int h, Geo& g) {
+  GeoX gx;
+  GeoY gy;
+  make_geo_x<kShift>(px, W, w, gx);
+  make_geo_y<kShift>(py, W, h, gy);
+  geo_join(gx, gy, g);
 }
 
-// Patch pixel (i, j) of the W x W patch.
-__device__ __forceinline__ float sample(const float* img, int w, const Geo& g, int i, int j) {
-  // Branch-free form of getRectSubPix's three cases (left edge column, interior bilinear, right edge
-  // column) and the zero-filled border: the four loads are unconditional (clamped to index 0 when the
-  // pixel is zero) so a wave's samples are all in flight together; each case's arithmetic is the
-  // reference expression, evaluated as written (FMA contraction is off in this file).
-  const bool zero = g.pw <= 0 || g.ph <= 0 || j < g.zx || i < g.zy;
+// Patch pixel (i, j) of the W x W patch: the four taps (taps) and their bilinear / edge combination (combine).
+// Branch-free form of getRectSubPix's three cases (left edge column, interior bilinear, right edge column) and
+// the zero-filled border: the four loads are unconditional (clamped to index 0 when the pixel is zero) so a
+// wave's samples are all in flight together; each case's arithmetic is the reference expression, evaluated as
+// written (FMA contraction is off in this file).
+struct Taps {
+  float v11, v12, v21, v22;
+  bool zero, edge;
+};
+__device__ __forceinline__ float combine(const Taps& t, const Geo& g) {
+  const float re = t.v11 * g.b1 + t.v21 * g.b2;
+  const float rb = t.v11 * g.a11 + t.v12 * g.a12 + t.v21 * g.a21 + t.v22 * g.a22;
+  return t.zero ? 0.f : (t.edge ? re : rb);
+}
+__device__ __forceinline__ Taps taps_global(const float* img, int w, const Geo& g, int i, int j) {
+  Taps t;
+  t.zero = g.pw <= 0 || g.ph <= 0 || j < g.zx || i < g.zy;
   const int ii = i - g.zy, jj = j - g.zx;
   const bool same = (ii < g.ry || ii >= g.rh);
   const int row = g.base_row + max(0, min(ii, g.rh) - g.ry);
   const bool left = jj < g.rx, right = !left && jj >= g.rw;
-  const bool edge = left || right;
+  t.edge = left || right;
   const int ce = g.col0 + (left ? g.rx : g.rw);
-  const int c0 = zero ? 0 : (edge ? ce : g.col0 + jj);
-  const int c1 = zero ? 0 : (edge ? ce : g.col0 + jj + 1);
-  const size_t r1 = zero ? 0 : (size_t)row * w;
-  const size_t r2 = (zero || same) ? r1 : r1 + w;
+  const int c0 = t.zero ? 0 : (t.edge ? ce : g.col0 + jj);
+  const int c1 = t.zero ? 0 : (t.edge ? ce : g.col0 + jj + 1);
+  const size_t r1 = t.zero ? 0 : (size_t)row * w;
+  const size_t r2 = (t.zero || same) ? r1 : r1 + w;
   // image levels live in device global memory: global (not flat) loads, so the waits count vmcnt only
   const __attribute__((address_space(1))) float* gi = (const __attribute__((address_space(1))) float*)img;
-  const float v11 = gi[r1 + c0], v12 = gi[r1 + c1], v21 = gi[r2 + c0], v22 = gi[r2 + c1];
-  const float re = v11 * g.b1 + v21 * g.b2;
-  const float rb = v11 * g.a11 + v12 * g.a12 + v21 * g.a21 + v22 * g.a22;
-  return zero ? 0.f : (edge ? re : rb);
+  t.v11 = gi[r1 + c0];
+  t.v12 = gi[r1 + c1];
+  t.v21 = gi[r2 + c0];
+  t.v22 = gi[r2 + c1];
+  return t;
+}
+__device__ __forceinline__ float sample(const float* img, int w, const Geo& g, int i, int j) {
+  return combine(taps_global(img, w, g, i, j), g);
 }
 
 // Staged sampling (Track's Newton probes): each wave copies a kStT x kStT tile of the destination level around
@@ -213,22 +270,27 @@ struct Stage {
   bool on = false;
 };
 
-__device__ __forceinline__ float sample_lds(const float* tile, const Stage& st, const Geo& g, int i, int j) {
-  const bool zero = g.pw <= 0 || g.ph <= 0 || j < g.zx || i < g.zy;
+__device__ __forceinline__ Taps taps_lds(const float* tile, const Stage& st, const Geo& g, int i, int j) {
+  Taps t;
+  t.zero = g.pw <= 0 || g.ph <= 0 || j < g.zx || i < g.zy;
   const int ii = i - g.zy, jj = j - g.zx;
   const bool same = (ii < g.ry || ii >= g.rh);
   const int row = g.base_row + max(0, min(ii, g.rh) - g.ry);
   const bool left = jj < g.rx, right = !left && jj >= g.rw;
-  const bool edge = left || right;
+  t.edge = left || right;
   const int ce = g.col0 + (left ? g.rx : g.rw);
-  const int c0 = zero ? 0 : (edge ? ce : g.col0 + jj) - st.c0;
-  const int c1 = zero ? 0 : (edge ? ce : g.col0 + jj + 1) - st.c0;
-  const int r1 = zero ? 0 : (row - st.r0) * kStT;
-  const int r2 = (zero || same) ? r1 : r1 + kStT;
-  const float v11 = tile[r1 + c0], v12 = tile[r1 + c1], v21 = tile[r2 + c0], v22 = tile[r2 + c1];
-  const float re = v11 * g.b1 + v21 * g.b2;
-  const float rb = v11 * g.a11 + v12 * g.a12 + v21 * g.a21 + v22 * g.a22;
-  return zero ? 0.f : (edge ? re : rb);
+  const int c0 = t.zero ? 0 : (t.edge ? ce : g.col0 + jj) - st.c0;
+  const int c1 = t.zero ? 0 : (t.edge ? ce : g.col0 + jj + 1) - st.c0;
+  const int r1 = t.zero ? 0 : (row - st.r0) * kStT;
+  const int r2 = (t.zero || same) ? r1 : r1 + kStT;
+  t.v11 = tile[r1 + c0];
+  t.v12 = tile[r1 + c1];
+  t.v21 = tile[r2 + c0];
+  t.v22 = tile[r2 + c1];
+  return t;
+}
+__device__ __forceinline__ float sample_lds(const float* tile, const Stage& st, const Geo& g, int i, int j) {
+  return combine(taps_lds(tile, st, g, i, j), g);
 }
 
 // Every tap of the six probes around (x, y) lies in the staged tile (wave-uniform): the probes' windows span
@@ -368,29 +430,54 @@ __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev&
                                               float* mdyy, const float* tile, const Stage& st) {
   c.ts->mark(0);
   const double hh = 0.02;
-  float px[6], py[6];
-  px[0] = x;              py[0] = y;                // sad0
-  px[1] = (float)(x - hh); py[1] = y;               // sadn1x
-  px[2] = x;              py[2] = (float)(y - hh);  // sadn1y
-  px[3] = (float)(x + hh); py[3] = y;               // sadp1x
-  px[4] = x;              py[4] = (float)(y + hh);  // sadp1y
-  px[5] = (float)(x + hh); py[5] = (float)(y + hh); // sadxy
-  float pv[6][NK], ps[6], pq[6];
+  // probes: sad0 (x, y), sadn1x (x - h, y), sadn1y (x, y - h), sadp1x (x + h, y), sadp1y (x, y + h), sadxy
+  // (x + h, y + h).  Their column geometry is one of three (x, x - h, x + h), the row geometry one of three.
+  GeoX gx[3];
+  GeoY gy[3];
+  make_geo_x(x, c.W, L.w, gx[0]);
+  make_geo_x((float)(x - hh), c.W, L.w, gx[1]);
+  make_geo_x((float)(x + hh), c.W, L.w, gx[2]);
+  make_geo_y(y, c.W, L.h, gy[0]);
+  make_geo_y((float)(y - hh), c.W, L.h, gy[1]);
+  make_geo_y((float)(y + hh), c.W, L.h, gy[2]);
+  constexpr int kXi[6] = {0, 1, 0, 2, 0, 2}, kYi[6] = {0, 0, 1, 0, 2, 2};
+  Geo g[6];
 #pragma unroll
-  for (int r = 0; r < 6; ++r) {
-    Geo g;
-    make_geo(px[r], py[r], c.W, L.w, L.h, g);
-    float s = 0.f, q = 0.f;
+  for (int r = 0; r < 6; ++r) geo_join(gx[kXi[r]], gy[kYi[r]], g[r]);
+  // Unless a probe crosses a pixel boundary (or the border), the six share their integer geometry and so every
+  // tap: the taps are read once and combined with each probe's weights — the same floats as six samples.
+  const bool shared = geo_x_same(gx[0], gx[1]) && geo_x_same(gx[0], gx[2]) && geo_y_same(gy[0], gy[1]) &&
+                      geo_y_same(gy[0], gy[2]);
+  float pv[6][NK], ps[6], pq[6];
+  if (shared) {
+#pragma unroll
+    for (int r = 0; r < 6; ++r) ps[r] = pq[r] = 0.f;
 #pragma unroll
     for (int k = 0; k < NK; ++k) {
-      const float sv = kLds ? sample_lds(tile, st, g, c.pi[k], c.pj[k]) : sample(L.img, L.w, g, c.pi[k], c.pj[k]);
-      const float v = k < c.nk ? sv : 0.f;   // 0 past the patch
-      pv[r][k] = v;
-      s += v;
-      q += v * v;
+      const Taps t = kLds ? taps_lds(tile, st, g[0], c.pi[k], c.pj[k]) : taps_global(L.img, L.w, g[0], c.pi[k], c.pj[k]);
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        const float v = k < c.nk ? combine(t, g[r]) : 0.f;   // 0 past the patch
+        pv[r][k] = v;
+        ps[r] += v;
+        pq[r] += v * v;
+      }
     }
-    ps[r] = s;
-    pq[r] = q;
+  } else {
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int k = 0; k < NK; ++k) {
+        const float sv = kLds ? sample_lds(tile, st, g[r], c.pi[k], c.pj[k]) : sample(L.img, L.w, g[r], c.pi[k], c.pj[k]);
+        const float v = k < c.nk ? sv : 0.f;   // 0 past the patch
+        pv[r][k] = v;
+        s += v;
+        q += v * v;
+      }
+      ps[r] = s;
+      pq[r] = q;
+    }
   }
   c.ts->mark(1);
 #pragma unroll
