@@ -346,7 +346,12 @@ __device__ __forceinline__ float wave_tree_sum(float v) {
   v = v + dpp_f<0x4E>(v);    // (l, l^2)
   v = v + dpp_f<0x141>(v);   // half-row mirror: octets
   v = v + dpp_f<0x140>(v);   // row mirror: 16-lane rows
-  return (readlane_f(v, 0) + readlane_f(v, 16)) + (readlane_f(v, 32) + readlane_f(v, 48));
+  // (row 0 + row 1) + (row 2 + row 3) by gfx950 row swaps, in every lane (addition commutes: the same bits as
+  // the readlane form (r0 + r16) + (r32 + r48), three instructions fewer)
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  const float w = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(w), __float_as_uint(w), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
 struct Tmpl {
@@ -432,32 +437,53 @@ __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev&
   const double hh = 0.02;
   // probes: sad0 (x, y), sadn1x (x - h, y), sadn1y (x, y - h), sadp1x (x + h, y), sadp1y (x, y + h), sadxy
   // (x + h, y + h).  Their column geometry is one of three (x, x - h, x + h), the row geometry one of three.
+  // The three column and three row geometries are formed on lanes 0-2 (lane v: x, x - h, x + h and y, y - h,
+  // y + h: the same float operations, so the same values) and broadcast by readlane.
   GeoX gx[3];
   GeoY gy[3];
-  make_geo_x(x, c.W, L.w, gx[0]);
-  make_geo_x((float)(x - hh), c.W, L.w, gx[1]);
-  make_geo_x((float)(x + hh), c.W, L.w, gx[2]);
-  make_geo_y(y, c.W, L.h, gy[0]);
-  make_geo_y((float)(y - hh), c.W, L.h, gy[1]);
-  make_geo_y((float)(y + hh), c.W, L.h, gy[2]);
-  constexpr int kXi[6] = {0, 1, 0, 2, 0, 2}, kYi[6] = {0, 0, 1, 0, 2, 2};
-  Geo g[6];
+  {
+    const int v = min(c.lane, 2);
+    const float xv = v == 0 ? x : (float)(v == 1 ? x - hh : x + hh);
+    const float yv = v == 0 ? y : (float)(v == 1 ? y - hh : y + hh);
+    GeoX lx;
+    GeoY ly;
+    make_geo_x(xv, c.W, L.w, lx);
+    make_geo_y(yv, c.W, L.h, ly);
 #pragma unroll
-  for (int r = 0; r < 6; ++r) geo_join(gx[kXi[r]], gy[kYi[r]], g[r]);
+    for (int u = 0; u < 3; ++u) {
+      gx[u].zx = __builtin_amdgcn_readlane(lx.zx, u);
+      gx[u].pw = __builtin_amdgcn_readlane(lx.pw, u);
+      gx[u].col0 = __builtin_amdgcn_readlane(lx.col0, u);
+      gx[u].rx = __builtin_amdgcn_readlane(lx.rx, u);
+      gx[u].rw = __builtin_amdgcn_readlane(lx.rw, u);
+      gx[u].a = readlane_f(lx.a, u);
+      gy[u].zy = __builtin_amdgcn_readlane(ly.zy, u);
+      gy[u].ph = __builtin_amdgcn_readlane(ly.ph, u);
+      gy[u].base_row = __builtin_amdgcn_readlane(ly.base_row, u);
+      gy[u].ry = __builtin_amdgcn_readlane(ly.ry, u);
+      gy[u].rh = __builtin_amdgcn_readlane(ly.rh, u);
+      gy[u].b = readlane_f(ly.b, u);
+    }
+  }
+  constexpr int kXi[6] = {0, 1, 0, 2, 0, 2}, kYi[6] = {0, 0, 1, 0, 2, 2};
   // Unless a probe crosses a pixel boundary (or the border), the six share their integer geometry and so every
   // tap: the taps are read once and combined with each probe's weights — the same floats as six samples.
   const bool shared = geo_x_same(gx[0], gx[1]) && geo_x_same(gx[0], gx[2]) && geo_y_same(gy[0], gy[1]) &&
                       geo_y_same(gy[0], gy[2]);
   float pv[6][NK], ps[6], pq[6];
   if (shared) {
+    Geo g0;
+    geo_join(gx[0], gy[0], g0);
 #pragma unroll
     for (int r = 0; r < 6; ++r) ps[r] = pq[r] = 0.f;
 #pragma unroll
     for (int k = 0; k < NK; ++k) {
-      const Taps t = kLds ? taps_lds(tile, st, g[0], c.pi[k], c.pj[k]) : taps_global(L.img, L.w, g[0], c.pi[k], c.pj[k]);
+      const Taps t = kLds ? taps_lds(tile, st, g0, c.pi[k], c.pj[k]) : taps_global(L.img, L.w, g0, c.pi[k], c.pj[k]);
 #pragma unroll
       for (int r = 0; r < 6; ++r) {
-        const float v = k < c.nk ? combine(t, g[r]) : 0.f;   // 0 past the patch
+        Geo g;
+        geo_join(gx[kXi[r]], gy[kYi[r]], g);   // (the weights; the integer fields are g0's)
+        const float v = k < c.nk ? combine(t, g) : 0.f;   // 0 past the patch
         pv[r][k] = v;
         ps[r] += v;
         pq[r] += v * v;
@@ -466,10 +492,12 @@ __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev&
   } else {
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
+      Geo g;
+      geo_join(gx[kXi[r]], gy[kYi[r]], g);
       float s = 0.f, q = 0.f;
 #pragma unroll
       for (int k = 0; k < NK; ++k) {
-        const float sv = kLds ? sample_lds(tile, st, g[r], c.pi[k], c.pj[k]) : sample(L.img, L.w, g[r], c.pi[k], c.pj[k]);
+        const float sv = kLds ? sample_lds(tile, st, g, c.pi[k], c.pj[k]) : sample(L.img, L.w, g, c.pi[k], c.pj[k]);
         const float v = k < c.nk ? sv : 0.f;   // 0 past the patch
         pv[r][k] = v;
         s += v;
