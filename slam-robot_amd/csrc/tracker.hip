@@ -354,6 +354,30 @@ __device__ __forceinline__ float wave_tree_sum(float v) {
   return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
+// N tree sums at once, stage by stage (the wave_tree_sum order for each), so the DPP and row-swap latencies of one
+// sum overlap the others' instead of running back to back with wait states between.
+template <int N>
+__device__ __forceinline__ void wave_tree_sums(float (&v)[N]) {
+#pragma unroll
+  for (int r = 0; r < N; ++r) v[r] = v[r] + dpp_f<0xB1>(v[r]);
+#pragma unroll
+  for (int r = 0; r < N; ++r) v[r] = v[r] + dpp_f<0x4E>(v[r]);
+#pragma unroll
+  for (int r = 0; r < N; ++r) v[r] = v[r] + dpp_f<0x141>(v[r]);
+#pragma unroll
+  for (int r = 0; r < N; ++r) v[r] = v[r] + dpp_f<0x140>(v[r]);
+#pragma unroll
+  for (int r = 0; r < N; ++r) {
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[r]), __float_as_uint(v[r]), false, false);
+    v[r] = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  }
+#pragma unroll
+  for (int r = 0; r < N; ++r) {
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[r]), __float_as_uint(v[r]), false, false);
+    v[r] = __uint_as_float(b[0]) + __uint_as_float(b[1]);
+  }
+}
+
 struct Tmpl {
   float v[kNP];
   float mean, sumsq;
@@ -508,10 +532,19 @@ __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev&
     }
   }
   c.ts->mark(1);
+  {
+    float sums[12];
 #pragma unroll
-  for (int r = 0; r < 6; ++r) {
-    ps[r] = wave_tree_sum(ps[r]);
-    pq[r] = wave_tree_sum(pq[r]);
+    for (int r = 0; r < 6; ++r) {
+      sums[r] = ps[r];
+      sums[6 + r] = pq[r];
+    }
+    wave_tree_sums<12>(sums);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      ps[r] = sums[r];
+      pq[r] = sums[6 + r];
+    }
   }
   c.ts->mark(2);
   // each probe's lighting fit (ScorePatchMatch, hessian.h:131-133: mean, second moment, alpha, beta) on its own
@@ -550,8 +583,7 @@ __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev&
     sc[r] = acc;
   }
   c.ts->mark(3);
-#pragma unroll
-  for (int r = 0; r < 6; ++r) sc[r] = wave_tree_sum(sc[r]);
+  wave_tree_sums<6>(sc);
   const double sad0 = sc[0], sadn1x = sc[1], sadn1y = sc[2], sadp1x = sc[3], sadp1y = sc[4], sadxy = sc[5];
   // The six difference quotients of hessian.h:160-171, one per lane (lane e computes quotient e with the
   // reference's fp64 operations in the reference's order, so the bits are the same) and gathered by readlane:
@@ -604,6 +636,18 @@ __device__ __forceinline__ int track_pass(const TrackCtx& c, const LevelDev* __r
     const bool pre = stage_issue(Ld, x, y, c.lane, sv, st);
     get_patch_ctx<NK>(c, Ls, tx, ty, tp);
     if (pre) stage_commit(sv, c.lane, tile, st);
+#ifdef SG_X_DUPSTART   // timing-only A/B (tools/r5_trk_ab.sh): the level start's fetches done twice
+    {
+      float xo = x, yo = y, txo = tx, tyo = ty;
+      asm volatile("" : "+v"(xo), "+v"(yo), "+v"(txo), "+v"(tyo));
+      Tmpl tp2;
+      Stage st2 = st;
+      const bool pre2 = stage_issue(Ld, xo, yo, c.lane, sv, st2);
+      get_patch_ctx<NK>(c, Ls, txo, tyo, tp2);
+      if (pre2) stage_commit(sv, c.lane, tile, st2);
+      asm volatile("" ::"v"(tp2.mean), "v"(tp2.sumsq), "v"(tp2.v[0]));
+    }
+#endif
     c.ts->mark(6);
     const float margin = 0.01f;
     int it = 0;
@@ -619,6 +663,17 @@ __device__ __forceinline__ int track_pass(const TrackCtx& c, const LevelDev* __r
         brute_hessian<NK, true>(c, Ld, tp, x, y, &mdx, &mdy, &mdxx, &mdxy, &mdyx, &mdyy, tile, st);
       else
         brute_hessian<NK, false>(c, Ld, tp, x, y, &mdx, &mdy, &mdxx, &mdxy, &mdyx, &mdyy, tile, st);
+#ifdef SG_X_DUPITER   // timing-only A/B: every Newton iteration's probes and sums done twice
+      {
+        float xo = x, yo = y, d0, d1, d2, d3, d4, d5;
+        asm volatile("" : "+v"(xo), "+v"(yo));
+        if (stage_covers(st, xo, yo, c.W))
+          brute_hessian<NK, true>(c, Ld, tp, xo, yo, &d0, &d1, &d2, &d3, &d4, &d5, tile, st);
+        else
+          brute_hessian<NK, false>(c, Ld, tp, xo, yo, &d0, &d1, &d2, &d3, &d4, &d5, tile, st);
+        asm volatile("" ::"v"(d0), "v"(d1), "v"(d2), "v"(d3), "v"(d4), "v"(d5));
+      }
+#endif
       const double H00 = mdxx, H01 = mdxy, H10 = mdyx, H11 = mdyy;
       const double det = H00 * H11 - H10 * H01;
       const double invdet = 1.0 / det;
