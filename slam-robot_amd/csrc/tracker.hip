@@ -233,6 +233,15 @@ __device__ __forceinline__ float combine(const Taps& t, const Geo& g) {
   const float rb = t.v11 * g.a11 + t.v12 * g.a12 + t.v21 * g.a21 + t.v22 * g.a22;
   return t.zero ? 0.f : (t.edge ? re : rb);
 }
+// combine() as selects only: both forms are formed (same expressions, so the same bits), then picked; `on` false
+// (a slot past the patch) gives 0 as well.  (The ?: of combine() compiles to branches around the arithmetic.)
+__device__ __forceinline__ float combine_sel(const Taps& t, const Geo& g, bool on) {
+  float re = t.v11 * g.b1 + t.v21 * g.b2;
+  float rb = t.v11 * g.a11 + t.v12 * g.a12 + t.v21 * g.a21 + t.v22 * g.a22;
+  asm volatile("" : "+v"(re), "+v"(rb));
+  const float r = t.edge ? re : rb;
+  return (t.zero || !on) ? 0.f : r;
+}
 __device__ __forceinline__ Taps taps_global(const float* img, int w, const Geo& g, int i, int j) {
   Taps t;
   t.zero = g.pw <= 0 || g.ph <= 0 || j < g.zx || i < g.zy;
@@ -463,41 +472,43 @@ __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev&
   // (x + h, y + h).  Their column geometry is one of three (x, x - h, x + h), the row geometry one of three.
   // The three column and three row geometries are formed on lanes 0-2 (lane v: x, x - h, x + h and y, y - h,
   // y + h: the same float operations, so the same values) and broadcast by readlane.
-  GeoX gx[3];
-  GeoY gy[3];
-  {
-    const int v = min(c.lane, 2);
-    const float xv = v == 0 ? x : (float)(v == 1 ? x - hh : x + hh);
-    const float yv = v == 0 ? y : (float)(v == 1 ? y - hh : y + hh);
-    GeoX lx;
-    GeoY ly;
-    make_geo_x(xv, c.W, L.w, lx);
-    make_geo_y(yv, c.W, L.h, ly);
+  const int v = min(c.lane, 2);
+  const float xv = v == 0 ? x : (float)(v == 1 ? x - hh : x + hh);
+  const float yv = v == 0 ? y : (float)(v == 1 ? y - hh : y + hh);
+  GeoX lx;
+  GeoY ly;
+  make_geo_x(xv, c.W, L.w, lx);
+  make_geo_y(yv, c.W, L.h, ly);
+  // variant 0's integer geometry to every lane; lanes 1 and 2 compare theirs with it (one ballot)
+  GeoX gx0;
+  GeoY gy0;
+  gx0.zx = __builtin_amdgcn_readlane(lx.zx, 0);
+  gx0.pw = __builtin_amdgcn_readlane(lx.pw, 0);
+  gx0.col0 = __builtin_amdgcn_readlane(lx.col0, 0);
+  gx0.rx = __builtin_amdgcn_readlane(lx.rx, 0);
+  gx0.rw = __builtin_amdgcn_readlane(lx.rw, 0);
+  gy0.zy = __builtin_amdgcn_readlane(ly.zy, 0);
+  gy0.ph = __builtin_amdgcn_readlane(ly.ph, 0);
+  gy0.base_row = __builtin_amdgcn_readlane(ly.base_row, 0);
+  gy0.ry = __builtin_amdgcn_readlane(ly.ry, 0);
+  gy0.rh = __builtin_amdgcn_readlane(ly.rh, 0);
+  float av[3], bv[3];
 #pragma unroll
-    for (int u = 0; u < 3; ++u) {
-      gx[u].zx = __builtin_amdgcn_readlane(lx.zx, u);
-      gx[u].pw = __builtin_amdgcn_readlane(lx.pw, u);
-      gx[u].col0 = __builtin_amdgcn_readlane(lx.col0, u);
-      gx[u].rx = __builtin_amdgcn_readlane(lx.rx, u);
-      gx[u].rw = __builtin_amdgcn_readlane(lx.rw, u);
-      gx[u].a = readlane_f(lx.a, u);
-      gy[u].zy = __builtin_amdgcn_readlane(ly.zy, u);
-      gy[u].ph = __builtin_amdgcn_readlane(ly.ph, u);
-      gy[u].base_row = __builtin_amdgcn_readlane(ly.base_row, u);
-      gy[u].ry = __builtin_amdgcn_readlane(ly.ry, u);
-      gy[u].rh = __builtin_amdgcn_readlane(ly.rh, u);
-      gy[u].b = readlane_f(ly.b, u);
-    }
+  for (int u = 0; u < 3; ++u) {
+    av[u] = readlane_f(lx.a, u);
+    bv[u] = readlane_f(ly.b, u);
   }
+  gx0.a = av[0];
+  gy0.b = bv[0];
   constexpr int kXi[6] = {0, 1, 0, 2, 0, 2}, kYi[6] = {0, 0, 1, 0, 2, 2};
   // Unless a probe crosses a pixel boundary (or the border), the six share their integer geometry and so every
   // tap: the taps are read once and combined with each probe's weights — the same floats as six samples.
-  const bool shared = geo_x_same(gx[0], gx[1]) && geo_x_same(gx[0], gx[2]) && geo_y_same(gy[0], gy[1]) &&
-                      geo_y_same(gy[0], gy[2]);
+  const bool same = geo_x_same(lx, gx0) && geo_y_same(ly, gy0);
+  const bool shared = (__ballot(same) & 7ull) == 7ull;
   float pv[6][NK], ps[6], pq[6];
   if (shared) {
     Geo g0;
-    geo_join(gx[0], gy[0], g0);
+    geo_join(gx0, gy0, g0);
 #pragma unroll
     for (int r = 0; r < 6; ++r) ps[r] = pq[r] = 0.f;
 #pragma unroll
@@ -505,15 +516,43 @@ __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev&
       const Taps t = kLds ? taps_lds(tile, st, g0, c.pi[k], c.pj[k]) : taps_global(L.img, L.w, g0, c.pi[k], c.pj[k]);
 #pragma unroll
       for (int r = 0; r < 6; ++r) {
-        Geo g;
-        geo_join(gx[kXi[r]], gy[kYi[r]], g);   // (the weights; the integer fields are g0's)
-        const float v = k < c.nk ? combine(t, g) : 0.f;   // 0 past the patch
+        Geo g = g0;
+        const GeoX wx{0, 0, 0, 0, 0, av[kXi[r]]};
+        const GeoY wy{0, 0, 0, 0, 0, bv[kYi[r]]};
+        {
+          Geo w;
+          geo_join(wx, wy, w);   // the probe's weights (its integer fields are g0's)
+          g.a11 = w.a11;
+          g.a12 = w.a12;
+          g.a21 = w.a21;
+          g.a22 = w.a22;
+          g.b1 = w.b1;
+          g.b2 = w.b2;
+        }
+        const float v = combine_sel(t, g, k < c.nk);   // 0 past the patch
         pv[r][k] = v;
         ps[r] += v;
         pq[r] += v * v;
       }
     }
   } else {
+    GeoX gx[3];
+    GeoY gy[3];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      gx[u].zx = __builtin_amdgcn_readlane(lx.zx, u);
+      gx[u].pw = __builtin_amdgcn_readlane(lx.pw, u);
+      gx[u].col0 = __builtin_amdgcn_readlane(lx.col0, u);
+      gx[u].rx = __builtin_amdgcn_readlane(lx.rx, u);
+      gx[u].rw = __builtin_amdgcn_readlane(lx.rw, u);
+      gx[u].a = av[u];
+      gy[u].zy = __builtin_amdgcn_readlane(ly.zy, u);
+      gy[u].ph = __builtin_amdgcn_readlane(ly.ph, u);
+      gy[u].base_row = __builtin_amdgcn_readlane(ly.base_row, u);
+      gy[u].ry = __builtin_amdgcn_readlane(ly.ry, u);
+      gy[u].rh = __builtin_amdgcn_readlane(ly.rh, u);
+      gy[u].b = bv[u];
+    }
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
       Geo g;
