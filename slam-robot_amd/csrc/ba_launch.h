@@ -41,6 +41,9 @@ constexpr int kIntrFinThreads = 256;   // k_intr_fin
 // then k_update_lin's stamps
 constexpr int kTraceK = 128;
 constexpr int kUlStamp = 64 + 2 * kTraceK * 16;
+// k_schur per-segment stamps (SG_STAMP=1): 8 words per segment from kSegStamp (tools/schur_seg_stamps.py)
+constexpr int kSegStamp = kUlStamp + 16;
+constexpr int kSegStampMax = 1024;
 
 // ---- ba_sweep.hip
 void LaunchLinearizeK(int waves, int grid, hipStream_t s, const Dev& d);

@@ -316,6 +316,18 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d, int fin) {
   const int seg = (int)blockIdx.x - (fin ? 1 : 0);
   if (seg >= d.nseg) return;
   unsigned long long last_ = __builtin_amdgcn_s_memtime();
+  // per-segment stamps (a variant build with -DSG_SEG_STAMPS, run with SG_STAMP=1; segments < kSegStampMax,
+  // tools/schur_seg_stamps.py): the workgroup's span and each wave group's busy cycles (work between barriers)
+#ifdef SG_SEG_STAMPS
+  const bool sstamp = d.stamps != nullptr && seg < kSegStampMax;
+  const unsigned long long t_wg = last_;
+  unsigned long long busy = 0, tb = 0;
+#define SG_BUSY_BEGIN if (sstamp) tb = __builtin_amdgcn_s_memtime();
+#define SG_BUSY_END if (sstamp) busy += __builtin_amdgcn_s_memtime() - tb;
+#else
+#define SG_BUSY_BEGIN
+#define SG_BUSY_END
+#endif
   // the segment's descriptor load goes out beside LmState's (see k_S_reduce)
   const SchurSeg sg = d.segs[seg];
   if (st->done) return;
@@ -329,23 +341,29 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d, int fin) {
     __syncthreads();
     SG_SSTAMP(33)
     for (int s = 0; s <= nbt; ++s) {
+      SG_BUSY_BEGIN
       if (s < nbt)
         schur_cells(d, d.J[st->cur], d.sbatch[sg.bt0 + s], tid, c0w, sh.L[s % 3], sh.pinf[s % 3], sh.pob[s % 3], sh.cmap[s % 3],
                     sh.X[s & 1]);
+      SG_BUSY_END
       SG_SSTAMP(34)
       __syncthreads();
       SG_SSTAMP(36)
     }
   } else if (wave == kSchurCellWaves) {
     // the point wave
+    SG_BUSY_BEGIN
     if (nbt > 0) linfail += schur_points(d, st, d.sbatch[sg.bt0], lane, sh.L[0], sh.w[0], sh.pinf[0], sh.pob[0], sh.cmap[0]);
+    SG_BUSY_END
     __syncthreads();
     for (int s = 0; s <= nbt; ++s) {
+      SG_BUSY_BEGIN
       if (s + 1 < nbt) {
         const int q = (s + 1) % 3;
         linfail += schur_points(d, st, d.sbatch[sg.bt0 + s + 1], lane, sh.L[q], sh.w[q], sh.pinf[q], sh.pob[q],
                                 sh.cmap[q]);
       }
+      SG_BUSY_END
       SG_SSTAMP(35)
       __syncthreads();
       SG_SSTAMP(37)
@@ -360,6 +378,7 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d, int fin) {
     __syncthreads();
     SG_SSTAMP(41)
     for (int s = 0; s <= nbt; ++s) {
+      SG_BUSY_BEGIN
       if (s >= 1) {
         const SchurBatch B = d.sbatch[sg.bt0 + s - 1];
         const int npts = B.p1 - B.p0;
@@ -377,6 +396,7 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d, int fin) {
         }
         SG_SSTAMP(42)
       }
+      SG_BUSY_END
       __syncthreads();
       SG_SSTAMP(44)
     }
@@ -394,6 +414,25 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d, int fin) {
   }
   linfail = block_sum<kSchurThreads>(linfail, sh.red);
   if (tid == 0) d.seg_fail[seg] = linfail;
+#ifdef SG_SEG_STAMPS
+  if (sstamp && lane == 0) {
+    unsigned long long* ss = d.stamps + kSegStamp + 8 * seg;
+    if (wave == 0) {
+      ss[0] += __builtin_amdgcn_s_memtime() - t_wg;
+      ss[1] += busy;
+      ss[4] = sg.p0;
+      ss[5] = sg.p1;
+      ss[6] = nbt;
+      ss[7] += 1;
+    } else if (wave == kSchurCellWaves) {
+      ss[2] += busy;
+    } else if (wave == kSchurCellWaves + 1) {
+      ss[3] += busy;
+    }
+  }
+#endif
+#undef SG_BUSY_BEGIN
+#undef SG_BUSY_END
 }
 
 // A point spanning more blocks than a segment window (a whole-map solve's long track): one workgroup, the

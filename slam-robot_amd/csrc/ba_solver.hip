@@ -874,7 +874,7 @@ void BaSolver::Load(const sg_problem& p) {
     kpart_.Resize((size_t)(NB_ + 1) * ncam_ * 42);
   }
   stamp_on_ = getenv("SG_STAMP") && getenv("SG_STAMP")[0] == '1';
-  if (stamp_on_) stamps_.Resize(kUlStamp + 16);
+  if (stamp_on_) stamps_.Resize(kSegStamp + 8 * kSegStampMax);
   lap("resize");
   ResetState(s);
   if (host_timing) DevMark(s, 3);
