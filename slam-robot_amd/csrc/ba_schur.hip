@@ -122,18 +122,83 @@ struct SchurLds {
   double red[kSchurThreads / 64];
 };
 
-// Point wave, thread t < npts of batch B: its point block, table entries and cell map.
-__device__ __forceinline__ double schur_points(const Dev& d, const LmState* st, const SchurBatch& B, int t,
-                                               double* Lsh, double* wsh, int4* pinf, int2* pob, uint8_t* cmap) {
+// The point wave's inputs for one point (thread t of batch B), loaded one batch ahead of their use so that their
+// memory latency overlaps the previous batch's arithmetic; LmState's fields the pass reads are fixed for the
+// launch (ba_kernels.h's contract) and read once.
+struct PointPrm {
+  int cur, reuse;
+  double radius, min_diag, max_diag;
+};
+struct PointIn {
+  int2 pi;
+  int4 pm;
+  int free;
+  double V[10];
+  double4 s4, g4, d4;
+};
+__device__ __forceinline__ void point_load(const Dev& d, const PointPrm& pr, const SchurBatch& B, int t, PointIn& in) {
+  in.free = 0;
+  if (t >= B.p1 - B.p0) return;
+  const int p = B.p0 + t;
+  in.pi = d.pinfo[p];
+  in.pm = d.pmx[p];
+  in.free = d.pfree[p];
+  const double* Vp = d.V[pr.cur] + 10 * (size_t)p;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) in.V[i] = Vp[i];
+  in.s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
+  in.g4 = reinterpret_cast<const double4*>(d.g[pr.cur])[p];
+  if (pr.reuse) in.d4 = reinterpret_cast<const double4*>(d.diag_p)[p];
+}
+// point_block's arithmetic on preloaded inputs, then the point's table entries and cell map
+__device__ __forceinline__ double point_finish(const Dev& d, const PointPrm& pr, const SchurBatch& B, int t,
+                                               const PointIn& in, double* Lsh, double* wsh, int4* pinf, int2* pob,
+                                               uint8_t* cmap) {
   if (t >= B.p1 - B.p0) return 0.0;
   const int p = B.p0 + t;
-  const int2 pi = d.pinfo[p];
-  const int4 pm = d.pmx[p];   // operand offset, jhi, observation of the first block (-1), first cell
-  int span = pi.y & 0xff, jhi = pm.y;
+  int span = in.pi.y & 0xff, jhi = in.pm.y;
   double fail = 0.0;
-  if (d.pfree[p]) {
-    double Vi[10], Li[10], w[4];
-    if (!point_block(d, st, p, Vi, Li, w)) fail = 1.0;
+  if (in.free) {
+    const double sp[4] = {in.s4.x, in.s4.y, in.s4.z, in.s4.w};
+    const double gs[4] = {in.g4.x * sp[0], in.g4.y * sp[1], in.g4.z * sp[2], in.g4.w * sp[3]};
+    double dp[4];
+    if (!pr.reuse) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a) dp[a] = fmin(fmax(sp[a] * sp[a] * in.V[u4(a, a)], pr.min_diag), pr.max_diag);
+      reinterpret_cast<double4*>(d.diag_p)[p] = make_double4(dp[0], dp[1], dp[2], dp[3]);
+    } else {
+      dp[0] = in.d4.x; dp[1] = in.d4.y; dp[2] = in.d4.z; dp[3] = in.d4.w;
+    }
+    double Vt[10], Vi[10], Li[10];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (c >= a) Vt[u4(a, c)] = sp[a] * in.V[u4(a, c)] * sp[c] + (a == c ? dp[a] / pr.radius : 0.0);
+    if (!inv4_spd(Vt, Vi, Li)) {
+      fail = 1.0;
+#pragma unroll
+      for (int i = 0; i < 10; ++i) Vi[i] = Li[i] = NAN;
+    }
+    double tp[4], w[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      double s = 0.0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) s += sym4(Vi, a, c) * gs[c];
+      tp[a] = s;
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      double s = 0.0;
+#pragma unroll
+      for (int c = 0; c <= a; ++c) s += Li[l4(a, c)] * gs[c];
+      w[a] = s;
+    }
+    double* Vo = d.Vinv + 10 * (size_t)p;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) Vo[i] = Vi[i];
+    reinterpret_cast<double4*>(d.tp)[p] = make_double4(tp[0], tp[1], tp[2], tp[3]);
 #pragma unroll
     for (int i = 0; i < 10; ++i) Lsh[10 * t + i] = Li[i];
 #pragma unroll
@@ -142,17 +207,17 @@ __device__ __forceinline__ double schur_points(const Dev& d, const LmState* st, 
     span = 0;
     jhi = -1;
   }
-  pinf[t] = make_int4(pi.y >> 8, span, pm.x, jhi);
-  pob[t] = make_int2(pm.z, pm.w);
-  for (int k = 0; k < span; ++k) cmap[pm.w + k] = (uint8_t)t;
+  pinf[t] = make_int4(in.pi.y >> 8, span, in.pm.x, jhi);
+  pob[t] = make_int2(in.pm.z, in.pm.w);
+  for (int k = 0; k < span; ++k) cmap[in.pm.w + k] = (uint8_t)t;
   return fail;
 }
 
 // Cell waves: thread per cell (point p, block b) of batch B.  E_{p,b} = sum_o G_o J~c,o with
 // G_o = L^-1 J~p,o^T (4 x 2), written straight into the point's operand tiles: window column c = 6 b + a - c0w
 // goes to tile c >> 4, lane (c & 15) + 16 k.  A point observed once in every block of its span (obs sorted by
-// block at load) finds its observation at a fixed offset; others read the cell records.  The first and last
-// cell of a point also zero the columns of its tiles 0 .. jhi outside its span.
+// block at load) finds its observation at a fixed offset; others read the cell records.  The cells of a point
+// also zero the columns of its tiles 0 .. jhi outside its span (its margins), dealt round-robin over them.
 // Each thread takes two cells per round and issues the loads of both (the common single-observation cells:
 // J pairs and scales) before either's arithmetic, so two cells' memory latencies overlap (the same
 // arithmetic in the same order as one cell at a time: the same bits).
@@ -257,14 +322,17 @@ __device__ __forceinline__ void schur_cells(const Dev& d, const double* J, const
       double* xp = Xb + pi.z;
       const int col0 = 6 * b - c0w;
       auto at = [&](int col, int k) -> double& { return xp[64 * (col >> 4) + 16 * k + (col & 15)]; };
-      if (b == pi.x)   // left margin: the columns of tiles 0 .. jhi before the span (the consumer reads them all)
-        for (int col = 0; col < col0; ++col)
+      {
+        // the point's margins — the columns of its tiles 0 .. jhi outside its span, which the consumer reads —
+        // zeroed by all of its span cells, margin column m by cell m mod span (one cell per margin used to take
+        // them all: 40 % of the cell waves' time at C5, profiles/r5_s1_schur_ab.log)
+        const int q = b - pi.x, lo = 6 * pi.x - c0w, hi = lo + 6 * pi.y, nl = lo, nm = lo + 16 * (pi.w + 1) - hi;
+        for (int m = q; m < nm; m += pi.y) {
+          const int col = m < nl ? m : hi + (m - nl);
 #pragma unroll
           for (int k = 0; k < 4; ++k) at(col, k) = 0.0;
-      if (b == pi.x + pi.y - 1)   // right margin: after the span, to the end of tile jhi
-        for (int col = col0 + 6; col < 16 * (pi.w + 1); ++col)
-#pragma unroll
-          for (int k = 0; k < 4; ++k) at(col, k) = 0.0;
+        }
+      }
       if (simple[h]) {
         cell_apply(ops[h], L, col0, true, at);
         continue;
@@ -351,19 +419,36 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d, int fin) {
       SG_SSTAMP(36)
     }
   } else if (wave == kSchurCellWaves) {
-    // the point wave
+    // the point wave: batch k's point blocks in step k - 1, its inputs loaded in step k - 2
     SG_BUSY_BEGIN
-    if (nbt > 0) linfail += schur_points(d, st, d.sbatch[sg.bt0], lane, sh.L[0], sh.w[0], sh.pinf[0], sh.pob[0], sh.cmap[0]);
+    const PointPrm pr{st->cur, st->reuse_diag, st->radius, st->min_diag, st->max_diag};
+    PointIn pin, pnx;
+    SchurBatch Bk{}, Bn{};
+    if (nbt > 0) {
+      Bk = d.sbatch[sg.bt0];
+      point_load(d, pr, Bk, lane, pin);
+    }
+    if (nbt > 1) {
+      Bn = d.sbatch[sg.bt0 + 1];
+      point_load(d, pr, Bn, lane, pnx);
+    }
+    if (nbt > 0) linfail += point_finish(d, pr, Bk, lane, pin, sh.L[0], sh.w[0], sh.pinf[0], sh.pob[0], sh.cmap[0]);
     SG_BUSY_END
     __syncthreads();
     for (int s = 0; s <= nbt; ++s) {
       SG_BUSY_BEGIN
       if (s + 1 < nbt) {
         const int q = (s + 1) % 3;
-        linfail += schur_points(d, st, d.sbatch[sg.bt0 + s + 1], lane, sh.L[q], sh.w[q], sh.pinf[q], sh.pob[q],
-                                sh.cmap[q]);
+        Bk = Bn;
+        pin = pnx;
+        if (s + 2 < nbt) {
+          Bn = d.sbatch[sg.bt0 + s + 2];
+          point_load(d, pr, Bn, lane, pnx);
+        }
+        linfail += point_finish(d, pr, Bk, lane, pin, sh.L[q], sh.w[q], sh.pinf[q], sh.pob[q], sh.cmap[q]);
       }
       SG_BUSY_END
+
       SG_SSTAMP(35)
       __syncthreads();
       SG_SSTAMP(37)
