@@ -497,11 +497,66 @@ void BaSolver::Load(const sg_problem& p) {
     if (cell_obs.empty()) cell_obs.push_back(0);
   }
   {
-    // points per segment: one segment per CU (the workgroup's LDS holds one per CU; fewer, longer segments
-    // write fewer partial tiles and keep the producer/consumer pipeline full: 256 / 384 / 512 / 768 / 1024
-    // segments measured 35.9 / 46.5 / 40.9 / 47.8 / 53.0 us at C2, profiles/r2 segs sweep)
-    const int target = ncu_;
-    const int maxpts = std::max(16, (P_ + target - 1) / target);
+    // Segments: one per CU (the workgroup's LDS holds one per CU; fewer, longer segments write fewer partial tiles
+    // and keep the producer/consumer pipeline full: 256 / 384 / 512 / 768 / 1024 segments measured 35.9 / 46.5 /
+    // 40.9 / 47.8 / 53.0 us at C2, profiles/r2 segs sweep), balanced by the work of the busiest MFMA wave rather
+    // than by point count (round 5): a point costs its slots on that wave, ceil(schur_aug_base(jhi + 1) /
+    // kSchurCWaves) with jhi its last tile in the segment's window, plus kSegPointCost for its fetch (the MFMA
+    // waves are the bound once the producers are pipelined; 0 / 1 / 2 / 4 / 8 measured C5 k_schur 292 / 260 /
+    // 245 / 238 / 244 us against 259 with equal point counts, profiles/r5_s1_schur_ab.log).  The cap starts at the
+    // estimated total / CUs (each point's tiles counted from its own first tile) and is raised while the window
+    // breaks push the count past the CUs: two passes at C2 and C5.
+    constexpr int kSegMinPts = 16;      // small problems: no segment of a handful of points
+    constexpr int kSegPointCost = 4;
+    auto point_cost = [&](int j, int tile0) {
+      const int sp = sspan(j);
+      if (sp == 0) return kSegPointCost;
+      const int e = (6 * (pfirst[point_perm_[j]] + sp) - 1) / 16 - tile0;
+      return kSegPointCost + (schur_aug_base(e + 1) + kSchurCWaves - 1) / kSchurCWaves;
+    };
+    std::vector<int32_t> seg_end;   // exclusive end of each planned segment, in point order
+    auto plan = [&](long long cap) {
+      seg_end.clear();
+      for (int i = 0; i < P_;) {
+        if (sspan(i) > kSegNbMax) {   // a wide point: k_schur_wide (the build loop below)
+          ++i;
+          continue;
+        }
+        int clo = INT32_MAX, chi = -1, j = i;
+        long long acc = 0;
+        while (j < P_) {
+          const int sp = sspan(j);
+          if (sp > kSegNbMax) break;
+          int l2 = clo, h2 = chi;
+          if (sp > 0) {
+            const int pf = pfirst[point_perm_[j]];
+            l2 = std::min(clo, 6 * pf);
+            h2 = std::max(chi, 6 * (pf + sp));
+            if ((h2 + 15) / 16 - l2 / 16 > kSchurTW) break;
+          }
+          const int c = point_cost(j, l2 == INT32_MAX ? 0 : l2 / 16);
+          if (j - i >= kSegMinPts && acc + c > cap) break;
+          acc += c;
+          clo = l2;
+          chi = h2;
+          ++j;
+        }
+        seg_end.push_back(j);
+        i = j;
+      }
+    };
+    {
+      long long est = 0;
+      for (int j = 0; j < P_; ++j)
+        if (sspan(j) <= kSegNbMax) est += point_cost(j, sspan(j) ? 6 * pfirst[point_perm_[j]] / 16 : 0);
+      long long cap = std::max(1LL, (est + ncu_ - 1) / ncu_);
+      for (int pass = 0; pass < 8; ++pass) {
+        plan(cap);
+        if ((int)seg_end.size() <= ncu_) break;
+        cap += cap * (seg_end.size() - ncu_) * 3 / (2 * ncu_) + cap / 200 + 1;
+      }
+    }
+    size_t next_seg = 0;
     int cnext = 0;
     for (int i = 0; i < P_;) {
       if (sspan(i) > kSegNbMax) {
@@ -525,7 +580,9 @@ void BaSolver::Load(const sg_problem& p) {
       sg.p0 = i;
       int clo = INT32_MAX, chi = -1, blo = INT32_MAX, bhi = -1;   // columns [clo, chi), blocks [blo, bhi]
       int j = i;
-      while (j < P_ && j - i < maxpts) {
+      SG_REQUIRE(next_seg < seg_end.size() && seg_end[next_seg] > i, SG_EINVAL, "Schur segment plan out of step");
+      const int jend = seg_end[next_seg++];
+      while (j < jend) {
         const int sp = sspan(j);
         if (sp > kSegNbMax) break;
         if (sp > 0) {
