@@ -115,8 +115,9 @@ __device__ __forceinline__ bool point_block(const Dev& d, const LmState* st, int
 struct SchurLds {
   double X[2][kSchurXCap + 64 * kSchurTW];   // operand tiles of the batch's points; padding for over-reads
   double L[3][kSchurBatchPts * 10];          // L^-1 of the batch's points
-  double w[3][kSchurBatchPts * 4];           // w = L^-1 g~
-  int4 pinf[3][kSchurBatchPts];              // first block, span, operand offset, last window tile (jhi)
+  double w[3][kSchurBatchPts * 5];           // w = L^-1 g~ and a zero per point (schur_fetch)
+  int4 pinf[3][kSchurBatchPts];              // first block, span, operand offset | (jhi + 1) << 20, last window
+                                             // tile jhi
   int2 pob[3][kSchurBatchPts];               // observation of its first block (-1: cell records), first cell
   uint8_t cmap[3][kSchurBatchCells];         // batch-local cell -> point
   double red[kSchurThreads / 64];
@@ -202,12 +203,13 @@ __device__ __forceinline__ double point_finish(const Dev& d, const PointPrm& pr,
 #pragma unroll
     for (int i = 0; i < 10; ++i) Lsh[10 * t + i] = Li[i];
 #pragma unroll
-    for (int a = 0; a < 4; ++a) wsh[4 * t + a] = w[a];
+    for (int a = 0; a < 4; ++a) wsh[5 * t + a] = w[a];
+    wsh[5 * t + 4] = 0.0;
   } else {
     span = 0;
     jhi = -1;
   }
-  pinf[t] = make_int4(in.pi.y >> 8, span, in.pm.x, jhi);
+  pinf[t] = make_int4(in.pi.y >> 8, span, in.pm.x | ((jhi + 1) << 20), jhi);
   pob[t] = make_int2(in.pm.z, in.pm.w);
   for (int k = 0; k < span; ++k) cmap[in.pm.w + k] = (uint8_t)t;
   return fail;
@@ -319,7 +321,7 @@ __device__ __forceinline__ void schur_cells(const Dev& d, const double* J, const
       const int4 pi = pinf[t];
       const int b = bc[h];
       const double* L = Lsh + 10 * t;
-      double* xp = Xb + pi.z;
+      double* xp = Xb + (pi.z & 0xfffff);
       const int col0 = 6 * b - c0w;
       auto at = [&](int col, int k) -> double& { return xp[64 * (col >> 4) + 16 * k + (col & 15)]; };
       {

@@ -78,21 +78,24 @@ __device__ __forceinline__ void schur_mfma(f64x4 (&acc)[kSchurTPW], const double
   schur_slots<W, 0>(acc, X, wop, (nu - W + kSchurCWaves - 1) / kSchurCWaves);
 }
 
-// Operands of point t of the batch (point table pv, one point per lane: {.., .., xoff, jhi}; t >= npts: none):
-// every operand column the wave may use, X_j[lane i + 16 k] = E_p[k][16 j + i] at xoff + 64 j (reads past the
-// point's tiles land in the next point or the buffer's padding and feed only skipped slots), and the w operand
-// (lanes 16 k hold w_k).
+// Operands of point t of the batch (point table pv, one point per lane: {.., .., xoff | (jhi + 1) << 20, jhi};
+// t >= npts: none): every operand column the wave may use, X_j[lane i + 16 k] = E_p[k][16 j + i] at xoff + 64 j
+// (reads past the point's tiles land in the next point or the buffer's padding and feed only skipped slots), and
+// the w operand, read through the lane's own pointer wl into the point's 5-double w record {w_0 .. w_3, 0}: lanes
+// 16 k hold w_k, every other lane the zero (one VALU address per point, no select).  Every VALU instruction of an
+// MFMA wave between two MFMAs costs ~16 cycles (tools/mfma_interleave.hip), so the point's table word is one
+// v_readlane and the rest scalar.
 template <unsigned kNeed>
-__device__ __forceinline__ void schur_fetch(const double* Xb, const double* wsh, const int4& pv, int t, int npts,
+__device__ __forceinline__ void schur_fetch(const double* Xb, const double* wl, const int4& pv, int t, int npts,
                                             int lane, double (&X)[kSchurTW], double& wop, int& jhi) {
   const int tt = min(t, npts - 1);
-  jhi = t < npts ? __builtin_amdgcn_readlane(pv.w, tt) : -1;
-  const double* xp = Xb + __builtin_amdgcn_readlane(pv.z, tt) + lane;
+  const int v = __builtin_amdgcn_readlane(pv.z, tt);
+  jhi = t < npts ? (v >> 20) - 1 : -1;
+  const double* xp = Xb + (v & 0xfffff) + lane;
 #pragma unroll
   for (int j = 0; j < kSchurTW; ++j)
     if ((kNeed >> j) & 1u) X[j] = xp[64 * j];
-  const double wv = wsh[4 * tt + (lane >> 4)];
-  wop = (lane & 15) == 0 ? wv : 0.0;
+  wop = wl[5 * tt];
 }
 // The wave's work on one batch (whole wave active: the point table is read by v_readlane): the operands of
 // point t + 1 are read before the MFMAs of point t.
@@ -101,16 +104,17 @@ __device__ __forceinline__ void schur_wave_batch(f64x4 (&acc)[kSchurTPW], const 
                                                  const int4* pinf, int npts, int lane) {
   constexpr unsigned kNeed = schur_need(W);
   const int4 pv = pinf[min(lane, npts - 1)];   // npts <= 64
+  const double* wl = wsh + ((lane & 15) == 0 ? (lane >> 4) : 4);
   double XA[kSchurTW], XB[kSchurTW];
 #pragma unroll
   for (int j = 0; j < kSchurTW; ++j) XA[j] = XB[j] = 0.0;
   double wa, wb;
   int ha, hb;
-  schur_fetch<kNeed>(Xb, wsh, pv, 0, npts, lane, XA, wa, ha);
+  schur_fetch<kNeed>(Xb, wl, pv, 0, npts, lane, XA, wa, ha);
   for (int t = 0; t < npts; t += 2) {
-    schur_fetch<kNeed>(Xb, wsh, pv, t + 1, npts, lane, XB, wb, hb);
+    schur_fetch<kNeed>(Xb, wl, pv, t + 1, npts, lane, XB, wb, hb);
     schur_mfma<W>(acc, XA, wa, ha);
-    schur_fetch<kNeed>(Xb, wsh, pv, t + 2, npts, lane, XA, wa, ha);
+    schur_fetch<kNeed>(Xb, wl, pv, t + 2, npts, lane, XA, wa, ha);
     schur_mfma<W>(acc, XB, wb, hb);
   }
 }
