@@ -43,39 +43,20 @@ __host__ __device__ constexpr unsigned schur_need(int W) {
   return m;
 }
 
-// acc += A B with the accumulator tied in place.  A conditionally executed __builtin_amdgcn_mfma leaves the old
-// accumulator live beside the new one (a PHI), so the compiler picks the untied form and copies the
-// accumulators around every MFMA; the tied asm form keeps them in place.  The compiler does not see this as an
-// MFMA, so the hazards are ours: the s_nop covers a VALU write -> MFMA read of an operand (2 wait states; the
-// compiler may place a register copy of an operand right before the asm), and readers of the accumulators
-// must first call mfma_drain().  MFMA -> MFMA on the same accumulator is interlocked.
-__device__ __forceinline__ void mfma_acc(f64x4& acc, double a, double b) {
-  asm volatile("s_nop 1\n\tv_mfma_f64_16x16x4_f64 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
-}
+// The MFMAs run as inline asm (schur_chain.h): the compiler does not see them as MFMAs, so the hazards are ours.
+// Readers of the accumulators must first call mfma_drain(); MFMA -> MFMA on the same accumulator is interlocked.
 // wait states after the last asm MFMA before VALU / memory instructions read its accumulator
 __device__ __forceinline__ void mfma_drain() { asm volatile("s_nop 15\n\ts_nop 15" ::: "memory"); }
 
-// One point: wave W runs the prefix of its slots below schur_aug_base(jhi + 1), as nested tests (a not-taken
-// branch per MFMA, one taken branch out).  The point's operand tiles are 0 .. jhi of the window (zero outside
-// its columns), so tiles with r below its first tile multiply zeros.
-template <int W, int S>
-__device__ __forceinline__ void schur_slots(f64x4 (&acc)[kSchurTPW], const double (&X)[kSchurTW], double wop, int ns) {
-  if constexpr (S < kSchurTPW && W + kSchurCWaves * S < kSchurAug) {
-    constexpr int u = W + kSchurCWaves * S;
-    constexpr int c = schur_aug_c(u), r = schur_aug_r(u);
-    if (__builtin_expect(S < ns, 1)) {
-      if constexpr (r <= c)
-        mfma_acc(acc[S], X[r], X[c]);
-      else
-        mfma_acc(acc[S], X[c], wop);
-      schur_slots<W, S + 1>(acc, X, wop, ns);
-    }
-  }
-}
+// One point: wave W runs the prefix of its slots below schur_aug_base(jhi + 1): the generated asm chain
+// (schur_chain.h, tools/gen_schur_chain.py) entered at the offset that leaves exactly those slots, back to back.
+// The point's operand tiles are 0 .. jhi of the window (zero outside its columns), so tiles with r below its
+// first tile multiply zeros.
+#include "schur_chain.h"
 template <int W>
 __device__ __forceinline__ void schur_mfma(f64x4 (&acc)[kSchurTPW], const double (&X)[kSchurTW], double wop, int jhi) {
   const int nu = schur_aug_base(jhi + 1);
-  schur_slots<W, 0>(acc, X, wop, (nu - W + kSchurCWaves - 1) / kSchurCWaves);
+  SchurChain<W>::run(acc, X, wop, (nu - W + kSchurCWaves - 1) / kSchurCWaves);
 }
 
 // Operands of point t of the batch (point table pv, one point per lane: {.., .., xoff | (jhi + 1) << 20, jhi};
