@@ -21,6 +21,24 @@ __device__ __forceinline__ void lds_fence_wave() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
+// Point accumulators in LDS (V, g of the round's points; the pass-1 terms A_p^T u): the observations of a point
+// are consecutive lanes, so one LDS atomic instruction hits each of the point's addresses from ~8-10 lanes at
+// once and the LDS serialises them (the point-block atomics were 22 % of k_update_lin at C2, 9 % at C5: a
+// timing-only build without them, profiles/r5_s1_sweep_ab.log).  Each value has kPtCopies interleaved copies and
+// lane l adds into copy l mod kPtCopies, so a point's lanes split over the copies; readers sum the copies in copy
+// order (pt_sum).  Within one copy the hardware applies the lanes in lane order, so the sums stay deterministic.
+// (Two copies keep the one-wave k_update_lin workgroup inside the LDS share of twelve waves per CU.)
+constexpr int kPtCopies = 2;
+__device__ __forceinline__ void pt_add(double* pa, int v, int lane, double x) {
+  atomicAdd(pa + v * kPtCopies + (lane & (kPtCopies - 1)), x);
+}
+__device__ __forceinline__ double pt_sum(const double* pa, int v) {
+  double s = pa[v * kPtCopies];
+#pragma unroll
+  for (int c = 1; c < kPtCopies; ++c) s += pa[v * kPtCopies + c];
+  return s;
+}
+
 // The chunk's camera partial (the waves' window accumulators summed in wave order) into its cam_slab slot, and
 // wave 1's six chunk scalars into wave 0's (sums in wave order, gmax a maximum).  Every thread of the
 // workgroup calls it (a workgroup barrier).
@@ -51,7 +69,8 @@ __global__ __launch_bounds__(kLinThreads * kW) SG_LIN_ATTR void k_linearize(Dev 
   const bool first = st->first != 0;
   const LinChunk ch = d.lchunks[blockIdx.x];
   // per wave (wave w takes every kW-th round of the chunk, see LinChunk):
-  __shared__ double pacc_w[kW][kLinPts * 14];         // point blocks of the round: V (10) | g (4)
+  __shared__ double pacc_w[kW][kLinPts * 14 * kPtCopies];   // point blocks of the round: V (10) | g (4), kPtCopies
+                                                           // interleaved copies (pt_add)
   __shared__ double camacc_w[kW][kLinNbMax * kCamV];  // camera blocks of the window: upper Jc^T Jc | Jc^T r
   // the rarely-touched per-lane sums (failures, the fixed cost and |X|^2 of iteration 0) live in LDS, one slot
   // per lane, so they hold no registers across the projection (k_linearize's VGPR budget sets its occupancy)
@@ -67,7 +86,7 @@ __global__ __launch_bounds__(kLinThreads * kW) SG_LIN_ATTR void k_linearize(Dev 
   const double4* X4 = reinterpret_cast<const double4*>(d.X[cur]);
   const int ncv = ch.nb * kCamV;
   for (int i = lane; i < ncv; i += kLinThreads) camacc[i] = 0.0;
-  for (int i = lane; i < kLinPts * 14; i += kLinThreads) pacc[i] = 0.0;
+  for (int i = lane; i < kLinPts * 14 * kPtCopies; i += kLinThreads) pacc[i] = 0.0;
 #pragma unroll
   for (int k = 0; k < 4; ++k) lsum[k][lane] = 0.0;
   double cost = 0.0, gmax = 0.0;
@@ -145,13 +164,13 @@ __global__ __launch_bounds__(kLinThreads * kW) SG_LIN_ATTR void k_linearize(Dev 
         for (int i = 0; i < 4; ++i) Jo[64 * (7 + i)] = make_double2(Jp[2 * i], Jp[2 * i + 1]);
         Jo[64 * 11] = make_double2(c, 0.0);
         if (pf) {
-          double* pa = pacc + (p - Rc.p0) * 14;
+          double* pa = pacc + (p - Rc.p0) * 14 * kPtCopies;
 #pragma unroll
           for (int a = 0; a < 4; ++a) {
 #pragma unroll
             for (int cc = 0; cc < 4; ++cc)
-              if (cc >= a) atomicAdd(pa + u4(a, cc), Jp[a] * Jp[cc] + Jp[4 + a] * Jp[4 + cc]);
-            atomicAdd(pa + 10 + a, Jp[a] * rr[0] + Jp[4 + a] * rr[1]);
+              if (cc >= a) pt_add(pa, u4(a, cc), lane, Jp[a] * Jp[cc] + Jp[4 + a] * Jp[4 + cc]);
+            pt_add(pa, 10 + a, lane, Jp[a] * rr[0] + Jp[4 + a] * rr[1]);
           }
         }
         if (b >= 0) {
@@ -176,14 +195,14 @@ __global__ __launch_bounds__(kLinThreads * kW) SG_LIN_ATTR void k_linearize(Dev 
       const int np = Rc.p1 - Rc.p0;
       if (lane < np) {
         const int pp = Rc.p0 + lane;
-        double* pa = pacc + lane * 14;
+        double* pa = pacc + lane * 14 * kPtCopies;
         double V[10], g[4];
 #pragma unroll
-        for (int i = 0; i < 10; ++i) V[i] = pa[i];
+        for (int i = 0; i < 10; ++i) V[i] = pt_sum(pa, i);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) g[i] = pa[10 + i];
+        for (int i = 0; i < 4; ++i) g[i] = pt_sum(pa, 10 + i);
 #pragma unroll
-        for (int i = 0; i < 14; ++i) pa[i] = 0.0;
+        for (int i = 0; i < 14 * kPtCopies; ++i) pa[i] = 0.0;
         const bool pf = d.pfree[pp] != 0;
         double2* Vd = reinterpret_cast<double2*>(d.V[cur] + 10 * (size_t)pp);
 #pragma unroll
@@ -393,9 +412,9 @@ __device__ __forceinline__ void pu_pass1(const Dev& d, int cur, const LinRound& 
   }
   if (ob.b >= 0 || d.nk) {
     if (pacc && (m & kMetaPfree)) {
-      double* pa = pacc + (p - R.p0) * 4;
+      double* pa = pacc + (p - R.p0) * 4 * kPtCopies;
 #pragma unroll
-      for (int a = 0; a < 4; ++a) atomicAdd(pa + a, ob.Jp[a] * ob.u[0] + ob.Jp[4 + a] * ob.u[1]);
+      for (int a = 0; a < 4; ++a) pt_add(pa, a, lane, ob.Jp[a] * ob.u[0] + ob.Jp[4 + a] * ob.u[1]);
     }
   }
 }
@@ -435,13 +454,14 @@ __device__ __forceinline__ void pu_pass2(const Dev& d, int p0, int p1, int lane,
   const bool pf = d.pfree[p] != 0;
   const double4 Xv = reinterpret_cast<const double4*>(d.X[cur])[p];
   const double X[4] = {Xv.x, Xv.y, Xv.z, Xv.w};
-  double* pa = pacc + 4 * lane;
+  double* pa = pacc + 4 * kPtCopies * lane;
   double xp[4] = {0.0, 0.0, 0.0, 0.0}, Xn[4] = {X[0], X[1], X[2], X[3]};
   if (pf) {
     const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
     const double sp[4] = {s4.x, s4.y, s4.z, s4.w};
     const double4 g4 = reinterpret_cast<const double4*>(d.g[cur])[p];
-    const double rhs[4] = {g4.x * sp[0] - pa[0], g4.y * sp[1] - pa[1], g4.z * sp[2] - pa[2], g4.w * sp[3] - pa[3]};
+    const double rhs[4] = {g4.x * sp[0] - pt_sum(pa, 0), g4.y * sp[1] - pt_sum(pa, 1), g4.z * sp[2] - pt_sum(pa, 2),
+                           g4.w * sp[3] - pt_sum(pa, 3)};
     const double* Vi = d.Vinv + 10 * (size_t)p;
     double Vl[10];
 #pragma unroll
@@ -462,8 +482,9 @@ __device__ __forceinline__ void pu_pass2(const Dev& d, int p0, int p1, int lane,
     }
   }
 #pragma unroll
+  for (int i = 0; i < 4 * kPtCopies; ++i) pa[i] = 0.0;
+#pragma unroll
   for (int a = 0; a < 4; ++a) {
-    pa[a] = 0.0;
     xps[4 * lane + a] = xp[a];
     Xns[4 * lane + a] = Xn[a];
   }
@@ -485,9 +506,9 @@ __global__ __launch_bounds__(kLinThreads) void k_point_update(Dev d) {
   } else {
     ch = d.lchunks[-unit - 1];
   }
-  __shared__ double pacc[kLinPts * 4], xps[kLinPts * 4], Xns[kLinPts * 4];
+  __shared__ double pacc[kLinPts * 4 * kPtCopies], xps[kLinPts * 4], Xns[kLinPts * 4];
   const int lane = threadIdx.x;
-  for (int i = lane; i < kLinPts * 4; i += kLinThreads) pacc[i] = 0.0;
+  for (int i = lane; i < kLinPts * 4 * kPtCopies; i += kLinThreads) pacc[i] = 0.0;
   lds_fence_wave();
   double model = 0.0, candcost = 0.0, candfail = 0.0, step2 = 0.0, candx2 = 0.0;
   if (!ch.wide) {
@@ -605,16 +626,18 @@ __device__ __forceinline__ void ul_obs(const Dev& d, const LinRound& R, const Li
 #pragma unroll
   for (int i = 0; i < 4; ++i) Jo[64 * (7 + i)] = make_double2(Jp[2 * i], Jp[2 * i + 1]);
   Jo[64 * 11] = make_double2(c, 0.0);
+#ifndef SG_X_NOPATOM   // timing-only experiment build (results wrong): no point-block LDS atomics
   if (pf) {
-    double* pa = pacc + lp * 14;
+    double* pa = pacc + lp * 14 * kPtCopies;
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
 #pragma unroll
       for (int cc = 0; cc < 4; ++cc)
-        if (cc >= a) atomicAdd(pa + u4(a, cc), Jp[a] * Jp[cc] + Jp[4 + a] * Jp[4 + cc]);
-      atomicAdd(pa + 10 + a, Jp[a] * rr[0] + Jp[4 + a] * rr[1]);
+        if (cc >= a) pt_add(pa, u4(a, cc), lane, Jp[a] * Jp[cc] + Jp[4 + a] * Jp[4 + cc]);
+      pt_add(pa, 10 + a, lane, Jp[a] * rr[0] + Jp[4 + a] * rr[1]);
     }
   }
+#endif
   if (b >= 0) {
     auto add_cam = [&](double* dst) {
 #pragma unroll
@@ -635,14 +658,14 @@ __device__ __forceinline__ void ul_points(const Dev& d, int p0, int p1, int lane
                                           double& gmax) {
   if (lane >= p1 - p0) return;
   const int pp = p0 + lane;
-  double* pa = pacc + lane * 14;
+  double* pa = pacc + lane * 14 * kPtCopies;
   double V[10], g[4];
 #pragma unroll
-  for (int i = 0; i < 10; ++i) V[i] = pa[i];
+  for (int i = 0; i < 10; ++i) V[i] = pt_sum(pa, i);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) g[i] = pa[10 + i];
+  for (int i = 0; i < 4; ++i) g[i] = pt_sum(pa, 10 + i);
 #pragma unroll
-  for (int i = 0; i < 14; ++i) pa[i] = 0.0;
+  for (int i = 0; i < 14 * kPtCopies; ++i) pa[i] = 0.0;
   double2* Vd = reinterpret_cast<double2*>(d.V[nxt] + 10 * (size_t)pp);
 #pragma unroll
   for (int k = 0; k < 5; ++k) Vd[k] = make_double2(V[2 * k], V[2 * k + 1]);
@@ -675,10 +698,10 @@ __global__ __launch_bounds__(kLinThreads * kW) SG_LIN_ATTR void k_update_lin(Dev
   const LinChunk ch = d.lchunks[blockIdx.x];
   if (blockIdx.x == 0 && threadIdx.x == 0) d.st->spec_slot = nxt;   // (k_cam_reduce mode 1 reads it)
   // per wave (k_linearize's split of the chunk's rounds over its waves):
-  __shared__ double pacc_w[kW][kLinPts * 14];         // candidate point blocks of the round: V (10) | g (4)
+  __shared__ double pacc_w[kW][kLinPts * 14 * kPtCopies];   // candidate point blocks of the round (pt_add)
   __shared__ double camacc_w[kW][kLinNbMax * kCamV];  // candidate camera blocks of the window
   __shared__ double lsum_w[kW][2][kLinThreads];       // candidate failures: free, fixed observations
-  __shared__ double ua_w[kW][kLinPts * 4], xps_w[kW][kLinPts * 4], Xns_w[kW][kLinPts * 4];
+  __shared__ double ua_w[kW][kLinPts * 4 * kPtCopies], xps_w[kW][kLinPts * 4], Xns_w[kW][kLinPts * 4];
   __shared__ double wscal[8];                         // wave 1's chunk scalars
   const int lane = threadIdx.x & (kLinThreads - 1), wv = threadIdx.x / kLinThreads;
   double* pacc = pacc_w[wv];
@@ -689,8 +712,8 @@ __global__ __launch_bounds__(kLinThreads * kW) SG_LIN_ATTR void k_update_lin(Dev
   double* Xns = Xns_w[wv];   // X+
   const int ncv = ch.nb * kCamV;
   for (int i = lane; i < ncv; i += kLinThreads) camacc[i] = 0.0;
-  for (int i = lane; i < kLinPts * 14; i += kLinThreads) pacc[i] = 0.0;
-  for (int i = lane; i < kLinPts * 4; i += kLinThreads) ua[i] = 0.0;
+  for (int i = lane; i < kLinPts * 14 * kPtCopies; i += kLinThreads) pacc[i] = 0.0;
+  for (int i = lane; i < kLinPts * 4 * kPtCopies; i += kLinThreads) ua[i] = 0.0;
   lsum[0][lane] = 0.0;
   lsum[1][lane] = 0.0;
   lds_fence_wave();

@@ -57,6 +57,15 @@ __global__ void k(double* out, unsigned long long* cyc, int iters) {
 #define F "s_add_u32 %[s], %[s], 1\n\t"
       asm volatile(M(0) M(1) M(2) M(3) F F F F F F F F F F F F M(4) M(5) M(6) M(7) F F F F F F F F F F F F : OPS : INS : "scc");
 #undef F
+    else if constexpr (MODE == 9) {   // v_mfma_f64_4x4x4_4b_f64 (4 blocks of 4x4x4) on 8 independent accumulators
+      double d[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) d[i] = acc[i][0];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) d[i] = __builtin_amdgcn_mfma_f64_4x4x4f64(x, y, d[i], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i][0] = d[i];
+    }
   }
   __syncthreads();
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -88,5 +97,6 @@ int main() {
   run<6>(out, cyc, "s_nop 1 before each");
   run<7>(out, cyc, "6 ds_read_b64 after 8");
   run<8>(out, cyc, "12 SALU after 4");
+  run<9>(out, cyc, "v_mfma_f64_4x4x4_4b_f64 straight");
   return 0;
 }
