@@ -458,9 +458,13 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d, int fin) {
   } else {
     // MFMA waves: wave cw owns the augmented window slots u = cw + kSchurCWaves s
     const int cw = wave - kSchurCellWaves - 1;
-    f64x4 acc[kSchurTPW];
+    f64x4 acc[kSchurTPW];      // window-tile slots
+    double accr[kSchurTPW];    // rhs slots (schur_chain.h)
 #pragma unroll
-    for (int s = 0; s < kSchurTPW; ++s) acc[s] = f64x4{0.0, 0.0, 0.0, 0.0};
+    for (int s = 0; s < kSchurTPW; ++s) {
+      acc[s] = f64x4{0.0, 0.0, 0.0, 0.0};
+      accr[s] = 0.0;
+    }
     SG_SSTAMP(40)
     __syncthreads();
     SG_SSTAMP(41)
@@ -474,7 +478,7 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d, int fin) {
         const int4* pinf = sh.pinf[(s - 1) % 3];
         switch (cw) {
 #define SG_SCHUR_CASE(W) \
-          case W: schur_wave_batch<W>(acc, Xb, wsh, pinf, npts, lane); break;
+          case W: schur_wave_batch<W>(acc, accr, Xb, wsh, pinf, npts, lane); break;
           SG_SCHUR_CASE(0) SG_SCHUR_CASE(1) SG_SCHUR_CASE(2) SG_SCHUR_CASE(3)
 #if SG_SCHUR_CW > 4
           SG_SCHUR_CASE(4) SG_SCHUR_CASE(5) SG_SCHUR_CASE(6) SG_SCHUR_CASE(7)
@@ -490,7 +494,7 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d, int fin) {
     mfma_drain();
     switch (cw) {
 #define SG_SCHUR_CASE(W) \
-      case W: schur_store<W>(acc, slab, sg.ntw, lane); break;
+      case W: schur_store<W>(acc, accr, slab, sg.ntw, lane); break;
       SG_SCHUR_CASE(0) SG_SCHUR_CASE(1) SG_SCHUR_CASE(2) SG_SCHUR_CASE(3)
 #if SG_SCHUR_CW > 4
       SG_SCHUR_CASE(4) SG_SCHUR_CASE(5) SG_SCHUR_CASE(6) SG_SCHUR_CASE(7)

@@ -54,16 +54,18 @@ __device__ __forceinline__ void mfma_drain() { asm volatile("s_nop 15\n\ts_nop 1
 // first tile multiply zeros.
 #include "schur_chain.h"
 template <int W>
-__device__ __forceinline__ void schur_mfma(f64x4 (&acc)[kSchurTPW], const double (&X)[kSchurTW], double wop, int jhi) {
+__device__ __forceinline__ void schur_mfma(f64x4 (&acc)[kSchurTPW], double (&accr)[kSchurTPW], const double (&X)[kSchurTW],
+                                           double wop, int jhi) {
   const int nu = schur_aug_base(jhi + 1);
-  SchurChain<W>::run(acc, X, wop, (nu - W + kSchurCWaves - 1) / kSchurCWaves);
+  SchurChain<W>::run(acc, accr, X, wop, (nu - W + kSchurCWaves - 1) / kSchurCWaves);
 }
 
 // Operands of point t of the batch (point table pv, one point per lane: {.., .., xoff | (jhi + 1) << 20, jhi};
 // t >= npts: none): every operand column the wave may use, X_j[lane i + 16 k] = E_p[k][16 j + i] at xoff + 64 j
 // (reads past the point's tiles land in the next point or the buffer's padding and feed only skipped slots), and
-// the w operand, read through the lane's own pointer wl into the point's 5-double w record {w_0 .. w_3, 0}: lanes
-// 16 k hold w_k, every other lane the zero (one VALU address per point, no select).  Every VALU instruction of an
+// the w operand of the rhs slots' v_mfma_f64_4x4x4_4b_f64 (B of block b, k x j at lane j + 4 b + 16 k: column 0 is
+// w), read through the lane's own pointer wl into the point's 5-double w record {w_0 .. w_3, 0}: lanes with
+// lane % 4 == 0 hold w_{lane / 16}, every other lane the zero (one VALU address per point, no select).  Every VALU instruction of an
 // MFMA wave between two MFMAs costs ~16 cycles (tools/mfma_interleave.hip), so the point's table word is one
 // v_readlane and the rest scalar.
 template <unsigned kNeed>
@@ -81,11 +83,11 @@ __device__ __forceinline__ void schur_fetch(const double* Xb, const double* wl, 
 // The wave's work on one batch (whole wave active: the point table is read by v_readlane): the operands of
 // point t + 1 are read before the MFMAs of point t.
 template <int W>
-__device__ __forceinline__ void schur_wave_batch(f64x4 (&acc)[kSchurTPW], const double* Xb, const double* wsh,
-                                                 const int4* pinf, int npts, int lane) {
+__device__ __forceinline__ void schur_wave_batch(f64x4 (&acc)[kSchurTPW], double (&accr)[kSchurTPW], const double* Xb,
+                                                 const double* wsh, const int4* pinf, int npts, int lane) {
   constexpr unsigned kNeed = schur_need(W);
   const int4 pv = pinf[min(lane, npts - 1)];   // npts <= 64
-  const double* wl = wsh + ((lane & 15) == 0 ? (lane >> 4) : 4);
+  const double* wl = wsh + ((lane & 3) == 0 ? (lane >> 4) : 4);
   double XA[kSchurTW], XB[kSchurTW];
 #pragma unroll
   for (int j = 0; j < kSchurTW; ++j) XA[j] = XB[j] = 0.0;
@@ -94,16 +96,17 @@ __device__ __forceinline__ void schur_wave_batch(f64x4 (&acc)[kSchurTPW], const 
   schur_fetch<kNeed>(Xb, wl, pv, 0, npts, lane, XA, wa, ha);
   for (int t = 0; t < npts; t += 2) {
     schur_fetch<kNeed>(Xb, wl, pv, t + 1, npts, lane, XB, wb, hb);
-    schur_mfma<W>(acc, XA, wa, ha);
+    schur_mfma<W>(acc, accr, XA, wa, ha);
     schur_fetch<kNeed>(Xb, wl, pv, t + 2, npts, lane, XA, wa, ha);
-    schur_mfma<W>(acc, XB, wb, hb);
+    schur_mfma<W>(acc, accr, XB, wb, hb);
   }
 }
 
 // Slab of a segment: its ntw (ntw + 1) / 2 window tiles (row-major 16x16, column-major upper order), then the
 // rhs of its 16 ntw window columns.  The accumulators must be drained (mfma_drain) first.
 template <int W>
-__device__ __forceinline__ void schur_store(const f64x4 (&acc)[kSchurTPW], double* slab, int ntw, int lane) {
+__device__ __forceinline__ void schur_store(const f64x4 (&acc)[kSchurTPW], const double (&accr)[kSchurTPW], double* slab,
+                                            int ntw, int lane) {
   const int ntile = ntw * (ntw + 1) / 2;
 #pragma unroll
   for (int S = 0; S < kSchurTPW; ++S) {
@@ -115,10 +118,10 @@ __device__ __forceinline__ void schur_store(const f64x4 (&acc)[kSchurTPW], doubl
       double* t = slab + 256 * schur_tile_index(r, c) + lane;   // element (lk + 4 q, li) at 16 lk + li + 64 q
 #pragma unroll
       for (int q = 0; q < 4; ++q) t[64 * q] = -acc[S][q];
-    } else if ((lane & 15) == 0) {
-      // column 0 of E_c^T w: lanes 16 k hold window rows 16 c + k + 4 q
-#pragma unroll
-      for (int q = 0; q < 4; ++q) slab[256 * ntile + 16 * c + (lane >> 4) + 4 * q] = -acc[S][q];
+    } else if ((lane & 3) == 0) {
+      // E_c^T w (the 4 x 4 x 4 MFMA's D, block b row i column j at lane j + 4 b + 16 i): column 0, window row
+      // 16 c + 4 b + i
+      slab[256 * ntile + 16 * c + 4 * ((lane >> 2) & 3) + (lane >> 4)] = -accr[S];
     }
   }
 }
