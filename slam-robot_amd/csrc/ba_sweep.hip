@@ -250,7 +250,7 @@ __global__ __launch_bounds__(kLinThreads * kW) SG_LIN_ATTR void k_linearize(Dev 
 // per camera block: kCamSlices slices x 27 elements, each slice summing every kCamSlices-th partial of the
 // block's list, the slices combined in slice order; the last workgroup reduces the chunk scalars.
 constexpr int kCamSlices = 32;   // (kRedThreads >= kCamSlices * kCamV)
-__device__ void upd_reduce_body(const Dev& d, int fuse);
+__device__ void upd_reduce_body(const Dev& d, int fuse, int nunits);
 
 // mode 0: the current slot's partials (after a solve's first k_linearize, or after k_linearize in the two-pass
 //         chain), into xchg_cam / xcam_loc; a step that did not linearize (need_lin = 0) leaves them, and with
@@ -264,7 +264,7 @@ __device__ void upd_reduce_body(const Dev& d, int fuse);
 __global__ __launch_bounds__(kRedThreads) void k_cam_reduce(Dev d, int mode) {
   const LmState* st = d.st;
   if (mode >= 1 && (int)blockIdx.x == d.NB + 1) {
-    upd_reduce_body(d, mode == 2 ? 1 : 0);
+    upd_reduce_body(d, mode == 2 ? 1 : 0, d.nlin);   // k_update_lin writes one unit per chunk
     return;
   }
   if (st->done) return;
@@ -562,8 +562,8 @@ __global__ __launch_bounds__(kLinThreads) void k_point_update(Dev d) {
 // at the same point — so no k_linearize launch and no second sweep over the observations follow; a rejected
 // step leaves slot cur as it was (the next iteration re-reduces it when it must re-linearize).
 // Work decomposition: k_linearize's chunks (the candidate camera partials in k_linearize's order), and the
-// update scalars per round (k_point_update's units, in its lane order), so the solve is bitwise the one of
-// k_point_update + k_linearize (test_ba_gpu.py::test_speculative_linearization_is_bitwise_identical).
+// update scalars one unit per chunk (k_point_update writes one per round: the same sums in another order, so the
+// two chains agree to rounding, test_ba_gpu.py::test_speculative_linearization_matches_two_pass_chain).
 
 // One lane's observation of round R: the model term of the current linearization (ob, from pass 1), then
 // project.h + analytic Jacobian + Cauchy corrector at the candidate (k_linearize's body at x[nxt]): the J
@@ -673,23 +673,6 @@ __device__ __forceinline__ void ul_points(const Dev& d, int p0, int p1, int lane
   if (d.pfree[pp]) gmax = fmax(gmax, fmax(fmax(fabs(g[0]), fabs(g[1])), fmax(fabs(g[2]), fabs(g[3]))));
 }
 
-// k_point_update's per-unit scalars (its wave sums, in its order), then reset for the next unit.
-__device__ __forceinline__ void ul_unit_scalars(const Dev& d, int unit, int lane, double& model, double& candcost,
-                                                double& candfail, double& step2, double& candx2) {
-  const double m = wave_sum_full(model), cc = wave_sum_full(candcost), cf = wave_sum_full(candfail);
-  const double s2 = wave_sum_full(step2), x2 = wave_sum_full(candx2);
-  if (lane == 0) {
-    double* sc = d.chunk_scal + unit;   // structure of arrays: slot j at [j * npu + unit]
-    const size_t ns = d.npu;
-    sc[kModel * ns] = m;
-    sc[kCandCost * ns] = cc;
-    sc[kCandFail * ns] = cf;
-    sc[kStep2 * ns] = s2;
-    sc[kCandX2 * ns] = x2;
-  }
-  model = candcost = candfail = step2 = candx2 = 0.0;
-}
-
 template <bool kStamp, int kW>
 __global__ __launch_bounds__(kLinThreads * kW) SG_LIN_ATTR void k_update_lin(Dev d) {
   const LmState* st = d.st;
@@ -702,7 +685,7 @@ __global__ __launch_bounds__(kLinThreads * kW) SG_LIN_ATTR void k_update_lin(Dev
   __shared__ double camacc_w[kW][kLinNbMax * kCamV];  // candidate camera blocks of the window
   __shared__ double lsum_w[kW][2][kLinThreads];       // candidate failures: free, fixed observations
   __shared__ double ua_w[kW][kLinPts * 4 * kPtCopies], xps_w[kW][kLinPts * 4], Xns_w[kW][kLinPts * 4];
-  __shared__ double wscal[8];                         // wave 1's chunk scalars
+  __shared__ double wscal[16];                        // wave 1's chunk scalars and update scalars
   const int lane = threadIdx.x & (kLinThreads - 1), wv = threadIdx.x / kLinThreads;
   double* pacc = pacc_w[wv];
   double* camacc = camacc_w[wv];
@@ -748,8 +731,6 @@ __global__ __launch_bounds__(kLinThreads * kW) SG_LIN_ATTR void k_update_lin(Dev
       ul_points(d, R.p0, R.p1, lane, nxt, pacc, gmax);
       lds_fence_wave();
       ul_stamp(3);
-      ul_unit_scalars(d, ch.u0 + (r - ch.r0), lane, model, candcost, candfail, step2, candx2);
-      ul_stamp(4);
     }
   } else if (wv == 0) {
     // one point over several rounds: its back substitution needs every piece's A_p^T u first
@@ -768,10 +749,16 @@ __global__ __launch_bounds__(kLinThreads * kW) SG_LIN_ATTR void k_update_lin(Dev
     }
     lds_fence_wave();
     ul_points(d, ch.p0, ch.p1, lane, nxt, pacc, gmax);
-    lds_fence_wave();
-    ul_unit_scalars(d, ch.u0, lane, model, candcost, candfail, step2, candx2);
   }
   lds_fence_wave();
+  // the update scalars of the chunk (one unit per chunk, at the chunk's index: the decision's reduction reads nlin
+  // units instead of one per round, 30 k at C5, which a single workgroup took ~20 us to sum,
+  // profiles/r5_s1_sweep_ab.log); the two waves' sums combined in wave order with the chunk scalars below
+  double us[5] = {wave_sum_full(model), wave_sum_full(candcost), wave_sum_full(candfail), wave_sum_full(step2),
+                  wave_sum_full(candx2)};
+  if (kW > 1 && wv == 1 && lane == 0)
+#pragma unroll
+    for (int j = 0; j < 5; ++j) wscal[8 + j] = us[j];
   cost = wave_sum_full(cost);
   double fail = wave_sum_full(lsum[0][lane]);
   double ffail = wave_sum_full(lsum[1][lane]);
@@ -781,6 +768,18 @@ __global__ __launch_bounds__(kLinThreads * kW) SG_LIN_ATTR void k_update_lin(Dev
   lin_combine_waves<kW>(d.cam_slab[nxt] + ch.cam_off, camacc_w, ncv, wscal, wv, lane, cost, fail, fixed, ffail,
                         xn2, gmax);
   if (wv == 0 && lane == 0) {
+    {
+      double* su = d.chunk_scal + blockIdx.x;   // structure of arrays: slot j at [j * npu + chunk]
+      const size_t nu = d.npu;
+      if (kW > 1)
+#pragma unroll
+        for (int j = 0; j < 5; ++j) us[j] += wscal[8 + j];
+      su[kModel * nu] = us[0];
+      su[kCandCost * nu] = us[1];
+      su[kCandFail * nu] = us[2];
+      su[kStep2 * nu] = us[3];
+      su[kCandX2 * nu] = us[4];
+    }
     double* sc = d.lin_scal[nxt] + blockIdx.x;   // k_linearize's scalars of the candidate (never iteration 0)
     const size_t ns = d.nlin;
     sc[kCost * ns] = cost;
@@ -796,9 +795,10 @@ __global__ __launch_bounds__(kLinThreads * kW) SG_LIN_ATTR void k_update_lin(Dev
 
 
 // fuse: single rank, no all-reduce in between: thread 0 also runs k_decide's step (one launch less).
-__global__ __launch_bounds__(kRedThreads) void k_upd_reduce(Dev d, int fuse) { upd_reduce_body(d, fuse); }
+__global__ __launch_bounds__(kRedThreads) void k_upd_reduce(Dev d, int fuse) { upd_reduce_body(d, fuse, d.npu); }
 
-__device__ void upd_reduce_body(const Dev& d, int fuse) {
+// nunits: the work units whose update scalars are summed (k_point_update's rounds, or k_update_lin's chunks)
+__device__ void upd_reduce_body(const Dev& d, int fuse, int nunits) {
   const LmState* st = d.st;
   const int done = st->done;   // tested after the scalar loads are out (see k_S_reduce)
   __shared__ double red[kRedThreads / 64 * kUNum];
@@ -816,12 +816,12 @@ __device__ void upd_reduce_body(const Dev& d, int fuse) {
   // the Cholesky's hand-off time-outs ride in the scalar exchange, so every shard ends the solve together
   if (tid == 0) v[kUTimeout] = d.xchg_chol[kCTimeout];
   constexpr int kUpdU = 4;   // work units' loads in flight per thread (8 measured slower)
-  for (int c0 = tid; c0 < d.npu; c0 += kUpdU * kRedThreads) {
+  for (int c0 = tid; c0 < nunits; c0 += kUpdU * kRedThreads) {
     double t[kUpdU][5];
 #pragma unroll
     for (int u = 0; u < kUpdU; ++u) {
       const int c = c0 + u * kRedThreads;
-      const double* sc = d.chunk_scal + (c < d.npu ? c : 0);   // coalesced: slot j at [j * npu + unit]
+      const double* sc = d.chunk_scal + (c < nunits ? c : 0);   // coalesced: slot j at [j * npu + unit]
       const size_t ns = d.npu;
       t[u][0] = sc[kModel * ns];
       t[u][1] = sc[kCandCost * ns];
@@ -831,7 +831,7 @@ __device__ void upd_reduce_body(const Dev& d, int fuse) {
     }
 #pragma unroll
     for (int u = 0; u < kUpdU; ++u)
-      if (c0 + u * kRedThreads < d.npu) {
+      if (c0 + u * kRedThreads < nunits) {
         v[kUModel] += t[u][0];
         v[kUCandCost] += t[u][1];
         v[kUCandFail] += t[u][2];
