@@ -177,7 +177,8 @@ class BaSolver {
   int npu_ = 0;
   DBuf<double> seg_fail_;
   int nseg_ = 0, nwide_ = 0, nstile_ = 0;
-  double schur_mfma_ = 0.0;   // MFMA tile updates per k_schur launch (KernelWork)
+  double schur_mfma_ = 0.0;   // v_mfma_f64_16x16x4f64 tile updates per k_schur launch (KernelWork)
+  double schur_rhs_ = 0.0;    // v_mfma_f64_4x4x4_4b_f64 rhs updates per k_schur launch
   DBuf<SchurBatch> sbatch_;
   DBuf<WideSeg> wsegs_;
   DBuf<int32_t> pinfo_, pmx_, cells_, cell_obs_, stile_;

@@ -460,6 +460,7 @@ void BaSolver::Load(const sg_problem& p) {
   int ncell = 0;
   npairs_ = 0;
   schur_mfma_ = 0.0;
+  schur_rhs_ = 0.0;
   {
     std::vector<std::pair<int, int>> bo;
     cells.reserve(4 * (size_t)M_ + 4);
@@ -623,7 +624,8 @@ void BaSolver::Load(const sg_problem& p) {
           pmx[4 * k + 2] = simple_obs[k];
           pmx[4 * k + 3] = nc;
           nx += 64 * (pjhi(k) + 1);
-          schur_mfma_ += schur_aug_base(pjhi(k) + 1);
+          schur_mfma_ += schur_aug_base(pjhi(k) + 1) - (pjhi(k) + 1);   // window tiles (16x16x4)
+          schur_rhs_ += pjhi(k) + 1;                                      // rhs slots (4x4x4, 4 blocks)
           nc += sspan(k++);
         }
         B.p1 = k;
@@ -1716,7 +1718,7 @@ int BaSolver::KernelWork(double* bytes, double* flops, int max) {
   by[kKLin] = M * (16 + 4 + 1 + 192) + P * (32 + 4 + 80 + 32 + 1) + NB * kCamV * 8;
   fl[kKLin] = M * 420.0;
   by[kKSchur] = M * 192 + P * (80 + 32 + 32 + 32 + 80 + 32);
-  fl[kKSchur] = 2048.0 * schur_mfma_;   // v_mfma_f64_16x16x4f64 tile updates
+  fl[kKSchur] = 2048.0 * schur_mfma_ + 512.0 * schur_rhs_;   // 16x16x4 tile updates, 4x4x4 (4-block) rhs slots
   by[kKPointUpd] = M * (192 + 16 + 4) + P * (32 + 32 + 80 + 32 + 32);
   if (spec_) {   // k_update_lin: the update's traffic plus the candidate's linearization (a second J record, V, g)
     by[kKPointUpd] = M * (192 + 192 + 16 + 4 + 4 + 4) + P * (32 + 32 + 80 + 32 + 32 + 80 + 32) + NB * kCamV * 8;

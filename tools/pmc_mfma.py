@@ -4,7 +4,8 @@ SQ_WAVE_CYCLES and GRBM_GUI_ACTIVE (tools/profile_round.sh).
 SQ_VALU_MFMA_BUSY_CYCLES counts matrix-core busy cycles summed over the SIMDs (one v_mfma_f64_16x16x4f64 keeps
 a SIMD's matrix core busy 64 cycles: profiles/r4_schur_bench_pmc.log); GRBM_GUI_ACTIVE is the launch's GPU
 cycles summed over the 8 XCDs (MI355X_MICROARCH.md).  mfma_busy_frac = MFMA busy / (1024 SIMDs x GRBM_GUI_ACTIVE
-/ 8): the share of the chip's matrix-core cycles the launch kept busy; mfma_per_launch = MFMA busy / 64.
+/ 8): the share of the chip's matrix-core cycles the launch kept busy; mfma_busy_cycles_per_launch = the
+busy cycles (64 per 16x16x4 f64 MFMA; k_schur's rhs slots run v_mfma_f64_4x4x4_4b_f64 since round 5).
 Dispatches are grouped by (kernel, grid size).  Usage: pmc_mfma.py <pmc dir> <out.json> [profiled command]
 """
 import collections
@@ -31,7 +32,7 @@ def main():
         busy, gui = mean["SQ_VALU_MFMA_BUSY_CYCLES"], mean["GRBM_GUI_ACTIVE"]
         groups["%s@grid%d" % (name, grid)] = {
             "kernel": name, "grid_size": grid, "dispatches": len(cs["GRBM_GUI_ACTIVE"]), **mean,
-            "mfma_busy_frac": busy / (1024.0 * gui / 8.0) if gui else None, "mfma_per_launch": busy / 64.0}
+            "mfma_busy_frac": busy / (1024.0 * gui / 8.0) if gui else None, "mfma_busy_cycles_per_launch": busy}
     cmd = sys.argv[3] if len(sys.argv) > 3 else ""
     json.dump({"source": "rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE over "
                          + cmd, "formula": __doc__.split("\n\n")[1].replace("\n", " "), "kernels": groups},
