@@ -1,7 +1,8 @@
 // factor_lat.hip — diagnostic: latency of one 16x16 diagonal-tile factorisation in a lone wave (no SIMD mate,
-// no barrier), for the two k_chol_tiles variants: tile_factor (two pivots per LDS broadcast) and
-// tile_factor_mfma (registers, readlane 4x4 blocks, MFMA panel updates).  The device functions are copied
-// from slam-robot_amd/csrc/ba_solver.hip (keep in sync by hand; tool only).
+// no barrier), for the k_chol_tiles factor (tile_factor: two pivots per LDS broadcast), its generalisation to G
+// pivots per broadcast (tile_factor_g<G>: G = 2 is bitwise tile_factor; G = 4 / 8 derive more pivot rows per lane)
+// and the register form (tile_factor_mfma).  tile_factor is copied from slam-robot_amd/csrc/ba_chol.hip (keep in
+// sync by hand; tool only).  Round 5: profiles/r5_factor_pivots_per_broadcast.log.
 // Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/factor_lat.hip -o tools/factor_lat
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -118,6 +119,83 @@ __device__ __forceinline__ bool tile_factor(const double* D, const double* Yk, c
 }
 
 
+// tile_factor with G pivots per LDS broadcast: every lane derives the group's later pivot rows itself (row
+// k + 1 .. G - 1 updated by pivot k in registers), so the 16 pivots take 16 / G LDS round trips.  G = 2 is
+// bitwise tile_factor.
+template <int G>
+__device__ __forceinline__ bool tile_factor_g(const double* D, const double* Yk, const double* Id, double* prw,
+                                              double (&ca)[16]) {
+  const int lane = opaque_lane();
+  const int c = lane & 15;
+  const bool isy = lane == 32;
+  const double* b0 = isy ? Yk : ((lane >= 16 && lane < 32) ? Id + c : D + c);
+  const int rs = isy ? 1 : kTLd;
+#pragma unroll
+  for (int r = 0; r < kCholNb; ++r) ca[r] = b0[r * rs];
+  bool bad = false;
+  double u[G * kCholNb];
+  if (lane < kCholNb) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) prw[kCholNb * g + lane] = ca[g];
+  }
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int r = g; r < kCholNb; ++r) u[kCholNb * (g) + r] = prw[kCholNb * g + r];
+#pragma unroll
+  for (int j = 0; j < kCholNb; j += G) {
+    double rr[G], ii[G];
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+      const double p = u[kCholNb * (k) + j + k];
+      bad |= !(p > 0.0);
+      ii[k] = rsq_nr1(p);
+      rr[k] = ii[k] * ii[k];
+#pragma unroll
+      for (int g = k + 1; g < G; ++g) {
+        const double w = u[kCholNb * (k) + j + g] * rr[k];
+#pragma unroll
+        for (int r = j + g; r < kCholNb; ++r) u[kCholNb * (g) + r] = fma(-w, u[kCholNb * (k) + r], u[kCholNb * (g) + r]);
+      }
+    }
+    // this lane's column: the group's rows final, the next group's rows first (their broadcast goes out),
+    // then the rest
+    double t[G];
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+      const double a = ca[j + k];
+      t[k] = a * rr[k];
+      ca[j + k] = a * ii[k];
+#pragma unroll
+      for (int r = j + k + 1; r < j + G; ++r) ca[r] = fma(-u[kCholNb * (k) + r], t[k], ca[r]);
+    }
+    if (j + G < kCholNb) {
+#pragma unroll
+      for (int r = j + G; r < j + 2 * G; ++r)
+#pragma unroll
+        for (int k = 0; k < G; ++k) ca[r] = fma(-u[kCholNb * (k) + r], t[k], ca[r]);
+      if (lane < kCholNb) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) prw[kCholNb * g + lane] = ca[j + G + g];
+      }
+    }
+#pragma unroll
+    for (int r = j + 2 * G; r < kCholNb; ++r)
+#pragma unroll
+      for (int k = 0; k < G; ++k) ca[r] = fma(-u[kCholNb * (k) + r], t[k], ca[r]);
+#pragma unroll
+    for (int r = j; r < kCholNb; ++r) asm volatile("" : "+v"(ca[r]));
+    if (j + G < kCholNb) {
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int r = 0; r < kCholNb; ++r)   // (the whole row: a constant trip count unrolls; r < j + G + g is dead)
+          if (r >= j + G + g) u[kCholNb * (g) + r] = prw[kCholNb * g + r];
+    }
+  }
+  return bad;
+}
+
 // The four 16-lane rows' values of x at this lane's column: g[m] = x at lane li + 16 m (gfx950 permlane swaps,
 // as in sum_rows4: no LDS round trip).
 __device__ __forceinline__ void col_gather4(double x, double (&g)[4]) {
@@ -212,9 +290,10 @@ __device__ __forceinline__ bool tile_factor_mfma(const f64x4& D, double& ys, f64
 }
 
 
+template <int mode>
 __global__ __launch_bounds__(64) void k_lat(const double* Sg, const double* yg, int reps, double* out,
-                                             unsigned long long* cyc, int mode) {
-  __shared__ double Dw[16 * kTLd], Yw[16], Id[16 * kTLd], prw[32];
+                                             unsigned long long* cyc, double* res) {
+  __shared__ double Dw[16 * kTLd], Yw[16], Id[16 * kTLd], prw[16 * 8];
   const int lane = threadIdx.x, li = lane & 15, lk = lane >> 4;
   for (int i = lane; i < 16 * kTLd; i += 64) {
     Id[i] = (i / kTLd == i % kTLd) ? 1.0 : 0.0;
@@ -229,10 +308,15 @@ __global__ __launch_bounds__(64) void k_lat(const double* Sg, const double* yg, 
   bool bad = false;
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
   for (int r = 0; r < reps; ++r) {
-    if (mode == 0) {
+    if constexpr (mode == 0 || mode >= 2) {
       double ca[16];
-      bad |= tile_factor(Dw, Yw, Id, prw, ca);
+      if constexpr (mode == 0) bad |= tile_factor(Dw, Yw, Id, prw, ca);
+      else bad |= tile_factor_g<mode>(Dw, Yw, Id, prw, ca);
       acc += ca[15];
+      if (r == 0) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) res[16 * lane + i] = ca[i];
+      }
       asm volatile("" ::: "memory");
     } else {
       double ys = yg[li] + acc * 1e-300;
@@ -262,13 +346,32 @@ int main() {
   hipMemcpy(dS, S.data(), 256 * 8, hipMemcpyHostToDevice);
   hipMemcpy(dy, y.data(), 128, hipMemcpyHostToDevice);
   const int reps = 2000;
-  for (int mode = 0; mode < 2; ++mode) {
-    hipLaunchKernelGGL(k_lat, dim3(1), dim3(64), 0, 0, dS, dy, 10, dout, dc, mode);
-    hipLaunchKernelGGL(k_lat, dim3(1), dim3(64), 0, 0, dS, dy, reps, dout, dc, mode);
+  double* dres;
+  hipMalloc(&dres, 64 * 16 * 8);
+  std::vector<double> ref(64 * 16), got(64 * 16);
+  const int modes[5] = {0, 2, 4, 8, 1};
+  for (int mode : modes) {
+    auto kf = mode == 0 ? k_lat<0> : mode == 1 ? k_lat<1> : mode == 2 ? k_lat<2> : mode == 4 ? k_lat<4> : k_lat<8>;
+    hipLaunchKernelGGL(kf, dim3(1), dim3(64), 0, 0, dS, dy, 10, dout, dc, dres);
+    hipLaunchKernelGGL(kf, dim3(1), dim3(64), 0, 0, dS, dy, reps, dout, dc, dres);
     unsigned long long c = 0;
     hipMemcpy(&c, dc, 8, hipMemcpyDeviceToHost);
-    std::printf("%s: %.0f cycles per 16x16 factorisation (lone wave)\n", mode ? "tile_factor_mfma" : "tile_factor (LDS)",
-                (double)c / reps);
+    hipMemcpy(got.data(), dres, 64 * 16 * 8, hipMemcpyDeviceToHost);
+    if (mode == 0) ref = got;
+    double md = 0.0;
+    int neq = 0;
+    for (int l = 0; l < 33; ++l)
+      for (int i = 0; i < 16; ++i) {
+        const double a = ref[16 * l + i], b = got[16 * l + i];
+        md = std::fmax(md, std::fabs(a - b) / std::fmax(1e-300, std::fabs(a)));
+        neq += a != b;
+      }
+    if (mode == 1)
+      std::printf("tile_factor_mfma: %.0f cycles per 16x16 factorisation (lone wave)\n", (double)c / reps);
+    else
+      std::printf("%s G=%d: %.0f cycles per 16x16 factorisation (lone wave); vs tile_factor: %d of 528 differ, "
+                  "max rel %.2e\n", mode == 0 ? "tile_factor (LDS)" : "tile_factor_g", mode == 0 ? 2 : mode,
+                  (double)c / reps, neq, md);
   }
   return 0;
 }
