@@ -230,7 +230,7 @@ struct Dev {
   double* xchg_chol;             // [kCNum]
   double* xc;                    // [n] camera solution (scaled)
   double* work;                  // [n] solver scratch
-  const int32_t* fd_pair;        // [NB][NB] (I<J): FrameDistance residual coupling blocks I and J, or -1
+  const int32_t* fd_pair;        // [NB][NB] (I<J): 2 * FrameDistance residual coupling blocks I and J + (its frame a is block J), or -1
   int32_t assemble;              // this rank adds blockdiag(U) + FD + damping to S (rank 0 of a shard group)
   const int32_t* obs_pnt;        // [M] point (device order) of each observation
   const int32_t* obs_meta;       // [M] packed block / camera / freedom flags (kMeta*)

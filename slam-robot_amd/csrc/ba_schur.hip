@@ -658,10 +658,10 @@ __global__ __launch_bounds__(256) void k_S_reduce(Dev d, int amode) {
         e_fd = (fd_here && a >= 3 && c >= 3) ? d.fd_D[9 * I + 3 * (a - 3) + (c - 3)] : 0.0;
         e_dg = (amode == 1 && a == c) ? d.diag_c[i] : 0.0;
       } else if (fd_here && a >= 3 && c >= 3) {
-        const int dd = d.fd_pair[I * d.NB + Jb];
-        if (dd >= 0) {
-          const double* Xd = d.fd_X + 9 * dd;   // J_a J_b^T, rows: frame a's translation
-          e_x = d.frame_block[d.fd_a[dd]] == I ? Xd[3 * (a - 3) + (c - 3)] : Xd[3 * (c - 3) + (a - 3)];
+        const int e = d.fd_pair[I * d.NB + Jb];   // 2 * residual + (frame a is block Jb)
+        if (e >= 0) {
+          const double* Xd = d.fd_X + 9 * (e >> 1);   // J_a J_b^T, rows: frame a's translation
+          e_x = (e & 1) == 0 ? Xd[3 * (a - 3) + (c - 3)] : Xd[3 * (c - 3) + (a - 3)];
         }
       }
     }

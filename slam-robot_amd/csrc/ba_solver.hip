@@ -857,11 +857,14 @@ void BaSolver::Load(const sg_problem& p) {
   stg.Add(fd_bidx_, fd_bidx.empty() ? std::vector<int32_t>{0} : fd_bidx);
   stg.Add(work_i_, panel_jmax);
   {
-    // FrameDistance cross-block lookup for the on-the-fly assembly: fd_pair[I*NB+J] (I<J) = residual
+    // FrameDistance cross-block lookup for the on-the-fly assembly: fd_pair[I*NB+J] (I<J) = 2 * residual +
+    // (1 if the residual's frame a is block J, not I), so k_S_reduce reads the orientation with the index
+    // instead of two more dependent loads (fd_a, frame_block)
     std::vector<int32_t> fd_pair((size_t)std::max(NB_, 1) * std::max(NB_, 1), -1);
     for (int dd = 0; dd < D_; ++dd) {
       const int ba = frame_block[fd_a[dd]], bb = frame_block[fd_b[dd]];
-      if (ba >= 0 && bb >= 0 && ba != bb) fd_pair[(size_t)std::min(ba, bb) * NB_ + std::max(ba, bb)] = dd;
+      if (ba >= 0 && bb >= 0 && ba != bb)
+        fd_pair[(size_t)std::min(ba, bb) * NB_ + std::max(ba, bb)] = 2 * dd + (ba < bb ? 0 : 1);
     }
     stg.Add(fd_pair_, fd_pair);
     rdg_.Resize((size_t)std::max(n_, 1) + kCholNb);   // + padding rows of the last panel
