@@ -151,6 +151,24 @@ __device__ __forceinline__ void point_load(const Dev& d, const PointPrm& pr, con
   in.g4 = reinterpret_cast<const double4*>(d.g[pr.cur])[p];
   if (pr.reuse) in.d4 = reinterpret_cast<const double4*>(d.diag_p)[p];
 }
+// The first batch's loads from the segment descriptor alone (the batch starts at the segment's first point), so
+// they do not wait for the batch descriptor: lanes past the batch but inside the segment load real points that
+// point_finish then skips (it tests the batch's count first).
+__device__ __forceinline__ void point_load_first(const Dev& d, const PointPrm& pr, int p0, int pend, int t,
+                                                 PointIn& in) {
+  in.free = 0;
+  const int p = p0 + t;
+  if (p >= pend) return;
+  in.pi = d.pinfo[p];
+  in.pm = d.pmx[p];
+  in.free = d.pfree[p];
+  const double* Vp = d.V[pr.cur] + 10 * (size_t)p;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) in.V[i] = Vp[i];
+  in.s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
+  in.g4 = reinterpret_cast<const double4*>(d.g[pr.cur])[p];
+  if (pr.reuse) in.d4 = reinterpret_cast<const double4*>(d.diag_p)[p];
+}
 // point_block's arithmetic on preloaded inputs, then the point's table entries and cell map
 __device__ __forceinline__ double point_finish(const Dev& d, const PointPrm& pr, const SchurBatch& B, int t,
                                                const PointIn& in, double* Lsh, double* wsh, int4* pinf, int2* pob,
@@ -428,7 +446,7 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d, int fin) {
     SchurBatch Bk{}, Bn{};
     if (nbt > 0) {
       Bk = d.sbatch[sg.bt0];
-      point_load(d, pr, Bk, lane, pin);
+      point_load_first(d, pr, sg.p0, sg.p1, lane, pin);
     }
     if (nbt > 1) {
       Bn = d.sbatch[sg.bt0 + 1];
