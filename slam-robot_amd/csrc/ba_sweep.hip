@@ -676,9 +676,15 @@ __device__ __forceinline__ void ul_points(const Dev& d, int p0, int p1, int lane
 template <bool kStamp, int kW>
 __global__ __launch_bounds__(kLinThreads * kW) SG_LIN_ATTR void k_update_lin(Dev d) {
   const LmState* st = d.st;
-  if (st->done) return;
+  const int done = st->done;
   const int cur = st->cur, nxt = cur ^ 1;
   const LinChunk ch = d.lchunks[blockIdx.x];
+  // the wave's first round descriptor goes out beside LmState's, before the done test (as in k_S_reduce): at C2
+  // a wave has one round, so this round trip is on the launch's critical path
+  const int wv0 = threadIdx.x / kLinThreads;
+  LinRound Rn{};
+  if (!ch.wide && ch.r0 + wv0 < ch.r1) Rn = d.lrounds[ch.r0 + wv0];
+  if (done) return;
   if (blockIdx.x == 0 && threadIdx.x == 0) d.st->spec_slot = nxt;   // (k_cam_reduce mode 1 reads it)
   // per wave (k_linearize's split of the chunk's rounds over its waves):
   __shared__ double pacc_w[kW][kLinPts * 14 * kPtCopies];   // candidate point blocks of the round (pt_add)
@@ -717,7 +723,8 @@ __global__ __launch_bounds__(kLinThreads * kW) SG_LIN_ATTR void k_update_lin(Dev
   ul_stamp(-1);
   if (!ch.wide) {
     for (int r = ch.r0 + wv; r < ch.r1; r += kW) {
-      const LinRound R = d.lrounds[r];
+      const LinRound R = Rn;
+      if (r + kW < ch.r1) Rn = d.lrounds[r + kW];   // the next round's descriptor a round ahead
       PuObs ob;
       pu_pass1(d, cur, R, lane, ua, ob);
       lds_fence_wave();
