@@ -204,12 +204,16 @@ struct Dev {
   // chunks and partials
   const int32_t* cam_loff;       // [NB+1] CSR: per camera block, offsets of its partials in cam_slab
   const int32_t* cam_lidx;
-  const int32_t* s_loff;         // [nstile+1] CSR: per band tile of S, offsets of its partial tiles in S_slab
+  const int32_t* s_loff;         // [nstile]: per band tile of S, the count of its partial tiles in S_slab, whose
+                                 // offsets are s_lidx[s_lstride * tile ...] (rows padded to s_lstride, a multiple of 256)
   const int32_t* s_lidx;
   const int32_t* stile;          // [nstile] band tiles (R << 16) | C, R <= C, of the frame columns
   int32_t nstile;
-  const int32_t* r_loff;         // [NB+1] CSR: per block, offsets of its rhs partials in S_slab
+  const int32_t* r_loff;         // [NB]: per block, the count of its rhs partials in S_slab (offsets: r_lidx rows of
+                                 // r_lstride, a multiple of 256)
   const int32_t* r_lidx;
+  int32_t s_lstride, r_lstride;  // padded row lengths of s_lidx / r_lidx (k_S_reduce reads a row's first 256
+                                 // entries with no bound: its list loads go out beside the counts')
   double* cam_slab[2];
   double* S_slab;
   double* chunk_scal;            // [npu][kNScal] k_point_update scalars (per work unit)

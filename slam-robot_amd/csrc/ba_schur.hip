@@ -683,13 +683,15 @@ __global__ __launch_bounds__(256) void k_S_reduce(Dev d, int amode) {
         }
       }
     }
-    const int j0 = d.s_loff[wv], j1 = d.s_loff[wv + 1];
+    // the tile's padded list row: its first chunk of offsets goes out beside the count (no dependent round trip)
+    const int j0 = wv * d.s_lstride, nlist = d.s_loff[wv];
     __shared__ double wsum[4][256];
     double s[4] = {0.0, 0.0, 0.0, 0.0};
     constexpr int kSR = 8;
-    for (int base = j0 + part; base < j1; base += 4 * 64) {
-      const int cnt = min(64, (j1 - base + 3) / 4);
-      const int myoff = d.s_lidx[lane < cnt ? base + 4 * lane : j0];
+    int myoff = d.s_lidx[j0 + part + 4 * lane];
+    for (int base = part; base < nlist; base += 4 * 64) {
+      const int cnt = min(64, (nlist - base + 3) / 4);
+      const int nxt = base + 4 * 64 < nlist ? d.s_lidx[j0 + base + 4 * 64 + 4 * lane] : 0;
       for (int k = 0; k < cnt; k += kSR) {
         double v[kSR][4];
 #pragma unroll
@@ -704,6 +706,7 @@ __global__ __launch_bounds__(256) void k_S_reduce(Dev d, int amode) {
 #pragma unroll
             for (int m = 0; m < 4; ++m) s[m] += v[u][m];
       }
+      myoff = nxt;
     }
 #pragma unroll
     for (int m = 0; m < 4; ++m) wsum[part][lane + 64 * m] = s[m];
@@ -735,7 +738,7 @@ __global__ __launch_bounds__(256) void k_S_reduce(Dev d, int amode) {
   // speculative linearization: clear block I of the candidate slot's wide-chunk camera accumulator before
   // k_update_lin adds to it (k_cam_reduce keeps the current slot's)
   if (d.spec && part == 1 && lane < kCamV) d.cam_wide[st->cur ^ 1][(size_t)I * kCamV + lane] = 0.0;
-  const int j0 = d.r_loff[I], j1 = d.r_loff[I + 1];
+  const int j0 = I * d.r_lstride, j1 = j0 + d.r_loff[I];   // padded row: the first chunk needs no bound
   const int el = lane < 6 ? lane : 0;
   const int ei = 6 * I + el;
   const double e_acc = d.rhs[ei];
@@ -743,10 +746,10 @@ __global__ __launch_bounds__(256) void k_S_reduce(Dev d, int amode) {
   __shared__ double rsum[4][6];
   constexpr int kSR = 32;
   double s = 0.0;
-  int myoff = d.r_lidx[(j0 + 64 * part + lane < j1) ? j0 + 64 * part + lane : 0];
+  int myoff = d.r_lidx[j0 + 64 * part + lane];
   for (int base = j0 + 64 * part; base < j1; base += 256) {
     const int cnt = min(64, j1 - base);
-    const int nxt = d.r_lidx[(base + 256 + lane < j1) ? base + 256 + lane : 0];
+    const int nxt = base + 256 < j1 ? d.r_lidx[base + 256 + lane] : 0;
     for (int k = 0; k < cnt; k += kSR) {
       double v[kSR];
 #pragma unroll

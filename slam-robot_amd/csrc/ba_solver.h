@@ -85,6 +85,7 @@ class BaSolver {
   int chol_nd_ = 0;            // dissected band: tile rows the second workgroup factors bottom-up (0: one WG)
   DBuf<int32_t> tflag_;        // dissected band hand-off counters {bottom done, top done}
   bool chol_cand_lds_ = false;   // candidate-pass operands staged in the Cholesky's LDS (small problems)
+  int s_lstride_ = 256, r_lstride_ = 256;   // k_S_reduce's padded list rows (Dev::s_lstride / r_lstride)
   // tests only: force the dissected Cholesky's separator wait to time out (k_chol_tiles flags bit 2)
   bool chol_force_tmo_ = getenv("SG_CHOL_FORCE_TIMEOUT") && atoi(getenv("SG_CHOL_FORCE_TIMEOUT")) != 0;
   bool pack_force_ = getenv("SG_PACK_S") != nullptr;   // pack/unpack S on one rank too (tests the path)

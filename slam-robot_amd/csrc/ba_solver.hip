@@ -657,14 +657,17 @@ void BaSolver::Load(const sg_problem& p) {
       for (int i = 0; i < sg.nb; ++i)
         rl[sg.b_lo + i].push_back(sg.s_off + 256 * ntile + 6 * (sg.b_lo + i) - 16 * sg.t0);
     }
+    size_t rmax = 0;
+    for (int b = 0; b < NB_; ++b) rmax = std::max(rmax, rl[b].size());
+    r_lstride_ = (int)std::max<size_t>(256, (rmax + 255) / 256 * 256);   // rows padded (k_S_reduce's unbounded reads)
+    r_lidx.assign((size_t)std::max(NB_, 1) * r_lstride_, 0);
     for (int b = 0; b < NB_; ++b) {
       cam_loff[b + 1] = cam_loff[b] + (int)cl[b].size();
       cam_lidx.insert(cam_lidx.end(), cl[b].begin(), cl[b].end());
-      r_loff[b + 1] = r_loff[b] + (int)rl[b].size();
-      r_lidx.insert(r_lidx.end(), rl[b].begin(), rl[b].end());
+      r_loff[b] = (int)rl[b].size();
+      std::copy(rl[b].begin(), rl[b].end(), r_lidx.begin() + (size_t)b * r_lstride_);
     }
     if (cam_lidx.empty()) cam_lidx.push_back(0);
-    if (r_lidx.empty()) r_lidx.push_back(0);
   }
   lap("reduce-lists");
   // FrameDistance
@@ -805,7 +808,7 @@ void BaSolver::Load(const sg_problem& p) {
   }
   // k_S_reduce work: the band tiles (R <= C) of the frame columns, and per tile the segment tiles covering it
   // (segment order).  A segment tile outside the band is zero (no point couples its rows and columns).
-  std::vector<int32_t> stile, s_loff(1, 0), s_lidx;
+  std::vector<int32_t> stile, s_loff, s_lidx;
   {
     const int nft = (6 * NB_ + kCholNb - 1) / kCholNb;
     std::vector<int32_t> row_off(nft + 1, 0), cend(nft, 0);
@@ -820,13 +823,17 @@ void BaSolver::Load(const sg_problem& p) {
         const int R = sg.t0 + schur_tile_r(u), C = sg.t0 + schur_tile_c(u);
         if (R < nft && C < cend[R]) tl[row_off[R] + C - R].push_back(sg.s_off + 256 * u);
       }
-    for (const auto& l : tl) {
-      s_loff.push_back(s_loff.back() + (int)l.size());
-      s_lidx.insert(s_lidx.end(), l.begin(), l.end());
+    size_t smax = 0;
+    for (const auto& l : tl) smax = std::max(smax, l.size());
+    s_lstride_ = (int)std::max<size_t>(256, (smax + 255) / 256 * 256);   // rows padded (k_S_reduce's unbounded reads)
+    s_lidx.assign(std::max<size_t>(tl.size(), 1) * s_lstride_, 0);
+    for (size_t t = 0; t < tl.size(); ++t) {
+      s_loff.push_back((int)tl[t].size());
+      std::copy(tl[t].begin(), tl[t].end(), s_lidx.begin() + t * s_lstride_);
     }
     nstile_ = (int)stile.size();
     if (stile.empty()) stile.push_back(0);
-    if (s_lidx.empty()) s_lidx.push_back(0);
+    if (s_loff.empty()) s_loff.push_back(0);
   }
   lap("envelope");
   // upload batch 2 — the work lists: one pinned staging copy and one scatter launch (stager.h)
@@ -1216,6 +1223,8 @@ Dev BaSolver::MakeDev() {
   d.s_lidx = s_lidx_.ptr;
   d.r_loff = r_loff_.ptr;
   d.r_lidx = r_lidx_.ptr;
+  d.s_lstride = s_lstride_;
+  d.r_lstride = r_lstride_;
   d.S_slab = S_slab_.ptr;
   d.chunk_scal = chunk_scal_.ptr;
   d.S_wide = S_wide_.ptr;
