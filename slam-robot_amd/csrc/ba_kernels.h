@@ -137,7 +137,8 @@ struct LinChunk {
 // bookkeeping; `cur`, `spec_slot`, `reuse_diag` and `radius` are changed only by launches in which nothing else
 // reads them (the decision of k_cam_reduce mode 2 flips `cur` / sets `radius` for the NEXT launch, and its
 // readers in that launch read `done` / `spec_slot` only).  An edit that breaks this must hand the readers their
-// fields through a separate word written by an earlier launch.
+// fields through a separate word written by an earlier launch.  Those launches store through lm_store_shared
+// (ba_lm.h), which writes only the fields listed here, so a stray edit of a read field cannot reach memory.
 struct LmState {
   // options (copied from sg_solver_options)
   int32_t max_iter, max_invalid, disable_term, jacobi;

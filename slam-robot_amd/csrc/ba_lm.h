@@ -82,6 +82,54 @@ __device__ __forceinline__ void fin_count(LmState& s0) {
 // decide 2: one rank: the decision was taken by k_cam_reduce mode 2; an accepted step's candidate blocks are
 // taken here (LmState::accepted).
 static __device__ void decide_step(LmState& s, const double* u, const double* c);
+
+// The write-back of a launch whose other workgroups read LmState while one thread stores it (the concurrency
+// contract in ba_kernels.h): only the fields that launch may change are stored, so the contract holds by
+// construction, not by the readers' fields happening to be rewritten with the values they had.  kDecision: the
+// launch takes the step decision (k_cam_reduce mode 2), which sets cur, radius, decrease_factor and reuse_diag
+// for the NEXT launch (its own readers read done / spec_slot only); otherwise those stay as they are.
+// spec_slot (k_update_lin's) and the options are never stored here.
+template <bool kDecision>
+__device__ __forceinline__ void lm_store_shared(LmState* st, const LmState& s) {
+  if (kDecision) {
+    st->cur = s.cur;
+    st->radius = s.radius;
+    st->decrease_factor = s.decrease_factor;
+    st->reuse_diag = s.reuse_diag;
+  }
+  st->need_lin = s.need_lin;
+  st->first = s.first;
+  st->done = s.done;
+  st->termination = s.termination;
+  st->ok = s.ok;
+  st->pushed = s.pushed;
+  st->lm_iters = s.lm_iters;
+  st->n_succ = s.n_succ;
+  st->n_unsucc = s.n_unsucc;
+  st->n_invalid = s.n_invalid;
+  st->consecutive_invalid = s.consecutive_invalid;
+  st->sync_timeouts = s.sync_timeouts;
+  st->accepted = s.accepted;
+  st->cost = s.cost;
+  st->fixed_cost = s.fixed_cost;
+  st->initial_cost = s.initial_cost;
+  st->x_norm = s.x_norm;
+  st->abs_gtol = s.abs_gtol;
+  st->min_pushed_cost = s.min_pushed_cost;
+  st->last_model = s.last_model;
+  st->last_new_cost = s.last_new_cost;
+  st->last_rel_decrease = s.last_rel_decrease;
+  st->last_step_norm = s.last_step_norm;
+}
+// cam_finalize_body's write-back: k_cam_finalize runs alone (one workgroup) and may take the decision (decide 1):
+// the whole struct; k_schur's finalize workgroup (decide 0 / 2, where nothing changes cur, radius, reuse_diag or
+// spec_slot) runs beside the segments that read them: the contract's fields only.
+__device__ __forceinline__ void fin_store(LmState* st, const LmState& s, int decide) {
+  if (decide == 1)
+    *st = s;
+  else
+    lm_store_shared<false>(st, s);
+}
 // LDS of the finalize pass: its own in k_cam_finalize, carved from k_schur's operand buffer when a k_schur launch
 // runs it in one extra workgroup (k_schur's fin).
 struct FinLds {
@@ -180,7 +228,7 @@ __device__ __forceinline__ void cam_finalize_body(const Dev& d, int mode, int de
     cur = dsh[0];
     lin = dsh[1];
     if (dsh[2]) {
-      if (tid == 0) *st = s0;
+      if (tid == 0) fin_store(st, s0, decide);
       return;
     }
     if (dsh[3]) {   // accepted: the candidate's blocks and scalars are the current ones from here on
@@ -225,7 +273,7 @@ __device__ __forceinline__ void cam_finalize_body(const Dev& d, int mode, int de
     if (tid == 0) {
       fin_count(s0);
       done_sh = s0.done;
-      *st = s0;
+      fin_store(st, s0, decide);
     }
     __syncthreads();
     if (done_sh) return;
@@ -333,7 +381,7 @@ __device__ __forceinline__ void cam_finalize_body(const Dev& d, int mode, int de
       if (tid < kXNum + d.nranks) txs[tid] = d.xcam_loc[nv + tid];
       if (tid == 0) {
         txs[kXNum + d.nranks] = fd_here ? fd_total : 0.0;
-        if (decide) *st = s0;   // the decision taken above (the bookkeeping follows the exchange, mode 2)
+        if (decide) fin_store(st, s0, decide);   // the decision taken above (the bookkeeping follows the exchange, mode 2)
       }
       return;
     }
@@ -375,14 +423,14 @@ __device__ __forceinline__ void cam_finalize_body(const Dev& d, int mode, int de
   if (mode == 1) {
     // not linearized (a rejected step): the tail is not read after the exchange; keep it finite
     for (int i = tid; act && i < 2 * nf + kXNum + d.nranks + 1; i += 256) d.xtail[i] = 0.0;
-    if (decide && tid == 0) *st = s0;
+    if (decide && tid == 0) fin_store(st, s0, decide);
     return;
   }
   __syncthreads();
   if (tid == 0) {
     fin_count(s0);
     done_sh = s0.done;
-    *st = s0;
+    fin_store(st, s0, decide);
   }
   __syncthreads();
   if (done_sh) return;
@@ -428,7 +476,7 @@ __device__ __forceinline__ void fin_merged_bookkeeping(const Dev& d, double* red
   }
   if (tid == 0) {
     fin_count(s0);
-    *st = s0;
+    lm_store_shared<false>(st, s0);   // (k_S_unpack_fin: the unpack workgroups read LmState beside it)
   }
 }
 

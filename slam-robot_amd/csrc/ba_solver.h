@@ -180,6 +180,7 @@ class BaSolver {
   int nseg_ = 0, nwide_ = 0, nstile_ = 0;
   double schur_mfma_ = 0.0;   // v_mfma_f64_16x16x4f64 tile updates per k_schur launch (KernelWork)
   double schur_rhs_ = 0.0;    // v_mfma_f64_4x4x4_4b_f64 rhs updates per k_schur launch
+  double schur_useful_ = 0.0; // flops of the slots that multiply each point's own tiles (no zero tiles)
   DBuf<SchurBatch> sbatch_;
   DBuf<WideSeg> wsegs_;
   DBuf<int32_t> pinfo_, pmx_, cells_, cell_obs_, stile_;

@@ -461,6 +461,7 @@ void BaSolver::Load(const sg_problem& p) {
   npairs_ = 0;
   schur_mfma_ = 0.0;
   schur_rhs_ = 0.0;
+  schur_useful_ = 0.0;
   {
     std::vector<std::pair<int, int>> bo;
     cells.reserve(4 * (size_t)M_ + 4);
@@ -604,6 +605,9 @@ void BaSolver::Load(const sg_problem& p) {
         sg.b_lo = blo;
         sg.nb = bhi - blo + 1;
       }
+      // k_schur's asm chain (schur_chain.h) is entered at an offset computed from a point's last window tile:
+      // every point must end inside the window (jhi <= kSchurTW - 1)
+      SG_REQUIRE(sg.ntw <= kSchurTW, SG_EINVAL, "Schur segment window wider than kSchurTW");
       sg.s_off = s_off;
       s_off += sg.ntw * (sg.ntw + 1) / 2 * 256 + 16 * sg.ntw;
       // last window tile of each point's columns (-1: no Schur terms)
@@ -619,6 +623,7 @@ void BaSolver::Load(const sg_problem& p) {
         int nc = 0, nx = 0;
         while (k < j && k - B.p0 < kSchurBatchPts && nx + 64 * (pjhi(k) + 1) <= kSchurXCap &&
                nc + sspan(k) <= 64 * kSchurCellWaves) {
+          SG_REQUIRE(pjhi(k) < sg.ntw, SG_EINVAL, "point ends outside its Schur segment window");
           pmx[4 * k] = nx;
           pmx[4 * k + 1] = pjhi(k);
           pmx[4 * k + 2] = simple_obs[k];
@@ -626,6 +631,10 @@ void BaSolver::Load(const sg_problem& p) {
           nx += 64 * (pjhi(k) + 1);
           schur_mfma_ += schur_aug_base(pjhi(k) + 1) - (pjhi(k) + 1);   // window tiles (16x16x4)
           schur_rhs_ += pjhi(k) + 1;                                      // rhs slots (4x4x4, 4 blocks)
+          if (pjhi(k) >= 0) {   // the slots that multiply the point's own tiles (the rest multiply zeros)
+            const double nu = pjhi(k) - (6 * pfirst[point_perm_[k]] - 16 * sg.t0) / 16 + 1;
+            schur_useful_ += 2048.0 * nu * (nu + 1) / 2 + 512.0 * nu;
+          }
           nc += sspan(k++);
         }
         B.p1 = k;
@@ -1742,6 +1751,22 @@ int BaSolver::KernelWork(double* bytes, double* flops, int max) {
   for (; k < std::min(max, (int)kKNum); ++k) {
     bytes[k] = by[k];
     flops[k] = fl[k];
+  }
+  // derived figures after the kernels (bench.py's roofline fields):
+  //   [kKNum]     k_schur's useful flops: the MFMA slots of each point's own tiles (its first to its last window
+  //               tile), without the slots that multiply the zero tiles left of its first column
+  //   [kKNum + 1] SURVEY 8d's algorithmic bytes of one linearization sweep at the reference's f64: per observation
+  //               uv 16 + frame index 4 + r 16 + W_ip 192, per point CSR offset 4 + X 32 + V_p 80 + g_p 32, per
+  //               camera block pose 56 + U_i / g_c 8 (21 + 6)
+  if (max > kKNum) {
+    bytes[kKNum] = 0.0;
+    flops[kKNum] = schur_useful_;
+    ++k;
+  }
+  if (max > kKNum + 1) {
+    bytes[kKNum + 1] = M * 228.0 + P * 148.0 + NB * (56.0 + 8.0 * 27);
+    flops[kKNum + 1] = 0.0;
+    ++k;
   }
   return k;
 }

@@ -854,7 +854,7 @@ __device__ void upd_reduce_body(const Dev& d, int fuse, int nunits) {
     for (int j = 0; j < kUNum; ++j) d.xchg_upd[j] = v[j];
     if (fuse) {
       decide_step(s, v, cc);
-      *d.st = s;
+      lm_store_shared<true>(d.st, s);   // k_cam_reduce mode 2: workgroups 0..NB read done / spec_slot beside it
     }
   }
 }

@@ -211,7 +211,12 @@ class BundleAdjuster:
                                          fl.ctypes.data_as(C.POINTER(C.c_double)), 32), "sg_ba_kernel_work")
         names = ["linearize", "cam_reduce", "cam_finalize", "schur", "S_reduce", "cholesky", "point_update",
                  "upd_reduce", "decide"]
-        return {n: (float(by[i]), float(fl[i])) for i, n in enumerate(names)}
+        out = {n: (float(by[i]), float(fl[i])) for i, n in enumerate(names)}
+        # derived figures after the kernels' slots (KernelWork, ba_solver.hip): k_schur's useful flops (no zero
+        # tiles) and SURVEY 8d's algorithmic bytes of one linearization sweep at f64
+        out["schur_useful"] = (0.0, float(fl[10]))
+        out["sweep_survey_model"] = (float(by[11]), 0.0)
+        return out
 
 
 class Slam:

@@ -23,7 +23,8 @@ def test_world_size_mismatch_exits_nonzero():
 
 
 def test_rccl_needs_one_gpu_per_rank():
-    # under a launcher (WORLD_SIZE set) on a box with fewer GPUs than ranks: refused before any HIP call
-    r = _run(["--gpus", "2", "--comm", "rccl"], WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", HIP_VISIBLE_DEVICES="")
+    # under a launcher (WORLD_SIZE set) on a box with fewer GPUs than ranks: refused before any rendezvous (64 ranks:
+    # more GPUs than any box has, so the refusal does not depend on how HIP reads an empty HIP_VISIBLE_DEVICES)
+    r = _run(["--gpus", "64", "--comm", "rccl"], WORLD_SIZE="64", RANK="0", LOCAL_RANK="0")
     assert r.returncode != 0 and "one GPU per rank" in r.stderr
     assert r.stdout.strip() == ""
