@@ -1049,7 +1049,13 @@ __device__ __forceinline__ bool tile_diag(const f64x4& D, double ypart, TileShar
   const double ys = sum_rows4(ypart);
   if (lk == 0) sh.Yw[li] = ys;
   double ca[kCholNb];
+#ifdef SG_X_NOFACTOR   // timing-only A/B (round 6): the posts without the 16-pivot factor (results wrong)
+  const bool bad = false;
+#pragma unroll
+  for (int r = 0; r < kCholNb; ++r) ca[r] = sh.Dw[r * kTLd + (lane & 15)];
+#else
   const bool bad = tile_factor(sh.Dw, sh.Yw, sh.Id, sh.prw, ca);
+#endif
   double* Zs = sh.Zs[K & 3];
   double* zk = sh.zK[K & 3];
   if (lane >= 16 && lane < 32) {
@@ -1093,9 +1099,23 @@ __device__ __forceinline__ void tile_zp(const TileShared& sh, double* zp, int K,
   }
 // Per-phase absolute times (SG_STAMP=1 builds; tools/phase_trace.py): d.stamps[64 + (wg 128 + K) 16 + slot],
 // slots 0-7 the waves' barrier arrivals, 8-12 the owner's chain (start, after (0), TRSM, D update, factor).
+#ifdef SG_X_ARRIVE   // diagnostic build (round 6): barrier arrivals per column offset instead of the traces
+#define SG_PTRACE(K, slot) {}
+#undef SG_TSTAMP
+#define SG_TSTAMP(slot) {}
+// per-role step stamps in registers (lane 0): late wave 0-3 (+4 arrival), owner 5-8 (+9), others 10-12 (+13)
+#define SG_AST(slot)                                                             \
+  if (kStamp && lane == 0) {                                                     \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime();               \
+    tacc[slot] += now_ - tlast;                                                  \
+    tlast = now_;                                                                \
+  }
+#else
+#define SG_AST(slot) {}
 #define SG_PTRACE(K, slot)                                                                  \
   if (kStamp && lane == 0 && (K) < kTraceK)                                                \
     d.stamps[64 + ((size_t)blockIdx.x * kTraceK + (K)) * 16 + (slot)] = __builtin_amdgcn_s_memtime();
+#endif
 
 // W_KJ = Z_K^T U_KJ (= U_KK^-1 U_KJ) of one row-K tile, and its store to global memory for the back
 // substitution (kept apart so that loads issued in between do not reuse the stores' data registers, which
@@ -1154,21 +1174,35 @@ __device__ __forceinline__ void tile_phase(f64x4 (&acc)[kTB], double& ypart, int
                                            int lane, int li, int lk, const TileSrc& ts, double* zg,
                                            unsigned long long (&tacc)[16], unsigned long long& tlast) {
   if (late) {
+#ifdef SG_X_NOLATE   // timing-only A/B (round 6): the late wave's W tile, reload and z' skipped (results wrong)
+    J += kTB;
+    late = false;
+    return;
+#endif
     // the previous phase's owner (column J = K): its row K-1 tile (slot 0) -> W, then column J + 8, which
     // row K + 1 touches first
     const bool hasw = J < tend[K - 1];
     f64x4 Wt = {0.0, 0.0, 0.0, 0.0};
     if (hasw) Wt = tile_w(acc[0], sh.Zs[(K - 1) & 3], li, lk);
+    SG_AST(0)
     const int Jw = J;
     J += kTB;
+#ifndef SG_X_NOLOAD   // timing-only A/B (round 6): no column reload (results wrong)
     tile_col_load(acc, ypart, d, J, K, li, lk, ts);
+#endif
+    SG_AST(1)
     if (hasw) tile_w_store(Wt, Wg, K - 1, Jw, lane);
+    SG_AST(2)
     tile_zp(sh, zp, K, lane, zg);   // the diagonal this wave factored last phase
+    SG_AST(3)
     late = false;
     SG_TSTAMP(13)
     return;
   }
   if (J == K + 1) SG_PTRACE(K, 8)
+#ifdef SG_X_PRIO   // A/B (round 6): the owner's chain at raised issue priority over its SIMD mate
+  if (J == K + 1) __builtin_amdgcn_s_setprio(3);
+#endif
 #ifdef SG_X_IDLE   // timing-only A/B (tools/r5_chol_ab.sh): the waves off the owner's chain do nothing
   if (J != K + 1) return;
 #endif
@@ -1192,6 +1226,7 @@ __device__ __forceinline__ void tile_phase(f64x4 (&acc)[kTB], double& ypart, int
     }
   }
   SG_TSTAMP(8)
+  if (J == K + 1) { SG_AST(5) } else { SG_AST(10) }
   if (J == K + 1) SG_PTRACE(K, 9)
   // (1) TRSM of row K's tile
   const int te = tend[K];
@@ -1239,6 +1274,7 @@ __device__ __forceinline__ void tile_phase(f64x4 (&acc)[kTB], double& ypart, int
     }
   }
   SG_TSTAMP(9)
+  if (J == K + 1) { SG_AST(6) } else { SG_AST(11) }
   if (J == K + 1) {
     SG_PTRACE(K, 10)
     // (2) the next diagonal: apply row K, factor, post; its W tile and the reload follow next phase
@@ -1249,16 +1285,22 @@ __device__ __forceinline__ void tile_phase(f64x4 (&acc)[kTB], double& ypart, int
       acc[2] = mfma_f64_k16(a, acc[1], acc[2]);
     }
     SG_TSTAMP(10)
+    SG_AST(7)
     SG_PTRACE(K, 11)
     if (K + 1 < NT) {
       bad |= tile_diag(acc[2], ypart, sh, zp, K + 1, lane, li, lk);
     }
+    SG_AST(8)
+#ifdef SG_X_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
     SG_PTRACE(K, 12)
     late = true;
     SG_TSTAMP(11)
   } else if (act) {
     // (3) back-substitution tile
     tile_w_store(tile_w(acc[1], Zs, li, lk), Wg, K, J, lane);
+    SG_AST(12)
     SG_TSTAMP(12)
   }
 }
@@ -1337,14 +1379,22 @@ __device__ __forceinline__ void sep_merge(f64x4 (&acc)[kTB], double& ypart, int 
 // layout) and x_{K+d}[li] in registers (xw[d-1]; zero past the last row, and W tiles outside the band are
 // zero), so the d >= 2 terms are formed before x_{K+1} is known.  The 16-lane row sums run as a DPP butterfly
 // (quad xor 1, quad xor 2, half-row mirror, row mirror: bitwise the same sum in every lane), and one shuffle
-// moves x_K[li] (row li & 3, register li >> 2) to every lane.  W rows are prefetched two rows ahead (two
-// register buffers, the loop unrolled by two); z' is read one row ahead.  kRev: the rows are the bottom
+// moves x_K[li] (row li & 3, register li >> 2) to every lane.  W rows and z' are prefetched kBsBuf rows ahead
+// (kBsBuf register buffers, the loop unrolled by kBsBuf).  kRev: the rows are the bottom
 // half's reversed order, x_K[li] is stored at S-order index 16 (NT-1-K) + 15 - li.
+#ifndef SG_BS_BUF
+#define SG_BS_BUF 2
+#endif
+constexpr int kBsBuf = SG_BS_BUF;
 template <bool kRev>
 __device__ __forceinline__ void bs_chain(const double* __restrict__ Wb, const double* zsrc, double* xs, int Khi,
                                          int Klo, double (&xw)[kTB - 1], int NT, int lane, int li, int lk) {
   auto wload = [&](double (&w)[kTB - 1][4], int K) {
+#ifdef SG_X_BSHOT   // timing-only A/B (round 6): every W row read from row 0 (cache-hot; results wrong)
+    const double* src = Wb + (size_t)0 * (K >= 0 ? K : 0) + lane;
+#else
     const double* src = Wb + (size_t)(K >= 0 ? K : 0) * kTB * 256 + lane;
+#endif
 #pragma unroll
     for (int dd = 1; dd < kTB; ++dd)
 #pragma unroll
@@ -1353,7 +1403,13 @@ __device__ __forceinline__ void bs_chain(const double* __restrict__ Wb, const do
   const int srcl = 16 * (li & 3) + li;   // the lane holding x_K[li] after the row sums
   unsigned qbits = 1u << (li >> 2);
   asm volatile("" : "+v"(qbits));
-  auto bs_row = [&](int K, double (&w)[kTB - 1][4], const double (&zk)[4]) {
+  // kBsBuf register buffers: row K's W tiles and z' are loaded kBsBuf rows ahead of the chain (round 6: two rows
+  // ahead left the chain waiting on its L2 loads)
+  auto zload = [&](double (&zk)[4], int K) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) zk[q] = zsrc[16 * (K >= 0 ? K : 0) + lk + 4 * q];
+  };
+  auto bs_row = [&](int K, double (&w)[kTB - 1][4], double (&zk)[4]) {
     double p[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int dd = kTB - 1; dd >= 1; --dd)
@@ -1384,23 +1440,23 @@ __device__ __forceinline__ void bs_chain(const double* __restrict__ Wb, const do
 #pragma unroll
     for (int dd = kTB - 2; dd >= 1; --dd) xw[dd] = xw[dd - 1];
     xw[0] = xk;
-    wload(w, K - 2);   // this buffer's next row
+    wload(w, K - kBsBuf);   // this buffer's next row
+    zload(zk, K - kBsBuf);
   };
-  double wA[kTB - 1][4], wB[kTB - 1][4], zA[4], zB[4];
-  wload(wA, Khi);
-  wload(wB, Khi - 1);
+  double wb[kBsBuf][kTB - 1][4], zb[kBsBuf][4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) zA[q] = zsrc[16 * Khi + lk + 4 * q];
-  int K = Khi;
-  for (; K >= Klo + 1; K -= 2) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) zB[q] = zsrc[16 * (K - 1) + lk + 4 * q];
-    bs_row(K, wA, zA);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) zA[q] = zsrc[16 * (K >= 2 ? K - 2 : 0) + lk + 4 * q];
-    bs_row(K - 1, wB, zB);
+  for (int b = 0; b < kBsBuf; ++b) {
+    wload(wb[b], Khi - b);
+    zload(zb[b], Khi - b);
   }
-  if (K == Klo) bs_row(K, wA, zA);
+  int K = Khi;
+  for (; K >= Klo + kBsBuf - 1; K -= kBsBuf) {
+#pragma unroll
+    for (int b = 0; b < kBsBuf; ++b) bs_row(K - b, wb[b], zb[b]);
+  }
+#pragma unroll
+  for (int b = 0; b < kBsBuf - 1; ++b)
+    if (K - b >= Klo) bs_row(K - b, wb[b], zb[b]);
 }
 
 // The same chain on two waves: wave `par` takes rows Khi - par, Khi - par - 2, ..., so each wave has two
@@ -1414,7 +1470,11 @@ __device__ __forceinline__ void bs_chain2(const double* __restrict__ Wb, const d
                                           int lane, int li, int lk, bool& tmo) {
   auto xat = [&](int K) -> double& { return kRev ? xs[16 * (NT - 1 - K) + 15 - li] : xs[16 * K + li]; };
   auto wload = [&](double (&w)[kTB - 1][4], int K) {
+#ifdef SG_X_BSHOT   // timing-only A/B (round 6): every W row read from row 0 (cache-hot; results wrong)
+    const double* src = Wb + (size_t)0 * (K >= 0 ? K : 0) + lane;
+#else
     const double* src = Wb + (size_t)(K >= 0 ? K : 0) * kTB * 256 + lane;
+#endif
 #pragma unroll
     for (int dd = 1; dd < kTB; ++dd)
 #pragma unroll
@@ -1577,7 +1637,11 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
       cnt[sw] += 1;
       if (w < wave && sw == my) rank += 1;
     }
+#ifdef SG_X_PAIR4   // A/B (round 6): columns c and c + 4 on one SIMD
+    if (cnt[0] == 2 && cnt[1] == 2 && cnt[2] == 2 && cnt[3] == 2) col = my + 4 * rank;
+#else
     if (cnt[0] == 2 && cnt[1] == 2 && cnt[2] == 2 && cnt[3] == 2) col = 2 * my + rank;
+#endif
   }
   {
     f64x4 acc[kTB];
@@ -1621,8 +1685,18 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
     SG_TSTAMP(0)
     __syncthreads();
     SG_TSTAMP(1)
+#ifdef SG_X_ARRIVE
+    // per column offset d = J - K at the phase start: the cycles from this wave's phase start (barrier exit) to
+    // its barrier arrival, summed / max / count (tools/arrive_trace.py)
+    unsigned long long ar_sum[8] = {}, ar_max[8] = {}, ar_cnt[8] = {};
+    unsigned long long t_ph = __builtin_amdgcn_s_memtime();
+#endif
 #pragma nounroll
     for (int K = 0; K < NTf; ++K) {
+#ifdef SG_X_ARRIVE
+      const int d0 = min(max(J - K, 0), 7);
+      const int role = late ? 0 : (J == K + 1 ? 1 : 2);
+#endif
       if (nd > 0 && !bottom && K == m - 1) {
         // relaxed polls, one acquire (an acquiring poll would invalidate the cache on every round)
         int spin = 0;
@@ -1639,10 +1713,42 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
       // the owner of the next diagonal (now late) is on the critical path until the barrier: it rotates after
       if (!late) tile_rotate(acc);
       SG_PTRACE(K, wave)
+#ifdef SG_X_ARRIVE
+      if (role == 0) { SG_AST(4) } else if (role == 1) { SG_AST(9) } else { SG_AST(13) }
+      if (kStamp) {
+        const unsigned long long ta = __builtin_amdgcn_s_memtime() - t_ph;
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (q == d0) {
+            ar_sum[q] += ta;
+            ar_max[q] = ar_max[q] > ta ? ar_max[q] : ta;
+            ar_cnt[q] += 1;
+          }
+      }
+#endif
       lds_barrier();
       if (late) tile_rotate(acc);
+#ifdef SG_X_ARRIVE
+      t_ph = __builtin_amdgcn_s_memtime();
+      tlast = t_ph;
+#endif
       SG_TSTAMP(3)
     }
+#ifdef SG_X_ARRIVE
+    if (kStamp && lane == 0) {
+      unsigned long long* o = reinterpret_cast<unsigned long long*>(d.stamps) + kSegStamp + blockIdx.x * 256 + wave * 24;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        o[q] += ar_sum[q];
+        o[8 + q] = o[8 + q] > ar_max[q] ? o[8 + q] : ar_max[q];
+        o[16 + q] += ar_cnt[q];
+      }
+      unsigned long long* o2 = reinterpret_cast<unsigned long long*>(d.stamps) + kSegStamp + 512 + blockIdx.x * 256 +
+                               wave * 16;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) o2[q] += tacc[q];
+    }
+#endif
     if (bottom) {
       // row nd-1's updates of the separator columns (slots of phase nd), then the hand-off
       tile_final(acc, J, late, sh, Wb, tend, nd, lane, li, lk);
