@@ -154,37 +154,76 @@ __device__ __forceinline__ int u4(int a, int c) { return a * (7 - a) / 2 + c; }
 // packed index of a window block pair (i <= j < nb)
 __device__ __forceinline__ int wp(int i, int j, int nb) { return i * nb - i * (i - 1) / 2 + (j - i); }
 
-// Observation records J (r~ 2 | Jc 12 | Jp 8 | cost, pad) in blocks of 64 observations, element pairs
-// interleaved: pair e2 (0..11) of observation o at double2 index ((o >> 6) * 12 + e2) * 64 + (o & 63).  A wave's
-// lanes reading (or writing) one element pair of 64 consecutive observations touch one contiguous KiB instead
-// of a 16-byte piece of 64 different 192-byte records.
-__device__ __forceinline__ size_t jidx2(int o, int e2) { return ((size_t)(o >> 6) * 12 + e2) * 64 + (o & 63); }
+// Observation records J in blocks of 64 observations, element pairs interleaved: pair e2 (0..kJPairs-1) of
+// observation o at double2 index ((o >> 6) * kJPairs + e2) * 64 + (o & 63).  A wave's lanes reading (or writing)
+// one element pair of 64 consecutive observations touch one contiguous KiB instead of a 16-byte piece of 64
+// different records.  Pairs: 0 r~ | 1-3 the rotation columns of J~c (rows 0, 1: J~c[0..2], J~c[6..8]; zero unless
+// the frame's rotation is free) | 4-7 J~p (2 x 4), stored for every observation whatever the point's freedom.
+// The translation columns are not stored: project.h's d(uv)/dt = -X.w d(uv)/d(X.xyz), so J~t = -X.w J~p[:, 0:3]
+// (LinearizeObservation forms them that way, so every reader gets the same bits) — 128 bytes per observation
+// instead of 192 (round 6).
+__device__ __forceinline__ size_t jidx2(int o, int e2) { return ((size_t)(o >> 6) * kJPairs + e2) * 64 + (o & 63); }
 __device__ __forceinline__ double2 jload2(const double* J, int o, int e2) {
   return reinterpret_cast<const double2*>(J)[jidx2(o, e2)];
 }
-
-// Load the corrected Jacobian of observation o and apply Jacobi scaling.
-__device__ __forceinline__ void load_scaled_J(const Dev& d, const double* J, int o, int b, const double* sp,
-                                              double* r, double* Jc, double* Jp) {
-  double buf[22];
+// Write one observation's record (rr, Jc rotation columns, Jp) — the translation columns are implied.
+__device__ __forceinline__ void jstore(double* J, int o, const double* rr, const double* Jc, const double* Jp) {
+  double2* Jo = reinterpret_cast<double2*>(J) + jidx2(o, 0);   // pair e2 at Jo[64 e2]
+  Jo[0] = make_double2(rr[0], rr[1]);
+  Jo[64 * 1] = make_double2(Jc[0], Jc[1]);
+  Jo[64 * 2] = make_double2(Jc[2], Jc[6]);
+  Jo[64 * 3] = make_double2(Jc[7], Jc[8]);
 #pragma unroll
-  for (int i = 0; i < 11; ++i) {
-    const double2 v = jload2(J, o, i);
-    buf[2 * i] = v.x;
-    buf[2 * i + 1] = v.y;
-  }
-  r[0] = buf[0];
-  r[1] = buf[1];
+  for (int i = 0; i < 4; ++i) Jo[64 * (4 + i)] = make_double2(Jp[2 * i], Jp[2 * i + 1]);
+}
+__device__ __forceinline__ void jstore_zero(double* J, int o) {
+  double2* Jo = reinterpret_cast<double2*>(J) + jidx2(o, 0);
+#pragma unroll
+  for (int i = 0; i < kJPairs; ++i) Jo[64 * i] = make_double2(0.0, 0.0);
+}
+// The unscaled J~c (2 x 6, row-major) of a record from its pairs 1-3 (rotation) and 4-5 (J~p[:, 0:3]), the
+// translation columns -X.w J~p[:, c] when the frame's translation is free (tmask), else zero.
+__device__ __forceinline__ void jc_from_pairs(const double2 (&jr)[3], const double2& p4, const double2& p5,
+                                              const double2& p6, const double2& p7, double xw, bool tmask,
+                                              double* Jc) {
+  Jc[0] = jr[0].x; Jc[1] = jr[0].y; Jc[2] = jr[1].x;
+  Jc[6] = jr[1].y; Jc[7] = jr[2].x; Jc[8] = jr[2].y;
+  const double nx = -xw;
+  Jc[3] = tmask ? nx * p4.x : 0.0;
+  Jc[4] = tmask ? nx * p4.y : 0.0;
+  Jc[5] = tmask ? nx * p5.x : 0.0;
+  Jc[9] = tmask ? nx * p6.x : 0.0;
+  Jc[10] = tmask ? nx * p6.y : 0.0;
+  Jc[11] = tmask ? nx * p7.x : 0.0;
+}
+__device__ __forceinline__ bool meta_tmask(int m) { return (m & kMetaTrans) != 0 && meta_block(m) >= 0; }
+
+// Load the corrected Jacobian of observation o (meta m, its point's X.w) and apply Jacobi scaling; J~p is zero
+// for a point that is not free, J~c for an observation of a frame without a free block.
+__device__ __forceinline__ void load_scaled_J(const Dev& d, const double* J, int o, int b, const double* sp,
+                                              int m, double xw, double* r, double* Jc, double* Jp) {
+  double2 v[kJPairs];
+#pragma unroll
+  for (int i = 0; i < kJPairs; ++i) v[i] = jload2(J, o, i);
+  r[0] = v[0].x;
+  r[1] = v[0].y;
   if (b >= 0) {
+    const double2 jr[3] = {v[1], v[2], v[3]};
+    double Jraw[12];
+    jc_from_pairs(jr, v[4], v[5], v[6], v[7], xw, meta_tmask(m), Jraw);
     const double* sc = d.scale_c + 6 * b;
 #pragma unroll
-    for (int i = 0; i < 12; ++i) Jc[i] = buf[2 + i] * sc[i % 6];
+    for (int i = 0; i < 12; ++i) Jc[i] = Jraw[i] * sc[i % 6];
   } else {
 #pragma unroll
     for (int i = 0; i < 12; ++i) Jc[i] = 0.0;
   }
+  const bool pf = (m & kMetaPfree) != 0;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) Jp[i] = buf[14 + i] * sp[i % 4];
+  for (int i = 0; i < 4; ++i) {
+    Jp[2 * i] = pf ? v[4 + i].x * sp[(2 * i) % 4] : 0.0;
+    Jp[2 * i + 1] = pf ? v[4 + i].y * sp[(2 * i + 1) % 4] : 0.0;
+  }
 }
 
 // packed index of a lower-triangular 4x4 (c <= i)

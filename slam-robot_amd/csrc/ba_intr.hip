@@ -118,11 +118,11 @@ __global__ __launch_bounds__(kIntrFkThreads) void k_intr_fk(Dev d, int nsl) {
       const double2 rv = jload2(J, o, 0);
       r[0] = rv.x;
       r[1] = rv.y;
-#pragma unroll
-      for (int e = 0; e < 6; ++e) {
-        const double2 v = jload2(J, o, 1 + e);   // raw J_c (zero outside the frame's free parts)
-        Jc[2 * e] = v.x;
-        Jc[2 * e + 1] = v.y;
+      {
+        // raw J~c (zero outside the frame's free parts): rotation pairs 1-3, translation from J~p (jc_from_pairs)
+        const double2 jr[3] = {jload2(J, o, 1), jload2(J, o, 2), jload2(J, o, 3)};
+        const double xw = d.X[cur][4 * (size_t)d.obs_pnt[o] + 3];
+        jc_from_pairs(jr, jload2(J, o, 4), jload2(J, o, 5), jload2(J, o, 6), jload2(J, o, 7), xw, meta_tmask(m), Jc);
       }
       if (b < d.NB) {
 #pragma unroll
@@ -145,7 +145,7 @@ __global__ __launch_bounds__(kIntrFkThreads) void k_intr_fk(Dev d, int nsl) {
       const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
       const double sp[4] = {s4.x, s4.y, s4.z, s4.w};
       double r[2], Jc[12], Jp[8];
-      load_scaled_J(d, J, o, b, sp, r, Jc, Jp);
+      load_scaled_J(d, J, o, b, sp, m, d.X[cur][4 * (size_t)p + 3], r, Jc, Jp);
       const double* Y = d.Yk + ((size_t)p * ncam + c) * 28;
       double Mx[14];   // A_p Y^T (2x7)
 #pragma unroll
@@ -383,12 +383,13 @@ __device__ __forceinline__ void intr_schur_point(const Dev& d, int p, bool act, 
       if ((m & kMetaFixed) || meta_cam(m) != c) continue;
       any = true;
       const double* Jk = d.Jk + 14 * (size_t)o;
-      double Jr[8];   // corrected Jp (2x4)
+      double Jr[8];   // corrected Jp (2x4; zero for a point that is not free)
+      const bool pfo = (m & kMetaPfree) != 0;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const double2 v = jload2(d.J[d.st->cur], o, 7 + i);
-        Jr[2 * i] = v.x;
-        Jr[2 * i + 1] = v.y;
+        const double2 v = jload2(d.J[d.st->cur], o, 4 + i);
+        Jr[2 * i] = pfo ? v.x : 0.0;
+        Jr[2 * i + 1] = pfo ? v.y : 0.0;
       }
 #pragma unroll
       for (int j = 0; j < 7; ++j) {

@@ -25,7 +25,10 @@
 namespace sg {
 
 constexpr int kCamV = 27;           // per camera block: upper(Jc^T Jc) 21 + Jc^T r 6
-constexpr int kJStride = 24;
+// Observation record (ba_device.h jidx2): r~ 2 | rotation Jacobian 2x3 | point Jacobian 2x4 = 16 doubles; the
+// translation Jacobian is not stored (J~t = -X.w J~p[:, 0:3], jc_trans)
+constexpr int kJPairs = 8;
+constexpr int kJStride = 2 * kJPairs;
 constexpr int kNScal = 16;          // per-chunk scalar slots
 constexpr int kCholThreads = 512;
 constexpr int kCholNb = 16;

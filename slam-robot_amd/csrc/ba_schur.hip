@@ -32,20 +32,23 @@ __global__ __launch_bounds__(256) void k_cam_finalize(Dev d, int mode, int decid
 //      segment) add the cells' rhs terms.
 // Points spanning more than kSegNbMax blocks take k_schur_wide (observation pairs, global atomics).
 
-__device__ __forceinline__ void load_Jc_scaled(const Dev& d, const double* J, int o, int b, double* Jc) {
+// J~c of observation o (block b >= 0, point X.w xw) with Jacobi scaling: its rotation pairs and the translation
+// columns -X.w J~p[:, 0:3] (ba_device.h jc_from_pairs; load_scaled_J's arithmetic)
+__device__ __forceinline__ void load_Jc_scaled(const Dev& d, const double* J, int o, int b, double xw, double* Jc) {
   const double* sc = d.scale_c + 6 * b;
+  const double2 jr[3] = {jload2(J, o, 1), jload2(J, o, 2), jload2(J, o, 3)};
+  double Jraw[12];
+  jc_from_pairs(jr, jload2(J, o, 4), jload2(J, o, 5), jload2(J, o, 6), jload2(J, o, 7), xw,
+                meta_tmask(d.obs_meta[o]), Jraw);
 #pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    const double2 v = jload2(J, o, 1 + i);   // (pair 0: r)
-    Jc[2 * i] = v.x * sc[(2 * i) % 6];
-    Jc[2 * i + 1] = v.y * sc[(2 * i + 1) % 6];
-  }
+  for (int i = 0; i < 12; ++i) Jc[i] = Jraw[i] * sc[i % 6];
 }
+// J~p of observation o of a free point, scaled
 __device__ __forceinline__ void load_Jp_scaled(const double* J, int o, const double4& s4, double* Jp) {
   const double sp[4] = {s4.x, s4.y, s4.z, s4.w};
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const double2 v = jload2(J, o, 7 + i);   // (pairs 0-6: r, Jc)
+    const double2 v = jload2(J, o, 4 + i);   // (pairs 0-3: r, rotation)
     Jp[2 * i] = v.x * sp[(2 * i) % 4];
     Jp[2 * i + 1] = v.y * sp[(2 * i + 1) % 4];
   }
@@ -242,18 +245,23 @@ __device__ __forceinline__ double point_finish(const Dev& d, const PointPrm& pr,
 // J pairs and scales) before either's arithmetic, so two cells' memory latencies overlap (the same
 // arithmetic in the same order as one cell at a time: the same bits).
 struct CellOps {
-  double2 jp[4], jc[6];
+  double2 jp[4], jr[3];
   double4 s4;
   double sc[6];
+  double xw;   // the point's X.w (the translation columns are -X.w J~p[:, 0:3])
+  int tm;      // the frame's translation is free
 };
-__device__ __forceinline__ void cell_load(const Dev& d, const double* J, int o, int b, int p, CellOps& c) {
+__device__ __forceinline__ void cell_load(const Dev& d, const double* J, const double* X, int o, int b, int p,
+                                          CellOps& c) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) c.jp[i] = jload2(J, o, 7 + i);   // (pairs 0-6: r, Jc)
+  for (int i = 0; i < 4; ++i) c.jp[i] = jload2(J, o, 4 + i);   // (pairs 0-3: r, rotation)
 #pragma unroll
-  for (int i = 0; i < 6; ++i) c.jc[i] = jload2(J, o, 1 + i);   // (pair 0: r)
+  for (int i = 0; i < 3; ++i) c.jr[i] = jload2(J, o, 1 + i);   // (pair 0: r)
   c.s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
 #pragma unroll
   for (int i = 0; i < 6; ++i) c.sc[i] = d.scale_c[6 * b + i];
+  c.xw = X[4 * (size_t)p + 3];
+  c.tm = meta_tmask(d.obs_meta[o]) ? 1 : 0;
 }
 // E_{p,b} += (or =) the observation's G J~c from preloaded operands (load_Jp_scaled / load_Jc_scaled's
 // arithmetic)
@@ -281,10 +289,11 @@ __device__ __forceinline__ void cell_apply(const CellOps& c, const double* L, in
     }
   }
   double Jc[12];
+  {
+    double Jraw[12];
+    jc_from_pairs(c.jr, c.jp[0], c.jp[1], c.jp[2], c.jp[3], c.xw, c.tm != 0, Jraw);
 #pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    Jc[2 * i] = c.jc[i].x * c.sc[(2 * i) % 6];
-    Jc[2 * i + 1] = c.jc[i].y * c.sc[(2 * i + 1) % 6];
+    for (int i = 0; i < 12; ++i) Jc[i] = Jraw[i] * c.sc[i % 6];
   }
   if (first) {
 #pragma unroll
@@ -298,7 +307,8 @@ __device__ __forceinline__ void cell_apply(const CellOps& c, const double* L, in
       for (int a = 0; a < 6; ++a) at(col0 + a, kk) += G[kk][0] * Jc[a] + G[kk][1] * Jc[6 + a];
   }
 }
-__device__ __forceinline__ void schur_cells(const Dev& d, const double* J, const SchurBatch& B, int tid, int c0w,
+__device__ __forceinline__ void schur_cells(const Dev& d, const double* J, const double* X, const SchurBatch& B,
+                                            int tid, int c0w,
                                             const double* Lsh,
                                             const int4* pinf, const int2* pob, const uint8_t* cmap, double* Xb) {
   const int ncell = B.c1 - B.c0;
@@ -327,7 +337,7 @@ __device__ __forceinline__ void schur_cells(const Dev& d, const double* J, const
         if (po.x >= 0) {
           simple[h] = true;
           oc[h] = po.x + (bc[h] - pi.x);
-          cell_load(d, J, oc[h], bc[h], B.p0 + t, ops[h]);
+          cell_load(d, J, X, oc[h], bc[h], B.p0 + t, ops[h]);
         }
       }
     }
@@ -372,7 +382,7 @@ __device__ __forceinline__ void schur_cells(const Dev& d, const double* J, const
       for (int k = k1 - 1; k < k2; ++k) {
         const int o = k < k1 ? o0 : d.cell_obs[k];
         CellOps c;
-        cell_load(d, J, o, b, B.p0 + t, c);
+        cell_load(d, J, X, o, b, B.p0 + t, c);
         cell_apply(c, L, col0, k < k1, at);
       }
     }
@@ -431,7 +441,7 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur(Dev d, int fin) {
     for (int s = 0; s <= nbt; ++s) {
       SG_BUSY_BEGIN
       if (s < nbt)
-        schur_cells(d, d.J[st->cur], d.sbatch[sg.bt0 + s], tid, c0w, sh.L[s % 3], sh.pinf[s % 3], sh.pob[s % 3], sh.cmap[s % 3],
+        schur_cells(d, d.J[st->cur], d.X[st->cur], d.sbatch[sg.bt0 + s], tid, c0w, sh.L[s % 3], sh.pinf[s % 3], sh.pob[s % 3], sh.cmap[s % 3],
                     sh.X[s & 1]);
       SG_BUSY_END
       SG_SSTAMP(34)
@@ -596,12 +606,13 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur_wide(Dev d) {
   const int obs_lo = d.poff[p], obs_hi = d.poff[p + 1];
   const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
   const double* Jw = d.J[st->cur];
+  const double xw = d.X[st->cur][4 * (size_t)p + 3];
   for (int o = obs_lo + tid; o < obs_hi; o += kSchurThreads) {
     const int b = d.frame_block[d.obs_frame[o]];
     if (b < 0) continue;
     double Jp[8], Jc[12];
     load_Jp_scaled(Jw, o, s4, Jp);
-    load_Jc_scaled(d, Jw, o, b, Jc);
+    load_Jc_scaled(d, Jw, o, b, xw, Jc);
     const double e0 = Jp[0] * tpv[0] + Jp[1] * tpv[1] + Jp[2] * tpv[2] + Jp[3] * tpv[3];
     const double e1 = Jp[4] * tpv[0] + Jp[5] * tpv[1] + Jp[6] * tpv[2] + Jp[7] * tpv[3];
 #pragma unroll
@@ -612,8 +623,8 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur_wide(Dev d) {
     const int os = obs_lo + (pr.x >> 16), ot = obs_lo + (pr.x & 0xffff);
     const int bs = pr.y >> 16, bt = pr.y & 0xffff;
     double Jcs[12], Jct[12], Jpt[8], Jps[8], Ps[8];
-    load_Jc_scaled(d, Jw, os, bs, Jcs);
-    load_Jc_scaled(d, Jw, ot, bt, Jct);
+    load_Jc_scaled(d, Jw, os, bs, xw, Jcs);
+    load_Jc_scaled(d, Jw, ot, bt, xw, Jct);
     load_Jp_scaled(Jw, ot, s4, Jpt);
     load_Jp_scaled(Jw, os, s4, Jps);
 #pragma unroll

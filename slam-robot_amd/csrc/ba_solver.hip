@@ -1734,15 +1734,18 @@ int BaSolver::KernelWork(double* bytes, double* flops, int max) {
   double npairs = 0.0;  // observation pairs of free points on free frames are not tracked here: use M*k/2
   (void)npairs;
   std::vector<double> by(kKNum, 0.0), fl(kKNum, 0.0);
-  // linearize: read obs (16 B pt + 4 B frame + 1 B fixed) + point X 32 B + offsets 4 B; write J 192 B,
-  // V 80 B, g 32 B per point; camera partials
-  by[kKLin] = M * (16 + 4 + 1 + 192) + P * (32 + 4 + 80 + 32 + 1) + NB * kCamV * 8;
+  // linearize: read obs (16 B pt + 4 B frame + 1 B fixed) + point X 32 B + offsets 4 B; write the J record
+  // (kJStride doubles: 128 B since round 6), V 80 B, g 32 B per point; camera partials
+  const double jrec = 8.0 * kJStride;
+  by[kKLin] = M * (16 + 4 + 1 + jrec) + P * (32 + 4 + 80 + 32 + 1) + NB * kCamV * 8;
   fl[kKLin] = M * 420.0;
-  by[kKSchur] = M * 192 + P * (80 + 32 + 32 + 32 + 80 + 32);
+  // k_schur: the record less r~ (rotation pairs + J~p) and the observation meta; per point V, g, scales, X.w and
+  // the written Vinv / t / diag
+  by[kKSchur] = M * (jrec - 16 + 4) + P * (80 + 32 + 32 + 8 + 32 + 80 + 32);
   fl[kKSchur] = 2048.0 * schur_mfma_ + 512.0 * schur_rhs_;   // 16x16x4 tile updates, 4x4x4 (4-block) rhs slots
-  by[kKPointUpd] = M * (192 + 16 + 4) + P * (32 + 32 + 80 + 32 + 32);
+  by[kKPointUpd] = M * (jrec + 16 + 4) + P * (32 + 32 + 80 + 32 + 32);
   if (spec_) {   // k_update_lin: the update's traffic plus the candidate's linearization (a second J record, V, g)
-    by[kKPointUpd] = M * (192 + 192 + 16 + 4 + 4 + 4) + P * (32 + 32 + 80 + 32 + 32 + 80 + 32) + NB * kCamV * 8;
+    by[kKPointUpd] = M * (jrec + jrec + 16 + 4 + 4 + 4) + P * (32 + 32 + 80 + 32 + 32 + 80 + 32) + NB * kCamV * 8;
     fl[kKPointUpd] = M * 420.0;
   }
   by[kKChol] = n * n * 8 * 2;

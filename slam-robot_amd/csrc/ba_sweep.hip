@@ -133,7 +133,6 @@ __global__ __launch_bounds__(kLinThreads * kW) SG_LIN_ATTR void k_linearize(Dev 
       double rr[2], Jc[12], Jp[8], c;
       const bool ok = LinearizeObservation(d.q[cur] + 4 * f, d.t[cur] + 3 * f, d.k[cur] + 7 * meta_cam(m), X, pt,
                                            d.b, d.inv_b, rr, Jc, Jp, &c);
-      double2* Jo = reinterpret_cast<double2*>(d.J[cur]) + jidx2(o, 0);   // pair e2 at Jo[64 e2]
       if (!ok || fx) {
         if (!ok) {
           if (fx) lsum[2][lane] += 1.0;
@@ -141,8 +140,7 @@ __global__ __launch_bounds__(kLinThreads * kW) SG_LIN_ATTR void k_linearize(Dev 
         } else if (first) {
           lsum[1][lane] += c;
         }
-#pragma unroll
-        for (int i = 0; i < kJStride / 2; ++i) Jo[64 * i] = make_double2(0.0, 0.0);
+        jstore_zero(d.J[cur], o);
       } else {
         cost += c;
         const int b = meta_block(m);
@@ -153,16 +151,9 @@ __global__ __launch_bounds__(kLinThreads * kW) SG_LIN_ATTR void k_linearize(Dev 
           if (!(m & kMetaRot)) { Jc[0] = Jc[1] = Jc[2] = Jc[6] = Jc[7] = Jc[8] = 0.0; }
           if (!(m & kMetaTrans)) { Jc[3] = Jc[4] = Jc[5] = Jc[9] = Jc[10] = Jc[11] = 0.0; }
         }
-        if (!pf) {
-#pragma unroll
-          for (int i = 0; i < 8; ++i) Jp[i] = 0.0;
-        }
-        Jo[0] = make_double2(rr[0], rr[1]);
-#pragma unroll
-        for (int i = 0; i < 6; ++i) Jo[64 * (1 + i)] = make_double2(Jc[2 * i], Jc[2 * i + 1]);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) Jo[64 * (7 + i)] = make_double2(Jp[2 * i], Jp[2 * i + 1]);
-        Jo[64 * 11] = make_double2(c, 0.0);
+        // the record keeps J~p whatever the point's freedom (the translation columns come from it); the point
+        // terms below use it only for a free point
+        jstore(d.J[cur], o, rr, Jc, Jp);
         if (pf) {
           double* pa = pacc + (p - Rc.p0) * 14 * kPtCopies;
 #pragma unroll
@@ -391,7 +382,7 @@ __device__ __forceinline__ void pu_pass1(const Dev& d, int cur, const LinRound& 
   const double4 s4 = reinterpret_cast<const double4*>(d.scale_p)[p];
   const double sp[4] = {s4.x, s4.y, s4.z, s4.w};
   double Jc[12];
-  load_scaled_J(d, d.J[cur], o, ob.b, sp, ob.r, Jc, ob.Jp);
+  load_scaled_J(d, d.J[cur], o, ob.b, sp, m, d.X[cur][4 * (size_t)p + 3], ob.r, Jc, ob.Jp);
   ob.u[0] = ob.u[1] = 0.0;
   if (ob.b >= 0) {
     const double* xc = d.xc + 6 * ob.b;
@@ -599,11 +590,9 @@ __device__ __forceinline__ void ul_obs(const Dev& d, const LinRound& R, const Li
     candfail += ok ? 0.0 : 1.0;
     candcost += ok ? c : 0.0;
   }
-  double2* Jo = reinterpret_cast<double2*>(d.J[nxt]) + jidx2(o, 0);   // pair e2 at Jo[64 e2]
   if (!ok || fx) {
     if (!ok) lsum[fx ? 1 : 0][lane] += 1.0;   // (a fixed observation's cost counts at iteration 0 only)
-#pragma unroll
-    for (int i = 0; i < kJStride / 2; ++i) Jo[64 * i] = make_double2(0.0, 0.0);
+    jstore_zero(d.J[nxt], o);
     return;
   }
   cost += c;
@@ -616,16 +605,7 @@ __device__ __forceinline__ void ul_obs(const Dev& d, const LinRound& R, const Li
     if (!(m & kMetaRot)) { Jc[0] = Jc[1] = Jc[2] = Jc[6] = Jc[7] = Jc[8] = 0.0; }
     if (!(m & kMetaTrans)) { Jc[3] = Jc[4] = Jc[5] = Jc[9] = Jc[10] = Jc[11] = 0.0; }
   }
-  if (!pf) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) Jp[i] = 0.0;
-  }
-  Jo[0] = make_double2(rr[0], rr[1]);
-#pragma unroll
-  for (int i = 0; i < 6; ++i) Jo[64 * (1 + i)] = make_double2(Jc[2 * i], Jc[2 * i + 1]);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) Jo[64 * (7 + i)] = make_double2(Jp[2 * i], Jp[2 * i + 1]);
-  Jo[64 * 11] = make_double2(c, 0.0);
+  jstore(d.J[nxt], o, rr, Jc, Jp);   // (J~p kept whatever the point's freedom; the point terms take it if free)
 #ifndef SG_X_NOPATOM   // timing-only experiment build (results wrong): no point-block LDS atomics
   if (pf) {
     double* pa = pacc + lp * 14 * kPtCopies;

@@ -203,10 +203,14 @@ SG_HD bool LinearizeObservation(const T* q, const T* t, const T* k, const T* X, 
   const T sr = sqrt(rho1);
   r[0] = sr * r0;
   r[1] = sr * r1;
+  // d(uv)/dt = -X.w d(uv)/d(X.xyz) (ProjectJacobian: Jt = -X.w GR, JX[:, 0:3] = GR), so the corrected translation
+  // columns are formed from the corrected point columns, -X.w J~p[:, c]: the device stores J~p only and every reader
+  // recomputes the translation columns with this same product (ba_device.h jc_from_pairs), bit for bit
+  (void)Jt;
   for (int i = 0; i < 2; ++i) {
     for (int c = 0; c < 3; ++c) Jc[6 * i + c] = sr * Jr[3 * i + c];
-    for (int c = 0; c < 3; ++c) Jc[6 * i + 3 + c] = sr * Jt[3 * i + c];
     for (int c = 0; c < 4; ++c) Jp[4 * i + c] = sr * JX[4 * i + c];
+    for (int c = 0; c < 3; ++c) Jc[6 * i + 3 + c] = -X[3] * Jp[4 * i + c];
   }
   if (Jk)
     for (int c = 0; c < 14; ++c) Jk[c] *= sr;
