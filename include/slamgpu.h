@@ -250,6 +250,7 @@ typedef struct sg_ba_info {
                                                 iterations (0 on one rank) */
   int32_t lin_waves;                         /* waves per Jacobian-sweep chunk (1, or 2 when the doubled grid
                                                 fits the device at once) */
+  int32_t cholesky_separator;                /* tiled path with a split: the separator's tile rows (<= 7) */
 } sg_ba_info;
 int sg_ba_info_get(const sg_ba* h, sg_ba_info* out);
 

@@ -1332,12 +1332,13 @@ __device__ __forceinline__ void tile_final(f64x4 (&acc)[kTB], int J, bool& late,
 }
 
 // Separator hand-off.  The bottom half writes its contribution to the separator tiles (its columns
-// ND..ND+6, rows >= ND) mapped back to S's order — reversed tile (I', J') element (a, b) is tile
+// ND..ND+ns-1, rows >= ND) mapped back to S's order — reversed tile (I', J') element (a, b) is tile
 // (NT-1-J', NT-1-I') element (15-b, 15-a) — in the top half's accumulator layout, and its rhs partials
 // summed over the lane rows.
 __device__ __forceinline__ void sep_write(const f64x4 (&acc)[kTB], double ypart, int J, int ND, int NT, int m,
-                                          double* __restrict__ sepb, double* __restrict__ sepy, int li, int lk) {
-  if (J < ND || J >= ND + 7) return;
+                                          int ns, double* __restrict__ sepb, double* __restrict__ sepy, int li,
+                                          int lk) {
+  if (J < ND || J >= ND + ns) return;
   const double ys = sum_rows4(ypart);
   const int Io = NT - 1 - J;
 #pragma unroll
@@ -1358,10 +1359,10 @@ __device__ __forceinline__ void sep_write(const f64x4 (&acc)[kTB], double ypart,
 
 // The top half adds the bottom half's separator contribution to the separator columns it holds (before
 // the first separator diagonal is factored).
-__device__ __forceinline__ void sep_merge(f64x4 (&acc)[kTB], double& ypart, int J, int m,
+__device__ __forceinline__ void sep_merge(f64x4 (&acc)[kTB], double& ypart, int J, int m, int ns,
                                           const double* __restrict__ sepb, const double* __restrict__ sepy,
                                           int lane, int li, int lk) {
-  if (J < m || J >= m + 7) return;
+  if (J < m || J >= m + ns) return;
 #pragma unroll
   for (int u = 0; u < kTB; ++u) {
     const int I = J - ((J - (u + m - 2)) & 7);   // slots of phase m - 1
@@ -1557,11 +1558,12 @@ __device__ __forceinline__ void bs_chain2(const double* __restrict__ Wb, const d
   if (K >= Klo) bs_row(K, wA, zA, first);
 }
 
-// Dissected band (nd > 0: two workgroups).  With m = NT - nd - 7, the tile rows split into the top part
-// A = [0, m), the separator [m, m+7) and the bottom part B = [m+7, NT).  The band is at most 8 tiles wide,
-// so A and B never couple: eliminating A, then B, then the separator is an exact Cholesky of S in that
-// order (nested dissection), and A and B are factored at the same time.
-//   * blockIdx 0 (top) runs the phases of rows 0 .. m+6 of S (band ends clamped to the separator); at
+// Dissected band (nd > 0: two workgroups).  With m = NT - nd - ns, the tile rows split into the top part
+// A = [0, m), the separator [m, m+ns) and the bottom part B = [m+ns, NT).  ns (flags bits 8-11, 1..7; 0 means
+// 7) covers every band of A (the host picks m with max_{K<m} tend[K] = m + ns: at C2, whose rows are 6-7 tiles
+// wide, a 5-row separator), so A and B never couple: eliminating A, then B, then the separator is an exact
+// Cholesky of S in that order (nested dissection), and A and B are factored at the same time.
+//   * blockIdx 0 (top) runs the phases of rows 0 .. m+ns-1 of S (band ends clamped to the separator); at
 //     phase m-1 each wave waits for the bottom half and adds its separator contribution, then factors the
 //     separator rows as usual.
 //   * blockIdx 1 (bottom) runs the phases of B in reversed order (P S P: rows NT-1 .. m+7 of S, then the
@@ -1569,7 +1571,7 @@ __device__ __forceinline__ void bs_chain2(const double* __restrict__ Wb, const d
 //     W tiles, and signals with a release counter.
 //   * Back substitution (top workgroup): the separator rows, then A (wave 0) and B (wave 1, reversed W
 //     tiles) side by side.
-// The chain drops from NT tile rows to m + 7 (C2: 18 -> 13, C5: 75 -> 42).  The wait is bounded: on a
+// The chain drops from NT tile rows to m + ns (C2: 18 -> 12, C5: 75 -> 42).  The wait is bounded: on a
 // time-out the launch reports it (kCTimeout) and the LM decision ends the solve with SG_DEVICE_TIMEOUT
 // instead of hanging or silently rejecting the step.
 //   flags bit 2 (SG_CHOL_FORCE_TIMEOUT, tests only): the bottom workgroup sleeps ~2 ms before its work and
@@ -1591,8 +1593,10 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
   const int li = lane & 15, lk = lane >> 4;
   const int NT = (n + 15) >> 4;
   const bool bottom = nd > 0 && blockIdx.x == 1;
-  const int m = nd > 0 ? NT - nd - 7 : NT;   // first separator tile row (S order)
-  const int NTf = nd > 0 ? (bottom ? nd : m + 7) : NT;   // tile rows this workgroup factors
+  const int nsf = (flags >> 8) & 15;
+  const int ns = nsf > 0 && nsf < kTB ? nsf : kTB - 1;   // separator tile rows
+  const int m = nd > 0 ? NT - nd - ns : NT;   // first separator tile row (S order)
+  const int NTf = nd > 0 ? (bottom ? nd : m + ns) : NT;   // tile rows this workgroup factors
   double* Wb = bottom ? Wg + (size_t)NT * kTB * 256 : Wg;
   double* zpg = Wg + (size_t)2 * NT * kTB * 256;   // [16 nd] the bottom half's z'
   double* sepb = zpg + 16 * NT;                     // [49][256] separator contribution
@@ -1672,7 +1676,7 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
         int lo = c;
         for (int i = max(0, c - kTB); i < c; ++i)
           if (((panel_jend[i] + 15) >> 4) > c) { lo = i; break; }
-        tend[k] = min(NT - lo, nd + 7);
+        tend[k] = min(NT - lo, nd + ns);
       }
     }
     if (done) return;
@@ -1705,7 +1709,7 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
           __builtin_amdgcn_s_sleep(1);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         tmo |= spin >= spin_max;
-        sep_merge(acc, ypart, J, m, sepb, sepy, lane, li, lk);
+        sep_merge(acc, ypart, J, m, ns, sepb, sepy, lane, li, lk);
       }
       tile_phase<kStamp>(acc, ypart, J, late, bad, tmo, sh, d, Wb, zp, tend, K, NTf, lane, li, lk, ts, zg,
                          tacc, tlast);
@@ -1752,7 +1756,7 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
     if (bottom) {
       // row nd-1's updates of the separator columns (slots of phase nd), then the hand-off
       tile_final(acc, J, late, sh, Wb, tend, nd, lane, li, lk);
-      sep_write(acc, ypart, J, nd, NT, m, sepb, sepy, li, lk);
+      sep_write(acc, ypart, J, nd, NT, m, ns, sepb, sepy, li, lk);
     }
   }
   if (bottom) {
@@ -1788,11 +1792,12 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
       }
     } else {
       // separator rows (one wave), then A (waves 0, 1) beside B (waves 2, 3, reversed)
-      if (wave == 0) bs_chain<false>(Wg, zp, xs, m + 6, m, xw, NT, lane, li, lk);
+      if (wave == 0) bs_chain<false>(Wg, zp, xs, m + ns - 1, m, xw, NT, lane, li, lk);
       __syncthreads();
       if (wave < 2) {
 #pragma unroll
-        for (int dd = 1; dd < kTB; ++dd) xw[dd - 1] = xs[16 * (m - 1 + dd) + li];
+        // the separator's x; past it (rows of B, solved beside this chain) zeros: A's W tiles there are zero
+        for (int dd = 1; dd < kTB; ++dd) xw[dd - 1] = dd <= ns ? xs[16 * (m - 1 + dd) + li] : 0.0;
         if (m >= kBs2Rows)
           bs_chain2<false>(Wg, zp, xs, rdone, m - 1, 0, xw, NT, wave, lane, li, lk, tmo);
         else if (wave == 0)
@@ -1800,7 +1805,7 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
       } else if (wave < 4) {
         // x of reversed rows nd .. nd+6 (the separator, S tile rows m+6 .. m)
 #pragma unroll
-        for (int dd = 1; dd < kTB; ++dd) xw[dd - 1] = xs[16 * (NT - nd - dd) + 15 - li];
+        for (int dd = 1; dd < kTB; ++dd) xw[dd - 1] = dd <= ns ? xs[16 * (NT - nd - dd) + 15 - li] : 0.0;
         if (nd >= kBs2Rows)
           bs_chain2<true>(Wg + (size_t)NT * kTB * 256, zpg, xs, rdone_b, nd - 1, 0, xw, NT, wave - 2, lane, li,
                           lk, tmo);

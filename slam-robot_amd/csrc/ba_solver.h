@@ -83,6 +83,7 @@ class BaSolver {
   size_t tile_lds_ = 0;        // its dynamic LDS
   DBuf<double> Wg_;            // its back-substitution tiles W_KJ = U_KK^-1 U_KJ (+ the bottom half's)
   int chol_nd_ = 0;            // dissected band: tile rows the second workgroup factors bottom-up (0: one WG)
+  int chol_ns_ = 7;            // ... and the separator's tile rows (<= 7)
   DBuf<int32_t> tflag_;        // dissected band hand-off counters {bottom done, top done}
   bool chol_cand_lds_ = false;   // candidate-pass operands staged in the Cholesky's LDS (small problems)
   int s_lstride_ = 256, r_lstride_ = 256;   // k_S_reduce's padded list rows (Dev::s_lstride / r_lstride)

@@ -55,7 +55,7 @@ void BaSolver::LaunchCholTiles(bool stamp, dim3 grid, const Dev& d, int flags) {
   // bordered: the frame band ends follow the arrowhead's panel ends in work_i_
   const int32_t* pj = (const int32_t*)work_i_.ptr + (chol_border_ ? (n_ + kCholNb - 1) / kCholNb : 0);
   if (chol_border_) flags |= 8;
-  LaunchCholTilesK(stamp, grid, tile_lds_, stream_, d, pj, Wg_.ptr, tflag_.ptr, chol_nd_, flags);
+  LaunchCholTilesK(stamp, grid, tile_lds_, stream_, d, pj, Wg_.ptr, tflag_.ptr, chol_nd_, flags | (chol_ns_ << 8));
   if (chol_border_) {
     const int ntf = (6 * NB_ + kCholNb - 1) / kCholNb;
     LaunchCholBorderK(border_flags_, border_lds_doubles(ntf, border_flags_, F_, D_, n_) * sizeof(double), stream_, d,
@@ -792,11 +792,32 @@ void BaSolver::Load(const sg_problem& p) {
     }
   }
   // dissected band: a second workgroup factors the bottom nd tile rows (reversed) while the first factors
-  // the top, both meeting at a 7-tile separator (k_chol_tiles); worth it from about 12 tile rows
+  // the top rows [0, m), both meeting at a separator of ns <= 7 tile rows (k_chol_tiles); worth it from about 12
+  // tile rows.  The separator must hold every band of the top part: ns(m) = max_{K<m} tend[K] - m.  The chain is
+  // priced in phases as max(m, nd + h) + ns, h = 2.5 phases for the bottom's hand-off (round-2 stamps: nd = 3 / 4 /
+  // 5 at ns = 7 took 198 / 188 / 193 k cycles at C2), and the cheapest m is taken (C2, whose rows are 6-7 tiles
+  // wide: m = 7, ns = 5, nd = 6 — 12 phases on the top chain instead of 14; C5, 8 tiles: ns = 7, nd = 33 as before).
+  // SG_CHOL_SEP=7: the fixed 7-row separator (tests).
   chol_nd_ = 0;
+  chol_ns_ = kTB - 1;
   if (chol_tiles_ && !chol_border_ && npanel >= kSplitMinNT &&
-      !(getenv("SG_CHOL_SPLIT") && atoi(getenv("SG_CHOL_SPLIT")) == 0))
-    chol_nd_ = (npanel - 9) / 2;   // the bottom (nd rows + hand-off) done before the top reaches row m - 1
+      !(getenv("SG_CHOL_SPLIT") && atoi(getenv("SG_CHOL_SPLIT")) == 0)) {
+    const bool fixed7 = getenv("SG_CHOL_SEP") && atoi(getenv("SG_CHOL_SEP")) == kTB - 1;
+    double best = 1e30;
+    int reach = 0;   // max_{K<m} tend[K]
+    for (int m = 1; m < npanel; ++m) {
+      reach = std::max(reach, std::min(npanel, (panel_jmax[m - 1] + kCholNb - 1) / kCholNb));
+      const int ns = fixed7 ? kTB - 1 : reach - m;
+      const int nd = npanel - m - ns;
+      if (ns < 1 || ns > kTB - 1 || reach - m > ns || nd < 2) continue;
+      const double cost = std::max((double)m, nd + 2.5) + ns;
+      if (cost < best) {
+        best = cost;
+        chol_nd_ = nd;
+        chol_ns_ = ns;
+      }
+    }
+  }
   if (chol_tiles_) {
     // W tiles of the top and bottom halves, the bottom's z' (+ failure slot), the separator contribution
     // and its rhs, then the constants {0, 1}
@@ -1789,6 +1810,7 @@ void BaSolver::Info(sg_ba_info* o) const {
   o->nranks = comm_ ? comm_->nranks() : 1;
   o->num_allreduces = nallreduce_;
   o->lin_waves = lin_waves_;
+  o->cholesky_separator = chol_tiles_ && chol_nd_ > 0 ? chol_ns_ : 0;
 }
 
 double BaSolver::ReprojectMap(sg_map* m) {

@@ -81,7 +81,7 @@ class SgSolverSummary(C.Structure):
 class SgBaInfo(C.Structure):
     _fields_ = [(n, C.c_int32) for n in ("num_frames", "num_points", "num_obs", "num_blocks", "n", "band_tiles",
                                          "cholesky_path", "num_pairs", "rank", "nranks", "cholesky_split",
-                                         "num_allreduces", "lin_waves")]
+                                         "num_allreduces", "lin_waves", "cholesky_separator")]
     CHOLESKY_PATHS = {0: "tiled band (k_chol_tiles)", 1: "LDS window (k_cholesky_window)",
                       2: "global memory (k_cholesky_global, LDS-staged panel rows)",
                       3: "global memory (k_cholesky_global, unstaged)",

@@ -371,8 +371,9 @@ def test_dissected_band_matches_one_workgroup(gpu_lib, monkeypatch, frames, poin
     """The tiled Cholesky factors the band from both ends at once (k_chol_tiles: a second workgroup factors
     the bottom tile rows of the index-reversed system and hands its separator contribution over; DESIGN.md
     4).  Against the one-workgroup factorisation (SG_CHOL_SPLIT=0) the solve must be the same up to rounding
-    (the separator sums in another order): same steps, cost rel 1e-12, poses 1e-10.  Frame counts give
-    n = 204 (13 tile rows, padded: 2 bottom), 228 (15, padded: 3 bottom) and C2's 288 (18: 4 bottom)."""
+    (the separator sums in another order): same steps, cost rel 1e-12, poses 1e-10 — with the fixed 7-row
+    separator (SG_CHOL_SEP=7: n = 204 -> 13 tile rows, 2 bottom; 228 -> 15, 3; C2's 288 -> 18, 4) and with the
+    separator sized to the band (round 6: C2's rows are 6-7 tiles wide, so 5 rows and 6 bottom)."""
     if points is None:
         m = make_config("C2")
     else:
@@ -380,26 +381,36 @@ def test_dissected_band_matches_one_workgroup(gpu_lib, monkeypatch, frames, poin
     pa = ba.problem_from_map_frames(m, m.num_frames - 2, m.num_frames, 2.0)
     nt = (6 * (m.num_frames - 2) + 15) // 16
     out = []
-    for split in (False, True):
-        monkeypatch.setenv("SG_CHOL_SPLIT", "1" if split else "0")
+    for mode in ("one", "sep7", "adaptive"):
+        monkeypatch.setenv("SG_CHOL_SPLIT", "0" if mode == "one" else "1")
+        monkeypatch.setenv("SG_CHOL_SEP", "7" if mode == "sep7" else "0")
         p = pa.copy()
         g = ba.BundleAdjuster()
         g.load(p)
         info = g.info()
         assert info["cholesky"].startswith("tiled band")
-        assert info["cholesky_split"] == ((nt - 9) // 2 if split else 0)
+        if mode == "one":
+            assert info["cholesky_split"] == 0
+        elif mode == "sep7":
+            assert info["cholesky_split"] == (nt - 9) // 2 and info["cholesky_separator"] == 7
+        else:
+            ns, nd = info["cholesky_separator"], info["cholesky_split"]
+            assert 1 <= ns <= 7 and nd >= 2 and nt - nd - ns >= 1
+            if points is None:
+                assert (ns, nd) == (5, 6)
         s = g.solve(default_solver_options(max_num_iterations=8))
         out.append((s, p))
         g.close()
-    (s0, p0), (s1, p1) = out
-    assert s0["ok"] == s1["ok"] == 1
-    assert s0["sync_timeouts"] == s1["sync_timeouts"] == 0
-    assert s0["num_iterations"] == s1["num_iterations"]
-    assert s0["num_successful_steps"] == s1["num_successful_steps"]
-    assert abs(s0["final_cost"] - s1["final_cost"]) <= 1e-12 * s0["final_cost"]
-    np.testing.assert_allclose(p0.q, p1.q, rtol=0, atol=1e-10)
-    np.testing.assert_allclose(p0.t, p1.t, rtol=1e-10, atol=1e-10)
-    np.testing.assert_allclose(p0.X, p1.X, rtol=1e-9, atol=1e-10)
+    s0, p0 = out[0]
+    for s1, p1 in out[1:]:
+        assert s0["ok"] == s1["ok"] == 1
+        assert s0["sync_timeouts"] == s1["sync_timeouts"] == 0
+        assert s0["num_iterations"] == s1["num_iterations"]
+        assert s0["num_successful_steps"] == s1["num_successful_steps"]
+        assert abs(s0["final_cost"] - s1["final_cost"]) <= 1e-12 * s0["final_cost"]
+        np.testing.assert_allclose(p0.q, p1.q, rtol=0, atol=1e-10)
+        np.testing.assert_allclose(p0.t, p1.t, rtol=1e-10, atol=1e-10)
+        np.testing.assert_allclose(p0.X, p1.X, rtol=1e-9, atol=1e-10)
 
 def _intrinsics_scene(seed=1):
     """C1-sized scene whose intrinsics start off the generating camera (focal +0.4 %, principal point +1.5 px,
@@ -634,7 +645,7 @@ def test_speculative_linearization_matches_two_pass_chain(gpu_lib, monkeypatch, 
     difference in the trust-region ratio).  A full solve from the perturbed start: the same steps, cost 1e-12
     relative, poses 1e-10 / 1e-6 mm, point directions 1e-9.  60 iterations of the benchmark regime (termination
     off, a rejected step re-reduces the current slot instead of re-linearizing), past convergence into rejected
-    and invalid steps, where the trust radius follows rounding: the same minimum (cost 1e-10, poses 1e-8 /
+    and invalid steps, where the trust radius follows rounding: the same minimum (cost 2e-9, poses 1e-8 /
     1e-5 mm)."""
     m = make_config("C2")
     pa = ba.problem_from_map_frames(m, 48, 50, 2.0)
@@ -655,7 +666,9 @@ def test_speculative_linearization_matches_two_pass_chain(gpu_lib, monkeypatch, 
                                    x0 / np.linalg.norm(x0, axis=1, keepdims=True), rtol=0, atol=1e-9)
     else:
         assert s1["num_unsuccessful_steps"] > 0 and s1["num_lm_iterations"] == s0["num_lm_iterations"] == 60
-        assert abs(s0["final_cost"] - s1["final_cost"]) <= 1e-10 * s0["final_cost"]   # measured 6e-11
+        # measured 6e-11 with the 7-row separator, 7.2e-10 with C2's 5-row one (round 6): past convergence the
+        # accept / reject sequence follows rounding, so the two chains end at the same minimum by different paths
+        assert abs(s0["final_cost"] - s1["final_cost"]) <= 2e-9 * s0["final_cost"]
         np.testing.assert_allclose(p1.q, p0.q, rtol=0, atol=1e-8)
         np.testing.assert_allclose(p1.t, p0.t, rtol=0, atol=1e-5)
 
