@@ -1183,12 +1183,23 @@ __device__ __forceinline__ void tile_phase(f64x4 (&acc)[kTB], double& ypart, int
     // row K + 1 touches first
     const bool hasw = J < tend[K - 1];
     f64x4 Wt = {0.0, 0.0, 0.0, 0.0};
+#ifdef SG_X_LATECOPY   // A/B (round 6): the W tile's MFMA reads a copy of slot 0, so the reload need not wait for it
+    f64x4 a0 = acc[0];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) asm volatile("" : "+v"(a0[q]));
+    const int Jw = J;
+    J += kTB;
+    tile_col_load(acc, ypart, d, J, K, li, lk, ts);
+    if (hasw) Wt = tile_w(a0, sh.Zs[(K - 1) & 3], li, lk);
+    SG_AST(0)
+#else
     if (hasw) Wt = tile_w(acc[0], sh.Zs[(K - 1) & 3], li, lk);
     SG_AST(0)
     const int Jw = J;
     J += kTB;
 #ifndef SG_X_NOLOAD   // timing-only A/B (round 6): no column reload (results wrong)
     tile_col_load(acc, ypart, d, J, K, li, lk, ts);
+#endif
 #endif
     SG_AST(1)
     if (hasw) tile_w_store(Wt, Wg, K - 1, Jw, lane);
@@ -1363,14 +1374,27 @@ __device__ __forceinline__ void sep_merge(f64x4 (&acc)[kTB], double& ypart, int 
                                           const double* __restrict__ sepb, const double* __restrict__ sepy,
                                           int lane, int li, int lk) {
   if (J < m || J >= m + ns) return;
+  // two tiles' loads in flight per wait (unconditional loads from clamped addresses, the sums selected): written as
+  // acc[u][q] += src[q * 64] the compiler waited for every load before the next (one global round trip per
+  // element on the hand-off's critical path)
 #pragma unroll
-  for (int u = 0; u < kTB; ++u) {
-    const int I = J - ((J - (u + m - 2)) & 7);   // slots of phase m - 1
-    if (I >= m) {
-      const double* src = sepb + ((I - m) * 7 + (J - m)) * 256 + lane;
+  for (int u0 = 0; u0 < kTB; u0 += 2) {
+    f64x4 t[2];
+    bool use[2];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) acc[u][q] += src[q * 64];
+    for (int h = 0; h < 2; ++h) {
+      const int u = u0 + h;
+      const int I = J - ((J - (u + m - 2)) & 7);   // slots of phase m - 1
+      use[h] = I >= m;
+      const double* src = sepb + (use[h] ? ((I - m) * 7 + (J - m)) * 256 : 0) + lane;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) t[h][q] = src[q * 64];
     }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (use[h])
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[u0 + h][q] += t[h][q];
   }
   if (lk == 0) ypart += sepy[(J - m) * 16 + li];
 }
@@ -1673,9 +1697,17 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
         // reversed row k = column c = NT-1-k of S: its band reaches back to lo(c), the first row whose band
         // covers c (band ends are non-decreasing), so the reversed row ends at NT - lo(c)
         const int c = NT - 1 - k;
+        // the kTB candidate rows' band ends loaded together (a loop that breaks at the first hit loaded them one
+        // round trip at a time), then the first hit in row order
+        int te[kTB];
+#pragma unroll
+        for (int h = 0; h < kTB; ++h) te[h] = panel_jend[max(0, c - kTB + h)];
         int lo = c;
-        for (int i = max(0, c - kTB); i < c; ++i)
-          if (((panel_jend[i] + 15) >> 4) > c) { lo = i; break; }
+#pragma unroll
+        for (int h = kTB - 1; h >= 0; --h) {
+          const int i = c - kTB + h;
+          if (i >= 0 && ((te[h] + 15) >> 4) > c) lo = i;
+        }
         tend[k] = min(NT - lo, nd + ns);
       }
     }
