@@ -1183,23 +1183,12 @@ __device__ __forceinline__ void tile_phase(f64x4 (&acc)[kTB], double& ypart, int
     // row K + 1 touches first
     const bool hasw = J < tend[K - 1];
     f64x4 Wt = {0.0, 0.0, 0.0, 0.0};
-#ifdef SG_X_LATECOPY   // A/B (round 6): the W tile's MFMA reads a copy of slot 0, so the reload need not wait for it
-    f64x4 a0 = acc[0];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) asm volatile("" : "+v"(a0[q]));
-    const int Jw = J;
-    J += kTB;
-    tile_col_load(acc, ypart, d, J, K, li, lk, ts);
-    if (hasw) Wt = tile_w(a0, sh.Zs[(K - 1) & 3], li, lk);
-    SG_AST(0)
-#else
     if (hasw) Wt = tile_w(acc[0], sh.Zs[(K - 1) & 3], li, lk);
     SG_AST(0)
     const int Jw = J;
     J += kTB;
 #ifndef SG_X_NOLOAD   // timing-only A/B (round 6): no column reload (results wrong)
     tile_col_load(acc, ypart, d, J, K, li, lk, ts);
-#endif
 #endif
     SG_AST(1)
     if (hasw) tile_w_store(Wt, Wg, K - 1, Jw, lane);
