@@ -6,6 +6,7 @@
 // here the solved blocks are copied back by sg_problem_write_back (same observable effect).
 #include <algorithm>
 #include <cstring>
+#include <memory>
 #include <numeric>
 #include <string>
 #include <vector>
@@ -24,6 +25,13 @@ struct ProblemStorage {
   std::vector<int32_t> frame_camera, frame_map_index, point_map_index, obs_frame, obs_point, dist_frame,
       dist_prev;
   std::vector<uint8_t> frame_rot_free, frame_trans_free, point_free;
+
+  void Clear() {
+    for (auto* v : {&k, &q, &t, &X, &obs_pt}) v->clear();
+    for (auto* v : {&frame_camera, &frame_map_index, &point_map_index, &obs_frame, &obs_point, &dist_frame, &dist_prev})
+      v->clear();
+    for (auto* v : {&frame_rot_free, &frame_trans_free, &point_free}) v->clear();
+  }
 
   void Bind(sg_problem* p) {
     p->k = k.data();
@@ -50,10 +58,39 @@ struct ProblemStorage {
   }
 };
 
+// A freed problem's storage is kept for the thread's next problem (main.cpp builds one per SolveFrames call,
+// each about the size of the last): its vectors keep their capacity, so a build neither allocates nor
+// page-faults.  Build's scratch arrays are kept the same way.
+constexpr size_t kStoragePool = 2;
+thread_local std::vector<std::unique_ptr<ProblemStorage>> t_pool;
+
+ProblemStorage* TakeStorage() {
+  if (t_pool.empty()) return new ProblemStorage;
+  ProblemStorage* st = t_pool.back().release();
+  t_pool.pop_back();
+  st->Clear();
+  return st;
+}
+
+void ReturnStorage(ProblemStorage* st) {
+  if (t_pool.size() < kStoragePool)
+    t_pool.emplace_back(st);
+  else
+    delete st;
+}
+
+struct BuildScratch {
+  std::vector<uint8_t> frame_used, point_in, point_fluid;
+  std::vector<int32_t> obs_in, point_index, pts, frame_index;
+};
+thread_local BuildScratch t_scratch;
+
 constexpr int kUnusableMask = (1 << SG_BAD_LOCATION) | (1 << SG_NO_BASELINE) | (1 << SG_NO_OBSERVATIONS) |
                               (1 << SG_BAD_FEATURE);  // TrackedPoint::slam_usable, localmap.h:242-248
 
-void CheckMap(const sg_map* m) {
+// Validates the map; returns whether its observations are ordered by frame (a LocalMap's are: each frame's
+// observations are appended when the frame is tracked), which lets Build walk only the presented frames' range.
+bool CheckMap(const sg_map* m) {
   SG_REQUIRE(m != nullptr, SG_EINVAL, "null map");
   SG_REQUIRE(m->num_frames >= 0 && m->num_points >= 0 && m->num_obs >= 0 && m->num_cameras >= 0, SG_EINVAL,
              "negative map sizes");
@@ -62,27 +99,58 @@ void CheckMap(const sg_map* m) {
                "frame_camera out of range");
     SG_REQUIRE(m->frame_prev[f] >= -1 && m->frame_prev[f] < m->num_frames, SG_EINVAL, "frame_prev out of range");
   }
+  // one branch-free sweep (the range tests and the order test accumulate), then the failing index if any
+  const uint32_t F = (uint32_t)m->num_frames, P = (uint32_t)m->num_points;
+  bool bad = false, sorted = true;
+  int32_t prev = 0;
   for (int32_t o = 0; o < m->num_obs; ++o) {
-    SG_REQUIRE(m->obs_frame[o] >= 0 && m->obs_frame[o] < m->num_frames, SG_EINVAL, "obs_frame out of range");
-    SG_REQUIRE(m->obs_point[o] >= 0 && m->obs_point[o] < m->num_points, SG_EINVAL, "obs_point out of range");
+    const int32_t f = m->obs_frame[o];
+    bad |= ((uint32_t)f >= F) | ((uint32_t)m->obs_point[o] >= P);
+    sorted &= f >= prev;
+    prev = f;
   }
+  if (bad)
+    for (int32_t o = 0; o < m->num_obs; ++o) {
+      SG_REQUIRE(m->obs_frame[o] >= 0 && m->obs_frame[o] < m->num_frames, SG_EINVAL, "obs_frame out of range");
+      SG_REQUIRE(m->obs_point[o] >= 0 && m->obs_point[o] < m->num_points, SG_EINVAL, "obs_point out of range");
+    }
+  return sorted;
 }
 
 // role[f]: 0 = not presented, 1 = presented & solved, 2 = presented & constant.
-bool Build(const sg_map* m, const std::vector<uint8_t>& role, double range, bool cameras_free,
+bool Build(const sg_map* m, const std::vector<uint8_t>& role, double range, bool cameras_free, bool obs_by_frame,
            sg_problem* out) {
   const int F = m->num_frames, P = m->num_points, M = m->num_obs;
-  // Pass 1 (slam.cpp:274-303): usable observations of presented frames.
-  std::vector<uint8_t> frame_used(F, 0), point_in(P, 0), point_fluid(P, 0), obs_in(M, 0);
-  for (int o = 0; o < M; ++o) {
+  // Observations to visit: all of them, or (observations ordered by frame) the range of the presented frames.
+  int o_lo = 0, o_hi = M;
+  if (obs_by_frame) {
+    int fmin = F, fmax = -1;
+    for (int f = 0; f < F; ++f)
+      if (role[f]) {
+        fmin = std::min(fmin, f);
+        fmax = std::max(fmax, f);
+      }
+    o_lo = (int)(std::lower_bound(m->obs_frame, m->obs_frame + M, fmin) - m->obs_frame);
+    o_hi = (int)(std::upper_bound(m->obs_frame + o_lo, m->obs_frame + M, fmax) - m->obs_frame);
+  }
+  // Pass 1 (slam.cpp:274-303): usable observations of presented frames, in map order (branch-free: the
+  // selection is data-dependent, so the marks are or-ed in and the list is compacted by its running count).
+  BuildScratch& sc = t_scratch;
+  std::vector<uint8_t>&frame_used = sc.frame_used, &point_in = sc.point_in, &point_fluid = sc.point_fluid;
+  frame_used.assign(F, 0);
+  point_in.assign(P, 0);
+  point_fluid.assign(P, 0);
+  std::vector<int32_t>& obs_in = sc.obs_in;
+  obs_in.resize(std::max(o_hi - o_lo, 0));
+  size_t nin = 0;
+  for (int o = o_lo; o < o_hi; ++o) {
     const int f = m->obs_frame[o], pt = m->obs_point[o];
-    if (!role[f]) continue;
-    if (m->obs_disabled[o]) continue;
-    if (m->point_flags[pt] & kUnusableMask) continue;
-    obs_in[o] = 1;
-    frame_used[f] = 1;
-    point_in[pt] = 1;
-    if (role[f] == 1) point_fluid[pt] = 1;
+    const uint8_t use = (role[f] != 0) & (m->obs_disabled[o] == 0) & ((m->point_flags[pt] & kUnusableMask) == 0);
+    obs_in[nin] = o;
+    nin += use;
+    frame_used[f] |= use;
+    point_in[pt] |= use;
+    point_fluid[pt] |= use & (role[f] == 1);
   }
   int used = 0;
   for (int f = 0; f < F; ++f) {
@@ -90,8 +158,9 @@ bool Build(const sg_map* m, const std::vector<uint8_t>& role, double range, bool
   }
   if (used < 2) return false;  // "Slam aborted due to frame set too small" (slam.cpp:305-308)
 
-  auto* st = new ProblemStorage;
-  std::vector<int32_t> frame_index(F, -1);
+  auto* st = TakeStorage();
+  std::vector<int32_t>& frame_index = sc.frame_index;
+  frame_index.assign(F, -1);
   auto add_frame = [&](int f, bool rot_free, bool trans_free) {
     frame_index[f] = (int32_t)st->frame_camera.size();
     st->frame_camera.push_back(m->frame_camera[f]);
@@ -115,21 +184,33 @@ bool Build(const sg_map* m, const std::vector<uint8_t>& role, double range, bool
     st->dist_prev.push_back(frame_index[prev]);
   }
   // Points (slam.cpp:345-354).
-  std::vector<int32_t> point_index(P, -1);
-  for (int pt = 0; pt < P; ++pt) {
-    if (!point_in[pt]) continue;
-    point_index[pt] = (int32_t)st->point_free.size();
-    st->point_map_index.push_back(pt);
-    const bool is_const = m->point_uncertainty[pt] <= 100.0 && !point_fluid[pt];
-    st->point_free.push_back(!is_const);
-    st->X.insert(st->X.end(), m->X + 4 * pt, m->X + 4 * pt + 4);
+  std::vector<int32_t>&point_index = sc.point_index, &pts = sc.pts;
+  point_index.assign(P, -1);
+  pts.resize(P);
+  size_t npt = 0;
+  for (int pt = 0; pt < P; ++pt) {   // compaction of the marked points, in map order
+    pts[npt] = pt;
+    npt += point_in[pt];
   }
-  for (int o = 0; o < M; ++o) {
-    if (!obs_in[o]) continue;
-    st->obs_pt.push_back(m->obs_pt[2 * o]);
-    st->obs_pt.push_back(m->obs_pt[2 * o + 1]);
-    st->obs_frame.push_back(frame_index[m->obs_frame[o]]);
-    st->obs_point.push_back(point_index[m->obs_point[o]]);
+  st->point_map_index.assign(pts.begin(), pts.begin() + npt);
+  st->point_free.resize(npt);
+  st->X.resize(4 * npt);
+  for (size_t i = 0; i < npt; ++i) {
+    const int pt = pts[i];
+    point_index[pt] = (int32_t)i;
+    const bool is_const = m->point_uncertainty[pt] <= 100.0 && !point_fluid[pt];
+    st->point_free[i] = !is_const;
+    std::memcpy(st->X.data() + 4 * i, m->X + 4 * (size_t)pt, 4 * sizeof(double));
+  }
+  st->obs_pt.resize(2 * nin);
+  st->obs_frame.resize(nin);
+  st->obs_point.resize(nin);
+  for (size_t i = 0; i < nin; ++i) {
+    const int o = obs_in[i];
+    st->obs_pt[2 * i] = m->obs_pt[2 * o];
+    st->obs_pt[2 * i + 1] = m->obs_pt[2 * o + 1];
+    st->obs_frame[i] = frame_index[m->obs_frame[o]];
+    st->obs_point[i] = point_index[m->obs_point[o]];
   }
   st->k.assign(m->k, m->k + 7 * m->num_cameras);
   std::memset(out, 0, sizeof(*out));
@@ -195,7 +276,7 @@ void sg_device_options_default(sg_device_options* o) {
 int sg_problem_from_map_frames(const sg_map* map, int32_t num_to_solve, int32_t num_to_present, double range,
                                sg_problem* out, int32_t* built) {
   SG_CAPI_BEGIN
-  sg::CheckMap(map);
+  const bool obs_by_frame = sg::CheckMap(map);
   SG_REQUIRE(out && built, SG_EINVAL, "null output");
   // slam.cpp:423-434: the newest num_to_solve frames are solved, the next ones up to num_to_present are
   // presented as constant.
@@ -206,23 +287,23 @@ int sg_problem_from_map_frames(const sg_map* map, int32_t num_to_solve, int32_t 
     else if (i < num_to_present) role[f] = 2;
     else break;
   }
-  *built = sg::Build(map, role, range, false, out) ? 1 : 0;
+  *built = sg::Build(map, role, range, false, obs_by_frame, out) ? 1 : 0;
   SG_CAPI_END
 }
 
 int sg_problem_from_map_all(const sg_map* map, double range, int32_t solve_cameras, sg_problem* out,
                             int32_t* built) {
   SG_CAPI_BEGIN
-  sg::CheckMap(map);
+  const bool obs_by_frame = sg::CheckMap(map);
   SG_REQUIRE(out && built, SG_EINVAL, "null output");
   std::vector<uint8_t> role(map->num_frames, 1);  // slam.cpp:449-452
-  *built = sg::Build(map, role, range, solve_cameras != 0, out) ? 1 : 0;
+  *built = sg::Build(map, role, range, solve_cameras != 0, obs_by_frame, out) ? 1 : 0;
   SG_CAPI_END
 }
 
 void sg_problem_free(sg_problem* p) {
   if (p && p->owner_) {
-    delete static_cast<sg::ProblemStorage*>(p->owner_);
+    sg::ReturnStorage(static_cast<sg::ProblemStorage*>(p->owner_));
     p->owner_ = nullptr;
   }
 }

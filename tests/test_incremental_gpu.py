@@ -109,3 +109,49 @@ def test_slam_repeated_solve_reuses_structure(gpu_lib, oracle_lib):
     # a different window (main.cpp:580-592 alternates 2/5 and 10/20) rebuilds
     assert slam.SolveFrames(m, 6, 10, 2.0)
     assert slam.load_counts() == (2, 1)
+
+
+def _first_frames(full, F):
+    """The map as main.cpp holds it after frame F-1 was tracked: frames [0, F) and their observations."""
+    sel = np.flatnonzero(full.obs_frame < F)
+    kw = {}
+    for f in full.__dataclass_fields__:
+        v = getattr(full, f)
+        if v is None:
+            kw[f] = None
+        elif f in ("q", "q_true"):
+            kw[f] = v[:4 * F].copy()
+        elif f in ("t", "t_true"):
+            kw[f] = v[:3 * F].copy()
+        elif f in ("frame_camera", "frame_prev", "frame_keyframe"):
+            kw[f] = v[:F].copy()
+        elif f in ("obs_frame", "obs_point", "obs_disabled"):
+            kw[f] = v[sel].copy()
+        elif f in ("obs_pt", "obs_error"):
+            kw[f] = v.reshape(-1, 2)[sel].reshape(-1).copy()
+        else:
+            kw[f] = v.copy()
+    return type(full)(**kw)
+
+
+def test_slam_shifted_windows_match_fresh_handles(gpu_lib):
+    """main.cpp:580-592's pattern on one Slam object: SolveFrames(2, 5) as the map grows by a frame, with a
+    (10, 20) call in between.  Every window differs from the last (a new frame enters, the oldest leaves, so the
+    points, their order and every work list change), so each load rebuilds — on the buffers, staging memory and
+    scratch of the previous loads — and each solve must equal a fresh Slam's on the same map state."""
+    full = make_scene(num_frames=18, num_points=1500, seed=9, run_max=8)
+    slam = ba.Slam()
+    calls = 0
+    for F in range(12, 18):
+        for ns, npres in ((2, 5),) + (((10, 20),) if F == 15 else ()):
+            m = _first_frames(full, F)
+            mf = m.copy()
+            assert slam.SolveFrames(m, ns, npres, 2.0)
+            calls += 1
+            fresh = ba.Slam()
+            assert fresh.SolveFrames(mf, ns, npres, 2.0)
+            assert abs(slam.error() - fresh.error()) <= 1e-9 * fresh.error(), (F, ns)
+            np.testing.assert_allclose(m.t, mf.t, atol=1e-6)
+            np.testing.assert_allclose(m.q, mf.q, atol=1e-9)
+            np.testing.assert_allclose(m.X, mf.X, rtol=1e-7, atol=1e-9)
+    assert slam.load_counts() == (calls, 0)

@@ -100,3 +100,28 @@ def test_landmark_shards_partition_the_problem(nranks):
     if nranks > 1:
         counts = np.array([s.num_obs for s in shards])
         assert counts.max() <= 1.5 * pa.num_obs / nranks + 50
+
+
+def _permuted(m, order):
+    m = m.copy()
+    for f in ("obs_frame", "obs_point", "obs_disabled"):
+        setattr(m, f, np.ascontiguousarray(getattr(m, f)[order]))
+    for f in ("obs_pt", "obs_error"):
+        v = getattr(m, f)
+        if v is not None:
+            setattr(m, f, np.ascontiguousarray(v.reshape(-1, 2)[order].reshape(-1)))
+    return m
+
+
+@pytest.mark.parametrize("solve,present", [(2, 5), (10, 20), (14, 14)])
+def test_setup_with_observations_out_of_frame_order(oracle_lib, solve, present):
+    """A LocalMap's observations come ordered by frame, and the setup then walks only the presented frames'
+    range; any other order takes the full walk.  Both give the oracle's problem (observations in map order)."""
+    base = _edge_map()
+    assert np.all(np.diff(base.obs_frame) >= 0)   # the fast path's precondition holds for the scene maps
+    rng = np.random.default_rng(5)
+    last_first = np.r_[1:base.num_obs, 0]          # one observation of frame 0 moved to the end
+    for order in (rng.permutation(base.num_obs), last_first):
+        m = _permuted(base, order)
+        _same(ba.problem_from_map_frames(m, solve, present, 2.0),
+              oracle_lib.problem_from_map_frames(m, solve, present, 2.0))
