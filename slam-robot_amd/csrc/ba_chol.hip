@@ -1388,12 +1388,40 @@ __device__ __forceinline__ void sep_merge(f64x4 (&acc)[kTB], double& ypart, int 
   if (lk == 0) ypart += sepy[(J - m) * 16 + li];
 }
 
+// The row sums of one back-substitution step, reduced and scattered: lane (li, lk) holds the partials p[q] of
+// rows lk + 4q (its column li of the W tiles).  Two quad-perm exchanges leave it one of the four rows, q = 2 b0
+// + b1 (b0 = li & 1, b1 = (li >> 1) & 1), summed over its quad; two row rotations (by 4 and 8 lanes) then sum the
+// four quads of the lane row.  Ten DPP moves and five adds, where four full butterflies took 32 and 16.  Lanes
+// li, li + 4, li + 8, li + 12 hold the same row's total, each summed in its own order: readers take it from one
+// fixed lane (bs_src_lane), so every x is the same bits everywhere.
+template <int kCtrl>
+__device__ __forceinline__ double dpp_mv(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), kCtrl, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), kCtrl, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double bs_rowsum(const double (&p)[4], bool b0, bool b1) {
+  const double k0 = b0 ? p[2] : p[0], k1 = b0 ? p[3] : p[1];
+  const double s0 = b0 ? p[0] : p[2], s1 = b0 ? p[1] : p[3];
+  const double a0 = k0 + dpp_mv<0xB1>(s0), a1 = k1 + dpp_mv<0xB1>(s1);   // quad_perm [1,0,3,2]
+  const double k = b1 ? a1 : a0, sd = b1 ? a0 : a1;
+  double v = k + dpp_mv<0x4E>(sd);   // quad_perm [2,3,0,1]
+  v += dpp_mv<0x124>(v);             // row_ror:4
+  v += dpp_mv<0x128>(v);             // row_ror:8
+  return v;
+}
+// The lane holding row li's total after bs_rowsum (row li = lk' + 4 q', q' = li >> 2 = 2 b0' + b1').
+__device__ __forceinline__ int bs_src_lane(int li) {
+  const int q = li >> 2;
+  return (((q >> 1) & 1) | ((q & 1) << 1)) + 16 * (li & 3);
+}
+
 // Back substitution of tile rows Khi .. Klo in one wave:  x_K = z'_K - sum_{d=1..7} W_{K,K+d} x_{K+d}, with no
 // LDS round trip on the row-to-row chain.  Lane (li, lk) holds rows lk + 4q, column li of each W tile (acc
 // layout) and x_{K+d}[li] in registers (xw[d-1]; zero past the last row, and W tiles outside the band are
-// zero), so the d >= 2 terms are formed before x_{K+1} is known.  The 16-lane row sums run as a DPP butterfly
-// (quad xor 1, quad xor 2, half-row mirror, row mirror: bitwise the same sum in every lane), and one shuffle
-// moves x_K[li] (row li & 3, register li >> 2) to every lane.  W rows and z' are prefetched kBsBuf rows ahead
+// zero), so the d >= 2 terms are formed before x_{K+1} is known.  The 16-lane row sums are reduced and scattered
+// by DPP (bs_rowsum: each lane is left one row's total), and one shuffle moves x_K[li] from its one source lane
+// (bs_src_lane) to every lane.  W rows and z' are prefetched kBsBuf rows ahead
 // (kBsBuf register buffers, the loop unrolled by kBsBuf).  kRev: the rows are the bottom
 // half's reversed order, x_K[li] is stored at S-order index 16 (NT-1-K) + 15 - li.
 #ifndef SG_BS_BUF
@@ -1414,39 +1442,21 @@ __device__ __forceinline__ void bs_chain(const double* __restrict__ Wb, const do
 #pragma unroll
       for (int q = 0; q < 4; ++q) w[dd - 1][q] = src[dd * 256 + q * 64];
   };
-  const int srcl = 16 * (li & 3) + li;   // the lane holding x_K[li] after the row sums
-  unsigned qbits = 1u << (li >> 2);
-  asm volatile("" : "+v"(qbits));
+  const int srcl = bs_src_lane(li);   // the lane holding x_K[li] after the row sums
+  int lb = li;
+  asm volatile("" : "+v"(lb));   // (opaque: the selects stay per-lane v_cndmask, hoisted nowhere)
+  const bool b0 = (lb & 1) != 0, b1 = (lb & 2) != 0;
+  const int qs = 2 * (li & 1) + ((li >> 1) & 1);   // the row lk + 4 qs this lane sums (bs_rowsum)
   // kBsBuf register buffers: row K's W tiles and z' are loaded kBsBuf rows ahead of the chain (round 6: two rows
   // ahead left the chain waiting on its L2 loads)
-  auto zload = [&](double (&zk)[4], int K) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) zk[q] = zsrc[16 * (K >= 0 ? K : 0) + lk + 4 * q];
-  };
-  auto bs_row = [&](int K, double (&w)[kTB - 1][4], double (&zk)[4]) {
+  auto zload = [&](double& zk, int K) { zk = zsrc[16 * (K >= 0 ? K : 0) + lk + 4 * qs]; };
+  auto bs_row = [&](int K, double (&w)[kTB - 1][4], double& zk) {
     double p[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int dd = kTB - 1; dd >= 1; --dd)
 #pragma unroll
       for (int q = 0; q < 4; ++q) p[q] = fma(w[dd - 1][q], xw[dd - 1], p[q]);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      double v = p[q];
-      v += dpp_d<0xB1>(v);
-      v += dpp_d<0x4E>(v);
-      v += dpp_d<0x141>(v);
-      v += dpp_d<0x140>(v);
-      p[q] = zk[q] - v;   // x_K[lk + 4q], the same bits in every lane of the row
-    }
-    // register p[li >> 2] by opaque bit masks (a lane-dependent ?: chain compiles to divergent branches)
-    unsigned long long mb = 0ull;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      int msk;
-      asm volatile("v_bfe_i32 %0, %1, %2, 1" : "=v"(msk) : "v"(qbits), "n"(q));
-      mb |= (unsigned long long)__double_as_longlong(p[q]) & (unsigned long long)(long long)msk;
-    }
-    const double xk = __shfl(__longlong_as_double((long long)mb), srcl);
+    const double xk = __shfl(zk - bs_rowsum(p, b0, b1), srcl);
     if (kRev)
       xs[16 * (NT - 1 - K) + 15 - li] = xk;
     else
@@ -1457,7 +1467,7 @@ __device__ __forceinline__ void bs_chain(const double* __restrict__ Wb, const do
     wload(w, K - kBsBuf);   // this buffer's next row
     zload(zk, K - kBsBuf);
   };
-  double wb[kBsBuf][kTB - 1][4], zb[kBsBuf][4];
+  double wb[kBsBuf][kTB - 1][4], zb[kBsBuf];
 #pragma unroll
   for (int b = 0; b < kBsBuf; ++b) {
     wload(wb[b], Khi - b);
@@ -1473,7 +1483,8 @@ __device__ __forceinline__ void bs_chain(const double* __restrict__ Wb, const do
     if (K - b >= Klo) bs_row(K - b, wb[b], zb[b]);
 }
 
-// The same chain on two waves: wave `par` takes rows Khi - par, Khi - par - 2, ..., so each wave has two
+// The same chain on two waves (its row sums are the four full butterflies: bs_rowsum's selects push this
+// variant's registers past the budget): wave `par` takes rows Khi - par, Khi - par - 2, ..., so each wave has two
 // rows' time to bring in its next W rows (its register buffers hold rows 2 and 4 ahead of the chain); the
 // other wave's newest x arrives through LDS behind a per-row flag (`done[K]`: set after x_K is written; the
 // LDS accesses of one wave execute in order).  xw: x_{Khi+1 .. Khi+7} (zero past the system).  The flag wait
