@@ -1652,9 +1652,19 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
   // late wave of column K (one W tile, a reload) or with column K+2 (its first few tiles), not with a
   // column four ahead and its full band of trailing MFMAs.  SIMD ids from HW_ID; any other placement than
   // two waves per SIMD keeps column = wave.
+  // D_0 (no updates: the wave that gets column 0 factors it first), its rhs and the LmState flag do not depend on
+  // the column mapping: every wave's loads of them go out before the mapping's barrier, an LDS-only one, so they
+  // stay in flight across it
+  const f64x4 D0 = tile_load(d.S, 0, 0, li, lk, ts);
+  double y0;
+  {
+    const int sj0 = ts.rev ? ts.np - 1 - li : li, ld = ts.ld;
+    y0 = d.S[(lk == 0 && sj0 < n && 0 < ts.sep) ? ld * ld + sj0 : ld * ld + ld];
+  }
+  const int done = st->done;
   if (lane == 0) sh.simd[wave] = __builtin_amdgcn_s_getreg((1 << 11) | (4 << 6) | 4);   // HW_ID.SIMD_ID
   for (int i = tid; i < 16 * kTLd; i += kTileThreads) sh.Id[i] = (i / kTLd == i % kTLd) ? 1.0 : 0.0;
-  __syncthreads();
+  lds_barrier();
   int col = wave;
   {
     const int my = sh.simd[wave];
@@ -1676,18 +1686,8 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
     double ypart = 0.0;
     int J = col;
     bool late = false;
-    // the first column's loads go out before the LmState read returns (a finished solve exits after them)
-    f64x4 D0;
-    double y0 = 0.0;
-    if (J == 0) {
-      // D_0 has no updates: load it and column 8 together, then factor D_0 while column 8 arrives
-      D0 = tile_load(d.S, 0, 0, li, lk, ts);
-      const int sj0 = ts.rev ? ts.np - 1 - li : li, ld = ts.ld;
-      y0 = d.S[(lk == 0 && sj0 < n && 0 < ts.sep) ? ld * ld + sj0 : ld * ld + ld];
-      J = kTB;
-    }
-    const int done = st->done;
-    asm volatile("" ::: "memory");   // the LmState load goes out before column 8's (its wait then skips them)
+    // column 0's wave loads column 8 instead (D_0 is in flight) and factors D_0 while it arrives
+    if (J == 0) J = kTB;
     tile_col_load(acc, ypart, d, J, 0, li, lk, ts);   // slots of phase 0
     // band ends (read first in phase 0, after the barrier below): their loads follow the column's
     for (int k = tid; k < NT; k += kTileThreads) {
