@@ -2,6 +2,7 @@
 // the default dissected tiled band Cholesky k_chol_tiles (MFMA trailing updates, back substitution, candidate
 // poses), the bordered band of free intrinsics k_chol_border, and the window / global Cholesky for other shapes.
 #include "ba_lm.h"
+#include "ba_tile.h"
 
 namespace sg {
 
@@ -17,15 +18,6 @@ __device__ __forceinline__ double& Wn(double* win, int i, int j) {
   return win[(i & (kCholWS - 1)) * kCholLd + (j & (kCholWS - 1))];
 }
 
-// 1/sqrt(x): v_rsq_f64 and one Newton step in FMA form, y (1.5 - x y^2 / 2) (relative error ~1e-14, far
-// inside the solver's parity tolerances; the pivot chain of the panel factorisation runs through it).
-__device__ __forceinline__ double rsq_nr1(double x) {
-  const double y = __builtin_amdgcn_rsq(x);
-  const double h = 0.5 * x;
-  const double e = fma(-(h * y), y, 0.5);
-  return fma(y, e, y);
-}
-
 // Wave-uniform broadcast of lane `l`'s double (v_readlane pair: no LDS round trip).
 __device__ __forceinline__ double readlane_d(double v, int l) {
   const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
@@ -33,13 +25,6 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
   return __hiloint2double(hi, lo);
 }
 
-// The lane id through an opaque move: comparisons against it inside a loop are not hoisted out as
-// loop-invariant 64-bit lane masks (which would otherwise pile up in SGPRs and spill).
-__device__ __forceinline__ int opaque_lane() {
-  int v = __lane_id();
-  asm volatile("v_mov_b32 %0, %0" : "+v"(v));
-  return v;
-}
 
 
 // Unblocked factorisation of the w x w diagonal block held column-per-lane (lanes 0..w-1, col[r] =
@@ -893,7 +878,6 @@ __global__ __launch_bounds__(kCholThreads) void k_cholesky_global(Dev d, const i
 //     prefetched four rows ahead), one barrier per tile row, every wave sums the partials in the same order.
 // Requires a band of at most 8 tiles per tile row (the sliding window's co-visibility band at the configured
 // window sizes); wider bands take k_cholesky_global.
-constexpr int kTLd = 17;                       // LDS pitch of a 16 x 16 tile
 struct TileShared {
   double Zs[4][16 * kTLd];     // Z_K = U_KK^-T (lower triangular), row-major; 4 deep: the previous owner
   double zK[4][16];            // reads Z_K one phase late.  z_K = Z_K y_K
@@ -970,76 +954,6 @@ __device__ __forceinline__ f64x4 tile_load(const double* __restrict__ S, int I, 
   return t;
 }
 
-
-// Factor one 16x16 diagonal tile D (upper triangle, pitch kTLd) with the identity (lanes 16-31) and the rhs
-// (lane 32) as augmented columns; lanes 0-15 hold the columns of D.  Right-looking, two pivots per LDS
-// broadcast (every lane derives pivot row j+1 after pivot j itself).  On return lanes 16-31 hold the columns
-// of Z = U^-T and lane 32 holds z = U^-T y.  Returns true on a non-positive pivot.
-__device__ __forceinline__ bool tile_factor(const double* D, const double* Yk, const double* Id, double* prw,
-                                            double (&ca)[16]) {
-  const int lane = opaque_lane();
-  const int c = lane & 15;
-  const bool isy = lane == 32;
-  // D arrives with its lower triangle zeroed and the identity is a constant LDS tile, so every lane just
-  // loads its column (no per-element masking on the critical path)
-  const double* b0 = isy ? Yk : ((lane >= 16 && lane < 32) ? Id + c : D + c);
-  const int rs = isy ? 1 : kTLd;
-#pragma unroll
-  for (int r = 0; r < kCholNb; ++r) ca[r] = b0[r * rs];
-  bool bad = false;
-  double u0[kCholNb], u1[kCholNb];
-  double* prw2 = prw + kCholNb;
-  if (lane < kCholNb) {
-    prw[lane] = ca[0];
-    prw2[lane] = ca[1];
-  }
-#pragma unroll
-  for (int r = 0; r < kCholNb; ++r) {
-    u0[r] = prw[r];
-    u1[r] = prw2[r];
-  }
-#pragma unroll
-  for (int j = 0; j < kCholNb; j += 2) {
-    const double p0 = u0[j];
-    bad |= !(p0 > 0.0);
-    const double i0 = rsq_nr1(p0);
-    const double r0 = i0 * i0;
-    const double w1 = u0[j + 1] * r0;
-    double v1[kCholNb];
-#pragma unroll
-    for (int r = j + 1; r < kCholNb; ++r) v1[r] = fma(-w1, u0[r], u1[r]);
-    const double p1 = v1[j + 1];
-    bad |= !(p1 > 0.0);
-    const double i1 = rsq_nr1(p1);
-    const double r1 = i1 * i1;
-    const double aj = ca[j];
-    const double t0 = aj * r0;
-    ca[j] = aj * i0;
-    const double aj1 = fma(-u0[j + 1], t0, ca[j + 1]);
-    const double t1 = aj1 * r1;
-    ca[j + 1] = aj1 * i1;
-    if (j + 2 < kCholNb) {
-      ca[j + 2] = fma(-v1[j + 2], t1, fma(-u0[j + 2], t0, ca[j + 2]));
-      ca[j + 3] = fma(-v1[j + 3], t1, fma(-u0[j + 3], t0, ca[j + 3]));
-      if (lane < kCholNb) {
-        prw[lane] = ca[j + 2];
-        prw2[lane] = ca[j + 3];
-      }
-    }
-#pragma unroll
-    for (int r = j + 4; r < kCholNb; ++r) ca[r] = fma(-v1[r], t1, fma(-u0[r], t0, ca[r]));
-#pragma unroll
-    for (int r = j; r < kCholNb; ++r) asm volatile("" : "+v"(ca[r]));
-    if (j + 2 < kCholNb) {
-#pragma unroll
-      for (int r = j + 2; r < kCholNb; ++r) {
-        u0[r] = prw[r];
-        u1[r] = prw2[r];
-      }
-    }
-  }
-  return bad;
-}
 
 // The owner of the next diagonal: D (acc layout) and its rhs partials -> Z, z and Z^T z of tile row K.
 __device__ __forceinline__ bool tile_diag(const f64x4& D, double ypart, TileShared& sh, double* zp, int K,
@@ -1416,6 +1330,22 @@ __device__ __forceinline__ int bs_src_lane(int li) {
   return (((q >> 1) & 1) | ((q & 1) << 1)) + 16 * (li & 3);
 }
 
+// The first owner's posts when k_S_reduce has factored D_0 (flags bit 4): Z_0 (acc layout: rows lk + 4q, column
+// li) into the LDS ring and z_0 = Z_0 y_0 (row sums by bs_rowsum; row r's total from one fixed lane).
+__device__ __forceinline__ void tile_diag_pre(const f64x4& Z, double ypart, TileShared& sh, int li, int lk) {
+  double* Zs = sh.Zs[0];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) Zs[(lk + 4 * q) * kTLd + li] = Z[q];
+  const double y = sum_rows4(ypart);   // y_0[li] in every lane
+  double p[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) p[q] = Z[q] * y;
+  int lb = li;
+  asm volatile("" : "+v"(lb));
+  const double tot = bs_rowsum(p, (lb & 1) != 0, (lb & 2) != 0);
+  if (li < 4) sh.zK[0][lk + 4 * (2 * (li & 1) + ((li >> 1) & 1))] = tot;
+}
+
 // Back substitution of tile rows Khi .. Klo in one wave:  x_K = z'_K - sum_{d=1..7} W_{K,K+d} x_{K+d}, with no
 // LDS round trip on the row-to-row chain.  Lane (li, lk) holds rows lk + 4q, column li of each W tile (acc
 // layout) and x_{K+d}[li] in registers (xw[d-1]; zero past the last row, and W tiles outside the band are
@@ -1655,7 +1585,17 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
   // D_0 (no updates: the wave that gets column 0 factors it first), its rhs and the LmState flag do not depend on
   // the column mapping: every wave's loads of them go out before the mapping's barrier, an LDS-only one, so they
   // stay in flight across it
-  const f64x4 D0 = tile_load(d.S, 0, 0, li, lk, ts);
+  // flags bit 4: k_S_reduce has factored D_0 (the top workgroup loads Z_0 instead)
+  const bool zpre_in = (flags & 16) != 0 && !bottom;
+  f64x4 D0;
+  bool zbad = false;
+  if (zpre_in) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) D0[q] = d.zpre[(lk + 4 * q) * 16 + li];
+    zbad = d.zpre[256] != 0.0;
+  } else {
+    D0 = tile_load(d.S, 0, 0, li, lk, ts);
+  }
   double y0;
   {
     const int sj0 = ts.rev ? ts.np - 1 - li : li, ld = ts.ld;
@@ -1713,7 +1653,12 @@ __global__ __launch_bounds__(kTileThreads) void k_chol_tiles(Dev d, const int32_
     }
     if (done) return;
     if (col == 0) {
-      bad |= tile_diag(D0, y0, sh, zp, 0, lane, li, lk);
+      if (zpre_in) {
+        tile_diag_pre(D0, y0, sh, li, lk);
+        bad |= zbad;
+      } else {
+        bad |= tile_diag(D0, y0, sh, zp, 0, lane, li, lk);
+      }
       tile_zp(sh, zp, 0, lane, zg);   // (the wave's own LDS writes: visible to it in order)
     }
     else if (cand_lds)   // the seven waves that wait at the first barrier

@@ -223,6 +223,7 @@ struct Dev {
   double* chunk_scal;            // [npu][kNScal] k_point_update scalars (per work unit)
   double* cam_wide[2];           // [NB][27] (wide chunks, global atomics)
   double* S_wide;                // [n][n]   (wide chunks, global atomics)
+  double* zpre;                  // [257] Z_0 = U_00^-T of S's first diagonal tile, factored by k_S_reduce (+ failure)
   // exchange buffers (all-reduced across landmark shards)
   double* xchg_cam;              // [NB*27 + kXNum + nranks]: camera blocks, scalars, per-rank max |g| slots
                                  // (summed over the shards by the camera-block all-reduce)

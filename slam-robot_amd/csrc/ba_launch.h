@@ -61,7 +61,7 @@ void LaunchReprojectMapK(int M, int nb, hipStream_t s, const double* k, const do
 void LaunchCamFinalizeK(hipStream_t s, const Dev& d, int mode, int decide);
 // fin: 0 none; 1 one workgroup runs k_cam_finalize's pass (one rank, mode 0); 2 its mode 1 (merged shards)
 void LaunchSchurK(int nseg, int nwide, int fin, hipStream_t s, const Dev& d);
-void LaunchSReduceK(int grid, hipStream_t s, const Dev& d, int amode);
+void LaunchSReduceK(int grid, hipStream_t s, const Dev& d, int amode, int pre = 0);
 void LaunchSPackK(dim3 grid, hipStream_t s, double* S, int n, const int32_t* panel_jend, const int32_t* off,
                   int npanel, double* Spk, int dir);
 // the merged chain's unpack + k_cam_finalize mode 2 (grid: LaunchSPackK's; one bookkeeping workgroup is added)

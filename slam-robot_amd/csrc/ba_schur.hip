@@ -3,6 +3,7 @@
 // v_mfma_f64_16x16x4f64 per point and tile of S), k_schur_wide, the fixed-order reduce k_S_reduce, the landmark
 // shards' band packing k_S_pack, and the camera finalize pass k_cam_finalize (FrameDistance, slam.cpp:86-105).
 #include "ba_lm.h"
+#include "ba_tile.h"
 
 namespace sg {
 
@@ -657,7 +658,33 @@ __global__ __launch_bounds__(kSchurThreads) void k_schur_wide(Dev d) {
 // 1 blockdiag(U) of the summed camera blocks + FrameDistance + damping (one rank; rank 0 of shards in the
 // first iteration); 2 this rank's own camera blocks, the FrameDistance terms on rank 0, no damping (landmark
 // shards after the first iteration: summed with S in one exchange, k_cam_finalize mode 2 adds the damping).
-__global__ __launch_bounds__(256) void k_S_reduce(Dev d, int amode) {
+// One element of a band tile of S: the four wave sums of its partials (in wave order), the wide-point
+// accumulator and, on the assembling rank, the camera-only terms; written to S and returned.
+__device__ __forceinline__ double s_tile_elem(const Dev& d, const double (&wsum)[4][256], int tid, size_t gi,
+                                              double e_acc, int amode, int I, int Jb, int a, int c, double e_u,
+                                              double e_fd, double e_si, double e_sj, double e_dg, double e_x,
+                                              double radius) {
+  double t = ((wsum[0][tid] + wsum[1][tid]) + wsum[2][tid]) + wsum[3][tid];
+  t += e_acc;
+  if (d.nwide) d.S_wide[gi] = 0.0;
+  if (amode != 0) {   // assembly_term, from the prefetched operands
+    double v;
+    if (I == Jb) {
+      v = (e_u + e_fd) * (e_si * e_sj);
+      if (a == c) v += e_dg / radius;
+    } else {
+      v = e_x * e_si * e_sj;
+    }
+    t += v;
+  }
+  d.S[gi] = t;
+  return t;
+}
+
+// pre: the workgroup of tile (0, 0) also factors it (tile_factor, as k_chol_tiles' first owner would) into
+// d.zpre: Z_0 = U_00^-T row-major [16][16], then a failure marker; k_chol_tiles (flags bit 4) starts from it, so
+// the 16-pivot factor of D_0 is off the Cholesky's opening path (one rank, no free intrinsics: S is final here).
+__global__ __launch_bounds__(256) void k_S_reduce(Dev d, int amode, int pre) {
   // LmState is read beside the first work-list loads, not ahead of them: the done test comes after the
   // partial walk (a finished solve's trailing launches walk once more; every other launch saves a round trip)
   const LmState* st = d.st;
@@ -722,26 +749,38 @@ __global__ __launch_bounds__(256) void k_S_reduce(Dev d, int amode) {
 #pragma unroll
     for (int m = 0; m < 4; ++m) wsum[part][lane + 64 * m] = s[m];
     __syncthreads();
+    if (pre && rc == 0) {   // tile (0, 0), factored here (a workgroup-uniform branch: its barrier is safe)
+      __shared__ double Dt[16 * kTLd], It[16 * kTLd], Yt[16], prt[2 * kCholNb];
+      double t = 0.0;
+      if (!done && live && up) t = s_tile_elem(d, wsum, tid, gi, e_acc, amode, I, Jb, a, c, e_u, e_fd, e_si, e_sj,
+                                               e_dg, e_x, radius);
+      if (!done && live && !up) {
+        d.S[gi] = 0.0;
+        if (d.nwide) d.S_wide[gi] = 0.0;
+      }
+      // as k_chol_tiles' tile_load pads past the system: 1 on the diagonal, 0 elsewhere
+      const int ti = tid >> 4, tj = tid & 15;
+      Dt[ti * kTLd + tj] = live ? (up ? t : 0.0) : (ti == tj ? 1.0 : 0.0);
+      It[ti * kTLd + tj] = ti == tj ? 1.0 : 0.0;
+      if (tid < 16) Yt[tid] = 0.0;
+      __syncthreads();
+      if (!done && tid < 64) {
+        double ca[kCholNb];
+        const bool bad = tile_factor(Dt, Yt, It, prt, ca);
+        if (lane >= 16 && lane < 32)
+#pragma unroll
+          for (int r = 0; r < kCholNb; ++r) d.zpre[r * 16 + (lane - 16)] = ca[r];
+        if (lane == 0) d.zpre[256] = bad ? 1.0 : 0.0;
+      }
+      return;
+    }
     if (done || !live) return;
     if (!up) {
       d.S[gi] = 0.0;
       if (d.nwide) d.S_wide[gi] = 0.0;   // schur_pair_add also adds a diagonal block's lower half: keep it clean
       return;
     }
-    double t = ((wsum[0][tid] + wsum[1][tid]) + wsum[2][tid]) + wsum[3][tid];
-    t += e_acc;
-    if (d.nwide) d.S_wide[gi] = 0.0;
-    if (amode != 0) {   // assembly_term, from the prefetched operands
-      double v;
-      if (I == Jb) {
-        v = (e_u + e_fd) * (e_si * e_sj);
-        if (a == c) v += e_dg / radius;
-      } else {
-        v = e_x * e_si * e_sj;
-      }
-      t += v;
-    }
-    d.S[gi] = t;
+    s_tile_elem(d, wsum, tid, gi, e_acc, amode, I, Jb, a, c, e_u, e_fd, e_si, e_sj, e_dg, e_x, radius);
     return;
   }
   // rhs block I: one wave per 64-entry chunk of its partial list (in list order), lanes 0..5
@@ -871,8 +910,8 @@ void LaunchSUnpackFinK(dim3 grid, hipStream_t s, const Dev& d, const int32_t* pa
   hipLaunchKernelGGL(k_S_unpack_fin, dim3(grid.x + 1, grid.y), dim3(256), 0, s, d, panel_jend, off, npanel, Spk);
 }
 
-void LaunchSReduceK(int grid, hipStream_t s, const Dev& d, int amode) {
-  hipLaunchKernelGGL(k_S_reduce, dim3(grid), dim3(256), 0, s, d, amode);
+void LaunchSReduceK(int grid, hipStream_t s, const Dev& d, int amode, int pre) {
+  hipLaunchKernelGGL(k_S_reduce, dim3(grid), dim3(256), 0, s, d, amode, pre);
 }
 
 void LaunchSPackK(dim3 grid, hipStream_t s, double* S, int n, const int32_t* panel_jend, const int32_t* off,

@@ -89,6 +89,8 @@ class BaSolver {
   int s_lstride_ = 256, r_lstride_ = 256;   // k_S_reduce's padded list rows (Dev::s_lstride / r_lstride)
   // tests only: force the dissected Cholesky's separator wait to time out (k_chol_tiles flags bit 2)
   bool chol_force_tmo_ = getenv("SG_CHOL_FORCE_TIMEOUT") && atoi(getenv("SG_CHOL_FORCE_TIMEOUT")) != 0;
+  // SG_CHOL_ZPRE=0: k_chol_tiles factors D_0 itself instead of starting from k_S_reduce's Z_0 (A/B, tests)
+  bool chol_zpre_off_ = getenv("SG_CHOL_ZPRE") && atoi(getenv("SG_CHOL_ZPRE")) == 0;
   bool pack_force_ = getenv("SG_PACK_S") != nullptr;   // pack/unpack S on one rank too (tests the path)
   // speculative linearization (k_update_lin: the candidate pass linearizes at the candidate; k_linearize runs
   // only in a solve's first iteration); SG_SPEC=0: k_point_update + k_linearize every iteration
@@ -150,7 +152,7 @@ class BaSolver {
   DBuf<LmState> st_;
   DBuf<double> k_, q_, t_, X_, obs_pt_, J_, V_, g_, scale_p_, diag_p_, Vinv_, tp_, scale_c_, diag_c_, camdiag_,
       camg_, cam_slab_, S_slab_, chunk_scal_, cam_wide_, S_wide_, xchg_cam_, S_, rhs_, xchg_upd_,
-      xchg_chol_, work_, fd_r_, fd_J_, fd_D_, fd_X_, red_;
+      xchg_chol_, work_, fd_r_, fd_J_, fd_D_, fd_X_, red_, zpre_;
   DBuf<int32_t> frame_cam_, frame_block_, poff_, obs_frame_, fd_a_, fd_b_, fd_boff_, fd_bidx_, cam_loff_,
       cam_lidx_, s_loff_, s_lidx_, r_loff_, r_lidx_, mobs_frame_, mobs_point_, mframe_cam_;
   DBuf<uint8_t> rot_free_, trans_free_, pfree_, obs_fixed_;

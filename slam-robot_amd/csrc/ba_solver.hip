@@ -955,6 +955,7 @@ void BaSolver::Load(const sg_problem& p) {
   lap("flush");
   cam_wide_.Resize(2 * (size_t)std::max(NB_, 1) * kCamV);
   S_wide_.Resize(nn * nn);
+  zpre_.Resize(257);
   xchg_cam_.Resize(3 * ((size_t)NB_ * kCamV + kXNum + nranks()));   // summed | this rank's | candidate
   S_.Resize(nn * nn + nn + 2);   // S, then the rhs partial xc (one all-reduce covers both), then {0, 1}
   rhs_.Resize(nn);
@@ -1258,6 +1259,7 @@ Dev BaSolver::MakeDev() {
   d.S_slab = S_slab_.ptr;
   d.chunk_scal = chunk_scal_.ptr;
   d.S_wide = S_wide_.ptr;
+  d.zpre = zpre_.ptr;
   d.xchg_cam = xchg_cam_.ptr;
   d.xcam_loc = xchg_cam_.ptr + (size_t)NB_ * kCamV + kXNum + nranks();
   d.xchg_cand = xchg_cam_.ptr + 2 * ((size_t)NB_ * kCamV + kXNum + nranks());
@@ -1517,7 +1519,12 @@ void BaSolver::EnqueueIterations(int n) {
     TimedLaunchEnd(kKSchur);
     TimedLaunchBegin(kKSReduce);
     const int nwv = nstile_ + NB_;
-    LaunchSReduceK(std::max(nwv, 1), stream_, d, merged ? 2 : (d.assemble ? 1 : 0));
+    // S is final after k_S_reduce (one rank, no free intrinsics, no exchange): it also factors the first
+    // diagonal tile for k_chol_tiles (flags bit 4)
+    const int samode = merged ? 2 : (d.assemble ? 1 : 0);
+    const bool zpre = chol_tiles_ && !chol_border_ && nk_ == 0 && samode == 1 && !(multi_x || pack_force_ || merged) &&
+                      !chol_zpre_off_;
+    LaunchSReduceK(std::max(nwv, 1), stream_, d, samode, zpre ? 1 : 0);
     TimedLaunchEnd(kKSReduce);
     if (nk_) {
       LaunchIntrSchurK(stream_, d, n_, nk_, NB_, ncam_, P_, intr_nsl_);
@@ -1547,7 +1554,7 @@ void BaSolver::EnqueueIterations(int n) {
     TimedLaunchBegin(kKChol);
     if (chol_tiles_)
       LaunchCholTiles(d.stamps != nullptr, dim3(chol_nd_ > 0 ? 2 : 1), d,
-                      (chol_cand_lds_ ? 2 : 0) | (chol_force_tmo_ ? 4 : 0));
+                      (chol_cand_lds_ ? 2 : 0) | (chol_force_tmo_ ? 4 : 0) | (zpre ? 16 : 0));
     else if (chol_window_)
       LaunchCholWindowK(d.stamps != nullptr, stream_, d, (const int32_t*)work_i_.ptr, rdg_.ptr);
     else

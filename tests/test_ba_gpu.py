@@ -373,7 +373,9 @@ def test_dissected_band_matches_one_workgroup(gpu_lib, monkeypatch, frames, poin
     4).  Against the one-workgroup factorisation (SG_CHOL_SPLIT=0) the solve must be the same up to rounding
     (the separator sums in another order): same steps, cost rel 1e-12, poses 1e-10 — with the fixed 7-row
     separator (SG_CHOL_SEP=7: n = 204 -> 13 tile rows, 2 bottom; 228 -> 15, 3; C2's 288 -> 18, 4) and with the
-    separator sized to the band (round 6: C2's rows are 6-7 tiles wide, so 5 rows and 6 bottom)."""
+    separator sized to the band (round 6: C2's rows are 6-7 tiles wide, so 5 rows and 6 bottom).  By default
+    k_S_reduce factors the first diagonal tile (Z_0) for k_chol_tiles; "own_d0" (SG_CHOL_ZPRE=0) has the Cholesky
+    factor it itself, as before round 6 (z_0 then comes from the augmented column, not Z_0 y_0: rounding only)."""
     if points is None:
         m = make_config("C2")
     else:
@@ -381,9 +383,10 @@ def test_dissected_band_matches_one_workgroup(gpu_lib, monkeypatch, frames, poin
     pa = ba.problem_from_map_frames(m, m.num_frames - 2, m.num_frames, 2.0)
     nt = (6 * (m.num_frames - 2) + 15) // 16
     out = []
-    for mode in ("one", "sep7", "adaptive"):
+    for mode in ("one", "sep7", "adaptive", "own_d0"):
         monkeypatch.setenv("SG_CHOL_SPLIT", "0" if mode == "one" else "1")
         monkeypatch.setenv("SG_CHOL_SEP", "7" if mode == "sep7" else "0")
+        monkeypatch.setenv("SG_CHOL_ZPRE", "0" if mode == "own_d0" else "1")
         p = pa.copy()
         g = ba.BundleAdjuster()
         g.load(p)
