@@ -229,6 +229,76 @@ __device__ __forceinline__ void chol_candidates_lds(const Dev& d, const double* 
   __shared__ double red[4 * NT / 64];
   const int tid = threadIdx.x;
   const int nxt = cur ^ 1;
+  if (d.F <= 64 && d.D <= 64) {
+    // one wave (C2: 50 frames, 49 FrameDistance pairs): a frame and a pair per lane, the sums by the wave's DPP
+    // butterfly — no workgroup barrier and no LDS reduction at the end of the launch
+    if (tid >= 64) return;
+    double step2 = 0.0, candx2 = 0.0, model = 0.0, candcost = 0.0;
+    const int f = tid;
+    if (f < d.F) {
+      const double* q = c.q + 4 * f;
+      const double* t = c.t + 3 * f;
+      const int b = c.fb[f];
+      const int fl = c.fl[f];
+      double qq[4] = {q[0], q[1], q[2], q[3]}, tt[3] = {t[0], t[1], t[2]};
+      if (b >= 0) {
+        if (fl & 1) {
+          double dl[3];
+          for (int a = 0; a < 3; ++a) dl[a] = -y[6 * b + a] * c.sc[6 * b + a];
+          QuatPlus(q, dl, qq);
+          for (int a = 0; a < 4; ++a) {
+            step2 += (qq[a] - q[a]) * (qq[a] - q[a]);
+            candx2 += qq[a] * qq[a];
+          }
+        }
+        if (fl & 2) {
+          for (int a = 0; a < 3; ++a) {
+            tt[a] = t[a] - y[6 * b + 3 + a] * c.sc[6 * b + 3 + a];
+            step2 += (tt[a] - t[a]) * (tt[a] - t[a]);
+            candx2 += tt[a] * tt[a];
+          }
+        }
+      }
+      for (int a = 0; a < 4; ++a) d.q[nxt][4 * f + a] = qq[a];
+      for (int a = 0; a < 3; ++a) {
+        d.t[nxt][3 * f + a] = tt[a];
+        c.tn[3 * f + a] = tt[a];
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the wave's own LDS writes, in order, before its reads
+    const int dd = tid;
+    if (dd < d.D) {
+      const int fa = c.fa[dd], fb = c.fbb[dd];
+      const int ba = c.ba[dd], bb = c.bb[dd];
+      const double* Jd = c.J + 6 * dd;
+      double m = 0.0;
+      for (int j = 0; j < 3; ++j) {
+        if (ba >= 0) m += Jd[j] * c.sc[6 * ba + 3 + j] * (-y[6 * ba + 3 + j]);
+        if (bb >= 0) m += Jd[3 + j] * c.sc[6 * bb + 3 + j] * (-y[6 * bb + 3 + j]);
+      }
+      model = -m * (c.r[dd] + 0.5 * m);
+      const double* ta = c.tn + 3 * fa;
+      const double* tb = c.tn + 3 * fb;
+      const double e0 = ta[0] - tb[0], e1 = ta[1] - tb[1], e2 = ta[2] - tb[2];
+      const double r = 0.1 * (sqrt(e0 * e0 + e1 * e1 + e2 * e2) - d.fd_target);
+      double rho0, rho1;
+      Cauchy(r * r, d.fd_b2, d.fd_inv_b2, &rho0, &rho1);
+      candcost = 0.5 * rho0;
+    }
+    step2 = wave_sum_full(step2);
+    candx2 = wave_sum_full(candx2);
+    model = wave_sum_full(model);
+    candcost = wave_sum_full(candcost);
+    if (tid == 0) {
+      d.xchg_chol[kCStep2] = step2;
+      d.xchg_chol[kCCandX2] = candx2;
+      d.xchg_chol[kCModel] = model;
+      d.xchg_chol[kCCandCost] = candcost;
+      d.xchg_chol[kCFail] = fail ? 1.0 : 0.0;
+      d.xchg_chol[kCTimeout] = tmo ? 1.0 : 0.0;
+    }
+    return;
+  }
   double step2 = 0.0, candx2 = 0.0, model = 0.0, candcost = 0.0;
   for (int f = tid; f < d.F; f += NT) {
     const double* q = c.q + 4 * f;
