@@ -193,31 +193,38 @@ __device__ __forceinline__ void chol_candidates(const Dev& d, const double* y, i
 // stores.  Same arithmetic and summation order as chol_candidates.
 struct CandLds {
   double *q, *t, *sc, *J, *r, *tn;
-  int *fb, *fl, *fa, *fbb, *ba, *bb;
+  int *fb, *fl, *fa, *fbb;   // (a pair's blocks are read through fb[fa], fb[fbb]: no dependent global load)
   static size_t bytes(int F, int D, int n) {
-    return (size_t)(7 * F + n + 7 * D + 3 * F) * sizeof(double) + (size_t)(2 * F + 4 * D) * sizeof(int);
+    return (size_t)(7 * F + n + 7 * D + 3 * F) * sizeof(double) + (size_t)(2 * F + 2 * D) * sizeof(int);
   }
   __device__ void carve(double* base, int F, int D, int n) {
     q = base; t = q + 4 * F; sc = t + 3 * F; J = sc + n; r = J + 6 * D; tn = r + D;
-    fb = reinterpret_cast<int*>(tn + 3 * F); fl = fb + F; fa = fl + F; fbb = fa + D; ba = fbb + D; bb = ba + D;
+    fb = reinterpret_cast<int*>(tn + 3 * F); fl = fb + F; fa = fl + F; fbb = fa + D;
   }
 };
 
+// Threads i0, i0 + ni, ... stage the candidate pass's operands.  With five waves or more the three lists load
+// side by side: the frames on the first wave, the FrameDistance pairs on the second, the column scales on the rest.
 __device__ __forceinline__ void cand_prefetch(const Dev& d, const CandLds& c, int cur, int i0, int ni) {
-  for (int f = i0; f < d.F; f += ni) {
-    const int b = d.frame_block[f];
-    c.fb[f] = b;
+  int f0 = i0, fs = ni, e0 = i0, es = ni, s0 = i0, ss = ni;
+  if (ni >= 5 * 64) {
+    const int w = i0 >> 6, l = i0 & 63;
+    f0 = w == 0 ? l : d.F;
+    e0 = w == 1 ? l : d.D;
+    s0 = w >= 2 ? i0 - 128 : d.n;
+    fs = es = 64;
+    ss = ni - 128;
+  }
+  for (int f = f0; f < d.F; f += fs) {
+    c.fb[f] = d.frame_block[f];
     c.fl[f] = (d.rot_free[f] ? 1 : 0) | (d.trans_free[f] ? 2 : 0);
     for (int a = 0; a < 4; ++a) c.q[4 * f + a] = d.q[cur][4 * f + a];
     for (int a = 0; a < 3; ++a) c.t[3 * f + a] = d.t[cur][3 * f + a];
   }
-  for (int i = i0; i < d.n; i += ni) c.sc[i] = d.scale_c[i];
-  for (int e = i0; e < d.D; e += ni) {
-    const int fa = d.fd_a[e], fb = d.fd_b[e];
-    c.fa[e] = fa;
-    c.fbb[e] = fb;
-    c.ba[e] = d.frame_block[fa];
-    c.bb[e] = d.frame_block[fb];
+  for (int i = s0; i < d.n; i += ss) c.sc[i] = d.scale_c[i];
+  for (int e = e0; e < d.D; e += es) {
+    c.fa[e] = d.fd_a[e];
+    c.fbb[e] = d.fd_b[e];
     for (int j = 0; j < 6; ++j) c.J[6 * e + j] = d.fd_J[6 * e + j];
     c.r[e] = d.fd_r[e];
   }
@@ -269,7 +276,7 @@ __device__ __forceinline__ void chol_candidates_lds(const Dev& d, const double* 
     const int dd = tid;
     if (dd < d.D) {
       const int fa = c.fa[dd], fb = c.fbb[dd];
-      const int ba = c.ba[dd], bb = c.bb[dd];
+      const int ba = c.fb[fa], bb = c.fb[fb];
       const double* Jd = c.J + 6 * dd;
       double m = 0.0;
       for (int j = 0; j < 3; ++j) {
@@ -335,7 +342,7 @@ __device__ __forceinline__ void chol_candidates_lds(const Dev& d, const double* 
   __syncthreads();
   for (int dd = tid; dd < d.D; dd += NT) {
     const int fa = c.fa[dd], fb = c.fbb[dd];
-    const int ba = c.ba[dd], bb = c.bb[dd];
+    const int ba = c.fb[fa], bb = c.fb[fb];
     const double* Jd = c.J + 6 * dd;
     double m = 0.0;
     for (int j = 0; j < 3; ++j) {
