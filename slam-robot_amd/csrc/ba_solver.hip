@@ -1519,11 +1519,10 @@ void BaSolver::EnqueueIterations(int n) {
     TimedLaunchEnd(kKSchur);
     TimedLaunchBegin(kKSReduce);
     const int nwv = nstile_ + NB_;
-    // S is final after k_S_reduce (one rank, no free intrinsics, no exchange): it also factors the first
-    // diagonal tile for k_chol_tiles (flags bit 4)
+    // S is final after k_S_reduce (one rank, no free intrinsics, no merged damping; a forced pack / unpack on one
+    // rank is a copy): it also factors the first diagonal tile for k_chol_tiles (flags bit 4)
     const int samode = merged ? 2 : (d.assemble ? 1 : 0);
-    const bool zpre = chol_tiles_ && !chol_border_ && nk_ == 0 && samode == 1 && !(multi_x || pack_force_ || merged) &&
-                      !chol_zpre_off_;
+    const bool zpre = chol_tiles_ && !chol_border_ && nk_ == 0 && samode == 1 && !(multi_x || merged) && !chol_zpre_off_;
     LaunchSReduceK(std::max(nwv, 1), stream_, d, samode, zpre ? 1 : 0);
     TimedLaunchEnd(kKSReduce);
     if (nk_) {
