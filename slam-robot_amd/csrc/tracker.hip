@@ -429,6 +429,7 @@ struct TStamp {
 
 struct TrackCtx {
   int W, len, max_it;
+  float lenf, rlen;    // len as a float and its correctly rounded reciprocal (div_const)
   int nk;              // patch pixels per lane actually used: ceil(len / 64) <= kNP
   float threshold;
   int lane;
@@ -458,6 +459,22 @@ __device__ __forceinline__ void get_patch_ctx(const TrackCtx& c, const LevelDev&
   q = wave_tree_sum(q);
   t.mean = s / c.len;
   t.sumsq = q / c.len;
+}
+
+// Division by a constant divisor without the division sequence (Markstein): q0 = x r with r = RN(1 / b), the
+// residual x - q0 b exact by one FMA, one correction q0 + (x - q0 b) r: the correctly rounded quotient x / b for
+// every finite, normal x when r is the correctly rounded reciprocal (tests/test_const_division.py checks it on
+// random operands for the tracker's divisors; infinities pass through as x r).  Three instructions instead of a
+// correctly rounded division's eleven dependent ones, the same bits.
+__device__ __forceinline__ double div_const(double x, double b, double r) {
+  const double q0 = x * r;
+  const double q = fma(fma(-q0, b, x), r, q0);
+  return isinf(x) ? q0 : q;
+}
+__device__ __forceinline__ float div_const(float x, float b, float r) {
+  const float q0 = x * r;
+  const float q = fmaf(fmaf(-q0, b, x), r, q0);
+  return isinf(x) ? q0 : q;
 }
 
 // BruteHessian (hessian.h:147-172): the six probes sampled together, their sums reduced in batches.
@@ -594,7 +611,7 @@ __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev&
     const int r = min(c.lane, 5);
     const float psl = r == 0 ? ps[0] : r == 1 ? ps[1] : r == 2 ? ps[2] : r == 3 ? ps[3] : r == 4 ? ps[4] : ps[5];
     const float pql = r == 0 ? pq[0] : r == 1 ? pq[1] : r == 2 ? pq[2] : r == 3 ? pq[3] : r == 4 ? pq[4] : pq[5];
-    const float mean = psl / c.len, sumsq = pql / c.len;
+    const float mean = div_const(psl, c.lenf, c.rlen), sumsq = div_const(pql, c.lenf, c.rlen);   // psl / len, pql / len
     const float alpha = sqrtf(tp.sumsq / sumsq);
     const float beta = tp.mean - alpha * mean;
 #pragma unroll
@@ -638,9 +655,10 @@ __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev&
   const double qc = e == 2 || e == 3 ? sad0 : e == 4 ? sadp1x : sadp1y;
   const double qd = e == 2 ? sadn1x : e == 3 ? sadn1y : sad0;
   const double num = e < 2 ? 0.5 * (qa - qb) : (qa - qb);
-  const double q1 = num / hh;
-  const double q2 = (qc - qd) / hh;
-  const float res = (float)(e < 2 ? q1 : (q1 - q2) / hh);
+  constexpr double rh = 50.0;   // RN(1 / 0.02): the quotients by h as div_const (the same bits as "/ hh")
+  const double q1 = div_const(num, hh, rh);
+  const double q2 = div_const(qc - qd, hh, rh);
+  const float res = (float)(e < 2 ? q1 : div_const(q1 - q2, hh, rh));
   *mdx = readlane_f(res, 0);
   *mdy = readlane_f(res, 1);
   *mdxx = readlane_f(res, 2);
@@ -814,6 +832,8 @@ __global__ __launch_bounds__(64 * kTrackWaves) void k_track_fb(const LevelDev* _
   c.ts = &tst;
   c.W = prm.window;
   c.len = prm.window * prm.window;
+  c.lenf = (float)c.len;
+  c.rlen = 1.0f / c.lenf;
   c.nk = (c.len + 63) / 64;
   c.max_it = prm.max_iterations;
   c.threshold = prm.threshold;
@@ -871,6 +891,8 @@ __device__ __forceinline__ void init_ctx(TrackCtx& c, const TrackParams& prm, in
   // (the one-directional kernels are not stamped: c.ts points at an off TStamp set by the caller)
   c.W = prm.window;
   c.len = prm.window * prm.window;
+  c.lenf = (float)c.len;
+  c.rlen = 1.0f / c.lenf;
   c.nk = (c.len + 63) / 64;
   c.max_it = prm.max_iterations;
   c.threshold = prm.threshold;
