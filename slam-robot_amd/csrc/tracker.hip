@@ -588,6 +588,11 @@ __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev&
     }
   }
   c.ts->mark(1);
+  // The twelve tree sums (wave_tree_sum's order for each): the four DPP stages per value, then the two row stages
+  // for a probe's pair (ps, pq) at once — one row swap puts ps's rows 0 + 1 / 2 + 3 in rows 0 / 2 and pq's in rows
+  // 1 / 3 (the same additions, so the same bits), and the last swap finishes both: ps's total in rows 0 and 2,
+  // pq's in rows 1 and 3.  Half the row-swap instructions of twelve separate sums.
+  float tot[6];
   {
     float sums[12];
 #pragma unroll
@@ -595,11 +600,24 @@ __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev&
       sums[r] = ps[r];
       sums[6 + r] = pq[r];
     }
-    wave_tree_sums<12>(sums);
+#pragma unroll
+    for (int r = 0; r < 12; ++r) sums[r] = sums[r] + dpp_f<0xB1>(sums[r]);
+#pragma unroll
+    for (int r = 0; r < 12; ++r) sums[r] = sums[r] + dpp_f<0x4E>(sums[r]);
+#pragma unroll
+    for (int r = 0; r < 12; ++r) sums[r] = sums[r] + dpp_f<0x141>(sums[r]);
+#pragma unroll
+    for (int r = 0; r < 12; ++r) sums[r] = sums[r] + dpp_f<0x140>(sums[r]);
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
-      ps[r] = sums[r];
-      pq[r] = sums[6 + r];
+      const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(sums[r]), __float_as_uint(sums[6 + r]), false,
+                                                      false);
+      tot[r] = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+    }
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(tot[r]), __float_as_uint(tot[r]), false, false);
+      tot[r] = __uint_as_float(b[0]) + __uint_as_float(b[1]);
     }
   }
   c.ts->mark(2);
@@ -608,9 +626,11 @@ __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev&
   // of three divisions and a square root in the instruction stream instead of six
   float alphas[6], betas[6];
   {
-    const int r = min(c.lane, 5);
-    const float psl = r == 0 ? ps[0] : r == 1 ? ps[1] : r == 2 ? ps[2] : r == 3 ? ps[3] : r == 4 ? ps[4] : ps[5];
-    const float pql = r == 0 ? pq[0] : r == 1 ? pq[1] : r == 2 ? pq[2] : r == 3 ? pq[3] : r == 4 ? pq[4] : pq[5];
+    // probe r's ps total from lane r (row 0), its pq total from lane 16 + r (row 1), moved to row 0 by one swap
+    const int r = min(c.lane & 15, 5);
+    const float psl = r == 0 ? tot[0] : r == 1 ? tot[1] : r == 2 ? tot[2] : r == 3 ? tot[3] : r == 4 ? tot[4] : tot[5];
+    const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(psl), __float_as_uint(psl), false, false);
+    const float pql = __uint_as_float(sw[1]);
     const float mean = div_const(psl, c.lenf, c.rlen), sumsq = div_const(pql, c.lenf, c.rlen);   // psl / len, pql / len
     const float alpha = sqrtf(tp.sumsq / sumsq);
     const float beta = tp.mean - alpha * mean;
