@@ -659,7 +659,34 @@ __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev&
     sc[r] = acc;
   }
   c.ts->mark(3);
-  wave_tree_sums<6>(sc);
+  // the six score sums as the probe sums above: DPP stages per value, the row stages per pair (sc[2k] ends in rows
+  // 0 / 2, sc[2k+1] in rows 1 / 3, brought to row 0 by one more swap); the quotient lanes 0-5 are in row 0
+#pragma unroll
+  for (int r = 0; r < 6; ++r) sc[r] = sc[r] + dpp_f<0xB1>(sc[r]);
+#pragma unroll
+  for (int r = 0; r < 6; ++r) sc[r] = sc[r] + dpp_f<0x4E>(sc[r]);
+#pragma unroll
+  for (int r = 0; r < 6; ++r) sc[r] = sc[r] + dpp_f<0x141>(sc[r]);
+#pragma unroll
+  for (int r = 0; r < 6; ++r) sc[r] = sc[r] + dpp_f<0x140>(sc[r]);
+  float sct[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(sc[2 * k]), __float_as_uint(sc[2 * k + 1]), false,
+                                                    false);
+    sct[k] = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(sct[k]), __float_as_uint(sct[k]), false, false);
+    sct[k] = __uint_as_float(b[0]) + __uint_as_float(b[1]);
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const auto o = __builtin_amdgcn_permlane16_swap(__float_as_uint(sct[k]), __float_as_uint(sct[k]), false, false);
+    sc[2 * k] = sct[k];                      // (row 0)
+    sc[2 * k + 1] = __uint_as_float(o[1]);  // row 1's total, in row 0
+  }
   const double sad0 = sc[0], sadn1x = sc[1], sadn1y = sc[2], sadp1x = sc[3], sadp1y = sc[4], sadxy = sc[5];
   // The six difference quotients of hessian.h:160-171, one per lane (lane e computes quotient e with the
   // reference's fp64 operations in the reference's order, so the bits are the same) and gathered by readlane:
