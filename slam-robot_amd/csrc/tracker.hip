@@ -496,19 +496,25 @@ __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev&
   GeoY ly;
   make_geo_x(xv, c.W, L.w, lx);
   make_geo_y(yv, c.W, L.h, ly);
-  // variant 0's integer geometry to every lane; lanes 1 and 2 compare theirs with it (one ballot)
+  // variant 0's integer geometry to every lane; lanes 1 and 2 compare theirs with it (one ballot).  The five
+  // integers of each half travel as one packed word (zx, rx, rw: 0..W <= 16, 5 bits each; col0: 17 signed bits;
+  // pw = W - zx), so two readlanes and one compare per half instead of ten and five
+  const unsigned pkx = (unsigned)lx.zx | ((unsigned)lx.rx << 5) | ((unsigned)lx.rw << 10) | ((unsigned)lx.col0 << 15);
+  const unsigned pky = (unsigned)ly.zy | ((unsigned)ly.ry << 5) | ((unsigned)ly.rh << 10) |
+                       ((unsigned)ly.base_row << 15);
+  const unsigned px0 = __builtin_amdgcn_readfirstlane(pkx), py0 = __builtin_amdgcn_readfirstlane(pky);
   GeoX gx0;
   GeoY gy0;
-  gx0.zx = __builtin_amdgcn_readlane(lx.zx, 0);
-  gx0.pw = __builtin_amdgcn_readlane(lx.pw, 0);
-  gx0.col0 = __builtin_amdgcn_readlane(lx.col0, 0);
-  gx0.rx = __builtin_amdgcn_readlane(lx.rx, 0);
-  gx0.rw = __builtin_amdgcn_readlane(lx.rw, 0);
-  gy0.zy = __builtin_amdgcn_readlane(ly.zy, 0);
-  gy0.ph = __builtin_amdgcn_readlane(ly.ph, 0);
-  gy0.base_row = __builtin_amdgcn_readlane(ly.base_row, 0);
-  gy0.ry = __builtin_amdgcn_readlane(ly.ry, 0);
-  gy0.rh = __builtin_amdgcn_readlane(ly.rh, 0);
+  gx0.zx = (int)(px0 & 31u);
+  gx0.pw = c.W - gx0.zx;
+  gx0.rx = (int)((px0 >> 5) & 31u);
+  gx0.rw = (int)((px0 >> 10) & 31u);
+  gx0.col0 = (int)px0 >> 15;
+  gy0.zy = (int)(py0 & 31u);
+  gy0.ph = c.W - gy0.zy;
+  gy0.ry = (int)((py0 >> 5) & 31u);
+  gy0.rh = (int)((py0 >> 10) & 31u);
+  gy0.base_row = (int)py0 >> 15;
   float av[3], bv[3];
 #pragma unroll
   for (int u = 0; u < 3; ++u) {
@@ -520,7 +526,7 @@ __device__ __forceinline__ void brute_hessian(const TrackCtx& c, const LevelDev&
   constexpr int kXi[6] = {0, 1, 0, 2, 0, 2}, kYi[6] = {0, 0, 1, 0, 2, 2};
   // Unless a probe crosses a pixel boundary (or the border), the six share their integer geometry and so every
   // tap: the taps are read once and combined with each probe's weights — the same floats as six samples.
-  const bool same = geo_x_same(lx, gx0) && geo_y_same(ly, gy0);
+  const bool same = pkx == px0 && pky == py0;   // (the packing is one to one: geo_x_same && geo_y_same)
   const bool shared = (__ballot(same) & 7ull) == 7ull;
   float pv[6][NK], ps[6], pq[6];
   if (shared) {
