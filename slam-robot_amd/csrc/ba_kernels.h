@@ -120,8 +120,6 @@ constexpr int kLinMaxRounds = 4;   // measured best at 130k and 1.6M observation
 struct LinRound {
   int32_t o0, o1;     // observation range
   int32_t p0, p1;     // points (whole points; every piece of a wide point names it)
-  int32_t lst;        // offset in lin_list (uint16): [nb + 1] per-block offsets, then local indices by block
-  int32_t pad;
 };
 struct LinChunk {
   int32_t r0, r1;     // round range
@@ -245,7 +243,6 @@ struct Dev {
   const int32_t* obs_meta;       // [M] packed block / camera / freedom flags (kMeta*)
   const LinChunk* lchunks;       // [nlin] k_linearize workgroups
   const LinRound* lrounds;
-  const uint16_t* llist;         // per round: window-block offsets + local observation indices by block
   int32_t nlin;
   double* lin_scal[2];           // [nlin][kNScal] k_linearize scalars (cost, failures, |x|^2, max |g|)
   const int32_t* pu_units;       // [npu] k_point_update work units: round index, or -(chunk + 1) (wide chunk)

@@ -172,7 +172,6 @@ class BaSolver {
   DBuf<SchurSeg> segs_;
   DBuf<LinChunk> lchunks_d_;
   DBuf<LinRound> lrounds_d_;
-  DBuf<uint16_t> llist_d_;
   DBuf<double> lin_scal_;
   int nlin_ = 0;
   int lin_waves_ = 1;   // waves per k_linearize / k_update_lin chunk (2 when 2 nlin_ waves fit the chip at once)

@@ -241,6 +241,12 @@ void BaSolver::Load(const sg_problem& p) {
       inv_perm[i] = pos;
     }
   }
+  // the first / last free block of each point in device order (the work-list builders below read them per point)
+  std::vector<int32_t> dfirst(P_), dlast(P_);
+  for (int i = 0; i < P_; ++i) {
+    dfirst[i] = pfirst[point_perm_[i]];
+    dlast[i] = plast[point_perm_[i]];
+  }
   lap("point-order");
   // observations: CSR by device point order (stable in problem order)
   std::vector<int32_t> poff(P_ + 1, 0);
@@ -357,15 +363,12 @@ void BaSolver::Load(const sg_problem& p) {
   // grid still fills the chip.
   std::vector<LinRound> lrounds;
   std::vector<LinChunk> lchunks;
-  std::vector<uint16_t> llist;
-  llist.reserve((size_t)M_ + (size_t)M_ / 4 + 64);
   int lcam_off = 0;
-  std::vector<int> cnt;   // per round: window-block counters (scratch, reused)
   {
     int maxr = std::max(1, std::min(kLinMaxRounds, M_ / (kLinObs * 1024)));
     auto kobs = [&](int i) { return poff[i + 1] - poff[i]; };
-    auto constonly = [&](int i) { return pfirst[point_perm_[i]] >= NB_; };
-    auto pspan = [&](int i) { return constonly(i) ? 0 : plast[point_perm_[i]] - pfirst[point_perm_[i]] + 1; };
+    auto constonly = [&](int i) { return dfirst[i] >= NB_; };
+    auto pspan = [&](int i) { return constonly(i) ? 0 : dlast[i] - dfirst[i] + 1; };
     for (int i = 0; i < P_;) {
       LinChunk c{};
       c.p0 = i;
@@ -373,26 +376,26 @@ void BaSolver::Load(const sg_problem& p) {
       if (kobs(i) > kLinObs || pspan(i) > kLinNbMax) {
         c.wide = 1;
         for (int o = poff[i]; o < poff[i + 1]; o += kLinObs)
-          lrounds.push_back(LinRound{o, std::min(o + kLinObs, poff[i + 1]), i, i + 1, 0, 0});
+          lrounds.push_back(LinRound{o, std::min(o + kLinObs, poff[i + 1]), i, i + 1});
         c.p1 = ++i;
       } else {
         const bool co = constonly(i);
-        int lo = co ? 0 : pfirst[point_perm_[i]], hi = co ? -1 : plast[point_perm_[i]];
+        int lo = co ? 0 : dfirst[i], hi = co ? -1 : dlast[i];
         int j = i, nr = 0;
-        LinRound R{poff[i], poff[i], i, i, 0, 0};
+        LinRound R{poff[i], poff[i], i, i};
         while (j < P_) {
           if (kobs(j) > kLinObs || pspan(j) > kLinNbMax || constonly(j) != co) break;
           int l2 = lo, h2 = hi;
           if (!co) {
-            l2 = std::min(lo, pfirst[point_perm_[j]]);
-            h2 = std::max(hi, plast[point_perm_[j]]);
+            l2 = std::min(lo, dfirst[j]);
+            h2 = std::max(hi, dlast[j]);
             if (h2 - l2 + 1 > kLinNbMax) break;
           }
           if (R.o1 - R.o0 + kobs(j) > kLinObs || R.p1 - R.p0 >= kLinPts) {
             if (nr + 1 >= maxr) break;
             lrounds.push_back(R);
             ++nr;
-            R = LinRound{poff[j], poff[j], j, j, 0, 0};
+            R = LinRound{poff[j], poff[j], j, j};
           }
           R.o1 += kobs(j);
           R.p1 = j + 1;
@@ -409,25 +412,6 @@ void BaSolver::Load(const sg_problem& p) {
       c.r1 = (int)lrounds.size();
       c.cam_off = lcam_off;
       lcam_off += c.nb * kCamV;
-      // per round: the window-block offsets and the round-local observation indices sorted by block
-      for (int r = c.r0; r < c.r1; ++r) {
-        LinRound& R = lrounds[r];
-        R.lst = (int)llist.size();
-        if (c.nb == 0) continue;
-        cnt.assign(c.nb + 1, 0);
-        for (int o = R.o0; o < R.o1; ++o) {
-          const int b = frame_block[obs_frame[o]];
-          if (b >= 0) cnt[b - c.b_lo + 1]++;
-        }
-        for (int k = 0; k < c.nb; ++k) cnt[k + 1] += cnt[k];
-        const size_t base = llist.size();
-        llist.resize(base + c.nb + 1 + cnt[c.nb]);
-        for (int k = 0; k <= c.nb; ++k) llist[base + k] = (uint16_t)cnt[k];
-        for (int o = R.o0; o < R.o1; ++o) {
-          const int b = frame_block[obs_frame[o]];
-          if (b >= 0) llist[base + c.nb + 1 + cnt[b - c.b_lo]++] = (uint16_t)(o - R.o0);
-        }
-      }
       lchunks.push_back(c);
     }
   }
@@ -452,10 +436,9 @@ void BaSolver::Load(const sg_problem& p) {
   std::vector<int32_t> obs_blk(M_);
   for (int o = 0; o < M_; ++o) obs_blk[o] = frame_block[obs_frame[o]];
   // span in blocks of a free point's Schur terms (0: none)
-  auto sspan = [&](int i) {
-    const int pt = point_perm_[i];
-    return (pfree[i] && pfirst[pt] < NB_) ? plast[pt] - pfirst[pt] + 1 : 0;
-  };
+  std::vector<int32_t> ssp(std::max(P_, 1));
+  for (int i = 0; i < P_; ++i) ssp[i] = (pfree[i] && dfirst[i] < NB_) ? dlast[i] - dfirst[i] + 1 : 0;
+  auto sspan = [&](int i) { return ssp[i]; };
   std::vector<int32_t> simple_obs(std::max(P_, 1), -1);   // observation of the first block if one per block
   int ncell = 0;
   npairs_ = 0;
@@ -472,7 +455,7 @@ void BaSolver::Load(const sg_problem& p) {
       if (pfree[i]) npairs_ += kb * (kb + 1) / 2;
       const int sp = sspan(i);
       if (sp == 0 || sp > kSegNbMax) continue;
-      const int pf = pfirst[point_perm_[i]];
+      const int pf = dfirst[i];
       pinfo[2 * i] = (int)(cells.size() / 4);
       pinfo[2 * i + 1] = (pf << 8) | sp;
       bo.clear();
@@ -513,7 +496,7 @@ void BaSolver::Load(const sg_problem& p) {
     auto point_cost = [&](int j, int tile0) {
       const int sp = sspan(j);
       if (sp == 0) return kSegPointCost;
-      const int e = (6 * (pfirst[point_perm_[j]] + sp) - 1) / 16 - tile0;
+      const int e = (6 * (dfirst[j] + sp) - 1) / 16 - tile0;
       return kSegPointCost + (schur_aug_base(e + 1) + kSchurCWaves - 1) / kSchurCWaves;
     };
     std::vector<int32_t> seg_end;   // exclusive end of each planned segment, in point order
@@ -531,7 +514,7 @@ void BaSolver::Load(const sg_problem& p) {
           if (sp > kSegNbMax) break;
           int l2 = clo, h2 = chi;
           if (sp > 0) {
-            const int pf = pfirst[point_perm_[j]];
+            const int pf = dfirst[j];
             l2 = std::min(clo, 6 * pf);
             h2 = std::max(chi, 6 * (pf + sp));
             if ((h2 + 15) / 16 - l2 / 16 > kSchurTW) break;
@@ -550,7 +533,7 @@ void BaSolver::Load(const sg_problem& p) {
     {
       long long est = 0;
       for (int j = 0; j < P_; ++j)
-        if (sspan(j) <= kSegNbMax) est += point_cost(j, sspan(j) ? 6 * pfirst[point_perm_[j]] / 16 : 0);
+        if (sspan(j) <= kSegNbMax) est += point_cost(j, sspan(j) ? 6 * dfirst[j] / 16 : 0);
       long long cap = std::max(1LL, (est + ncu_ - 1) / ncu_);
       for (int pass = 0; pass < 8; ++pass) {
         plan(cap);
@@ -588,7 +571,7 @@ void BaSolver::Load(const sg_problem& p) {
         const int sp = sspan(j);
         if (sp > kSegNbMax) break;
         if (sp > 0) {
-          const int pf = pfirst[point_perm_[j]];
+          const int pf = dfirst[j];
           const int l2 = std::min(clo, 6 * pf), h2 = std::max(chi, 6 * (pf + sp));
           if ((h2 + 15) / 16 - l2 / 16 > kSchurTW) break;
           clo = l2;
@@ -613,7 +596,7 @@ void BaSolver::Load(const sg_problem& p) {
       // last window tile of each point's columns (-1: no Schur terms)
       auto pjhi = [&](int k) {
         const int sp = sspan(k);
-        return sp == 0 ? -1 : (6 * (pfirst[point_perm_[k]] + sp) - 1 - 16 * sg.t0) / 16;
+        return sp == 0 ? -1 : (6 * (dfirst[k] + sp) - 1 - 16 * sg.t0) / 16;
       };
       sg.bt0 = (int)sbatch.size();
       for (int k = i; k < j;) {
@@ -632,7 +615,7 @@ void BaSolver::Load(const sg_problem& p) {
           schur_mfma_ += schur_aug_base(pjhi(k) + 1) - (pjhi(k) + 1);   // window tiles (16x16x4)
           schur_rhs_ += pjhi(k) + 1;                                      // rhs slots (4x4x4, 4 blocks)
           if (pjhi(k) >= 0) {   // the slots that multiply the point's own tiles (the rest multiply zeros)
-            const double nu = pjhi(k) - (6 * pfirst[point_perm_[k]] - 16 * sg.t0) / 16 + 1;
+            const double nu = pjhi(k) - (6 * dfirst[k] - 16 * sg.t0) / 16 + 1;
             schur_useful_ += 2048.0 * nu * (nu + 1) / 2 + 512.0 * nu;
           }
           nc += sspan(k++);
@@ -869,8 +852,6 @@ void BaSolver::Load(const sg_problem& p) {
   // upload batch 2 — the work lists: one pinned staging copy and one scatter launch (stager.h)
   stg.Add(lchunks_d_, lchunks);
   stg.Add(lrounds_d_, lrounds);
-  if (llist.empty()) llist.push_back(0);
-  stg.Add(llist_d_, llist);
   stg.Add(segs_, segs.empty() ? std::vector<SchurSeg>(1) : segs);
   stg.Add(sbatch_, sbatch.empty() ? std::vector<SchurBatch>(1) : sbatch);
   stg.Add(wsegs_, wsegs.empty() ? std::vector<WideSeg>(1) : wsegs);
@@ -1032,7 +1013,6 @@ void BaSolver::Reserve(int F, int P, int M) {
   moved |= obs_pnt_.Reserve(m);
   moved |= cells_.Reserve(4 * m);
   moved |= cell_obs_.Reserve(m);
-  moved |= llist_d_.Reserve(2 * m);
   // per point
   moved |= X_.Reserve(8 * pp);
   moved |= V_.Reserve(2 * 10 * pp);
@@ -1277,7 +1257,6 @@ Dev BaSolver::MakeDev() {
   d.obs_pnt = obs_pnt_.ptr;
   d.lchunks = lchunks_d_.ptr;
   d.lrounds = lrounds_d_.ptr;
-  d.llist = llist_d_.ptr;
   d.nlin = nlin_;
   d.npu = npu_;
   d.pu_units = pu_units_.ptr;
