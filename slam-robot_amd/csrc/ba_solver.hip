@@ -804,9 +804,8 @@ void BaSolver::Load(const sg_problem& p) {
   if (chol_tiles_) {
     // W tiles of the top and bottom halves, the bottom's z' (+ failure slot), the separator contribution
     // and its rhs, then the constants {0, 1}
-    std::vector<double> wz((size_t)2 * npanel * kTB * 256 + 16 * (size_t)npanel + 49 * 256 + 7 * 16 + 2, 0.0);
-    wz.back() = 1.0;
-    stager_->Add(Wg_, wz);
+    // (zeroed and its constants set on the device by ResetState: no host fill, no staged zeros)
+    Wg_.Resize((size_t)2 * npanel * kTB * 256 + 16 * (size_t)npanel + 49 * 256 + 7 * 16 + 2);
     stager_->Add(tflag_, std::vector<int32_t>(2, 0));
     tile_lds_ = (size_t)npanel * 32 * sizeof(double) + (size_t)(3 * npanel + 1) / 2 * sizeof(double);
     chol_cand_lds_ = !chol_border_ && F_ <= kCandMax && D_ <= kCandMax &&
@@ -1077,21 +1076,22 @@ void BaSolver::SaveStructure(const sg_problem& p) {
 // LM state and accumulators a fresh solve starts from (zeroed on every Load)
 // Zero a few device buffers and set the tiled Cholesky's {0, 1} constants (after S and its rhs) in one launch
 // (hipMemsetAsync / a pageable hipMemcpyAsync would go through the copy engine).
+constexpr int kZeroBufs = 9;
 struct ZeroList {
-  double* p[8];
-  size_t n[8];   // doubles
-  double* c01;   // two doubles: {0, 1}
+  double* p[kZeroBufs];
+  size_t n[kZeroBufs];   // doubles
+  double* c01[2];        // two doubles each: {0, 1}
 };
 __global__ __launch_bounds__(256) void k_reset_buffers(ZeroList z) {
-  for (int b = 0; b < 8; ++b) {
+  for (int b = 0; b < kZeroBufs; ++b) {
     double* p = z.p[b];
     const size_t n = z.n[b];
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
       p[i] = 0.0;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0 && z.c01) {
-    z.c01[0] = 0.0;
-    z.c01[1] = 1.0;
+  if (blockIdx.x == 0 && threadIdx.x < 2 && z.c01[threadIdx.x]) {
+    z.c01[threadIdx.x][0] = 0.0;
+    z.c01[threadIdx.x][1] = 1.0;
   }
 }
 
@@ -1112,9 +1112,13 @@ void BaSolver::ResetState(hipStream_t s) {
   put(5, rhs_.ptr, rhs_.size * sizeof(double));
   put(6, chunk_scal_.ptr, chunk_scal_.size * sizeof(double));
   put(7, S_.ptr, (S_.size - 2) * sizeof(double));
-  z.c01 = S_.ptr + S_.size - 2;   // k_chol_tiles: padding entries of the last tile
+  z.c01[0] = S_.ptr + S_.size - 2;   // k_chol_tiles: padding entries of the last tile
+  if (chol_tiles_ && Wg_.size >= 2) {   // its W tiles, z', separator terms, then its own {0, 1}
+    put(8, Wg_.ptr, (Wg_.size - 2) * sizeof(double));
+    z.c01[1] = Wg_.ptr + Wg_.size - 2;
+  }
   size_t mx = 0;
-  for (int i = 0; i < 8; ++i) mx = std::max(mx, z.n[i]);
+  for (int i = 0; i < kZeroBufs; ++i) mx = std::max(mx, z.n[i]);
   const unsigned g = (unsigned)std::min<size_t>(512, std::max<size_t>(1, (mx + 255) / 256));
   hipLaunchKernelGGL(k_reset_buffers, dim3(g), dim3(256), 0, s, z);
   SG_HIP_CHECK(hipGetLastError());
